@@ -1,0 +1,274 @@
+/*
+ * orb_abi.h -- C ABI of the MI355X-native ORB front-end (extractor + Hamming matcher).
+ *
+ * This is the drop-in boundary.  Plain C: pointers, sizes, status codes; no
+ * OpenCV, no torch, no HIP types in any signature (streams are passed as
+ * `void*`, a hipStream_t, NULL = the handle's own stream).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference tree, yg838457845/ORB_SLAM2-Chinese-annotation):
+ *
+ *   orb_extractor_create/destroy   ORBextractor::ORBextractor  include/ORBextractor.h:51-54,
+ *                                  src/ORBextractor.cc:428-489
+ *   orb_extractor_get_*            ORBextractor::Get*          include/ORBextractor.h:63-83
+ *   orb_extractor_extract          ORBextractor::operator()    include/ORBextractor.h:59-61,
+ *                                  src/ORBextractor.cc:1091-1169
+ *   orb_extractor_pyramid_level    ORBextractor::mvImagePyramid include/ORBextractor.h:85
+ *   orb_extractor_extract_batch    (throughput form of operator(), many frames per launch)
+ *   orb_descriptor_distance        ORBmatcher::DescriptorDistance src/ORBmatcher.cc:1814-1830
+ *   orb_hamming_batch              batched DescriptorDistance (device)
+ *   orb_match_projection_local     ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, float)
+ *                                  src/ORBmatcher.cc:47-133 (+ Frame::GetFeaturesInArea
+ *                                  src/Frame.cc:368-424, AssignFeaturesToGrid :261-276)
+ *   orb_match_projection_local_batch  device-batched form of the above
+ *   orb_stereo_match               Frame::ComputeStereoMatches src/Frame.cc:516-704
+ *   orb_match_projection_frame     ORBmatcher::SearchByProjection(Frame&, const Frame&, float, bool)
+ *                                  src/ORBmatcher.cc:1460-1619
+ *   orb_match_bow                  ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+ *                                  src/ORBmatcher.cc:164-306
+ *
+ * Error behaviour: the reference has no status codes (an empty image returns
+ * silently with outputs untouched, src/ORBextractor.cc:1095-1096; a non-8UC1
+ * image asserts, :1100).  Here every call returns an orb_status_t; the C++
+ * wrapper (orb_slam2-chinese-annotation_amd/host/ORBextractor.h) maps
+ * ORB_EEMPTY to "return, outputs untouched" and ORB_EINVAL to an assert.
+ */
+#ifndef ORB_ABI_H
+#define ORB_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORB_ABI_VERSION 1
+#define ORB_DESC_BYTES 32
+#define ORB_GRID_COLS 64 /* FRAME_GRID_COLS, include/Frame.h:39 */
+#define ORB_GRID_ROWS 48 /* FRAME_GRID_ROWS, include/Frame.h:40 */
+
+typedef enum orb_status {
+  ORB_OK = 0,
+  ORB_EEMPTY = 1,     /* empty input: reference returns silently, outputs untouched */
+  ORB_EINVAL = -1,    /* bad argument (reference: assert) */
+  ORB_ENOMEM = -2,    /* device allocation failed */
+  ORB_EDEVICE = -3,   /* HIP runtime / kernel error */
+  ORB_ECAPACITY = -4, /* caller buffer too small; *n set to the required size */
+  ORB_ENODEV = -5     /* no gfx950 device visible */
+} orb_status_t;
+
+/* Mirrors cv::KeyPoint field-for-field (28 bytes). */
+typedef struct orb_keypoint {
+  float x, y;      /* pt */
+  float size;      /* int(31 * scale[octave]) */
+  float angle;     /* degrees, [0, 360] */
+  float response;  /* FAST-9/16 corner score */
+  int32_t octave;  /* pyramid level */
+  int32_t class_id;/* always -1 */
+} orb_keypoint_t;
+
+typedef struct orb_extractor orb_extractor_t;
+typedef struct orb_matcher orb_matcher_t;
+
+/* ---------------------------------------------------------------- extractor */
+
+orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels,
+                                  int ini_th_fast, int min_th_fast, int device,
+                                  orb_extractor_t** out);
+void orb_extractor_destroy(orb_extractor_t* h);
+
+int orb_extractor_get_levels(const orb_extractor_t* h);
+float orb_extractor_get_scale_factor(const orb_extractor_t* h);
+/* Each writes nlevels floats. */
+void orb_extractor_get_scale_factors(const orb_extractor_t* h, float* out);
+void orb_extractor_get_inverse_scale_factors(const orb_extractor_t* h, float* out);
+void orb_extractor_get_scale_sigma_squares(const orb_extractor_t* h, float* out);
+void orb_extractor_get_inverse_scale_sigma_squares(const orb_extractor_t* h, float* out);
+/* Per-level keypoint quotas (mnFeaturesPerLevel, src/ORBextractor.cc:453-464). */
+void orb_extractor_get_features_per_level(const orb_extractor_t* h, int32_t* out);
+/* Upper bound on keypoints one image of this size can produce. */
+int orb_extractor_capacity(const orb_extractor_t* h, int width, int height);
+
+/* ORBextractor::operator(): host image in, host keypoints + N x 32 descriptors out.
+ * Synchronous.  `capacity` = rows available in keypoints/descriptors; on
+ * ORB_ECAPACITY *n_keypoints holds the required count. */
+orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int width,
+                                   int height, size_t stride, orb_keypoint_t* keypoints,
+                                   uint8_t* descriptors, int capacity, int* n_keypoints);
+
+/* Host copy of mvImagePyramid[level] from the last orb_extractor_extract call.
+ * dst may be NULL to query the size. */
+orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t* dst,
+                                         size_t dst_stride, int* width, int* height);
+
+/* Throughput form: n_images device-resident images (image i at
+ * d_images + i*image_pitch, rows `stride` apart), all width x height.
+ * Outputs per image i: d_keypoints[i*capacity ...], d_descriptors[(i*capacity) * 32 ...],
+ * d_counts[i].  Asynchronous on `stream` (NULL = handle stream). */
+orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_images,
+                                         int n_images, int width, int height, size_t stride,
+                                         size_t image_pitch, orb_keypoint_t* d_keypoints,
+                                         uint8_t* d_descriptors, int capacity,
+                                         int32_t* d_counts, void* stream);
+
+/* Device pointer to pyramid level `level` of batch image `image` after
+ * orb_extractor_extract_batch (valid until the next call on this handle). */
+orb_status_t orb_extractor_batch_level(orb_extractor_t* h, int image, int level,
+                                       const uint8_t** d_level, int* width, int* height,
+                                       size_t* stride);
+
+/* Stream the handle launches on (a hipStream_t). */
+void* orb_extractor_stream(orb_extractor_t* h);
+
+/* Timing of the most expensive kernel of the last batch (HIP events on the
+ * handle stream): average milliseconds per launch and the kernel's name. */
+orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable);
+orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
+                                        int* launches, const char** name);
+
+/* ------------------------------------------------------------------ matcher */
+
+/* A frame as the matcher sees it (Frame members used by ORBmatcher). */
+typedef struct orb_frame {
+  int32_t n;                     /* N */
+  const orb_keypoint_t* keys;    /* mvKeysUn (== mvKeys at zero distortion) */
+  const uint8_t* descriptors;    /* mDescriptors, N x 32 */
+  const float* u_right;          /* mvuRight (N) or NULL for monocular (-1) */
+  float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+  int32_t n_levels;
+  const float* scale_factors;    /* mvScaleFactors */
+} orb_frame_t;
+
+/* MapPoint fields written by Frame::isInFrustum (include/MapPoint.h:92-97). */
+typedef struct orb_mp_track {
+  float proj_x, proj_y, proj_xr;  /* mTrackProjX, mTrackProjY, mTrackProjXR */
+  float view_cos;                 /* mTrackViewCos */
+  int32_t level;                  /* mnTrackScaleLevel */
+  uint8_t in_view;                /* mbTrackInView */
+  uint8_t bad;                    /* isBad() */
+  uint8_t has_obs;                /* Observations() > 0 (a claim by it locks the keypoint) */
+  uint8_t _pad;
+} orb_mp_track_t;
+
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+orb_status_t orb_matcher_create(int device, orb_matcher_t** out);
+void orb_matcher_destroy(orb_matcher_t* m);
+void* orb_matcher_stream(orb_matcher_t* m);
+
+/* dist[i] = DescriptorDistance(a + 32 i, b + 32 i), device pointers. */
+orb_status_t orb_hamming_batch(orb_matcher_t* m, const uint8_t* d_a, const uint8_t* d_b,
+                               int n, int32_t* d_dist, void* stream);
+
+/* SearchByProjection(F, vpMapPoints, th) with ORBmatcher(nnratio).
+ * kp_locked[i] != 0  <=>  F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0
+ * on entry.  Output kp_match[i] = index of the MapPoint assigned to keypoint i
+ * by THIS call (last writer wins, as F.mvpMapPoints[bestIdx]=pMP), or -1.
+ * Returns the reference's nmatches. Host buffers. */
+orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* frame,
+                                        const uint8_t* kp_locked, int n_mp,
+                                        const orb_mp_track_t* mps, const uint8_t* mp_desc,
+                                        float th, float nnratio, int32_t* kp_match,
+                                        int32_t* nmatches);
+
+/* Device-batched form: P independent (frame, local map) problems.
+ * Problem p: keypoints d_keys + p*kp_stride (count d_nkeys[p]), descriptors
+ * d_desc + p*kp_stride*32, locks d_locked + p*kp_stride (may be NULL),
+ * map points d_mps + p*mp_stride (count d_nmps[p]), their descriptors
+ * d_mp_desc + p*mp_stride*32.  Monocular (u_right = -1).  Frame bounds and
+ * scale factors are shared.  Outputs d_kp_match + p*kp_stride, d_nmatches[p]. */
+orb_status_t orb_match_projection_local_batch(
+    orb_matcher_t* m, int n_problems, const orb_keypoint_t* d_keys, const uint8_t* d_desc,
+    const int32_t* d_nkeys, const uint8_t* d_locked, int kp_stride,
+    const orb_mp_track_t* d_mps, const uint8_t* d_mp_desc, const int32_t* d_nmps,
+    int mp_stride, float min_x, float max_x, float min_y, float max_y, int n_levels,
+    const float* scale_factors, float th, float nnratio, int32_t* d_kp_match,
+    int32_t* d_nmatches, void* stream);
+
+/* Frame::ComputeStereoMatches for one rectified pair.  Left/right keypoints
+ * and descriptors as produced by the two extractors, plus both pyramids
+ * (level l of side s at pyr[s][l] with the given stride/size).  Writes
+ * mvuRight / mvDepth (-1 = no match). Host buffers. */
+typedef struct orb_stereo_input {
+  const orb_frame_t* left;       /* mvKeys, mDescriptors (u_right ignored) */
+  int32_t n_right;
+  const orb_keypoint_t* right_keys;
+  const uint8_t* right_desc;
+  int32_t n_levels;
+  const uint8_t* const* left_levels;   /* n_levels host pointers */
+  const uint8_t* const* right_levels;
+  const int32_t* level_width;    /* n_levels */
+  const int32_t* level_height;
+  const int64_t* level_stride;
+  const float* inv_scale_factors;/* mvInvScaleFactors */
+  float bf;                      /* mbf */
+  float fx;                      /* fx; mb = bf / fx */
+} orb_stereo_input_t;
+
+orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in,
+                              float* u_right, float* depth);
+
+/* SearchByProjection(CurrentFrame, LastFrame, th, bMono) with ORBmatcher(nnratio, checkOri).
+ * The last frame's map points are given already projected with the current
+ * pose (the float camera-space coordinates xc, yc and invzc computed exactly
+ * as src/ORBmatcher.cc:1500-1505).  valid[i]=0 for NULL or outlier entries. */
+typedef struct orb_last_mp {
+  float xc, yc, invzc;          /* Rcw*x3Dw + tcw, 1/z */
+  int32_t last_octave;          /* LastFrame.mvKeys[i].octave */
+  float last_angle;             /* LastFrame.mvKeysUn[i].angle */
+  uint8_t valid;                /* pMP && !mvbOutlier[i] */
+  uint8_t has_obs;              /* pMP->Observations() > 0 */
+  uint8_t _pad[2];
+  int32_t mp_id;                /* identity of pMP (same id => same MapPoint) */
+} orb_last_mp_t;
+
+typedef struct orb_camera {
+  float fx, fy, cx, cy, bf, mb;
+} orb_camera_t;
+
+orb_status_t orb_match_projection_frame(orb_matcher_t* m, const orb_frame_t* current,
+                                        const uint8_t* kp_locked, int n_last,
+                                        const orb_last_mp_t* last, const uint8_t* last_desc,
+                                        const orb_camera_t* cam, float tlc_z, float th,
+                                        int mono, int check_orientation,
+                                        int32_t* kp_match, int32_t* nmatches);
+
+/* SearchByBoW(pKF, F, vpMapPointMatches) with ORBmatcher(nnratio, checkOri).
+ * FeatureVectors are CSR: node ids ascending (nodes_*), feature lists
+ * offs_*[k]..offs_*[k+1] in feats_*.  kf_mp[i] = MapPoint id of KF keypoint i
+ * or -1 (NULL); kf_mp_bad[i] = isBad().  Output f_match[j] = MapPoint id or -1. */
+orb_status_t orb_match_bow(orb_matcher_t* m, int n_kf, const uint8_t* kf_desc,
+                           const float* kf_angle, const int32_t* kf_mp,
+                           const uint8_t* kf_mp_bad, int kf_nodes, const uint32_t* kf_node_ids,
+                           const int32_t* kf_offs, const uint32_t* kf_feats, int n_f,
+                           const uint8_t* f_desc, const float* f_angle, int f_nodes,
+                           const uint32_t* f_node_ids, const int32_t* f_offs,
+                           const uint32_t* f_feats, float nnratio, int check_orientation,
+                           int32_t* f_match, int32_t* nmatches);
+
+/* ---------------------------------------------------------- synthetic input */
+
+/* Deterministic synthetic grayscale images (integer-only generator, identical
+ * everywhere).  view 0 = left / mono, 1 = right (shapes shifted by their
+ * disparity, bf-consistent).  Frame `frame` of sequence `seed` applies the
+ * cumulative ego-motion of frames 0..frame-1. */
+void orb_synth_image(uint64_t seed, int frame, int view, int width, int height,
+                     uint8_t* out, size_t stride);
+
+/* Synthetic local map of n_mp points derived from one frame's keypoints
+ * (SURVEY §8(d) C5 recipe).  Writes mps[n_mp], mp_desc[n_mp*32],
+ * kp_locked[n_kp]. */
+void orb_synth_local_map(uint64_t seed, const orb_keypoint_t* keys,
+                         const uint8_t* desc, int n_kp, int n_mp, int width, int height,
+                         orb_mp_track_t* mps, uint8_t* mp_desc, uint8_t* kp_locked);
+
+/* Library / device info. */
+int orb_abi_version(void);
+orb_status_t orb_device_count(int* n);
+const char* orb_status_string(orb_status_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORB_ABI_H */

@@ -1,0 +1,231 @@
+"""ctypes wrapper of the CPU oracle (oracle/liborb_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / CPU baseline -- never by the
+product package.  Parity status: unpinned against a reference binary (see the
+header of orb_oracle.cpp and DESIGN.md §2).
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "liborb_oracle.so"
+
+KEYPOINT_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+     ("octave", "<i4"), ("class_id", "<i4")]
+)
+MP_TRACK_DTYPE = np.dtype(
+    [("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+     ("level", "<i4"), ("in_view", "u1"), ("bad", "u1"), ("has_obs", "u1"), ("_pad", "u1")]
+)
+
+_lib = None
+
+
+class _Frame(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32), ("keys", ctypes.c_void_p), ("descriptors", ctypes.c_void_p),
+        ("u_right", ctypes.c_void_p), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+        ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("n_levels", ctypes.c_int32),
+        ("scale_factors", ctypes.c_void_p),
+    ]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        build()
+    L = ctypes.CDLL(str(LIB_PATH))
+    vp, i32, f32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+    sig = {
+        "oracle_params": (i32, [i32, f32, i32, vp, vp, vp, vp, vp, vp]),
+        "oracle_level_sizes": (i32, [i32, i32, f32, i32, vp]),
+        "oracle_pyramid": (i32, [vp, i32, i32, sz, f32, i32, vp]),
+        "oracle_resize": (i32, [vp, i32, i32, vp, i32, i32]),
+        "oracle_blur7": (i32, [vp, i32, i32, vp]),
+        "oracle_fast": (i32, [vp, i32, i32, i32, vp, i32]),
+        "oracle_fast_atan2": (f32, [f32, f32]),
+        "oracle_sincos": (None, [f32, vp, vp]),
+        "oracle_descriptor_distance": (i32, [vp, vp]),
+        "oracle_candidates": (i32, [vp, i32, i32, sz, i32, f32, i32, i32, i32, vp, i32, vp]),
+        "oracle_distribute": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, i32]),
+        "oracle_extract": (i32, [vp, i32, i32, sz, i32, f32, i32, i32, i32, vp, vp, i32, vp]),
+        "oracle_match_projection_local": (i32, [vp, vp, i32, vp, vp, f32, f32, vp]),
+        "oracle_grid": (i32, [vp, i32, f32, f32, f32, f32, vp, vp]),
+        "oracle_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
+        "oracle_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _p(a):
+    return a.ctypes.data
+
+
+def params(nfeatures=1000, scale_factor=1.2, nlevels=8):
+    sc, isc, s2, is2 = (np.zeros(nlevels, np.float32) for _ in range(4))
+    q = np.zeros(nlevels, np.int32)
+    um = np.zeros(16, np.int32)
+    lib().oracle_params(nfeatures, scale_factor, nlevels, _p(sc), _p(isc), _p(s2), _p(is2), _p(q), _p(um))
+    return dict(scale=sc, inv_scale=isc, sigma2=s2, inv_sigma2=is2, quota=q, umax=um)
+
+
+def level_sizes(w, h, scale_factor=1.2, nlevels=8):
+    wh = np.zeros(2 * nlevels, np.int32)
+    lib().oracle_level_sizes(w, h, scale_factor, nlevels, _p(wh))
+    return [(int(wh[2 * l]), int(wh[2 * l + 1])) for l in range(nlevels)]
+
+
+def pyramid(img, scale_factor=1.2, nlevels=8):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    sizes = level_sizes(w, h, scale_factor, nlevels)
+    out = np.zeros(sum(a * b for a, b in sizes), np.uint8)
+    lib().oracle_pyramid(_p(img), w, h, w, scale_factor, nlevels, _p(out))
+    levels, off = [], 0
+    for (lw, lh) in sizes:
+        levels.append(out[off: off + lw * lh].reshape(lh, lw))
+        off += lw * lh
+    return levels
+
+
+def resize(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize(_p(src), src.shape[1], src.shape[0], _p(dst), dw, dh)
+    return dst
+
+
+def blur7(src):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    lib().oracle_blur7(_p(src), src.shape[1], src.shape[0], _p(dst))
+    return dst
+
+
+def fast(img, threshold):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = w * h
+    out = np.zeros(cap, KEYPOINT_DTYPE)
+    n = lib().oracle_fast(_p(img), w, h, threshold, _p(out), cap)
+    return out[:n].copy()
+
+
+def fast_atan2(y, x):
+    return lib().oracle_fast_atan2(y, x)
+
+
+def sincos(angle):
+    s, c = ctypes.c_float(), ctypes.c_float()
+    lib().oracle_sincos(angle, ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oracle_descriptor_distance(_p(a), _p(b))
+
+
+def candidates(img, nfeatures=1000, scale_factor=1.2, nlevels=8, ini=20, mn=7):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    per = np.zeros(nlevels, np.int32)
+    n = lib().oracle_candidates(_p(img), w, h, w, nfeatures, scale_factor, nlevels, ini, mn, None, 0, _p(per))
+    out = np.zeros(max(n, 1), KEYPOINT_DTYPE)
+    lib().oracle_candidates(_p(img), w, h, w, nfeatures, scale_factor, nlevels, ini, mn, _p(out), n, _p(per))
+    return out[:n], per
+
+
+def distribute(keys, min_x, max_x, min_y, max_y, n):
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    cap = max(len(keys), 1)
+    out = np.zeros(cap, KEYPOINT_DTYPE)
+    k = lib().oracle_distribute(_p(keys), len(keys), min_x, max_x, min_y, max_y, n, _p(out), cap)
+    return out[:k].copy()
+
+
+def extract(img, nfeatures=1000, scale_factor=1.2, nlevels=8, ini=20, mn=7):
+    """ORBextractor::operator() on the CPU: (keypoints, descriptors, per_level)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = nfeatures + 64 * nlevels
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        per = np.zeros(nlevels, np.int32)
+        n = lib().oracle_extract(_p(img), w, h, w, nfeatures, scale_factor, nlevels, ini, mn,
+                                 _p(kps), _p(desc), cap, _p(per))
+        if n >= 0:
+            return kps[:n].copy(), desc[:n].copy(), per
+        cap = -n - 1
+
+
+def frame_struct(keys, desc, scale, width, height, u_right=None):
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    scale = np.ascontiguousarray(scale, np.float32)
+    f = _Frame()
+    f.n = len(keys)
+    f.keys = _p(keys)
+    f.descriptors = _p(desc)
+    f.u_right = _p(u_right) if u_right is not None else None
+    f.min_x, f.max_x, f.min_y, f.max_y = 0.0, float(width), 0.0, float(height)
+    f.n_levels = len(scale)
+    f.scale_factors = _p(scale)
+    return f, (keys, desc, scale, u_right)
+
+
+def match_projection_local(keys, desc, scale, width, height, mps, mp_desc, th, nnratio,
+                           kp_locked=None, u_right=None):
+    f, keep = frame_struct(keys, desc, scale, width, height, u_right)
+    mps = np.ascontiguousarray(mps, MP_TRACK_DTYPE)
+    mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+    km = np.full(len(keys), -1, np.int32)
+    lk = None if kp_locked is None else np.ascontiguousarray(kp_locked, np.uint8)
+    n = lib().oracle_match_projection_local(ctypes.byref(f), _p(lk) if lk is not None else None,
+                                            len(mps), _p(mps), _p(mp_desc), th, nnratio, _p(km))
+    return n, km
+
+
+def grid(keys, width, height):
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    cs = np.zeros(64 * 48 + 1, np.int32)
+    idx = np.zeros(max(len(keys), 1), np.int32)
+    n = lib().oracle_grid(_p(keys), len(keys), 0.0, float(width), 0.0, float(height), _p(cs), _p(idx))
+    return cs, idx[:n]
+
+
+def synth_image(seed, frame, width, height, view=0):
+    img = np.empty((height, width), np.uint8)
+    lib().oracle_synth_image(seed, frame, view, width, height, _p(img), width)
+    return img
+
+
+def synth_local_map(seed, keys, desc, n_mp, width, height):
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    mps = np.zeros(n_mp, MP_TRACK_DTYPE)
+    mpd = np.zeros((n_mp, 32), np.uint8)
+    lk = np.zeros(len(keys), np.uint8)
+    lib().oracle_synth_local_map(seed, _p(keys), _p(desc), len(keys), n_mp, width, height,
+                                 _p(mps), _p(mpd), _p(lk))
+    return mps, mpd, lk

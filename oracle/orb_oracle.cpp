@@ -1,0 +1,1177 @@
+// orb_oracle.cpp -- CPU ORACLE for the ORB hot path.  TEST INFRASTRUCTURE ONLY.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+// load this library, and only as the checker / CPU baseline.  The product
+// (lib/liborb_amd.so) never links or calls it.
+//
+// What it is: a scalar, single-threaded restatement of the reference's
+// ORBextractor (src/ORBextractor.cc) and ORBmatcher / Frame matching code
+// (src/ORBmatcher.cc, src/Frame.cc) of yg838457845/ORB_SLAM2-Chinese-annotation,
+// with the OpenCV primitives it calls pinned to "OCV3-scalar" semantics
+// (SURVEY.md Appendix A): FAST-9/16 + NMS, 8U INTER_LINEAR resize with 11-bit
+// fixed-point weights, 8U 7x7 sigma-2 Gaussian with the integer kernel
+// [18,34,49,55,49,34,18], OpenCV fastAtan2, round-half-even cvRound, and a
+// pinned sin/cos (double evaluation, rounded to float).  Each function cites
+// the reference lines it follows.  Control flow that the reference makes
+// order-dependent (DistributeOctTree's std::list + pointer-sorted splits,
+// the matchers' first-come claims) is restated literally with std::list and
+// sequential loops; the pointer tie-break of src/ORBextractor.cc:703 is
+// pinned to node creation order.
+//
+// PARITY STATUS: parity UNPINNED against a reference binary.  The reference
+// cannot be built here (OpenCV/Eigen/Pangolin absent) and it
+// ships no tests, fixtures or golden vectors.  What IS pinned:
+// the constants the reference embeds (rBRIEF table, umax, per-level quotas,
+// scale tables), checked against the reference source text by
+// tests/test_oracle_constants.py when /root/reference is present, and the
+// golden vectors under tests/golden/ generated from this file
+// (tests/golden/make_golden.py) that freeze its behaviour.
+//
+// Build: oracle/Makefile (g++ -O2 -ffp-contract=off; no FMA contraction so the
+// float expressions round exactly as written).
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <list>
+#include <utility>
+#include <vector>
+
+#include "../include/orb_abi.h"
+#include "../orb_slam2-chinese-annotation_amd/csrc/orb_pattern_data.h"
+#include "../orb_slam2-chinese-annotation_amd/csrc/orb_synth.h"
+
+namespace oracle {
+
+typedef orb_keypoint_t KP;
+
+// ---------------------------------------------------------------- A.5 rounding
+static inline int cvRound(float v) { return (int)lrintf(v); }     // round half to even
+static inline int cvRoundD(double v) { return (int)lrint(v); }
+static inline int cvFloor(float v) { return (int)floorf(v); }
+static inline int cvCeil(float v) { return (int)ceilf(v); }
+static inline short sat_short(int v) { return (short)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+struct Img {
+  int w = 0, h = 0;
+  std::vector<uint8_t> px;
+  Img() {}
+  Img(int w_, int h_) : w(w_), h(h_), px((size_t)w_ * h_) {}
+  uint8_t at(int y, int x) const { return px[(size_t)y * w + x]; }
+  uint8_t* row(int y) { return &px[(size_t)y * w]; }
+  const uint8_t* row(int y) const { return &px[(size_t)y * w]; }
+};
+
+// ------------------------------------------------------------ a1: ctor tables
+// src/ORBextractor.cc:428-489 (note `double scaleFactor`, include/ORBextractor.h:98)
+struct Params {
+  int nfeatures, nlevels, iniTh, minTh;
+  double scaleFactor;
+  std::vector<float> scale, invScale, sigma2, invSigma2;
+  std::vector<int> quota;
+  int umax[16];
+};
+
+static Params make_params(int nfeatures, float scaleFactorF, int nlevels, int iniTh, int minTh) {
+  Params p;
+  p.nfeatures = nfeatures;
+  p.nlevels = nlevels;
+  p.iniTh = iniTh;
+  p.minTh = minTh;
+  p.scaleFactor = (double)scaleFactorF;
+  p.scale.assign(nlevels, 0.f);
+  p.sigma2.assign(nlevels, 0.f);
+  p.scale[0] = 1.0f;
+  p.sigma2[0] = 1.0f;
+  for (int i = 1; i < nlevels; ++i) {
+    p.scale[i] = (float)((double)p.scale[i - 1] * p.scaleFactor);  // :439
+    p.sigma2[i] = p.scale[i] * p.scale[i];                          // :440
+  }
+  p.invScale.resize(nlevels);
+  p.invSigma2.resize(nlevels);
+  for (int i = 0; i < nlevels; ++i) {
+    p.invScale[i] = 1.0f / p.scale[i];
+    p.invSigma2[i] = 1.0f / p.sigma2[i];
+  }
+  // :453-464 geometric per-level quotas
+  p.quota.assign(nlevels, 0);
+  const float factor = (float)(1.0f / p.scaleFactor);
+  float nDesired = (float)nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)nlevels));
+  int sum = 0;
+  for (int l = 0; l < nlevels - 1; ++l) {
+    p.quota[l] = cvRound(nDesired);
+    sum += p.quota[l];
+    nDesired *= factor;
+  }
+  p.quota[nlevels - 1] = std::max(nfeatures - sum, 0);
+  // :473-488 umax for the radius-15 circular patch
+  const int HP = 15;
+  int vmax = cvFloor(HP * sqrtf(2.f) / 2 + 1);
+  int vmin = cvCeil(HP * sqrtf(2.f) / 2);
+  const double hp2 = HP * HP;
+  for (int v = 0; v <= vmax; ++v) p.umax[v] = cvRoundD(sqrt(hp2 - v * v));
+  for (int v = HP, v0 = 0; v >= vmin; --v) {
+    while (p.umax[v0] == p.umax[v0 + 1]) ++v0;
+    p.umax[v] = v0;
+    ++v0;
+  }
+  return p;
+}
+
+// ------------------------------------------------- a3: A.2 INTER_LINEAR resize
+static Img resize_linear(const Img& src, int dw, int dh) {
+  Img dst(dw, dh);
+  const double scale_x = 1. / ((double)dw / src.w);
+  const double scale_y = 1. / ((double)dh / src.h);
+  std::vector<int> xofs(dw), yofs(dh);
+  std::vector<short> ialpha(2 * dw), ibeta(2 * dh);
+  int xmax = dw;
+  for (int dx = 0; dx < dw; ++dx) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cvFloor(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= src.w) {
+      xmax = std::min(xmax, dx);
+      if (sx >= src.w - 1) { fx = 0; sx = src.w - 1; }
+    }
+    xofs[dx] = sx;
+    ialpha[2 * dx] = sat_short(cvRound((1.f - fx) * 2048));
+    ialpha[2 * dx + 1] = sat_short(cvRound(fx * 2048));
+  }
+  for (int dy = 0; dy < dh; ++dy) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cvFloor(fy);
+    fy -= sy;
+    yofs[dy] = sy;
+    ibeta[2 * dy] = sat_short(cvRound((1.f - fy) * 2048));
+    ibeta[2 * dy + 1] = sat_short(cvRound(fy * 2048));
+  }
+  std::vector<int> h0(dw), h1(dw);
+  auto hpass = [&](int sy, std::vector<int>& D) {
+    const uint8_t* S = src.row(sy);
+    for (int dx = 0; dx < dw; ++dx) {
+      const int sx = xofs[dx];
+      D[dx] = dx < xmax ? S[sx] * ialpha[2 * dx] + S[sx + 1] * ialpha[2 * dx + 1] : S[sx] * 2048;
+    }
+  };
+  for (int dy = 0; dy < dh; ++dy) {
+    int s0 = yofs[dy], s1 = yofs[dy] + 1;
+    s0 = s0 < 0 ? 0 : (s0 >= src.h ? src.h - 1 : s0);
+    s1 = s1 < 0 ? 0 : (s1 >= src.h ? src.h - 1 : s1);
+    hpass(s0, h0);
+    hpass(s1, h1);
+    const int b0 = ibeta[2 * dy], b1 = ibeta[2 * dy + 1];
+    uint8_t* D = dst.row(dy);
+    for (int dx = 0; dx < dw; ++dx) D[dx] = sat_u8((h0[dx] * b0 + h1[dx] * b1 + (1 << 21)) >> 22);
+  }
+  return dst;
+}
+
+// src/ORBextractor.cc:1172-1207 (the padding is never read by any consumer)
+static std::vector<Img> compute_pyramid(const Params& p, const Img& image) {
+  std::vector<Img> pyr(p.nlevels);
+  pyr[0] = image;
+  for (int l = 1; l < p.nlevels; ++l) {
+    const float s = p.invScale[l];
+    const int w = cvRound((float)image.w * s), h = cvRound((float)image.h * s);
+    pyr[l] = resize_linear(pyr[l - 1], w, h);
+  }
+  return pyr;
+}
+
+// ----------------------------------------------------------- A.1 FAST-9/16
+static const int kCircle[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1},
+                                   {2, -2}, {1, -3},  {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
+                                   {-3, 0}, {-3, 1},  {-2, 2},  {-1, 3}};
+
+// OpenCV cornerScore<16>: max(t, best dark arc, best bright arc) - 1
+static int corner_score(const int d[25], int threshold) {
+  int a0 = threshold;
+  for (int k = 0; k < 16; k += 2) {
+    int a = std::min(d[k + 1], d[k + 2]);
+    a = std::min(a, d[k + 3]);
+    if (a <= a0) continue;
+    for (int m = 4; m <= 8; ++m) a = std::min(a, d[k + m]);
+    a0 = std::max(a0, std::min(a, d[k]));
+    a0 = std::max(a0, std::min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+  for (int k = 0; k < 16; k += 2) {
+    int b = std::max(d[k + 1], d[k + 2]);
+    for (int m = 3; m <= 5; ++m) b = std::max(b, d[k + m]);
+    if (b >= b0) continue;
+    for (int m = 6; m <= 8; ++m) b = std::max(b, d[k + m]);
+    b0 = std::min(b0, std::max(b, d[k]));
+    b0 = std::min(b0, std::max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// cv::FAST(roi, kps, threshold, nonmaxSuppression=true) on the ROI
+// rows [y0,y1) x cols [x0,x1) of `img`; keypoints relative to the ROI.
+static void fast_roi(const Img& img, int y0, int y1, int x0, int x1, int threshold,
+                     std::vector<KP>& kps) {
+  kps.clear();
+  const int rows = y1 - y0, cols = x1 - x0;
+  if (rows < 7 || cols < 7) return;
+  threshold = std::min(std::max(threshold, 0), 255);
+  std::vector<uint8_t> score((size_t)rows * cols, 0);
+  std::vector<std::vector<int>> corners(rows);
+  for (int i = 3; i < rows - 3; ++i) {
+    for (int j = 3; j < cols - 3; ++j) {
+      const int v = img.at(y0 + i, x0 + j);
+      int ring[25];
+      for (int k = 0; k < 16; ++k)
+        ring[k] = img.at(y0 + i + kCircle[k][1], x0 + j + kCircle[k][0]);
+      for (int k = 16; k < 25; ++k) ring[k] = ring[k - 16];
+      // OpenCV FAST_t pre-tests on opposite circle pixels (necessary conditions
+      // for a 9-arc; they only skip work, never change the result)
+      auto cls = [&](int x) { return x < v - threshold ? 1 : (x > v + threshold ? 2 : 0); };
+      int dm = cls(ring[0]) | cls(ring[8]);
+      if (dm == 0) continue;
+      dm &= cls(ring[2]) | cls(ring[10]);
+      dm &= cls(ring[4]) | cls(ring[12]);
+      dm &= cls(ring[6]) | cls(ring[14]);
+      if (dm == 0) continue;
+      dm &= cls(ring[1]) | cls(ring[9]);
+      dm &= cls(ring[3]) | cls(ring[11]);
+      dm &= cls(ring[5]) | cls(ring[13]);
+      dm &= cls(ring[7]) | cls(ring[15]);
+      if (dm == 0) continue;
+      int d[25];
+      for (int k = 0; k < 25; ++k) d[k] = v - ring[k];
+      bool corner = false;
+      int count = 0;
+      for (int k = 0; k < 25 && !corner; ++k) {  // dark arc: x < v - t
+        if (ring[k] < v - threshold) { if (++count > 8) corner = true; }
+        else count = 0;
+      }
+      count = 0;
+      for (int k = 0; k < 25 && !corner; ++k) {  // bright arc: x > v + t
+        if (ring[k] > v + threshold) { if (++count > 8) corner = true; }
+        else count = 0;
+      }
+      if (corner) {
+        corners[i].push_back(j);
+        score[(size_t)i * cols + j] = (uint8_t)corner_score(d, threshold);
+      }
+    }
+  }
+  for (int i = 3; i < rows - 3; ++i) {
+    for (int j : corners[i]) {
+      const int s = score[(size_t)i * cols + j];
+      bool keep = true;
+      for (int dy = -1; dy <= 1 && keep; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (!dy && !dx) continue;
+          if (!(s > score[(size_t)(i + dy) * cols + j + dx])) { keep = false; break; }
+        }
+      if (keep) {
+        KP k;
+        k.x = (float)j;
+        k.y = (float)i;
+        k.size = 7.f;
+        k.angle = -1.f;
+        k.response = (float)s;
+        k.octave = 0;
+        k.class_id = -1;
+        kps.push_back(k);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------ a5: DistributeOctTree
+// src/ORBextractor.cc:500-556 (DivideNode), :558-782 (DistributeOctTree)
+struct Node {
+  std::vector<KP> keys;
+  int ulx, uly, urx, ury, blx, bly, brx, bry;
+  std::list<Node>::iterator lit;
+  bool noMore = false;
+  long seq = 0;  // creation order: stands in for the node's heap address (H2)
+};
+
+static void divide_node(const Node& p, Node& n1, Node& n2, Node& n3, Node& n4) {
+  const int halfX = (int)ceilf((float)(p.urx - p.ulx) / 2);
+  const int halfY = (int)ceilf((float)(p.bry - p.uly) / 2);
+  n1.ulx = p.ulx; n1.uly = p.uly;
+  n1.urx = p.ulx + halfX; n1.ury = p.uly;
+  n1.blx = p.ulx; n1.bly = p.uly + halfY;
+  n1.brx = p.ulx + halfX; n1.bry = p.uly + halfY;
+  n2.ulx = n1.urx; n2.uly = n1.ury;
+  n2.urx = p.urx; n2.ury = p.ury;
+  n2.blx = n1.brx; n2.bly = n1.bry;
+  n2.brx = p.urx; n2.bry = p.uly + halfY;
+  n3.ulx = n1.blx; n3.uly = n1.bly;
+  n3.urx = n1.brx; n3.ury = n1.bry;
+  n3.blx = p.blx; n3.bly = p.bly;
+  n3.brx = n1.brx; n3.bry = p.bly;
+  n4.ulx = n3.urx; n4.uly = n3.ury;
+  n4.urx = n2.brx; n4.ury = n2.bry;
+  n4.blx = n3.brx; n4.bly = n3.bry;
+  n4.brx = p.brx; n4.bry = p.bry;
+  for (const KP& k : p.keys) {
+    if (k.x < n1.urx) {
+      if (k.y < n1.bry) n1.keys.push_back(k);
+      else n3.keys.push_back(k);
+    } else if (k.y < n1.bry) {
+      n2.keys.push_back(k);
+    } else {
+      n4.keys.push_back(k);
+    }
+  }
+  if (n1.keys.size() == 1) n1.noMore = true;
+  if (n2.keys.size() == 1) n2.noMore = true;
+  if (n3.keys.size() == 1) n3.noMore = true;
+  if (n4.keys.size() == 1) n4.noMore = true;
+}
+
+static std::vector<KP> distribute_oct_tree(const std::vector<KP>& toDistribute, int minX, int maxX,
+                                           int minY, int maxY, int N) {
+  const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
+  const float hX = (float)(maxX - minX) / nIni;
+  std::list<Node> nodes;
+  long seq = 0;
+  std::vector<Node*> ini(nIni);
+  for (int i = 0; i < nIni; ++i) {
+    Node n;
+    n.ulx = (int)(hX * (float)i); n.uly = 0;
+    n.urx = (int)(hX * (float)(i + 1)); n.ury = 0;
+    n.blx = n.ulx; n.bly = maxY - minY;
+    n.brx = n.urx; n.bry = maxY - minY;
+    n.seq = seq++;
+    nodes.push_back(n);
+    ini[i] = &nodes.back();
+  }
+  for (const KP& k : toDistribute) ini[(size_t)(k.x / hX)]->keys.push_back(k);
+  for (auto it = nodes.begin(); it != nodes.end();) {
+    if (it->keys.size() == 1) { it->noMore = true; ++it; }
+    else if (it->keys.empty()) it = nodes.erase(it);
+    else ++it;
+  }
+
+  typedef std::pair<int, Node*> SP;
+  auto sp_less = [](const SP& a, const SP& b) {
+    if (a.first != b.first) return a.first < b.first;
+    return a.second->seq < b.second->seq;  // pinned pointer order (H2)
+  };
+  std::vector<SP> sizeAndNode;
+  bool finish = false;
+  auto add_child = [&](Node& c, bool countExpand, int& nToExpand) {
+    if (c.keys.empty()) return;
+    c.seq = seq++;
+    nodes.push_front(c);
+    if (c.keys.size() > 1) {
+      if (countExpand) ++nToExpand;
+      sizeAndNode.push_back(SP((int)c.keys.size(), &nodes.front()));
+      nodes.front().lit = nodes.begin();
+    }
+  };
+  while (!finish) {
+    const int prevSize = (int)nodes.size();
+    int nToExpand = 0;
+    sizeAndNode.clear();
+    for (auto it = nodes.begin(); it != nodes.end();) {
+      if (it->noMore) { ++it; continue; }
+      Node n1, n2, n3, n4;
+      divide_node(*it, n1, n2, n3, n4);
+      add_child(n1, true, nToExpand);
+      add_child(n2, true, nToExpand);
+      add_child(n3, true, nToExpand);
+      add_child(n4, true, nToExpand);
+      it = nodes.erase(it);
+    }
+    if ((int)nodes.size() >= N || (int)nodes.size() == prevSize) {
+      finish = true;
+    } else if ((int)nodes.size() + nToExpand * 3 > N) {
+      while (!finish) {
+        const int prev = (int)nodes.size();
+        std::vector<SP> prevSizeAndNode = sizeAndNode;
+        sizeAndNode.clear();
+        std::sort(prevSizeAndNode.begin(), prevSizeAndNode.end(), sp_less);
+        int dummy = 0;
+        for (int j = (int)prevSizeAndNode.size() - 1; j >= 0; --j) {
+          Node n1, n2, n3, n4;
+          Node* parent = prevSizeAndNode[j].second;
+          divide_node(*parent, n1, n2, n3, n4);
+          add_child(n1, false, dummy);
+          add_child(n2, false, dummy);
+          add_child(n3, false, dummy);
+          add_child(n4, false, dummy);
+          nodes.erase(parent->lit);
+          if ((int)nodes.size() >= N) break;
+        }
+        if ((int)nodes.size() >= N || (int)nodes.size() == prev) finish = true;
+      }
+    }
+  }
+  std::vector<KP> result;
+  result.reserve(nodes.size());
+  for (const Node& n : nodes) {  // :763-779 first max response in node order
+    const KP* best = &n.keys[0];
+    float maxResp = best->response;
+    for (size_t k = 1; k < n.keys.size(); ++k)
+      if (n.keys[k].response > maxResp) { best = &n.keys[k]; maxResp = n.keys[k].response; }
+    result.push_back(*best);
+  }
+  return result;
+}
+
+// --------------------------------------------------------- a4: cells + octree
+// src/ORBextractor.cc:785-892
+struct LevelCandidates {
+  std::vector<KP> keys;  // vToDistributeKeys (relative to the border origin)
+};
+
+static void level_candidates(const Params& p, const Img& lvl, std::vector<KP>& toDistribute) {
+  const float W = 30;
+  const int minBorderX = 19 - 3, minBorderY = minBorderX;
+  const int maxBorderX = lvl.w - 19 + 3, maxBorderY = lvl.h - 19 + 3;
+  toDistribute.clear();
+  const float width = (float)(maxBorderX - minBorderX);
+  const float height = (float)(maxBorderY - minBorderY);
+  const int nCols = (int)(width / W), nRows = (int)(height / W);
+  const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+  std::vector<KP> cell;
+  for (int i = 0; i < nRows; ++i) {
+    const float iniY = (float)(minBorderY + i * hCell);
+    float maxY = iniY + hCell + 6;
+    if (iniY >= maxBorderY - 3) continue;
+    if (maxY > maxBorderY) maxY = (float)maxBorderY;
+    for (int j = 0; j < nCols; ++j) {
+      const float iniX = (float)(minBorderX + j * wCell);
+      float maxX = iniX + wCell + 6;
+      if (iniX >= maxBorderX - 6) continue;
+      if (maxX > maxBorderX) maxX = (float)maxBorderX;
+      fast_roi(lvl, (int)iniY, (int)maxY, (int)iniX, (int)maxX, p.iniTh, cell);
+      if (cell.empty()) fast_roi(lvl, (int)iniY, (int)maxY, (int)iniX, (int)maxX, p.minTh, cell);
+      for (KP k : cell) {
+        k.x += j * wCell;
+        k.y += i * hCell;
+        toDistribute.push_back(k);
+      }
+    }
+  }
+}
+
+// a6: IC_Angle + A.4 fastAtan2, src/ORBextractor.cc:77-113
+static float fast_atan2(float y, float x) {
+  const float r2d = (float)(180 / M_PI);
+  const float p1 = 0.9997878412794807f * r2d, p3 = -0.3258083974640975f * r2d;
+  const float p5 = 0.1555786518463281f * r2d, p7 = -0.04432655554792128f * r2d;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+static float ic_angle(const Img& img, float px, float py, const int* umax) {
+  int m01 = 0, m10 = 0;
+  const int cy = cvRound(py), cx = cvRound(px);
+  for (int u = -15; u <= 15; ++u) m10 += u * img.at(cy, cx + u);
+  for (int v = 1; v <= 15; ++v) {
+    int vsum = 0;
+    const int d = umax[v];
+    for (int u = -d; u <= d; ++u) {
+      const int plus = img.at(cy + v, cx + u), minus = img.at(cy - v, cx + u);
+      vsum += plus - minus;
+      m10 += u * (plus + minus);
+    }
+    m01 += v * vsum;
+  }
+  return fast_atan2((float)m01, (float)m10);
+}
+
+// a7: A.3 GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, src/ORBextractor.cc:1143-1145
+static inline int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+  }
+  return i;
+}
+
+static Img gaussian_blur7(const Img& src) {
+  static const int k[7] = {18, 34, 49, 55, 49, 34, 18};
+  Img dst(src.w, src.h);
+  std::vector<int> rowsum((size_t)src.w * src.h);
+  for (int y = 0; y < src.h; ++y)
+    for (int x = 0; x < src.w; ++x) {
+      int s = 0;
+      for (int i = 0; i < 7; ++i) s += k[i] * src.at(y, reflect101(x + i - 3, src.w));
+      rowsum[(size_t)y * src.w + x] = s;
+    }
+  for (int y = 0; y < src.h; ++y)
+    for (int x = 0; x < src.w; ++x) {
+      int s = 0;
+      for (int j = 0; j < 7; ++j) s += k[j] * rowsum[(size_t)reflect101(y + j - 3, src.h) * src.w + x];
+      dst.row(y)[x] = sat_u8((s + (1 << 15)) >> 16);
+    }
+  return dst;
+}
+
+// A.6 pinned sin/cos: fdlibm-style reduction and kernels in double, rounded to float.
+static void pinned_sincos(float angle, float* s_out, float* c_out) {
+  const double x = (double)angle;
+  const double invpio2 = 6.36619772367581382433e-01;
+  const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
+  const double k = nearbyint(x * invpio2);
+  const double r = (x - k * pio2_1) - k * pio2_1t;
+  const double z = r * r;
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double ps = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  const double sn = r + (z * r) * (S1 + z * ps);
+  const double pc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cs = w + (((1.0 - w) - hz) + z * pc);
+  const int q = ((int)k) & 3;
+  double s, c;
+  switch (q) {
+    case 0: s = sn; c = cs; break;
+    case 1: s = cs; c = -sn; break;
+    case 2: s = -sn; c = -cs; break;
+    default: s = -cs; c = sn; break;
+  }
+  *s_out = (float)s;
+  *c_out = (float)c;
+}
+
+// a8: computeOrbDescriptor, src/ORBextractor.cc:119-164
+static void orb_descriptor(const KP& kpt, const Img& blurred, uint8_t* desc) {
+  const float factorPI = (float)(M_PI / 180.f);
+  const float angle = kpt.angle * factorPI;
+  float a, b;
+  {
+    float s, c;
+    pinned_sincos(angle, &s, &c);
+    a = c;
+    b = s;
+  }
+  const int cy = cvRound(kpt.y), cx = cvRound(kpt.x);
+  auto value = [&](int idx) -> int {
+    const float px = (float)kOrbPatternXY[2 * idx], py = (float)kOrbPatternXY[2 * idx + 1];
+    const int dy = cvRound(px * b + py * a);
+    const int dx = cvRound(px * a - py * b);
+    return blurred.at(cy + dy, cx + dx);
+  };
+  for (int i = 0; i < 32; ++i) {
+    int val = 0;
+    for (int bit = 0; bit < 8; ++bit) {
+      const int t0 = value(16 * i + 2 * bit), t1 = value(16 * i + 2 * bit + 1);
+      val |= (t0 < t1) << bit;
+    }
+    desc[i] = (uint8_t)val;
+  }
+}
+
+// a2: operator(), src/ORBextractor.cc:1091-1169
+struct ExtractResult {
+  std::vector<KP> keys;
+  std::vector<uint8_t> desc;
+  std::vector<Img> pyramid;
+  std::vector<std::vector<KP>> candidates;  // per level, vToDistributeKeys
+  std::vector<int> perLevel;
+};
+
+static void extract(const Params& p, const Img& image, ExtractResult& out) {
+  out.pyramid = compute_pyramid(p, image);
+  std::vector<std::vector<KP>> all(p.nlevels);
+  out.candidates.assign(p.nlevels, {});
+  for (int l = 0; l < p.nlevels; ++l) {
+    const Img& lvl = out.pyramid[l];
+    std::vector<KP>& cand = out.candidates[l];
+    level_candidates(p, lvl, cand);
+    const int minBorderX = 16, minBorderY = 16;
+    const int maxBorderX = lvl.w - 16, maxBorderY = lvl.h - 16;
+    all[l] = distribute_oct_tree(cand, minBorderX, maxBorderX, minBorderY, maxBorderY, p.quota[l]);
+    const int scaledPatchSize = (int)(31 * p.scale[l]);
+    for (KP& k : all[l]) {
+      k.x += minBorderX;
+      k.y += minBorderY;
+      k.octave = l;
+      k.size = (float)scaledPatchSize;
+    }
+  }
+  for (int l = 0; l < p.nlevels; ++l)
+    for (KP& k : all[l]) k.angle = ic_angle(out.pyramid[l], k.x, k.y, p.umax);
+  int total = 0;
+  out.perLevel.assign(p.nlevels, 0);
+  for (int l = 0; l < p.nlevels; ++l) total += out.perLevel[l] = (int)all[l].size();
+  out.keys.clear();
+  out.keys.reserve(total);
+  out.desc.assign((size_t)total * 32, 0);
+  int offset = 0;
+  for (int l = 0; l < p.nlevels; ++l) {
+    if (all[l].empty()) continue;
+    const Img blurred = gaussian_blur7(out.pyramid[l]);
+    for (size_t i = 0; i < all[l].size(); ++i)
+      orb_descriptor(all[l][i], blurred, &out.desc[(size_t)(offset + i) * 32]);
+    offset += (int)all[l].size();
+    if (l != 0) {
+      const float scale = p.scale[l];
+      for (KP& k : all[l]) { k.x *= scale; k.y *= scale; }
+    }
+    out.keys.insert(out.keys.end(), all[l].begin(), all[l].end());
+  }
+}
+
+// ----------------------------------------------------------------- matcher
+// a10: DescriptorDistance, src/ORBmatcher.cc:1814-1830
+static int descriptor_distance(const uint8_t* a, const uint8_t* b) {
+  int dist = 0;
+  for (int i = 0; i < 8; ++i) {
+    uint32_t pa, pb;
+    memcpy(&pa, a + 4 * i, 4);
+    memcpy(&pb, b + 4 * i, 4);
+    uint32_t v = pa ^ pb;
+    v = v - ((v >> 1) & 0x55555555);
+    v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+    dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+  }
+  return dist;
+}
+
+// a12 + a13: Frame grid, src/Frame.cc:261-276, 368-436
+struct Grid {
+  float minX, maxX, minY, maxY, invW, invH;
+  std::vector<size_t> cell[ORB_GRID_COLS][ORB_GRID_ROWS];
+};
+
+static void assign_grid(Grid& g, const KP* keys, int n, float minX, float maxX, float minY,
+                        float maxY) {
+  g.minX = minX; g.maxX = maxX; g.minY = minY; g.maxY = maxY;
+  g.invW = (float)ORB_GRID_COLS / (maxX - minX);
+  g.invH = (float)ORB_GRID_ROWS / (maxY - minY);
+  for (int i = 0; i < ORB_GRID_COLS; ++i)
+    for (int j = 0; j < ORB_GRID_ROWS; ++j) g.cell[i][j].clear();
+  for (int i = 0; i < n; ++i) {
+    const int px = (int)roundf((keys[i].x - minX) * g.invW);
+    const int py = (int)roundf((keys[i].y - minY) * g.invH);
+    if (px < 0 || px >= ORB_GRID_COLS || py < 0 || py >= ORB_GRID_ROWS) continue;
+    g.cell[px][py].push_back((size_t)i);
+  }
+}
+
+static void features_in_area(const Grid& g, const KP* keys, float x, float y, float r,
+                             int minLevel, int maxLevel, std::vector<size_t>& out) {
+  out.clear();
+  const int nMinCellX = std::max(0, (int)floorf((x - g.minX - r) * g.invW));
+  if (nMinCellX >= ORB_GRID_COLS) return;
+  const int nMaxCellX = std::min(ORB_GRID_COLS - 1, (int)ceilf((x - g.minX + r) * g.invW));
+  if (nMaxCellX < 0) return;
+  const int nMinCellY = std::max(0, (int)floorf((y - g.minY - r) * g.invH));
+  if (nMinCellY >= ORB_GRID_ROWS) return;
+  const int nMaxCellY = std::min(ORB_GRID_ROWS - 1, (int)ceilf((y - g.minY + r) * g.invH));
+  if (nMaxCellY < 0) return;
+  const bool checkLevels = (minLevel > 0) || (maxLevel >= 0);
+  for (int ix = nMinCellX; ix <= nMaxCellX; ++ix)
+    for (int iy = nMinCellY; iy <= nMaxCellY; ++iy)
+      for (size_t idx : g.cell[ix][iy]) {
+        const KP& k = keys[idx];
+        if (checkLevels) {
+          if (k.octave < minLevel) continue;
+          if (maxLevel >= 0 && k.octave > maxLevel) continue;
+        }
+        const float dx = k.x - x, dy = k.y - y;
+        if (fabsf(dx) < r && fabsf(dy) < r) out.push_back(idx);
+      }
+}
+
+// a15: SearchByProjection(Frame&, const vector<MapPoint*>&, float th), src/ORBmatcher.cc:47-141
+static int search_by_projection_local(const orb_frame_t* F, const uint8_t* kp_locked, int nmp,
+                                      const orb_mp_track_t* mps, const uint8_t* mp_desc,
+                                      float th, float nnratio, int32_t* kp_match) {
+  static Grid g;
+  assign_grid(g, F->keys, F->n, F->min_x, F->max_x, F->min_y, F->max_y);
+  // lock[i]: F.mvpMapPoints[i] && ->Observations() > 0 ; updated by claims of has_obs points
+  std::vector<uint8_t> lock(F->n);
+  for (int i = 0; i < F->n; ++i) {
+    lock[i] = kp_locked ? kp_locked[i] : 0;
+    kp_match[i] = -1;
+  }
+  const bool bFactor = th != 1.0f;
+  int nmatches = 0;
+  std::vector<size_t> idxs;
+  for (int m = 0; m < nmp; ++m) {
+    const orb_mp_track_t& mp = mps[m];
+    if (!mp.in_view || mp.bad) continue;
+    const int lvl = mp.level;
+    float r = mp.view_cos > 0.998f ? 2.5f : 4.0f;
+    if (bFactor) r *= th;
+    const float rs = r * F->scale_factors[lvl];
+    features_in_area(g, F->keys, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl, idxs);
+    if (idxs.empty()) continue;
+    const uint8_t* d = mp_desc + (size_t)m * 32;
+    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+    for (size_t idx : idxs) {
+      if (lock[idx]) continue;
+      if (F->u_right && F->u_right[idx] > 0) {
+        const float er = fabsf(mp.proj_xr - F->u_right[idx]);
+        if (er > r * F->scale_factors[lvl]) continue;
+      }
+      const int dist = descriptor_distance(d, F->descriptors + idx * 32);
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestLevel2 = bestLevel;
+        bestLevel = F->keys[idx].octave;
+        bestIdx = (int)idx;
+      } else if (dist < bestDist2) {
+        bestLevel2 = F->keys[idx].octave;
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= 100) {
+      if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+      kp_match[bestIdx] = m;
+      if (mp.has_obs) lock[bestIdx] = 1;
+      ++nmatches;
+    }
+  }
+  return nmatches;
+}
+
+// a18: ComputeThreeMaxima, src/ORBmatcher.cc:1765-1809
+static void three_maxima(const std::vector<int>* histo, int L, int& ind1, int& ind2, int& ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  for (int i = 0; i < L; ++i) {
+    const int s = (int)histo[i].size();
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s; ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+  else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+static inline int rot_bin(float rot) {  // src/ORBmatcher.cc:1582-1588 (factor bug kept)
+  const float factor = 1.0f / 30;
+  if (rot < 0.0) rot += 360.0f;
+  int bin = (int)roundf(rot * factor);
+  if (bin == 30) bin = 0;
+  return bin;
+}
+
+// a16: SearchByProjection(Frame&, const Frame&, float, bool), src/ORBmatcher.cc:1460-1619
+static int search_by_projection_frame(const orb_frame_t* C, const uint8_t* kp_locked, int nlast,
+                                      const orb_last_mp_t* last, const uint8_t* last_desc,
+                                      const orb_camera_t* cam, float tlc_z, float th, int mono,
+                                      int checkOri, int32_t* kp_match) {
+  static Grid g;
+  assign_grid(g, C->keys, C->n, C->min_x, C->max_x, C->min_y, C->max_y);
+  // state[i]: 0 untouched, 1 assigned this call (holder slot[i]), 2 cleared this call
+  std::vector<int> slot(C->n, -1), state(C->n, 0);
+  std::vector<uint8_t> locked(C->n, 0);  // mvpMapPoints[i] && Observations() > 0
+  for (int i = 0; i < C->n; ++i) locked[i] = kp_locked ? kp_locked[i] : 0;
+  std::vector<int> rotHist[30];
+  const bool bForward = tlc_z > cam->mb && !mono;
+  const bool bBackward = -tlc_z > cam->mb && !mono;
+  int nmatches = 0;
+  std::vector<size_t> idxs;
+  for (int i = 0; i < nlast; ++i) {
+    const orb_last_mp_t& L = last[i];
+    if (!L.valid) continue;
+    const float invzc = L.invzc;
+    if (invzc < 0) continue;
+    const float u = cam->fx * L.xc * invzc + cam->cx;
+    const float v = cam->fy * L.yc * invzc + cam->cy;
+    if (u < C->min_x || u > C->max_x) continue;
+    if (v < C->min_y || v > C->max_y) continue;
+    const int nLastOctave = L.last_octave;
+    const float radius = th * C->scale_factors[nLastOctave];
+    if (bForward) features_in_area(g, C->keys, u, v, radius, nLastOctave, -1, idxs);
+    else if (bBackward) features_in_area(g, C->keys, u, v, radius, 0, nLastOctave, idxs);
+    else features_in_area(g, C->keys, u, v, radius, nLastOctave - 1, nLastOctave + 1, idxs);
+    if (idxs.empty()) continue;
+    const uint8_t* d = last_desc + (size_t)i * 32;
+    int bestDist = 256, bestIdx2 = -1;
+    for (size_t i2 : idxs) {
+      if (locked[i2]) continue;
+      if (C->u_right && C->u_right[i2] > 0) {
+        const float ur = u - cam->bf * invzc;
+        const float er = fabsf(ur - C->u_right[i2]);
+        if (er > radius) continue;
+      }
+      const int dist = descriptor_distance(d, C->descriptors + i2 * 32);
+      if (dist < bestDist) { bestDist = dist; bestIdx2 = (int)i2; }
+    }
+    if (bestDist <= 100) {
+      slot[bestIdx2] = L.mp_id;
+      state[bestIdx2] = 1;
+      locked[bestIdx2] = L.has_obs;
+      ++nmatches;
+      if (checkOri) rotHist[rot_bin(L.last_angle - C->keys[bestIdx2].angle)].push_back(bestIdx2);
+    }
+  }
+  if (checkOri) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, 30, ind1, ind2, ind3);
+    for (int b = 0; b < 30; ++b) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (int idx : rotHist[b]) { slot[idx] = -1; state[idx] = 2; locked[idx] = 0; --nmatches; }
+    }
+  }
+  // kp_match: MapPoint id assigned by this call, -1 untouched, -2 set to NULL by this call
+  for (int i = 0; i < C->n; ++i) kp_match[i] = state[i] == 1 ? slot[i] : (state[i] == 2 ? -2 : -1);
+  return nmatches;
+}
+
+// a17: SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&), src/ORBmatcher.cc:164-306
+static int search_by_bow(int n_kf, const uint8_t* kf_desc, const float* kf_angle,
+                         const int32_t* kf_mp, const uint8_t* kf_mp_bad, int kf_nodes,
+                         const uint32_t* kf_node_ids, const int32_t* kf_offs,
+                         const uint32_t* kf_feats, int n_f, const uint8_t* f_desc,
+                         const float* f_angle, int f_nodes, const uint32_t* f_node_ids,
+                         const int32_t* f_offs, const uint32_t* f_feats, float nnratio,
+                         int checkOri, int32_t* f_match) {
+  (void)n_kf;
+  for (int j = 0; j < n_f; ++j) f_match[j] = -1;
+  std::vector<int> rotHist[30];
+  int nmatches = 0;
+  int a = 0, b = 0;
+  while (a < kf_nodes && b < f_nodes) {
+    if (kf_node_ids[a] == f_node_ids[b]) {
+      for (int p = kf_offs[a]; p < kf_offs[a + 1]; ++p) {
+        const int realIdxKF = (int)kf_feats[p];
+        const int mp = kf_mp[realIdxKF];
+        if (mp < 0) continue;
+        if (kf_mp_bad && kf_mp_bad[realIdxKF]) continue;
+        const uint8_t* dKF = kf_desc + (size_t)realIdxKF * 32;
+        int best1 = 256, bestIdxF = -1, best2 = 256;
+        for (int q = f_offs[b]; q < f_offs[b + 1]; ++q) {
+          const int realIdxF = (int)f_feats[q];
+          if (f_match[realIdxF] >= 0) continue;
+          const int dist = descriptor_distance(dKF, f_desc + (size_t)realIdxF * 32);
+          if (dist < best1) { best2 = best1; best1 = dist; bestIdxF = realIdxF; }
+          else if (dist < best2) best2 = dist;
+        }
+        if (best1 <= 50 && (float)best1 < nnratio * (float)best2) {
+          f_match[bestIdxF] = mp;
+          if (checkOri) rotHist[rot_bin(kf_angle[realIdxKF] - f_angle[bestIdxF])].push_back(bestIdxF);
+          ++nmatches;
+        }
+      }
+      ++a;
+      ++b;
+    } else if (kf_node_ids[a] < f_node_ids[b]) {
+      a = (int)(std::lower_bound(kf_node_ids + a, kf_node_ids + kf_nodes, f_node_ids[b]) - kf_node_ids);
+    } else {
+      b = (int)(std::lower_bound(f_node_ids + b, f_node_ids + f_nodes, kf_node_ids[a]) - f_node_ids);
+    }
+  }
+  if (checkOri) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, 30, ind1, ind2, ind3);
+    for (int bb = 0; bb < 30; ++bb) {
+      if (bb == ind1 || bb == ind2 || bb == ind3) continue;
+      for (int idx : rotHist[bb]) { f_match[idx] = -1; --nmatches; }
+    }
+  }
+  return nmatches;
+}
+
+// a11: ComputeStereoMatches, src/Frame.cc:516-704 (debug ofstream of :556,652 omitted)
+static void stereo_matches(const orb_stereo_input_t* in, float* uRight, float* depth) {
+  const orb_frame_t* F = in->left;
+  const int N = F->n;
+  for (int i = 0; i < N; ++i) { uRight[i] = -1.0f; depth[i] = -1.0f; }
+  const int thOrbDist = (100 + 50) / 2;
+  const int nRows = in->level_height[0];
+  std::vector<std::vector<size_t>> rowIdx(nRows);
+  for (int iR = 0; iR < in->n_right; ++iR) {
+    const orb_keypoint_t& kp = in->right_keys[iR];
+    const float r = 2.0f * F->scale_factors[kp.octave];
+    const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
+    for (int yi = minr; yi <= maxr; ++yi) rowIdx[yi].push_back((size_t)iR);
+  }
+  const float mb = in->bf / in->fx;
+  const float minZ = mb, minD = 0, maxD = in->bf / minZ;
+  std::vector<std::pair<int, int>> distIdx;
+  for (int iL = 0; iL < N; ++iL) {
+    const orb_keypoint_t& kpL = F->keys[iL];
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    const std::vector<size_t>& cand = rowIdx[(size_t)vL];
+    if (cand.empty()) continue;
+    const float minU = uL - maxD, maxU = uL - minD;
+    if (maxU < 0) continue;
+    int bestDist = 100;
+    size_t bestIdxR = 0;
+    const uint8_t* dL = F->descriptors + (size_t)iL * 32;
+    for (size_t iR : cand) {
+      const orb_keypoint_t& kpR = in->right_keys[iR];
+      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+      const float uR = kpR.x;
+      if (uR >= minU && uR <= maxU) {
+        const int dist = descriptor_distance(dL, in->right_desc + iR * 32);
+        if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
+      }
+    }
+    if (bestDist < thOrbDist) {
+      const float uR0 = in->right_keys[bestIdxR].x;
+      const float scaleFactor = in->inv_scale_factors[kpL.octave];
+      const float scaleduL = roundf(kpL.x * scaleFactor);
+      const float scaledvL = roundf(kpL.y * scaleFactor);
+      const float scaleduR0 = roundf(uR0 * scaleFactor);
+      const int w = 5, L = 5;
+      const int lw = in->level_width[levelL];
+      const int64_t lsL = in->level_stride[levelL];
+      const uint8_t* IL = in->left_levels[levelL];
+      const uint8_t* IR = in->right_levels[levelL];
+      const int ry0 = (int)scaledvL - w, lx0 = (int)scaleduL - w;
+      const float iniu = scaleduR0 + L - w;
+      const float endu = scaleduR0 + L + w + 1;
+      if (iniu < 0 || endu >= lw) continue;
+      const float cL = (float)IL[(int64_t)(ry0 + w) * lsL + lx0 + w];
+      int bestSad = 2147483647;
+      int bestincR = 0;
+      float vDists[11];
+      for (int incR = -L; incR <= L; ++incR) {
+        const int rx0 = (int)scaleduR0 + incR - w;
+        const float cR = (float)IR[(int64_t)(ry0 + w) * lsL + rx0 + w];
+        float dist = 0.f;
+        double acc = 0.0;
+        for (int yy = 0; yy < 2 * w + 1; ++yy)
+          for (int xx = 0; xx < 2 * w + 1; ++xx) {
+            const float a = (float)IL[(int64_t)(ry0 + yy) * lsL + lx0 + xx] - cL;
+            const float b = (float)IR[(int64_t)(ry0 + yy) * lsL + rx0 + xx] - cR;
+            acc += fabs((double)a - (double)b);
+          }
+        dist = (float)acc;
+        if (dist < bestSad) { bestSad = (int)dist; bestincR = incR; }
+        vDists[L + incR] = dist;
+      }
+      if (bestincR == -L || bestincR == L) continue;
+      const float dist1 = vDists[L + bestincR - 1], dist2 = vDists[L + bestincR],
+                  dist3 = vDists[L + bestincR + 1];
+      const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+      if (deltaR < -1 || deltaR > 1) continue;
+      float bestuR = F->scale_factors[kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
+      float disparity = uL - bestuR;
+      if (disparity >= minD && disparity < maxD) {
+        if (disparity <= 0) { disparity = 0.01f; bestuR = (float)((double)uL - 0.01); }
+        depth[iL] = in->bf / disparity;
+        uRight[iL] = bestuR;
+        distIdx.push_back(std::make_pair(bestSad, iL));
+      }
+    }
+  }
+  if (distIdx.empty()) return;  // reference indexes an empty vector here (UB)
+  std::sort(distIdx.begin(), distIdx.end());
+  const float median = (float)distIdx[distIdx.size() / 2].first;
+  const float thDist = 1.5f * 1.4f * median;
+  for (int i = (int)distIdx.size() - 1; i >= 0; --i) {
+    if ((float)distIdx[i].first < thDist) break;
+    uRight[distIdx[i].second] = -1;
+    depth[distIdx[i].second] = -1;
+  }
+}
+
+}  // namespace oracle
+
+// ===================================================================== C API
+using namespace oracle;
+
+extern "C" {
+
+int oracle_params(int nfeatures, float scaleFactor, int nlevels, float* scale, float* inv_scale,
+                  float* sigma2, float* inv_sigma2, int32_t* quota, int32_t* umax16) {
+  const Params p = make_params(nfeatures, scaleFactor, nlevels, 20, 7);
+  for (int l = 0; l < nlevels; ++l) {
+    if (scale) scale[l] = p.scale[l];
+    if (inv_scale) inv_scale[l] = p.invScale[l];
+    if (sigma2) sigma2[l] = p.sigma2[l];
+    if (inv_sigma2) inv_sigma2[l] = p.invSigma2[l];
+    if (quota) quota[l] = p.quota[l];
+  }
+  if (umax16) for (int v = 0; v < 16; ++v) umax16[v] = p.umax[v];
+  return 0;
+}
+
+static Img to_img(const uint8_t* img, int w, int h, size_t stride) {
+  Img im(w, h);
+  for (int y = 0; y < h; ++y) memcpy(im.row(y), img + (size_t)y * stride, (size_t)w);
+  return im;
+}
+
+// Level sizes of the pyramid (2*nlevels ints: w0,h0,w1,h1,...).
+int oracle_level_sizes(int w, int h, float scaleFactor, int nlevels, int32_t* wh) {
+  const Params p = make_params(1000, scaleFactor, nlevels, 20, 7);
+  for (int l = 0; l < nlevels; ++l) {
+    wh[2 * l] = l ? cvRound((float)w * p.invScale[l]) : w;
+    wh[2 * l + 1] = l ? cvRound((float)h * p.invScale[l]) : h;
+  }
+  return 0;
+}
+
+// Pyramid levels packed tightly level after level into `out`.
+int oracle_pyramid(const uint8_t* img, int w, int h, size_t stride, float scaleFactor,
+                   int nlevels, uint8_t* out) {
+  const Params p = make_params(1000, scaleFactor, nlevels, 20, 7);
+  const std::vector<Img> pyr = compute_pyramid(p, to_img(img, w, h, stride));
+  size_t off = 0;
+  for (const Img& l : pyr) {
+    memcpy(out + off, l.px.data(), l.px.size());
+    off += l.px.size();
+  }
+  return (int)off;
+}
+
+int oracle_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh) {
+  const Img d = resize_linear(to_img(src, sw, sh, (size_t)sw), dw, dh);
+  memcpy(dst, d.px.data(), d.px.size());
+  return 0;
+}
+
+int oracle_blur7(const uint8_t* src, int w, int h, uint8_t* dst) {
+  const Img d = gaussian_blur7(to_img(src, w, h, (size_t)w));
+  memcpy(dst, d.px.data(), d.px.size());
+  return 0;
+}
+
+// cv::FAST(img, kps, threshold, true) on a whole (small) image.
+int oracle_fast(const uint8_t* img, int w, int h, int threshold, orb_keypoint_t* out, int cap) {
+  std::vector<KP> kps;
+  fast_roi(to_img(img, w, h, (size_t)w), 0, h, 0, w, threshold, kps);
+  const int n = (int)kps.size();
+  for (int i = 0; i < n && i < cap; ++i) out[i] = kps[i];
+  return n;
+}
+
+float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+
+void oracle_sincos(float angle, float* s, float* c) { pinned_sincos(angle, s, c); }
+
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
+
+// Per-level FAST candidates (vToDistributeKeys) of an image: writes up to cap
+// keys (relative to the border origin, octave = level) and per-level counts.
+int oracle_candidates(const uint8_t* img, int w, int h, size_t stride, int nfeatures,
+                      float scaleFactor, int nlevels, int iniTh, int minTh, orb_keypoint_t* out,
+                      int cap, int32_t* per_level) {
+  const Params p = make_params(nfeatures, scaleFactor, nlevels, iniTh, minTh);
+  const std::vector<Img> pyr = compute_pyramid(p, to_img(img, w, h, stride));
+  int n = 0;
+  std::vector<KP> cand;
+  for (int l = 0; l < nlevels; ++l) {
+    level_candidates(p, pyr[l], cand);
+    per_level[l] = (int)cand.size();
+    for (KP k : cand) {
+      k.octave = l;
+      if (n < cap) out[n] = k;
+      ++n;
+    }
+  }
+  return n;
+}
+
+// DistributeOctTree on an explicit key list (keys relative to the border origin).
+int oracle_distribute(const orb_keypoint_t* keys, int n, int minX, int maxX, int minY, int maxY,
+                      int N, orb_keypoint_t* out, int cap) {
+  std::vector<KP> in(keys, keys + n);
+  std::vector<KP> res = distribute_oct_tree(in, minX, maxX, minY, maxY, N);
+  for (int i = 0; i < (int)res.size() && i < cap; ++i) out[i] = res[i];
+  return (int)res.size();
+}
+
+// Full ORBextractor::operator(): returns N (or -N-1 if cap too small).
+int oracle_extract(const uint8_t* img, int w, int h, size_t stride, int nfeatures,
+                   float scaleFactor, int nlevels, int iniTh, int minTh, orb_keypoint_t* kps,
+                   uint8_t* desc, int cap, int32_t* per_level) {
+  const Params p = make_params(nfeatures, scaleFactor, nlevels, iniTh, minTh);
+  ExtractResult r;
+  extract(p, to_img(img, w, h, stride), r);
+  const int n = (int)r.keys.size();
+  if (per_level) for (int l = 0; l < nlevels; ++l) per_level[l] = r.perLevel[l];
+  if (n > cap) return -n - 1;
+  memcpy(kps, r.keys.data(), (size_t)n * sizeof(KP));
+  memcpy(desc, r.desc.data(), (size_t)n * 32);
+  return n;
+}
+
+int oracle_match_projection_local(const orb_frame_t* F, const uint8_t* kp_locked, int nmp,
+                                  const orb_mp_track_t* mps, const uint8_t* mp_desc, float th,
+                                  float nnratio, int32_t* kp_match) {
+  return search_by_projection_local(F, kp_locked, nmp, mps, mp_desc, th, nnratio, kp_match);
+}
+
+int oracle_match_projection_frame(const orb_frame_t* C, const uint8_t* kp_locked, int nlast,
+                                  const orb_last_mp_t* last, const uint8_t* last_desc,
+                                  const orb_camera_t* cam, float tlc_z, float th, int mono,
+                                  int checkOri, int32_t* kp_match) {
+  return search_by_projection_frame(C, kp_locked, nlast, last, last_desc, cam, tlc_z, th, mono,
+                                    checkOri, kp_match);
+}
+
+int oracle_match_bow(int n_kf, const uint8_t* kf_desc, const float* kf_angle,
+                     const int32_t* kf_mp, const uint8_t* kf_mp_bad, int kf_nodes,
+                     const uint32_t* kf_node_ids, const int32_t* kf_offs,
+                     const uint32_t* kf_feats, int n_f, const uint8_t* f_desc,
+                     const float* f_angle, int f_nodes, const uint32_t* f_node_ids,
+                     const int32_t* f_offs, const uint32_t* f_feats, float nnratio,
+                     int check_orientation, int32_t* f_match) {
+  return search_by_bow(n_kf, kf_desc, kf_angle, kf_mp, kf_mp_bad, kf_nodes, kf_node_ids,
+                       kf_offs, kf_feats, n_f, f_desc, f_angle, f_nodes, f_node_ids, f_offs,
+                       f_feats, nnratio, check_orientation, f_match);
+}
+
+int oracle_stereo_match(const orb_stereo_input_t* in, float* u_right, float* depth) {
+  stereo_matches(in, u_right, depth);
+  return 0;
+}
+
+// Grid CSR of a frame: cell_start[64*48+1] (cell index = ix*48 + iy), idx[].
+int oracle_grid(const orb_keypoint_t* keys, int n, float minX, float maxX, float minY,
+                float maxY, int32_t* cell_start, int32_t* idx) {
+  static Grid g;
+  assign_grid(g, keys, n, minX, maxX, minY, maxY);
+  int off = 0;
+  for (int ix = 0; ix < ORB_GRID_COLS; ++ix)
+    for (int iy = 0; iy < ORB_GRID_ROWS; ++iy) {
+      cell_start[ix * ORB_GRID_ROWS + iy] = off;
+      for (size_t k : g.cell[ix][iy]) idx[off++] = (int32_t)k;
+    }
+  cell_start[ORB_GRID_COLS * ORB_GRID_ROWS] = off;
+  return off;
+}
+
+void oracle_synth_image(uint64_t seed, int frame, int view, int w, int h, uint8_t* out,
+                        size_t stride) {
+  orb_synth::render(seed, frame, view, w, h, out, stride);
+}
+
+void oracle_synth_local_map(uint64_t seed, const orb_keypoint_t* keys, const uint8_t* desc,
+                            int n_kp, int n_mp, int w, int h, orb_mp_track_t* mps,
+                            uint8_t* mp_desc, uint8_t* kp_locked) {
+  orb_synth::local_map(seed, keys, desc, n_kp, n_mp, w, h, mps, mp_desc, kp_locked);
+}
+
+}  // extern "C"

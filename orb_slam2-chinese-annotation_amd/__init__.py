@@ -1,0 +1,351 @@
+"""MI355X-native ORB front-end: Python host mirror of the reference interface.
+
+Mirrors, over the C ABI in ``include/orb_abi.h`` (library ``lib/liborb_amd.so``):
+
+* ``ORBextractor``  -- ORB_SLAM2::ORBextractor (reference include/ORBextractor.h:45-114):
+  same constructor arguments, ``__call__(image, mask)`` = ``operator()``
+  (src/ORBextractor.cc:1091-1169), the ``Get*`` scale accessors and
+  ``mvImagePyramid``.
+* ``ORBmatcher``    -- ORB_SLAM2::ORBmatcher (include/ORBmatcher.h:37-102):
+  ``DescriptorDistance`` and ``SearchByProjection(Frame, local map, th)``
+  (src/ORBmatcher.cc:47-133).
+
+Every result is computed by the gfx950 HIP kernels; there is no CPU path.  If
+the library is missing or no gfx950 device is visible the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "lib" / "liborb_amd.so"
+
+ORB_OK, ORB_EEMPTY, ORB_EINVAL, ORB_ENOMEM, ORB_EDEVICE, ORB_ECAPACITY, ORB_ENODEV = 0, 1, -1, -2, -3, -4, -5
+
+KEYPOINT_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+     ("octave", "<i4"), ("class_id", "<i4")]
+)
+MP_TRACK_DTYPE = np.dtype(
+    [("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+     ("level", "<i4"), ("in_view", "u1"), ("bad", "u1"), ("has_obs", "u1"), ("_pad", "u1")]
+)
+assert KEYPOINT_DTYPE.itemsize == 28 and MP_TRACK_DTYPE.itemsize == 24
+
+
+class OrbError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {_status_str(status)} ({status})")
+
+
+_lib = None
+
+
+def _status_str(s: int) -> str:
+    if _lib is None:
+        return str(s)
+    return _lib.orb_status_string(s).decode()
+
+
+class _Frame(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32), ("keys", ctypes.c_void_p), ("descriptors", ctypes.c_void_p),
+        ("u_right", ctypes.c_void_p), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+        ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("n_levels", ctypes.c_int32),
+        ("scale_factors", ctypes.c_void_p),
+    ]
+
+
+def lib() -> ctypes.CDLL:
+    """Load liborb_amd.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise OrbError(ORB_ENODEV, f"{LIB_PATH} not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(str(LIB_PATH))
+    vp, i32, f32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+    sig = {
+        "orb_abi_version": (i32, []),
+        "orb_status_string": (ctypes.c_char_p, [i32]),
+        "orb_device_count": (i32, [vp]),
+        "orb_extractor_create": (i32, [i32, f32, i32, i32, i32, i32, vp]),
+        "orb_extractor_destroy": (None, [vp]),
+        "orb_extractor_get_levels": (i32, [vp]),
+        "orb_extractor_get_scale_factor": (f32, [vp]),
+        "orb_extractor_get_scale_factors": (None, [vp, vp]),
+        "orb_extractor_get_inverse_scale_factors": (None, [vp, vp]),
+        "orb_extractor_get_scale_sigma_squares": (None, [vp, vp]),
+        "orb_extractor_get_inverse_scale_sigma_squares": (None, [vp, vp]),
+        "orb_extractor_get_features_per_level": (None, [vp, vp]),
+        "orb_extractor_capacity": (i32, [vp, i32, i32]),
+        "orb_extractor_extract": (i32, [vp, vp, i32, i32, sz, vp, vp, i32, vp]),
+        "orb_extractor_pyramid_level": (i32, [vp, i32, vp, sz, vp, vp]),
+        "orb_extractor_extract_batch": (i32, [vp, vp, i32, i32, i32, sz, sz, vp, vp, i32, vp, vp]),
+        "orb_extractor_batch_level": (i32, [vp, i32, i32, vp, vp, vp, vp]),
+        "orb_extractor_stream": (vp, [vp]),
+        "orb_extractor_profile": (i32, [vp, i32]),
+        "orb_extractor_profile_read": (i32, [vp, i32, vp, vp, vp]),
+        "orb_descriptor_distance": (i32, [vp, vp]),
+        "orb_matcher_create": (i32, [i32, vp]),
+        "orb_matcher_destroy": (None, [vp]),
+        "orb_matcher_stream": (vp, [vp]),
+        "orb_hamming_batch": (i32, [vp, vp, vp, i32, vp, vp]),
+        "orb_match_projection_local": (i32, [vp, vp, vp, i32, vp, vp, f32, f32, vp, vp]),
+        "orb_match_projection_local_batch": (
+            i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, f32, f32, f32, f32, i32, vp,
+                  f32, f32, vp, vp, vp]),
+        "orb_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
+        "orb_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(status: int, what: str) -> int:
+    if status not in (ORB_OK,):
+        raise OrbError(status, what)
+    return status
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib().orb_device_count(ctypes.byref(n))
+    return n.value
+
+
+# --------------------------------------------------------------- synthetic input
+def synth_image(seed: int, frame: int, width: int, height: int, view: int = 0) -> np.ndarray:
+    """Deterministic synthetic grayscale frame (orb_synth_image)."""
+    img = np.empty((height, width), np.uint8)
+    lib().orb_synth_image(seed, frame, view, width, height, _ptr(img), width)
+    return img
+
+
+def synth_local_map(seed: int, keys: np.ndarray, desc: np.ndarray, n_mp: int, width: int,
+                    height: int):
+    """SURVEY §8(d) C5 synthetic local map: (mps, mp_desc, kp_locked)."""
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    mps = np.zeros(n_mp, MP_TRACK_DTYPE)
+    mp_desc = np.zeros((n_mp, 32), np.uint8)
+    locked = np.zeros(len(keys), np.uint8)
+    lib().orb_synth_local_map(seed, _ptr(keys), _ptr(desc), len(keys), n_mp, width, height,
+                              _ptr(mps), _ptr(mp_desc), _ptr(locked))
+    return mps, mp_desc, locked
+
+
+# ------------------------------------------------------------------- extractor
+class ORBextractor:
+    """ORB_SLAM2::ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)."""
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int,
+                 minThFAST: int, device: int = 0):
+        L = lib()
+        h = ctypes.c_void_p()
+        _check(L.orb_extractor_create(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                                      device, ctypes.byref(h)), "orb_extractor_create")
+        self._h = h
+        self.nlevels = nlevels
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orb_extractor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _floats(self, fn) -> list:
+        out = np.zeros(self.nlevels, np.float32)
+        fn(self._h, _ptr(out))
+        return out.tolist()
+
+    def GetLevels(self) -> int:
+        return lib().orb_extractor_get_levels(self._h)
+
+    def GetScaleFactor(self) -> float:
+        return lib().orb_extractor_get_scale_factor(self._h)
+
+    def GetScaleFactors(self) -> list:
+        return self._floats(lib().orb_extractor_get_scale_factors)
+
+    def GetInverseScaleFactors(self) -> list:
+        return self._floats(lib().orb_extractor_get_inverse_scale_factors)
+
+    def GetScaleSigmaSquares(self) -> list:
+        return self._floats(lib().orb_extractor_get_scale_sigma_squares)
+
+    def GetInverseScaleSigmaSquares(self) -> list:
+        return self._floats(lib().orb_extractor_get_inverse_scale_sigma_squares)
+
+    def features_per_level(self) -> list:
+        out = np.zeros(self.nlevels, np.int32)
+        lib().orb_extractor_get_features_per_level(self._h, _ptr(out))
+        return out.tolist()
+
+    def capacity(self, width: int, height: int) -> int:
+        return lib().orb_extractor_capacity(self._h, width, height)
+
+    def __call__(self, image: np.ndarray, mask=None):
+        """operator(): returns (keypoints[KEYPOINT_DTYPE], descriptors uint8 N x 32).
+
+        An empty image returns (None, None) -- the reference returns with its
+        outputs untouched (src/ORBextractor.cc:1095-1096).  A non-uint8 or
+        non-2D image is rejected like the reference's assert (:1100)."""
+        if image is None or image.size == 0:
+            return None, None
+        if image.dtype != np.uint8 or image.ndim != 2:
+            raise OrbError(ORB_EINVAL, "image must be 8UC1 (CV_8UC1)")
+        image = np.ascontiguousarray(image)
+        H, W = image.shape
+        cap = self.capacity(W, H)
+        if cap < 0:
+            raise OrbError(ORB_EINVAL, f"unsupported image size {W}x{H}")
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int(0)
+        _check(lib().orb_extractor_extract(self._h, _ptr(image), W, H, image.strides[0], _ptr(kps),
+                                           _ptr(desc), cap, ctypes.byref(n)),
+               "orb_extractor_extract")
+        return kps[: n.value].copy(), desc[: n.value].copy()
+
+    @property
+    def mvImagePyramid(self) -> list:
+        """Host copies of the last image's pyramid levels."""
+        L = lib()
+        out = []
+        for l in range(self.nlevels):
+            w, h = ctypes.c_int(0), ctypes.c_int(0)
+            _check(L.orb_extractor_pyramid_level(self._h, l, None, 0, ctypes.byref(w),
+                                                 ctypes.byref(h)), "pyramid_level")
+            a = np.zeros((h.value, w.value), np.uint8)
+            _check(L.orb_extractor_pyramid_level(self._h, l, _ptr(a), w.value, None, None),
+                   "pyramid_level")
+            out.append(a)
+        return out
+
+    def extract_batch(self, d_images: int, n_images: int, width: int, height: int, stride: int,
+                      image_pitch: int, d_keypoints: int, d_descriptors: int, capacity: int,
+                      d_counts: int, stream: int = 0):
+        """Device-resident batch form (raw device pointers, e.g. torch .data_ptr())."""
+        _check(lib().orb_extractor_extract_batch(self._h, d_images, n_images, width, height,
+                                                 stride, image_pitch, d_keypoints, d_descriptors,
+                                                 capacity, d_counts, stream or None),
+               "orb_extractor_extract_batch")
+
+    def stream(self) -> int:
+        return lib().orb_extractor_stream(self._h) or 0
+
+    def profile(self, enable: bool = True):
+        _check(lib().orb_extractor_profile(self._h, int(enable)), "profile")
+
+    def profile_read(self, stage: int):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int(0)
+        name = ctypes.c_char_p()
+        _check(lib().orb_extractor_profile_read(self._h, stage, ctypes.byref(ms), ctypes.byref(n),
+                                                ctypes.byref(name)), "profile_read")
+        return name.value.decode(), ms.value, n.value
+
+
+# --------------------------------------------------------------------- matcher
+class Frame:
+    """The Frame members ORBmatcher reads (src/Frame.cc, include/Frame.h)."""
+
+    def __init__(self, keys, descriptors, scale_factors, width, height, u_right=None,
+                 min_x=0.0, min_y=0.0):
+        self.mvKeysUn = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+        self.mDescriptors = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
+        self.mvScaleFactors = np.ascontiguousarray(scale_factors, np.float32)
+        self.mvuRight = None if u_right is None else np.ascontiguousarray(u_right, np.float32)
+        self.mnMinX, self.mnMaxX = float(min_x), float(width)
+        self.mnMinY, self.mnMaxY = float(min_y), float(height)
+        self.N = len(self.mvKeysUn)
+
+    def _c(self) -> _Frame:
+        f = _Frame()
+        f.n = self.N
+        f.keys = _ptr(self.mvKeysUn) if self.N else None
+        f.descriptors = _ptr(self.mDescriptors) if self.N else None
+        f.u_right = _ptr(self.mvuRight) if self.mvuRight is not None else None
+        f.min_x, f.max_x, f.min_y, f.max_y = self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY
+        f.n_levels = len(self.mvScaleFactors)
+        f.scale_factors = _ptr(self.mvScaleFactors)
+        return f
+
+
+class ORBmatcher:
+    """ORB_SLAM2::ORBmatcher(nnratio=0.6, checkOri=true)."""
+
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        h = ctypes.c_void_p()
+        _check(lib().orb_matcher_create(device, ctypes.byref(h)), "orb_matcher_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orb_matcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @staticmethod
+    def DescriptorDistance(a: np.ndarray, b: np.ndarray) -> int:
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return lib().orb_descriptor_distance(_ptr(a), _ptr(b))
+
+    def hamming_batch(self, d_a: int, d_b: int, n: int, d_out: int, stream: int = 0):
+        _check(lib().orb_hamming_batch(self._h, d_a, d_b, n, d_out, stream or None), "hamming")
+
+    def SearchByProjection(self, F: Frame, mps: np.ndarray, mp_desc: np.ndarray, th: float,
+                           kp_locked: np.ndarray | None = None):
+        """SearchByProjection(F, vpMapPoints, th): returns (nmatches, kp_match).
+
+        kp_match[i] = index of the map point assigned to keypoint i by this
+        call (F.mvpMapPoints[i] = vpMapPoints[kp_match[i]]) or -1."""
+        mps = np.ascontiguousarray(mps, MP_TRACK_DTYPE)
+        mp_desc = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        locked = None if kp_locked is None else np.ascontiguousarray(kp_locked, np.uint8)
+        kp_match = np.full(F.N, -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f = F._c()
+        _check(lib().orb_match_projection_local(
+            self._h, ctypes.byref(f), _ptr(locked) if locked is not None else None, len(mps),
+            _ptr(mps) if len(mps) else None, _ptr(mp_desc) if len(mps) else None, th,
+            self.mfNNratio, _ptr(kp_match), ctypes.byref(nm)), "SearchByProjection")
+        return nm.value, kp_match

@@ -1,0 +1,735 @@
+// extractor_kernels.hip -- gfx950 kernels of the ORB extractor (ORBextractor::operator()).
+//
+// Pipeline for a batch of B images (one launch per stage, every launch covers
+// all B images; HBM layout in DESIGN.md §3):
+//   k_pyr_resize   x (nlevels-1)  bilinear level l from level l-1   src/ORBextractor.cc:1172-1207
+//   k_fast_cells   x 1            FAST-9/16 score, cell-local NMS,    src/ORBextractor.cc:816-865
+//                                 iniTh -> minTh fallback, ordered compaction
+//   k_octree       x 1            DistributeOctTree, one workgroup   src/ORBextractor.cc:558-782
+//                                 per (image, level), list order emulated exactly
+//   k_orient_desc  x 1            IC_Angle + 7x7 blur + rBRIEF-256,   src/ORBextractor.cc:77-164,
+//                                 one wave per keypoint, rescale       1131-1167
+// Bit-exactness contract: every output byte equals the CPU oracle
+// (oracle/orb_oracle.cpp) on the same image.
+#include "orb_device.h"
+#include "orb_plan.h"
+#include "orb_pattern_data.h"
+#include "../../include/orb_abi.h"
+
+// ============================================================ k_pyr_resize
+// cv::resize(prev, level, sz, 0, 0, INTER_LINEAR) on 8U with OpenCV's 11-bit
+// fixed-point weights.  The weight tables are computed
+// on the host with the reference's float/double expressions; the kernel only
+// does the integer taps.  One thread per output pixel, 64x4 tiles.
+__global__ __launch_bounds__(256) void k_pyr_resize(
+    const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sh,
+    uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
+    const int* __restrict__ xofs, const short2* __restrict__ alpha,
+    const int* __restrict__ yofs, const short2* __restrict__ beta, int xmax) {
+  const int dx = blockIdx.x * 64 + threadIdx.x;
+  const int dy = blockIdx.y * 4 + threadIdx.y;
+  if (dx >= dw || dy >= dh) return;
+  const uint8_t* S = src + (long long)blockIdx.z * srcImgPitch;
+  const int sy = yofs[dy];
+  const int r0 = min(max(sy, 0), sh - 1), r1 = min(max(sy + 1, 0), sh - 1);
+  const uint8_t* p0 = S + (long long)r0 * srcStride;
+  const uint8_t* p1 = S + (long long)r1 * srcStride;
+  const int sx = xofs[dx];
+  int h0, h1;
+  if (dx < xmax) {
+    const short2 a = alpha[dx];
+    h0 = p0[sx] * a.x + p0[sx + 1] * a.y;
+    h1 = p1[sx] * a.x + p1[sx + 1] * a.y;
+  } else {
+    h0 = p0[sx] * 2048;
+    h1 = p1[sx] * 2048;
+  }
+  const short2 b = beta[dy];
+  const int v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
+  dst[(long long)blockIdx.z * dstImgPitch + (long long)dy * dstStride + dx] =
+      (uint8_t)min(max(v, 0), 255);
+}
+
+// ============================================================ k_fast_cells
+// FAST arc strength at the pixel `c` points to (LDS tile, row pitch `p`):
+// m = max(best dark 9-arc, best bright 9-arc), where an arc's strength is the
+// min over its 9 pixels of |I(p) - I(q)| on the matching side.  FAST(t) detects
+// the pixel iff m > t, and for a detected corner OpenCV's cornerScore<16> is
+// m - 1 whatever t is.
+__device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
+  const int v = c[0];
+  int d[16];
+  d[0] = v - c[3 * p];
+  d[1] = v - c[3 * p + 1];
+  d[2] = v - c[2 * p + 2];
+  d[3] = v - c[p + 3];
+  d[4] = v - c[3];
+  d[5] = v - c[-p + 3];
+  d[6] = v - c[-2 * p + 2];
+  d[7] = v - c[-3 * p + 1];
+  d[8] = v - c[-3 * p];
+  d[9] = v - c[-3 * p - 1];
+  d[10] = v - c[-2 * p - 2];
+  d[11] = v - c[-p - 3];
+  d[12] = v - c[-3];
+  d[13] = v - c[p - 3];
+  d[14] = v - c[2 * p - 2];
+  d[15] = v - c[3 * p - 1];
+  int mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    mn2[k] = min(d[k], d[(k + 1) & 15]);
+    mx2[k] = max(d[k], d[(k + 1) & 15]);
+  }
+  int mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+  }
+  int dark = -1024, brightNeg = 1024;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int a9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+    const int b9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+    dark = max(dark, a9);
+    brightNeg = min(brightNeg, b9);
+  }
+  return max(dark, -brightNeg);
+}
+
+// One workgroup per (cell, image).  Output: the cell's keypoints (row-major in
+// the cell's detection window, exactly cv::FAST's order) packed as
+// x | y<<12 | score<<24 in level coordinates, and their count.
+__global__ __launch_bounds__(256) void k_fast_cells(
+    const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
+    const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
+    const OrbCellDesc* __restrict__ cells, uint32_t* __restrict__ cellKeys,
+    int32_t* __restrict__ cellCount) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int scanTmp[17];
+  const int cell = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const OrbCellDesc cd = cells[cell];
+  const int l = cd.level;
+  const int rows = cd.y1 - cd.y0, cols = cd.x1 - cd.x0;
+  const long long slot = (long long)img * plan.ncells + cell;
+  if (rows < 7 || cols < 7) {
+    if (tid == 0) cellCount[slot] = 0;
+    return;
+  }
+  const uint8_t* lvl;
+  int pitch;
+  if (l == 0) {
+    lvl = img0 + (long long)img * img0Pitch;
+    pitch = img0Stride;
+  } else {
+    lvl = arena + (long long)img * arenaPitch + plan.lv[l].arenaOff;
+    pitch = plan.lv[l].pitch;
+  }
+  uint8_t* roi = smem;  // rows x cols
+  const int dh = rows - 6, dw = cols - 6, sp = dw + 2;
+  uint8_t* sc = smem + ((rows * cols + 15) & ~15);  // (dh+2) x (dw+2), zero border
+  for (int i = tid; i < rows * cols; i += 256) {
+    const int y = i / cols, x = i - y * cols;
+    roi[i] = lvl[(long long)(cd.y0 + y) * pitch + cd.x0 + x];
+  }
+  for (int i = tid; i < (dh + 2) * sp; i += 256) sc[i] = 0;
+  __syncthreads();
+  const int npix = dh * dw;
+  for (int i = tid; i < npix; i += 256) {
+    const int y = i / dw, x = i - y * dw;
+    const int s = fast_score(roi + (y + 3) * cols + (x + 3), cols);
+    sc[(y + 1) * sp + (x + 1)] = (uint8_t)min(max(s, 0), 255);
+  }
+  __syncthreads();
+  // cell-local NMS at threshold t (OpenCV FAST_t with nonmax_suppression):
+  // corners store score m-1, everything else (incl. outside the window) 0, and
+  // a corner survives iff its score beats all 8 stored neighbour scores.
+  const int per = (npix + 255) >> 8;
+  const int beg = min(tid * per, npix), end = min(beg + per, npix);
+  auto survives = [&](int i, int t) -> bool {
+    const int y = i / dw, x = i - y * dw;
+    const uint8_t* c = sc + (y + 1) * sp + (x + 1);
+    const int m = c[0];
+    if (m <= t || m < 2) return false;  // not a corner, or score 0 cannot beat a 0 neighbour
+    const int nb[8] = {c[-sp - 1], c[-sp], c[-sp + 1], c[-1], c[1], c[sp - 1], c[sp], c[sp + 1]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (nb[k] > t && nb[k] >= m) return false;
+    return true;
+  };
+  int t = min(max(plan.iniTh, 0), 255);
+  int mine = 0;
+  for (int i = beg; i < end; ++i) mine += survives(i, t);
+  int total;
+  int off = block_excl_scan(mine, scanTmp, &total);
+  if (total == 0) {  // src/ORBextractor.cc:846-850: retry the cell at minThFAST
+    t = min(max(plan.minTh, 0), 255);
+    mine = 0;
+    for (int i = beg; i < end; ++i) mine += survives(i, t);
+    off = block_excl_scan(mine, scanTmp, &total);
+  }
+  uint32_t* out = cellKeys + slot * plan.keyCap;
+  for (int i = beg; i < end && mine; ++i) {
+    if (survives(i, t)) {
+      const int y = i / dw, x = i - y * dw;
+      out[off++] = pack_key(cd.x0 + 3 + x, cd.y0 + 3 + y, sc[(y + 1) * sp + (x + 1)] - 1);
+    }
+  }
+  if (tid == 0) cellCount[slot] = total;
+}
+
+// ================================================================ k_octree
+// ExtractorNode::DivideNode + ORBextractor::DistributeOctTree
+// (src/ORBextractor.cc:500-782), one workgroup per (level, image).
+//
+// The reference grows a std::list with push_front and erase, sorts split
+// candidates by (size, node address) and stops mid-pass once the list holds
+// N nodes.  Its list order is fully determined by creation order:
+//   after a regular pass: [children in reverse creation order] ++ [untouched
+//   single-key nodes in previous order]; after a final-phase pass:
+//   [children in reverse creation order] ++ [surviving nodes in previous order].
+// So the kernel keeps the live nodes as an array in list order plus a creation
+// sequence number (the stand-in for the heap address), and
+// each pass is a handful of data-parallel steps: quadrant counts by key,
+// prefix sums over nodes to place children, and a key re-labelling.  A key's
+// node keeps the keys in vToDistributeKeys order, so the per-node winner is the
+// first key with maximal response (:763-779) = max of (response, -index).
+struct OctNode {
+  int16_t x0, y0, x1, y1;  // rectangle in border-relative coordinates (UL, BR)
+  int cnt;                 // vKeys.size()
+  int seq;                 // creation order
+};
+
+__device__ __forceinline__ int oct_quad(uint32_t key, const OctNode& n) {
+  const int kx = key_x(key) - 16, ky = key_y(key) - 16;  // minBorderX = minBorderY = 16
+  const int mx = n.x0 + ((n.x1 - n.x0 + 1) >> 1);        // ceil((UR.x-UL.x)/2), :502
+  const int my = n.y0 + ((n.y1 - n.y0 + 1) >> 1);
+  return (kx < mx ? 0 : 1) + (ky < my ? 0 : 2);  // n1, n2, n3, n4 = 0, 1, 2, 3 (:534-544)
+}
+
+__device__ __forceinline__ OctNode oct_child(const OctNode& p, int q, int cnt, int seq) {
+  const int mx = p.x0 + ((p.x1 - p.x0 + 1) >> 1);
+  const int my = p.y0 + ((p.y1 - p.y0 + 1) >> 1);
+  OctNode c;
+  c.x0 = (int16_t)((q & 1) ? mx : p.x0);
+  c.x1 = (int16_t)((q & 1) ? p.x1 : mx);
+  c.y0 = (int16_t)((q & 2) ? my : p.y0);
+  c.y1 = (int16_t)((q & 2) ? p.y1 : my);
+  c.cnt = cnt;
+  c.seq = seq;
+  return c;
+}
+
+// In-place chunked exclusive scan over an LDS int array of length n; returns the total.
+__device__ int block_scan_array(int* a, int n, int* tmp) {
+  const int T = blockDim.x, t = threadIdx.x;
+  const int per = (n + T - 1) / T;
+  const int b = min(t * per, n), e = min(b + per, n);
+  int s = 0;
+  for (int i = b; i < e; ++i) s += a[i];
+  int total;
+  int ex = block_excl_scan(s, tmp, &total);
+  for (int i = b; i < e; ++i) {
+    const int v = a[i];
+    a[i] = ex;
+    ex += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+__device__ void block_bitonic_desc(unsigned long long* v, int n2) {
+  for (int k = 2; k <= n2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = v[i], b = v[ixj];
+          const bool descBlock = (i & k) == 0;
+          if (descBlock ? (a < b) : (a > b)) {
+            v[i] = b;
+            v[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+#define OCT_MAX_PASSES 512
+
+__global__ __launch_bounds__(512) void k_octree(
+    OrbPlanDesc plan, const int32_t* __restrict__ cellCount, const uint32_t* __restrict__ cellKeys,
+    uint32_t* __restrict__ gKeys, uint16_t* __restrict__ gNid, int ldsKeyCap, int nodeCapMax,
+    int maxCellsPerLevel, uint32_t* __restrict__ outKeys, int32_t* __restrict__ outCount,
+    int32_t* __restrict__ errFlag) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int tmp[17];
+  __shared__ int sh[8];
+  const int l = blockIdx.x, img = blockIdx.y, T = blockDim.x, t = threadIdx.x;
+  const OrbLevelDesc& L = plan.lv[l];
+  const int NC = nodeCapMax;
+  int n2 = 1;
+  while (n2 < NC) n2 <<= 1;
+  // ---- LDS carve (all offsets multiples of 16)
+  unsigned char* p = smem;
+  unsigned long long* sortBuf = (unsigned long long*)p; p += (size_t)n2 * 8;
+  OctNode* A = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
+  OctNode* B = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
+  int* q4 = (int*)p; p += (size_t)NC * 16;       // quadrant counts, then child indices
+  int* g0 = (int*)p; p += (size_t)NC * 4;
+  int* g1 = (int*)p; p += (size_t)NC * 4;
+  int* g2 = (int*)p; p += (size_t)NC * 4;
+  int* rk = (int*)p; p += (size_t)NC * 4;
+  int* cellBase = (int*)p; p += (size_t)((maxCellsPerLevel + 3) & ~3) * 4;
+  uint32_t* Klds = (uint32_t*)p; p += (size_t)ldsKeyCap * 4;
+  uint16_t* Nlds = (uint16_t*)p;
+
+  const int cb = L.cellBeg, nc = L.cellEnd - L.cellBeg;
+  const long long cellSlot0 = (long long)img * plan.ncells + cb;
+  for (int i = t; i < nc; i += T) cellBase[i] = cellCount[cellSlot0 + i];
+  __syncthreads();
+  const int n = block_scan_array(cellBase, nc, tmp);
+  uint32_t* K;
+  uint16_t* NID;
+  if (n <= ldsKeyCap) {
+    K = Klds;
+    NID = Nlds;
+  } else {
+    K = gKeys + cellSlot0 * plan.keyCap;  // this level's slot range, reused compacted
+    NID = gNid + cellSlot0 * plan.keyCap;
+  }
+  if (n > 65535) {  // node/key labels are 16-bit
+    if (t == 0) { atomicOr(errFlag, 1); outCount[img * plan.nlevels + l] = 0; }
+    return;
+  }
+  for (int c = t; c < nc; c += T) {
+    const int cnt = cellCount[cellSlot0 + c], base = cellBase[c];
+    const uint32_t* src = cellKeys + (cellSlot0 + c) * plan.keyCap;
+    for (int i = 0; i < cnt; ++i) K[base + i] = src[i];
+  }
+  // ---- roots (src/ORBextractor.cc:562-604)
+  const int nIni = L.nIni;
+  const float hX = L.hX;
+  for (int i = t; i < nIni; i += T) g0[i] = 0;
+  __syncthreads();
+  for (int k = t; k < n; k += T) {
+    const float xr = (float)(key_x(K[k]) - 16);
+    const int r = min((int)__fdiv_rn(xr, hX), nIni - 1);  // vpIniNodes[kp.pt.x/hX]
+    NID[k] = (uint16_t)r;
+    atomicAdd(&g0[r], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int a = 0;
+    for (int i = 0; i < nIni; ++i) {
+      g1[i] = a;
+      if (g0[i] > 0) {
+        OctNode nd;
+        nd.x0 = (int16_t)(int)(hX * (float)i);
+        nd.x1 = (int16_t)(int)(hX * (float)(i + 1));
+        nd.y0 = 0;
+        nd.y1 = (int16_t)L.Hr;
+        nd.cnt = g0[i];
+        nd.seq = i;
+        A[a++] = nd;
+      }
+    }
+    sh[0] = a;
+  }
+  __syncthreads();
+  for (int k = t; k < n; k += T) NID[k] = (uint16_t)g1[NID[k]];
+  int alive = sh[0];
+  const int N = L.quota;
+  int seqNext = nIni;
+  bool finalPhase = false;
+  int pass = 0;
+  __syncthreads();
+  for (; pass < OCT_MAX_PASSES; ++pass) {
+    const int prev = alive;
+    if (!finalPhase) {
+      // ================= regular pass: divide every node with > 1 key (:625-684)
+      for (int i = t; i < alive * 4; i += T) q4[i] = 0;
+      __syncthreads();
+      for (int k = t; k < n; k += T) {
+        const int a = NID[k];
+        if (A[a].cnt > 1) atomicAdd(&q4[a * 4 + oct_quad(K[k], A[a])], 1);
+      }
+      __syncthreads();
+      int nteLocal = 0;
+      for (int a = t; a < alive; a += T) {
+        int nce = 0;
+        if (A[a].cnt > 1) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = q4[a * 4 + q];
+            nce += c > 0;
+            nteLocal += c > 1;
+          }
+        }
+        g0[a] = nce;
+        g1[a] = A[a].cnt > 1 ? 0 : 1;
+      }
+      int nToExpand;
+      block_excl_scan(nteLocal, tmp, &nToExpand);
+      const int S = block_scan_array(g0, alive, tmp);
+      const int NM = block_scan_array(g1, alive, tmp);
+      if (S + NM > NC) {
+        if (t == 0) atomicOr(errFlag, 2);
+        break;
+      }
+      for (int a = t; a < alive; a += T) {
+        const OctNode nd = A[a];
+        if (nd.cnt > 1) {
+          int pos = g0[a];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = q4[a * 4 + q];
+            if (c > 0) {
+              const int ni = S - 1 - pos;
+              B[ni] = oct_child(nd, q, c, seqNext + pos);
+              q4[a * 4 + q] = ni;
+              ++pos;
+            }
+          }
+        } else {
+          const int ni = S + g1[a];
+          B[ni] = nd;
+          q4[a * 4] = ni;
+        }
+      }
+      __syncthreads();
+      for (int k = t; k < n; k += T) {
+        const int a = NID[k];
+        const OctNode& nd = A[a];
+        NID[k] = (uint16_t)q4[a * 4 + (nd.cnt > 1 ? oct_quad(K[k], nd) : 0)];
+      }
+      __syncthreads();
+      OctNode* sw = A; A = B; B = sw;
+      alive = S + NM;
+      seqNext += S;
+      if (alive >= N || alive == prev) break;                 // :688-691
+      if (alive + nToExpand * 3 > N) finalPhase = true;      // :692
+    } else {
+      // ================= final phase pass (:695-756)
+      for (int a = t; a < alive; a += T) g0[a] = A[a].cnt > 1 ? 1 : 0;
+      __syncthreads();
+      const int ncand = block_scan_array(g0, alive, tmp);
+      if (ncand == 0) break;  // nothing to divide: size == prevSize
+      int m2 = 1;
+      while (m2 < ncand) m2 <<= 1;
+      for (int i = t; i < m2; i += T) sortBuf[i] = 0ull;
+      __syncthreads();
+      for (int a = t; a < alive; a += T) {
+        const OctNode nd = A[a];
+        if (nd.cnt > 1)  // sort key (size, creation order); node index rides in the low bits
+          sortBuf[g0[a]] = ((unsigned long long)nd.cnt << 48) |
+                           ((unsigned long long)(uint32_t)nd.seq << 16) | (unsigned)a;
+        q4[a * 4 + 0] = q4[a * 4 + 1] = q4[a * 4 + 2] = q4[a * 4 + 3] = 0;
+        rk[a] = 0x7fffffff;
+      }
+      __syncthreads();
+      block_bitonic_desc(sortBuf, m2);  // largest (size, seq) first == reverse of std::sort
+      for (int j = t; j < ncand; j += T) rk[(int)(sortBuf[j] & 0xFFFF)] = j;
+      for (int k = t; k < n; k += T) {
+        const int a = NID[k];
+        if (A[a].cnt > 1) atomicAdd(&q4[a * 4 + oct_quad(K[k], A[a])], 1);
+      }
+      if (t == 0) sh[1] = ncand - 1;
+      __syncthreads();
+      // node j in sorted order adds (non-empty children - 1) nodes; stop after
+      // the first division that brings the list to >= N (:749-750)
+      for (int j = t; j < ncand; j += T) {
+        const int a = (int)(sortBuf[j] & 0xFFFF);
+        int nce = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nce += q4[a * 4 + q] > 0;
+        g1[j] = nce;
+        g2[j] = nce - 1;
+      }
+      __syncthreads();
+      block_scan_array(g2, ncand, tmp);  // exclusive
+      for (int j = t; j < ncand; j += T)
+        if (alive + g2[j] + (g1[j] - 1) >= N) atomicMin(&sh[1], j);
+      __syncthreads();
+      const int jstop = sh[1];
+      for (int j = t; j < ncand; j += T)
+        if (j > jstop) g1[j] = 0;
+      __syncthreads();
+      const int S = block_scan_array(g1, ncand, tmp);  // child base per divided node
+      for (int a = t; a < alive; a += T) g2[a] = (rk[a] <= jstop) ? 0 : 1;
+      __syncthreads();
+      const int keep = block_scan_array(g2, alive, tmp);
+      if (S + keep > NC) {
+        if (t == 0) atomicOr(errFlag, 2);
+        break;
+      }
+      for (int a = t; a < alive; a += T) {
+        const OctNode nd = A[a];
+        const int j = rk[a];
+        if (j <= jstop) {
+          int pos = g1[j];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = q4[a * 4 + q];
+            if (c > 0) {
+              const int ni = S - 1 - pos;
+              B[ni] = oct_child(nd, q, c, seqNext + pos);
+              q4[a * 4 + q] = ni;
+              ++pos;
+            }
+          }
+        } else {
+          const int ni = S + g2[a];
+          B[ni] = nd;
+          q4[a * 4] = ni;
+        }
+      }
+      __syncthreads();
+      for (int k = t; k < n; k += T) {
+        const int a = NID[k];
+        const OctNode& nd = A[a];
+        NID[k] = (uint16_t)q4[a * 4 + (rk[a] <= jstop ? oct_quad(K[k], nd) : 0)];
+      }
+      __syncthreads();
+      OctNode* sw = A; A = B; B = sw;
+      alive = S + keep;
+      seqNext += S;
+      if (alive >= N || alive == prev) break;  // :753-754
+    }
+  }
+  if (pass >= OCT_MAX_PASSES && t == 0) atomicOr(errFlag, 4);
+  // ---- retain the best key of each node (:760-779)
+  uint32_t* best = (uint32_t*)g0;
+  for (int a = t; a < alive; a += T) best[a] = 0u;
+  __syncthreads();
+  for (int k = t; k < n; k += T)
+    atomicMax(&best[NID[k]], ((uint32_t)key_s(K[k]) << 24) | (uint32_t)(0xFFFFFF - k));
+  __syncthreads();
+  uint32_t* out = outKeys + (long long)img * plan.slotsPerImage + L.outOff;
+  for (int a = t; a < alive; a += T) out[a] = K[0xFFFFFF - (int)(best[a] & 0xFFFFFF)];
+  if (t == 0) outCount[img * plan.nlevels + l] = alive;
+}
+
+// =========================================================== k_orient_desc
+__constant__ int8_t c_pattern[2 * ORB_PATTERN_POINTS];
+__constant__ int c_umax[16];
+
+#define DESC_TILE 43  // 2 * (18 sample radius + 3 blur radius) + 1
+#define DESC_PITCH 44
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+  }
+  return i;
+}
+
+// GaussianBlur 7x7 sigma 2 (8U, integer kernel) of the
+// level evaluated at one tile position; the tile already holds reflect-101
+// extended pixels, so this equals the full-level blur at that pixel.
+__device__ __forceinline__ int blur7_at(const uint8_t* tile, int ty, int tx) {
+  const int k[7] = {18, 34, 49, 55, 49, 34, 18};
+  int acc = 0;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const uint8_t* r = tile + (ty + j - 3) * DESC_PITCH + tx - 3;
+    const int rs = k[0] * r[0] + k[1] * r[1] + k[2] * r[2] + k[3] * r[3] + k[4] * r[4] +
+                   k[5] * r[5] + k[6] * r[6];
+    acc += k[j] * rs;
+  }
+  return min((acc + (1 << 15)) >> 16, 255);
+}
+
+// One wave per keypoint.  slot -> (level, index) through plan.lv[].outOff.
+__global__ __launch_bounds__(256) void k_orient_desc(
+    const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
+    const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
+    const uint32_t* __restrict__ outKeys, const int32_t* __restrict__ outCount,
+    orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc, int capacity,
+    int32_t* __restrict__ counts) {
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[4][DESC_TILE * DESC_PITCH];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int img = blockIdx.y;
+  const int slot = blockIdx.x * 4 + w;
+  const int32_t* cnts = outCount + img * plan.nlevels;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int tot = 0;
+    for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
+    counts[img] = tot;
+  }
+  if (slot >= plan.slotsPerImage) return;
+  int l = 0;
+  while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot) ++l;
+  const int i = slot - plan.lv[l].outOff;
+  if (i >= cnts[l]) return;
+  int base = 0;
+  for (int j = 0; j < l; ++j) base += cnts[j];
+  const uint32_t key = outKeys[(long long)img * plan.slotsPerImage + slot];
+  const int cx = key_x(key), cy = key_y(key);
+  const OrbLevelDesc& L = plan.lv[l];
+  const uint8_t* lvl;
+  int pitch;
+  if (l == 0) {
+    lvl = img0 + (long long)img * img0Pitch;
+    pitch = img0Stride;
+  } else {
+    lvl = arena + (long long)img * arenaPitch + L.arenaOff;
+    pitch = L.pitch;
+  }
+  uint8_t* tile = tiles[w];
+  for (int e = lane; e < DESC_TILE * DESC_TILE; e += 64) {
+    const int ty = e / DESC_TILE, tx = e - ty * DESC_TILE;
+    const int yy = reflect101(cy - 21 + ty, L.h), xx = reflect101(cx - 21 + tx, L.w);
+    tile[ty * DESC_PITCH + tx] = lvl[(long long)yy * pitch + xx];
+  }
+  // the tile is private to this wave: a wave-scope fence orders the LDS stores
+  // before other lanes' loads (no block barrier: sibling waves may have exited)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // ---- IC_Angle on the un-blurred level (src/ORBextractor.cc:77-113)
+  int m01 = 0, m10 = 0;
+  if (lane < 31) {
+    const int u = lane - 15;
+    const uint8_t* c = tile + 21 * DESC_PITCH + 21;
+    m10 += u * c[u];
+    for (int v = 1; v <= 15; ++v) {
+      if (u < -c_umax[v] || u > c_umax[v]) continue;
+      const int plus = c[u + v * DESC_PITCH], minus = c[u - v * DESC_PITCH];
+      m01 += v * (plus - minus);
+      m10 += u * (plus + minus);
+    }
+  }
+  m01 = wave_sum(m01);
+  m10 = wave_sum(m10);
+  const float angle = fast_atan2_deg((float)m01, (float)m10);
+  // ---- rBRIEF on the blurred level (src/ORBextractor.cc:119-164)
+  const float factorPI = (float)(3.14159265358979323846 / 180.f);
+  float a, b;
+  {
+    float s, c;
+    pinned_sincos(angle * factorPI, &s, &c);
+    a = c;
+    b = s;
+  }
+  unsigned long long words[4];
+#pragma unroll
+  for (int kq = 0; kq < 4; ++kq) {
+    const int test = lane + 64 * kq;
+    int val[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float px = (float)c_pattern[2 * (2 * test + h)];
+      const float py = (float)c_pattern[2 * (2 * test + h) + 1];
+      const int dy = cv_round(px * b + py * a);
+      const int dx = cv_round(px * a - py * b);
+      val[h] = blur7_at(tile, 21 + dy, 21 + dx);
+    }
+    words[kq] = __ballot(val[0] < val[1]);
+  }
+  const long long o = (long long)img * capacity + base + i;
+  if (lane == 0) {
+    ulonglong4 d;
+    d.x = words[0];
+    d.y = words[1];
+    d.z = words[2];
+    d.w = words[3];
+    *reinterpret_cast<ulonglong4*>(desc + o * 32) = d;
+    orb_keypoint_t kp;
+    kp.x = l ? (float)cx * L.scale : (float)cx;  // pt *= mvScaleFactor[level] (:1157-1165)
+    kp.y = l ? (float)cy * L.scale : (float)cy;
+    kp.size = L.sizeF;
+    kp.angle = angle;
+    kp.response = (float)key_s(key);
+    kp.octave = l;
+    kp.class_id = -1;
+    kps[o] = kp;
+  }
+}
+
+// ------------------------------------------------------------ host launchers
+extern "C" {
+
+hipError_t orb_k_upload_constants(hipStream_t s) {
+  int8_t pat[2 * ORB_PATTERN_POINTS];
+  for (int i = 0; i < 2 * ORB_PATTERN_POINTS; ++i) pat[i] = (int8_t)kOrbPatternXY[i];
+  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_pattern), pat, sizeof(pat), 0,
+                                        hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  return hipSuccess;
+}
+
+hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s) {
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_umax), umax16, 16 * sizeof(int), 0,
+                                hipMemcpyHostToDevice, s);
+}
+
+hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sh,
+                            uint8_t* dst, long long dstImgPitch, int dstStride, int dw, int dh,
+                            const int* xofs, const void* alpha, const int* yofs, const void* beta,
+                            int xmax, int nimg, hipStream_t s) {
+  dim3 grid((dw + 63) / 64, (dh + 3) / 4, nimg), block(64, 4);
+  hipLaunchKernelGGL(k_pyr_resize, grid, block, 0, s, src, srcImgPitch, srcStride, sh, dst,
+                     dstImgPitch, dstStride, dw, dh, xofs, (const short2*)alpha, yofs,
+                     (const short2*)beta, xmax);
+  return hipGetLastError();
+}
+
+hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                            const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
+                            int nimg, hipStream_t s) {
+  const int rows = plan->maxCellRows, cols = plan->maxCellCols;
+  const size_t lds = (size_t)((rows * cols + 15) & ~15) + (size_t)(rows - 4) * (cols - 4);
+  dim3 grid(plan->ncells, nimg), block(256);
+  hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
+                     arenaPitch, *plan, cells, cellKeys, cellCount);
+  return hipGetLastError();
+}
+
+size_t orb_k_octree_lds(int nodeCapMax, int maxCellsPerLevel, int ldsKeyCap) {
+  int n2 = 1;
+  while (n2 < nodeCapMax) n2 <<= 1;
+  size_t b = (size_t)n2 * 8 + 2 * (size_t)nodeCapMax * sizeof(OctNode) + (size_t)nodeCapMax * 16 +
+             4 * (size_t)nodeCapMax * 4 + (size_t)((maxCellsPerLevel + 3) & ~3) * 4;
+  b += (size_t)ldsKeyCap * 4 + (size_t)ldsKeyCap * 2;
+  return b;
+}
+
+size_t orb_k_octree_node_bytes(int nodeCapMax, int maxCellsPerLevel) {
+  return orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, 0);
+}
+
+hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
+                        const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
+                        int nodeCapMax, int maxCellsPerLevel, uint32_t* outKeys,
+                        int32_t* outCount, int32_t* errFlag, int nimg, hipStream_t s) {
+  const size_t lds = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, ldsKeyCap);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_octree,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  dim3 grid(plan->nlevels, nimg), block(512);
+  hipLaunchKernelGGL(k_octree, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys, gNid,
+                     ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag);
+  return hipGetLastError();
+}
+
+hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                             const uint32_t* outKeys, const int32_t* outCount,
+                             orb_keypoint_t* kps, uint8_t* desc, int capacity, int32_t* counts,
+                             int nimg, hipStream_t s) {
+  dim3 grid((plan->slotsPerImage + 3) / 4, nimg), block(256);
+  hipLaunchKernelGGL(k_orient_desc, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
+                     arenaPitch, *plan, outKeys, outCount, kps, desc, capacity, counts);
+  return hipGetLastError();
+}
+
+}  // extern "C"

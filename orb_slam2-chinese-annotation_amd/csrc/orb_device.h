@@ -1,0 +1,127 @@
+// orb_device.h -- device-side helpers shared by the extractor and matcher kernels.
+//
+// Every float expression here is evaluated exactly as written: the library is
+// compiled with -ffp-contract=off and -fhip-fp32-correctly-rounded-divide-sqrt,
+// so results are bit-identical to the CPU oracle built with g++ -ffp-contract=off
+// (SURVEY.md §7 H4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ORB_MAX_LEVELS 16
+#define ORB_WAVE 64
+
+// ---------------------------------------------------------------- rounding
+// cvRound = round half to even
+__device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v); }
+// std::round / roundf: half away from zero (src/ORBmatcher.cc:254, src/Frame.cc:428)
+__device__ __forceinline__ float round_half_away(float v) { return __builtin_roundf(v); }
+
+// -------------------------------------------------- A.4 OpenCV fastAtan2
+__device__ __forceinline__ float fast_atan2_deg(float y, float x) {
+  const float r2d = (float)(180.0 / 3.14159265358979323846);
+  const float p1 = 0.9997878412794807f * r2d, p3 = -0.3258083974640975f * r2d;
+  const float p5 = 0.1555786518463281f * r2d, p7 = -0.04432655554792128f * r2d;
+  const float eps = (float)2.2204460492503131e-16;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a;
+  if (ax >= ay) {
+    const float c = __fdiv_rn(ay, ax + eps);
+    const float c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    const float c = __fdiv_rn(ax, ay + eps);
+    const float c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+// ---------------------------------------------- A.6 pinned sin/cos (double)
+// fdlibm-style Cody-Waite reduction by pi/2 and degree-13/14 kernels in double,
+// rounded once to float.  Same operation sequence as the oracle.
+__device__ __forceinline__ void pinned_sincos(float angle, float* s_out, float* c_out) {
+  const double x = (double)angle;
+  const double invpio2 = 6.36619772367581382433e-01;
+  const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
+  const double k = __builtin_rint(x * invpio2);
+  const double r = (x - k * pio2_1) - k * pio2_1t;
+  const double z = r * r;
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double ps = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  const double sn = r + (z * r) * (S1 + z * ps);
+  const double pc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cs = w + (((1.0 - w) - hz) + z * pc);
+  const int q = ((int)k) & 3;
+  double s, c;
+  if (q == 0) { s = sn; c = cs; }
+  else if (q == 1) { s = cs; c = -sn; }
+  else if (q == 2) { s = -sn; c = -cs; }
+  else { s = -cs; c = sn; }
+  *s_out = (float)s;
+  *c_out = (float)c;
+}
+
+// ------------------------------------------------------------- Hamming
+// DescriptorDistance (src/ORBmatcher.cc:1814-1830) == popcount(a ^ b) over 256 bits.
+__device__ __forceinline__ int hamming256(const ulonglong4 a, const ulonglong4 b) {
+  return __popcll(a.x ^ b.x) + __popcll(a.y ^ b.y) + __popcll(a.z ^ b.z) + __popcll(a.w ^ b.w);
+}
+__device__ __forceinline__ ulonglong4 load_desc(const uint8_t* p) {
+  return *reinterpret_cast<const ulonglong4*>(p);
+}
+
+// ------------------------------------------------------ wave primitives
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o, 64);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide exclusive scan of one value per thread; returns the exclusive
+// prefix, *total receives the block sum.  `tmp` = LDS scratch of >= 17 ints.
+// Must be called by all threads of the block.
+__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
+  const int l = lane_id(), w = (int)(threadIdx.x >> 6), nw = (int)((blockDim.x + 63) >> 6);
+  const int inc = wave_incl_scan(v);
+  if (l == 63) tmp[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < nw; ++i) { const int t = tmp[i]; tmp[i] = acc; acc += t; }
+    tmp[16] = acc;
+  }
+  __syncthreads();
+  const int r = tmp[w] + inc - v;
+  *total = tmp[16];
+  __syncthreads();
+  return r;
+}
+
+// Packed candidate keypoint: x (12b) | y (12b) << 12 | FAST score (8b) << 24.
+__device__ __forceinline__ uint32_t pack_key(int x, int y, int s) {
+  return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
+}
+__device__ __forceinline__ int key_x(uint32_t k) { return (int)(k & 0xFFFu); }
+__device__ __forceinline__ int key_y(uint32_t k) { return (int)((k >> 12) & 0xFFFu); }
+__device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 24); }

@@ -1,0 +1,51 @@
+// orb_plan.h -- per-image-size extraction plan shared by the host runtime and kernels.
+//
+// Everything that depends only on (width, height, nfeatures, scaleFactor,
+// nlevels) is computed once on the host -- level sizes, resize coefficient
+// tables, the FAST cell grid, octree root layout, output slot layout -- with
+// the exact float/double expressions of the reference
+// (src/ORBextractor.cc:428-489, 785-815, 558-582, 1172-1207), and handed to
+// the kernels by value.  The kernels then do only per-pixel / per-key work.
+#pragma once
+#include <stdint.h>
+
+#ifndef ORB_MAX_LEVELS
+#define ORB_MAX_LEVELS 16
+#endif
+
+struct OrbLevelDesc {
+  int w, h;          // level size (cvRound(W * invScale), src/ORBextractor.cc:1180)
+  int pitch;         // row pitch of the level in the pyramid arena (level 0: caller stride)
+  int _pad0;
+  long long arenaOff;// byte offset of the level inside one image's pyramid arena (l >= 1)
+  int cellBeg, cellEnd;  // range of this level's cells in the cell table
+  int quota;         // mnFeaturesPerLevel[l]
+  int nodeCap;       // max alive octree nodes == max keypoints this level can emit
+  int outOff;        // first output slot of this level inside one image's slot arena
+  int nIni;          // octree root count (src/ORBextractor.cc:562)
+  float hX;          // root width (src/ORBextractor.cc:564)
+  int Wr, Hr;        // maxBorderX-minBorderX, maxBorderY-minBorderY
+  float scale;       // mvScaleFactor[l]
+  float sizeF;       // (float)(int)(31 * scale), src/ORBextractor.cc:874
+  int rtabX, rtabY;  // offsets of this level's resize tables (x: xofs/alpha, y: yofs/beta)
+  int xmax;          // first dx whose source tap sx+1 falls outside (resize)
+  int _pad1;
+};
+
+struct OrbPlanDesc {
+  int nlevels;
+  int ncells;        // total FAST cells over all levels
+  int keyCap;        // per-cell candidate capacity (max strict NMS maxima in a cell window)
+  int slotsPerImage; // sum of nodeCap over levels
+  int iniTh, minTh;
+  int maxCellRows, maxCellCols;  // largest cell ROI (for LDS sizing)
+  int srcW, srcH;
+  OrbLevelDesc lv[ORB_MAX_LEVELS];
+};
+
+// One FAST cell: ROI rows [y0,y1) x cols [x0,x1) of its level image
+// (src/ORBextractor.cc:816-839).  Cells are ordered level-major, then
+// row-major, i.e. the order in which the reference appends to vToDistributeKeys.
+struct OrbCellDesc {
+  int16_t level, y0, y1, x0, x1, _pad;
+};

@@ -1,0 +1,827 @@
+// runtime.cpp -- host runtime behind the C ABI (include/orb_abi.h).
+//
+// Owns devices, streams, extraction plans and device scratch; launches the
+// gfx950 kernels of extractor_kernels.hip / matcher_kernels.hip.  There is no
+// CPU compute path: every ORB result comes from the HIP kernels, and every
+// entry point fails with ORB_ENODEV / ORB_EDEVICE if the GPU path cannot run.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/orb_abi.h"
+#include "orb_plan.h"
+#include "orb_synth.h"
+
+// ------------------------------------------------------- kernel launchers
+extern "C" {
+hipError_t orb_k_upload_constants(hipStream_t s);
+hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s);
+hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sh,
+                            uint8_t* dst, long long dstImgPitch, int dstStride, int dw, int dh,
+                            const int* xofs, const void* alpha, const int* yofs, const void* beta,
+                            int xmax, int nimg, hipStream_t s);
+hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                            const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
+                            int nimg, hipStream_t s);
+size_t orb_k_octree_lds(int nodeCapMax, int maxCellsPerLevel, int ldsKeyCap);
+hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
+                        const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
+                        int nodeCapMax, int maxCellsPerLevel, uint32_t* outKeys,
+                        int32_t* outCount, int32_t* errFlag, int nimg, hipStream_t s);
+hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                             const uint32_t* outKeys, const int32_t* outCount,
+                             orb_keypoint_t* kps, uint8_t* desc, int capacity, int32_t* counts,
+                             int nimg, hipStream_t s);
+hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out, hipStream_t s);
+hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
+                            float minX, float minY, float invW, float invH, int32_t* cellStart,
+                            int32_t* cellIdx, int nproblems, hipStream_t s);
+hipError_t orb_k_proj_local(const orb_keypoint_t* keys, const uint8_t* desc, const float* uright,
+                            const uint8_t* locked, const int32_t* nkeys, int kpStride,
+                            const orb_mp_track_t* mps, const uint8_t* mpDesc,
+                            const int32_t* nmps, int mpStride, int mpMax,
+                            const int32_t* cellStart, const int32_t* cellIdx, const void* params,
+                            uint32_t* topk, int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
+                            int nproblems, hipStream_t s);
+size_t orb_k_proj_params_size(void);
+}
+
+namespace {
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t _e = (expr);                             \
+    if (_e != hipSuccess) {                             \
+      if (getenv("ORB_AMD_DEBUG"))                      \
+        fprintf(stderr, "[orb_amd] %s:%d %s -> %s\n", __FILE__, __LINE__, #expr, \
+                hipGetErrorString(_e));                 \
+      return _e == hipErrorOutOfMemory ? ORB_ENOMEM : ORB_EDEVICE; \
+    }                                                   \
+  } while (0)
+
+static inline int cvRoundF(float v) { return (int)lrintf(v); }
+static inline short satShort(int v) { return (short)std::min(std::max(v, -32768), 32767); }
+
+// Growable device buffer.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  orb_status_t ensure(size_t n) {
+    if (n <= bytes) return ORB_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, n) != hipSuccess) return ORB_ENOMEM;
+    bytes = n;
+    return ORB_OK;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T* as() const { return (T*)p; }
+};
+
+orb_status_t check_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ORB_ENODEV;
+  if (device < 0 || device >= n) return ORB_EINVAL;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ORB_EDEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    if (getenv("ORB_AMD_DEBUG")) fprintf(stderr, "[orb_amd] device %d is %s, need gfx950\n", device, prop.gcnArchName);
+    return ORB_ENODEV;
+  }
+  return ORB_OK;
+}
+
+}  // namespace
+
+// ================================================================ extractor
+struct orb_extractor {
+  int device = 0;
+  int nfeatures = 0, nlevels = 0, iniTh = 0, minTh = 0;
+  float scaleFactorF = 1.2f;
+  double scaleFactor = 1.2;
+  std::vector<float> scale, invScale, sigma2, invSigma2;
+  std::vector<int> quota;
+  int umax[16];
+  hipStream_t stream = nullptr;
+  bool ownStream = false;
+  std::mutex mu;
+
+  // plan for the current image size
+  int planW = -1, planH = -1;
+  OrbPlanDesc plan;
+  std::vector<OrbCellDesc> cells;
+  long long arenaBytes = 0;
+  int maxCellsPerLevel = 0, nodeCapMax = 0, ldsKeyCap = 0;
+  DevBuf dCells, dRtab;
+
+  // batch scratch
+  int batchCap = 0;
+  DevBuf dArena, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
+  // single-image API scratch
+  DevBuf dImg, dKps, dDesc, dCounts;
+  int lastW = 0, lastH = 0;
+  size_t lastImgStride = 0;
+  const uint8_t* lastImg0 = nullptr;  // level 0 of the last batch (device)
+  size_t lastImg0Pitch = 0;
+  int lastImg0Stride = 0;
+
+  // profiling
+  bool profile = false;
+  hipEvent_t ev[8] = {};
+  double stageMs[5] = {0, 0, 0, 0, 0};
+  int stageLaunches[5] = {0, 0, 0, 0, 0};
+};
+
+static const char* kStageNames[5] = {"k_pyr_resize", "k_fast_cells", "k_octree",
+                                     "k_orient_desc", "extract_total"};
+
+static void compute_tables(orb_extractor* h) {
+  const int L = h->nlevels;
+  h->scale.assign(L, 0.f);
+  h->sigma2.assign(L, 0.f);
+  h->scale[0] = 1.0f;
+  h->sigma2[0] = 1.0f;
+  for (int i = 1; i < L; ++i) {  // src/ORBextractor.cc:437-441 (scaleFactor is a double member)
+    h->scale[i] = (float)((double)h->scale[i - 1] * h->scaleFactor);
+    h->sigma2[i] = h->scale[i] * h->scale[i];
+  }
+  h->invScale.resize(L);
+  h->invSigma2.resize(L);
+  for (int i = 0; i < L; ++i) {
+    h->invScale[i] = 1.0f / h->scale[i];
+    h->invSigma2[i] = 1.0f / h->sigma2[i];
+  }
+  h->quota.assign(L, 0);  // :453-464
+  const float factor = (float)(1.0f / h->scaleFactor);
+  float nDesired = (float)h->nfeatures * (1 - factor) /
+                   (1 - (float)pow((double)factor, (double)L));
+  int sum = 0;
+  for (int l = 0; l < L - 1; ++l) {
+    h->quota[l] = cvRoundF(nDesired);
+    sum += h->quota[l];
+    nDesired *= factor;
+  }
+  h->quota[L - 1] = std::max(h->nfeatures - sum, 0);
+  const int HP = 15;  // :473-488
+  const int vmax = (int)floorf(HP * sqrtf(2.f) / 2 + 1);
+  const int vmin = (int)ceilf(HP * sqrtf(2.f) / 2);
+  const double hp2 = HP * HP;
+  for (int v = 0; v <= vmax; ++v) h->umax[v] = (int)lrint(sqrt(hp2 - v * v));
+  for (int v = HP, v0 = 0; v >= vmin; --v) {
+    while (h->umax[v0] == h->umax[v0 + 1]) ++v0;
+    h->umax[v] = v0;
+    ++v0;
+  }
+}
+
+// Build the plan for a W x H input (level sizes, resize tables, FAST cells,
+// octree roots, output slots) and upload its tables.
+static orb_status_t build_plan(orb_extractor* h, int W, int H) {
+  if (h->planW == W && h->planH == H) return ORB_OK;
+  const int L = h->nlevels;
+  OrbPlanDesc P;
+  memset(&P, 0, sizeof(P));
+  P.nlevels = L;
+  P.iniTh = h->iniTh;
+  P.minTh = h->minTh;
+  P.srcW = W;
+  P.srcH = H;
+  std::vector<OrbCellDesc> cells;
+  std::vector<int32_t> rtab;
+  long long arena = 0;
+  int keyCap = 1, maxRows = 7, maxCols = 7, maxCellsPerLevel = 1, nodeCapMax = 1, slots = 0;
+  for (int l = 0; l < L; ++l) {
+    OrbLevelDesc& d = P.lv[l];
+    d.w = l ? cvRoundF((float)W * h->invScale[l]) : W;  // src/ORBextractor.cc:1180
+    d.h = l ? cvRoundF((float)H * h->invScale[l]) : H;
+    if (d.w < 40 || d.h < 40 || d.w > 4095 || d.h > 4095) return ORB_EINVAL;
+    d.pitch = (d.w + 63) & ~63;
+    d.arenaOff = l ? arena : 0;
+    if (l) arena += (long long)d.pitch * d.h;
+    d.scale = h->scale[l];
+    d.sizeF = (float)(int)(31 * h->scale[l]);
+    d.quota = h->quota[l];
+    // FAST cell grid, src/ORBextractor.cc:797-839
+    const int minBX = 16, minBY = 16, maxBX = d.w - 16, maxBY = d.h - 16;
+    const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
+    const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+    if (nCols <= 0 || nRows <= 0) return ORB_EINVAL;
+    const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+    d.cellBeg = (int)cells.size();
+    for (int i = 0; i < nRows; ++i) {
+      const float iniY = (float)(minBY + i * hCell);
+      float maxY = iniY + hCell + 6;
+      if (iniY >= maxBY - 3) continue;
+      if (maxY > maxBY) maxY = (float)maxBY;
+      for (int j = 0; j < nCols; ++j) {
+        const float iniX = (float)(minBX + j * wCell);
+        float maxX = iniX + wCell + 6;
+        if (iniX >= maxBX - 6) continue;
+        if (maxX > maxBX) maxX = (float)maxBX;
+        OrbCellDesc c;
+        c.level = (int16_t)l;
+        c.y0 = (int16_t)(int)iniY;
+        c.y1 = (int16_t)(int)maxY;
+        c.x0 = (int16_t)(int)iniX;
+        c.x1 = (int16_t)(int)maxX;
+        c._pad = 0;
+        cells.push_back(c);
+        const int rows = c.y1 - c.y0, cols = c.x1 - c.x0;
+        maxRows = std::max(maxRows, rows);
+        maxCols = std::max(maxCols, cols);
+        if (rows >= 7 && cols >= 7)
+          keyCap = std::max(keyCap, ((rows - 6 + 1) / 2) * ((cols - 6 + 1) / 2));
+      }
+    }
+    d.cellEnd = (int)cells.size();
+    maxCellsPerLevel = std::max(maxCellsPerLevel, d.cellEnd - d.cellBeg);
+    // octree roots, src/ORBextractor.cc:562-564
+    d.Wr = maxBX - minBX;
+    d.Hr = maxBY - minBY;
+    d.nIni = (int)roundf((float)d.Wr / d.Hr);
+    if (d.nIni <= 0) return ORB_EINVAL;
+    d.hX = (float)d.Wr / d.nIni;
+    d.nodeCap = std::max(d.quota + 4, 4 * d.nIni + 4);
+    nodeCapMax = std::max(nodeCapMax, d.nodeCap);
+    d.outOff = slots;
+    slots += d.nodeCap;
+    // resize tables (level l from level l-1), SURVEY.md Appendix A.2
+    if (l) {
+      const int sw = P.lv[l - 1].w, sh = P.lv[l - 1].h;
+      const double scale_x = 1. / ((double)d.w / sw), scale_y = 1. / ((double)d.h / sh);
+      d.rtabX = (int)rtab.size();
+      rtab.resize(rtab.size() + 2 * (size_t)d.w);
+      int xmax = d.w;
+      for (int dx = 0; dx < d.w; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)floorf(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+          xmax = std::min(xmax, dx);
+          if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        const short a0 = satShort(cvRoundF((1.f - fx) * 2048)), a1 = satShort(cvRoundF(fx * 2048));
+        rtab[d.rtabX + dx] = sx;
+        rtab[d.rtabX + d.w + dx] = (int32_t)(((uint32_t)(uint16_t)a1 << 16) | (uint16_t)a0);
+      }
+      d.xmax = xmax;
+      d.rtabY = (int)rtab.size();
+      rtab.resize(rtab.size() + 2 * (size_t)d.h);
+      for (int dy = 0; dy < d.h; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)floorf(fy);
+        fy -= sy;
+        const short b0 = satShort(cvRoundF((1.f - fy) * 2048)), b1 = satShort(cvRoundF(fy * 2048));
+        rtab[d.rtabY + dy] = sy;
+        rtab[d.rtabY + d.h + dy] = (int32_t)(((uint32_t)(uint16_t)b1 << 16) | (uint16_t)b0);
+      }
+    }
+  }
+  P.ncells = (int)cells.size();
+  P.keyCap = keyCap;
+  P.slotsPerImage = slots;
+  P.maxCellRows = maxRows;
+  P.maxCellCols = maxCols;
+  // octree LDS: node tables + as many keys as fit in ~150 KiB
+  const size_t nodeBytes = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, 0);
+  const size_t budget = 150 * 1024;
+  int ldsKeyCap = nodeBytes < budget ? (int)((budget - nodeBytes) / 6) : 0;
+  ldsKeyCap &= ~7;
+  if (nodeBytes + (size_t)ldsKeyCap * 6 > 160 * 1024) return ORB_EINVAL;
+
+  hipSetDevice(h->device);
+  orb_status_t st = h->dCells.ensure(cells.size() * sizeof(OrbCellDesc));
+  if (st) return st;
+  st = h->dRtab.ensure(std::max<size_t>(rtab.size(), 1) * 4);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(h->dCells.p, cells.data(), cells.size() * sizeof(OrbCellDesc),
+                         hipMemcpyHostToDevice, h->stream));
+  if (!rtab.empty())
+    HIP_TRY(hipMemcpyAsync(h->dRtab.p, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice,
+                           h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->plan = P;
+  h->cells.swap(cells);
+  h->arenaBytes = (arena + 255) & ~255LL;
+  h->maxCellsPerLevel = maxCellsPerLevel;
+  h->nodeCapMax = nodeCapMax;
+  h->ldsKeyCap = ldsKeyCap;
+  h->planW = W;
+  h->planH = H;
+  h->batchCap = 0;  // scratch layout depends on the plan
+  return ORB_OK;
+}
+
+static orb_status_t ensure_batch(orb_extractor* h, int B) {
+  if (B <= h->batchCap) return ORB_OK;
+  const OrbPlanDesc& P = h->plan;
+  const size_t cellSlots = (size_t)B * P.ncells * P.keyCap;
+  orb_status_t st;
+  if ((st = h->dArena.ensure((size_t)B * h->arenaBytes))) return st;
+  if ((st = h->dCellKeys.ensure(cellSlots * 4))) return st;
+  if ((st = h->dGKeys.ensure(cellSlots * 4))) return st;
+  if ((st = h->dGNid.ensure(cellSlots * 2))) return st;
+  if ((st = h->dCellCount.ensure((size_t)B * P.ncells * 4))) return st;
+  if ((st = h->dOutKeys.ensure((size_t)B * P.slotsPerImage * 4))) return st;
+  if ((st = h->dOutCount.ensure((size_t)B * P.nlevels * 4))) return st;
+  if ((st = h->dErr.ensure(16))) return st;
+  h->batchCap = B;
+  return ORB_OK;
+}
+
+static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, size_t stride,
+                              size_t imgPitch, orb_keypoint_t* d_kps, uint8_t* d_desc,
+                              int capacity, int32_t* d_counts, hipStream_t s) {
+  const OrbPlanDesc& P = h->plan;
+  const int32_t* rt = h->dRtab.as<int32_t>();
+  uint8_t* arena = h->dArena.as<uint8_t>();
+  const long long ap = h->arenaBytes;
+  if (h->profile) HIP_TRY(hipEventRecord(h->ev[0], s));
+  HIP_TRY(hipMemsetAsync(h->dErr.p, 0, 16, s));
+  for (int l = 1; l < P.nlevels; ++l) {
+    const OrbLevelDesc& d = P.lv[l];
+    const OrbLevelDesc& sd = P.lv[l - 1];
+    const uint8_t* src = l == 1 ? d_images : arena + sd.arenaOff;
+    const long long srcPitch = l == 1 ? (long long)imgPitch : ap;
+    const int srcStride = l == 1 ? (int)stride : sd.pitch;
+    HIP_TRY(orb_k_pyr_resize(src, srcPitch, srcStride, sd.h, arena + d.arenaOff, ap, d.pitch, d.w,
+                             d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
+                             rt + d.rtabY + d.h, d.xmax, B, s));
+  }
+  if (h->profile) HIP_TRY(hipEventRecord(h->ev[1], s));
+  HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                           h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
+                           h->dCellCount.as<int32_t>(), B, s));
+  if (h->profile) HIP_TRY(hipEventRecord(h->ev[2], s));
+  HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
+                       h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
+                       h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
+                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), B, s));
+  if (h->profile) HIP_TRY(hipEventRecord(h->ev[3], s));
+  HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                            h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(), d_kps, d_desc,
+                            capacity, d_counts, B, s));
+  if (h->profile) HIP_TRY(hipEventRecord(h->ev[4], s));
+  h->lastImg0 = d_images;
+  h->lastImg0Pitch = imgPitch;
+  h->lastImg0Stride = (int)stride;
+  return ORB_OK;
+}
+
+static void profile_collect(orb_extractor* h) {
+  if (!h->profile) return;
+  if (hipEventSynchronize(h->ev[4]) != hipSuccess) return;
+  for (int i = 0; i < 4; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]) == hipSuccess) {
+      h->stageMs[i] += ms;
+      h->stageLaunches[i] += (i == 0) ? std::max(h->nlevels - 1, 0) : 1;
+    }
+  }
+  float tot = 0.f;
+  if (hipEventElapsedTime(&tot, h->ev[0], h->ev[4]) == hipSuccess) {
+    h->stageMs[4] += tot;
+    h->stageLaunches[4] += 1;
+  }
+}
+
+extern "C" {
+
+int orb_abi_version(void) { return ORB_ABI_VERSION; }
+
+const char* orb_status_string(orb_status_t s) {
+  switch (s) {
+    case ORB_OK: return "ok";
+    case ORB_EEMPTY: return "empty input";
+    case ORB_EINVAL: return "invalid argument";
+    case ORB_ENOMEM: return "device out of memory";
+    case ORB_EDEVICE: return "HIP device error";
+    case ORB_ECAPACITY: return "buffer too small";
+    case ORB_ENODEV: return "no gfx950 device";
+  }
+  return "unknown";
+}
+
+orb_status_t orb_device_count(int* n) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  if (n) *n = c;
+  return c > 0 ? ORB_OK : ORB_ENODEV;
+}
+
+orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int ini_th_fast,
+                                  int min_th_fast, int device, orb_extractor_t** out) {
+  if (!out) return ORB_EINVAL;
+  *out = nullptr;
+  if (nfeatures < 0 || nlevels < 1 || nlevels > ORB_MAX_LEVELS || !(scale_factor > 1.0f) ||
+      nfeatures > 60000)
+    return ORB_EINVAL;
+  orb_status_t st = check_device(device);
+  if (st) return st;
+  orb_extractor* h = new orb_extractor();
+  h->device = device;
+  h->nfeatures = nfeatures;
+  h->scaleFactorF = scale_factor;
+  h->scaleFactor = (double)scale_factor;
+  h->nlevels = nlevels;
+  h->iniTh = ini_th_fast;
+  h->minTh = min_th_fast;
+  compute_tables(h);
+  hipSetDevice(device);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return ORB_EDEVICE;
+  }
+  h->ownStream = true;
+  for (int i = 0; i < 8; ++i) hipEventCreate(&h->ev[i]);
+  if (orb_k_upload_constants(h->stream) != hipSuccess ||
+      orb_k_upload_umax(h->umax, h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess) {
+    orb_extractor_destroy(h);
+    return ORB_EDEVICE;
+  }
+  *out = h;
+  return ORB_OK;
+}
+
+void orb_extractor_destroy(orb_extractor_t* h) {
+  if (!h) return;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  DevBuf* bufs[] = {&h->dCells, &h->dRtab, &h->dArena, &h->dCellKeys, &h->dCellCount,
+                    &h->dGKeys, &h->dGNid, &h->dOutKeys, &h->dOutCount, &h->dErr,
+                    &h->dImg, &h->dKps, &h->dDesc, &h->dCounts};
+  for (DevBuf* b : bufs) b->release();
+  for (int i = 0; i < 8; ++i)
+    if (h->ev[i]) hipEventDestroy(h->ev[i]);
+  if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int orb_extractor_get_levels(const orb_extractor_t* h) { return h ? h->nlevels : 0; }
+float orb_extractor_get_scale_factor(const orb_extractor_t* h) { return h ? (float)h->scaleFactor : 0.f; }
+void orb_extractor_get_scale_factors(const orb_extractor_t* h, float* o) {
+  if (h && o) std::copy(h->scale.begin(), h->scale.end(), o);
+}
+void orb_extractor_get_inverse_scale_factors(const orb_extractor_t* h, float* o) {
+  if (h && o) std::copy(h->invScale.begin(), h->invScale.end(), o);
+}
+void orb_extractor_get_scale_sigma_squares(const orb_extractor_t* h, float* o) {
+  if (h && o) std::copy(h->sigma2.begin(), h->sigma2.end(), o);
+}
+void orb_extractor_get_inverse_scale_sigma_squares(const orb_extractor_t* h, float* o) {
+  if (h && o) std::copy(h->invSigma2.begin(), h->invSigma2.end(), o);
+}
+void orb_extractor_get_features_per_level(const orb_extractor_t* h, int32_t* o) {
+  if (h && o) std::copy(h->quota.begin(), h->quota.end(), o);
+}
+
+int orb_extractor_capacity(const orb_extractor_t* hc, int width, int height) {
+  orb_extractor* h = const_cast<orb_extractor*>(hc);
+  if (!h) return -1;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (build_plan(h, width, height) != ORB_OK) return -1;
+  return h->plan.slotsPerImage;
+}
+
+void* orb_extractor_stream(orb_extractor_t* h) { return h ? (void*)h->stream : nullptr; }
+
+orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_images,
+                                         int n_images, int width, int height, size_t stride,
+                                         size_t image_pitch, orb_keypoint_t* d_keypoints,
+                                         uint8_t* d_descriptors, int capacity,
+                                         int32_t* d_counts, void* stream) {
+  if (!h || !d_images || !d_keypoints || !d_descriptors || !d_counts) return ORB_EINVAL;
+  if (n_images <= 0 || width <= 0 || height <= 0) return ORB_EEMPTY;
+  if (stride < (size_t)width || image_pitch < stride * (size_t)height) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  hipSetDevice(h->device);
+  orb_status_t st = build_plan(h, width, height);
+  if (st) return st;
+  if (capacity < h->plan.slotsPerImage) return ORB_ECAPACITY;
+  if ((st = ensure_batch(h, n_images))) return st;
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  st = run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors, capacity,
+                 d_counts, s);
+  if (st) return st;
+  h->lastW = width;
+  h->lastH = height;
+  if (h->profile && s == h->stream) profile_collect(h);
+  return ORB_OK;
+}
+
+orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int width,
+                                   int height, size_t stride, orb_keypoint_t* keypoints,
+                                   uint8_t* descriptors, int capacity, int* n_keypoints) {
+  if (!h) return ORB_EINVAL;
+  if (!image || width <= 0 || height <= 0) return ORB_EEMPTY;  // src/ORBextractor.cc:1095-1096
+  if (stride < (size_t)width || !n_keypoints) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  hipSetDevice(h->device);
+  orb_status_t st = build_plan(h, width, height);
+  if (st) return st;
+  const int cap = h->plan.slotsPerImage;
+  const size_t dstride = ((size_t)width + 63) & ~(size_t)63;
+  const size_t pitch = dstride * height;
+  if ((st = ensure_batch(h, 1))) return st;
+  if ((st = h->dImg.ensure(pitch))) return st;
+  if ((st = h->dKps.ensure((size_t)cap * sizeof(orb_keypoint_t)))) return st;
+  if ((st = h->dDesc.ensure((size_t)cap * 32))) return st;
+  if ((st = h->dCounts.ensure(16))) return st;
+  HIP_TRY(hipMemcpy2DAsync(h->dImg.p, dstride, image, stride, width, height,
+                           hipMemcpyHostToDevice, h->stream));
+  st = run_batch(h, h->dImg.as<uint8_t>(), 1, dstride, pitch, h->dKps.as<orb_keypoint_t>(),
+                 h->dDesc.as<uint8_t>(), cap, h->dCounts.as<int32_t>(), h->stream);
+  if (st) return st;
+  int32_t n = 0, err = 0;
+  HIP_TRY(hipMemcpyAsync(&n, h->dCounts.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipMemcpyAsync(&err, h->dErr.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  profile_collect(h);
+  h->lastW = width;
+  h->lastH = height;
+  if (err) {
+    if (getenv("ORB_AMD_DEBUG")) fprintf(stderr, "[orb_amd] kernel error flag %d\n", err);
+    return ORB_EDEVICE;
+  }
+  *n_keypoints = n;
+  if (n > capacity) return ORB_ECAPACITY;
+  if (n > 0) {
+    HIP_TRY(hipMemcpy(keypoints, h->dKps.p, (size_t)n * sizeof(orb_keypoint_t),
+                      hipMemcpyDeviceToHost));
+    if (descriptors)
+      HIP_TRY(hipMemcpy(descriptors, h->dDesc.p, (size_t)n * 32, hipMemcpyDeviceToHost));
+  }
+  return ORB_OK;
+}
+
+orb_status_t orb_extractor_batch_level(orb_extractor_t* h, int image, int level,
+                                       const uint8_t** d_level, int* width, int* height,
+                                       size_t* stride) {
+  if (!h || level < 0 || level >= h->nlevels || h->planW < 0 || !h->lastImg0) return ORB_EINVAL;
+  if (image < 0 || image >= h->batchCap) return ORB_EINVAL;
+  const OrbLevelDesc& d = h->plan.lv[level];
+  if (width) *width = d.w;
+  if (height) *height = d.h;
+  if (level == 0) {
+    if (d_level) *d_level = h->lastImg0 + (size_t)image * h->lastImg0Pitch;
+    if (stride) *stride = (size_t)h->lastImg0Stride;
+  } else {
+    if (d_level) *d_level = h->dArena.as<uint8_t>() + (size_t)image * h->arenaBytes + d.arenaOff;
+    if (stride) *stride = (size_t)d.pitch;
+  }
+  return ORB_OK;
+}
+
+orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t* dst,
+                                         size_t dst_stride, int* width, int* height) {
+  if (!h) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint8_t* src = nullptr;
+  int w = 0, hh = 0;
+  size_t sstride = 0;
+  orb_status_t st = orb_extractor_batch_level(h, 0, level, &src, &w, &hh, &sstride);
+  if (st) return st;
+  if (width) *width = w;
+  if (height) *height = hh;
+  if (!dst) return ORB_OK;
+  if (dst_stride < (size_t)w) return ORB_EINVAL;
+  hipSetDevice(h->device);
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy2D(dst, dst_stride, src, sstride, w, hh, hipMemcpyDeviceToHost));
+  return ORB_OK;
+}
+
+orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable) {
+  if (!h) return ORB_EINVAL;
+  h->profile = enable != 0;
+  for (int i = 0; i < 5; ++i) {
+    h->stageMs[i] = 0;
+    h->stageLaunches[i] = 0;
+  }
+  return ORB_OK;
+}
+
+orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
+                                        int* launches, const char** name) {
+  if (!h || stage < 0 || stage > 4) return ORB_EINVAL;
+  if (total_ms) *total_ms = h->stageMs[stage];
+  if (launches) *launches = h->stageLaunches[stage];
+  if (name) *name = kStageNames[stage];
+  return ORB_OK;
+}
+
+}  // extern "C"
+
+// ================================================================== matcher
+struct ProjParamsHost {  // mirrors ProjParams in matcher_kernels.hip
+  float minX, minY, invW, invH;
+  float th, nnratio;
+  int nLevels;
+  float scale[ORB_MAX_LEVELS];
+};
+
+struct orb_matcher {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
+      dNcand, dKpMatch, dNMatch, dA, dB, dOut;
+};
+
+extern "C" {
+
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+  // host-side convenience (static ORBmatcher::DescriptorDistance); the device
+  // path is orb_hamming_batch.
+  int d = 0;
+  for (int i = 0; i < 4; ++i) {
+    uint64_t x, y;
+    memcpy(&x, a + 8 * i, 8);
+    memcpy(&y, b + 8 * i, 8);
+    d += __builtin_popcountll(x ^ y);
+  }
+  return d;
+}
+
+orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
+  if (!out) return ORB_EINVAL;
+  *out = nullptr;
+  orb_status_t st = check_device(device);
+  if (st) return st;
+  if (orb_k_proj_params_size() != sizeof(ProjParamsHost)) return ORB_EINVAL;
+  orb_matcher* m = new orb_matcher();
+  m->device = device;
+  hipSetDevice(device);
+  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete m;
+    return ORB_EDEVICE;
+  }
+  *out = m;
+  return ORB_OK;
+}
+
+void orb_matcher_destroy(orb_matcher_t* m) {
+  if (!m) return;
+  hipSetDevice(m->device);
+  hipStreamSynchronize(m->stream);
+  DevBuf* bufs[] = {&m->dKeys, &m->dDesc, &m->dUr, &m->dLocked, &m->dNKeys, &m->dMps,
+                    &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
+                    &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut};
+  for (DevBuf* b : bufs) b->release();
+  hipStreamDestroy(m->stream);
+  delete m;
+}
+
+void* orb_matcher_stream(orb_matcher_t* m) { return m ? (void*)m->stream : nullptr; }
+
+orb_status_t orb_hamming_batch(orb_matcher_t* m, const uint8_t* d_a, const uint8_t* d_b, int n,
+                               int32_t* d_dist, void* stream) {
+  if (!m || n < 0 || (n > 0 && (!d_a || !d_b || !d_dist))) return ORB_EINVAL;
+  hipSetDevice(m->device);
+  HIP_TRY(orb_k_hamming(d_a, d_b, n, d_dist, stream ? (hipStream_t)stream : m->stream));
+  return ORB_OK;
+}
+
+static ProjParamsHost proj_params(float min_x, float max_x, float min_y, float max_y,
+                                  int n_levels, const float* scale, float th, float nnratio) {
+  ProjParamsHost P;
+  memset(&P, 0, sizeof(P));
+  P.minX = min_x;
+  P.minY = min_y;
+  // mfGridElementWidthInv / HeightInv, src/Frame.cc:240-241
+  P.invW = (float)ORB_GRID_COLS / (max_x - min_x);
+  P.invH = (float)ORB_GRID_ROWS / (max_y - min_y);
+  P.th = th;
+  P.nnratio = nnratio;
+  P.nLevels = n_levels;
+  for (int i = 0; i < n_levels && i < ORB_MAX_LEVELS; ++i) P.scale[i] = scale[i];
+  return P;
+}
+
+orb_status_t orb_match_projection_local_batch(
+    orb_matcher_t* m, int n_problems, const orb_keypoint_t* d_keys, const uint8_t* d_desc,
+    const int32_t* d_nkeys, const uint8_t* d_locked, int kp_stride,
+    const orb_mp_track_t* d_mps, const uint8_t* d_mp_desc, const int32_t* d_nmps,
+    int mp_stride, float min_x, float max_x, float min_y, float max_y, int n_levels,
+    const float* scale_factors, float th, float nnratio, int32_t* d_kp_match,
+    int32_t* d_nmatches, void* stream) {
+  if (!m || n_problems < 0 || kp_stride <= 0 || mp_stride < 0 || !scale_factors ||
+      n_levels <= 0 || n_levels > ORB_MAX_LEVELS || kp_stride >= (1 << 19) || !(max_x > min_x) ||
+      !(max_y > min_y))
+    return ORB_EINVAL;
+  if (n_problems == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  const ProjParamsHost P =
+      proj_params(min_x, max_x, min_y, max_y, n_levels, scale_factors, th, nnratio);
+  orb_status_t st;
+  if ((st = m->dCellStart.ensure((size_t)n_problems * (ORB_GRID_COLS * ORB_GRID_ROWS + 1) * 4)))
+    return st;
+  if ((st = m->dCellIdx.ensure((size_t)n_problems * kp_stride * 4))) return st;
+  if ((st = m->dTopk.ensure((size_t)n_problems * std::max(mp_stride, 1) * 16))) return st;
+  if ((st = m->dNcand.ensure((size_t)n_problems * std::max(mp_stride, 1) * 4))) return st;
+  HIP_TRY(orb_k_grid_build(d_keys, d_nkeys, kp_stride, P.minX, P.minY, P.invW, P.invH,
+                           m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), n_problems, s));
+  HIP_TRY(orb_k_proj_local(d_keys, d_desc, nullptr, d_locked, d_nkeys, kp_stride, d_mps,
+                           d_mp_desc, d_nmps, mp_stride, mp_stride, m->dCellStart.as<int32_t>(),
+                           m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
+                           m->dNcand.as<int32_t>(), d_kp_match, d_nmatches, n_problems, s));
+  return ORB_OK;
+}
+
+orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
+                                        const uint8_t* kp_locked, int n_mp,
+                                        const orb_mp_track_t* mps, const uint8_t* mp_desc,
+                                        float th, float nnratio, int32_t* kp_match,
+                                        int32_t* nmatches) {
+  if (!m || !F || n_mp < 0 || (n_mp > 0 && (!mps || !mp_desc)) || !kp_match || !nmatches)
+    return ORB_EINVAL;
+  if (F->n < 0 || (F->n > 0 && (!F->keys || !F->descriptors)) || !F->scale_factors ||
+      F->n_levels <= 0 || F->n_levels > ORB_MAX_LEVELS || F->n >= (1 << 19))
+    return ORB_EINVAL;
+  *nmatches = 0;
+  if (F->n == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  const int N = F->n, M = n_mp;
+  orb_status_t st;
+  if ((st = m->dKeys.ensure((size_t)N * sizeof(orb_keypoint_t)))) return st;
+  if ((st = m->dDesc.ensure((size_t)N * 32))) return st;
+  if ((st = m->dUr.ensure((size_t)N * 4))) return st;
+  if ((st = m->dLocked.ensure((size_t)N))) return st;
+  if ((st = m->dNKeys.ensure(16))) return st;
+  if ((st = m->dMps.ensure((size_t)std::max(M, 1) * sizeof(orb_mp_track_t)))) return st;
+  if ((st = m->dMpDesc.ensure((size_t)std::max(M, 1) * 32))) return st;
+  if ((st = m->dNMps.ensure(16))) return st;
+  if ((st = m->dKpMatch.ensure((size_t)N * 4))) return st;
+  if ((st = m->dNMatch.ensure(16))) return st;
+  if ((st = m->dCellStart.ensure((size_t)(ORB_GRID_COLS * ORB_GRID_ROWS + 1) * 4))) return st;
+  if ((st = m->dCellIdx.ensure((size_t)N * 4))) return st;
+  if ((st = m->dTopk.ensure((size_t)std::max(M, 1) * 16))) return st;
+  if ((st = m->dNcand.ensure((size_t)std::max(M, 1) * 4))) return st;
+  hipStream_t s = m->stream;
+  HIP_TRY(hipMemcpyAsync(m->dKeys.p, F->keys, (size_t)N * sizeof(orb_keypoint_t),
+                         hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(m->dDesc.p, F->descriptors, (size_t)N * 32, hipMemcpyHostToDevice, s));
+  if (F->u_right)
+    HIP_TRY(hipMemcpyAsync(m->dUr.p, F->u_right, (size_t)N * 4, hipMemcpyHostToDevice, s));
+  if (kp_locked)
+    HIP_TRY(hipMemcpyAsync(m->dLocked.p, kp_locked, (size_t)N, hipMemcpyHostToDevice, s));
+  const int32_t nk = N, nm = M;
+  HIP_TRY(hipMemcpyAsync(m->dNKeys.p, &nk, 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(m->dNMps.p, &nm, 4, hipMemcpyHostToDevice, s));
+  if (M > 0) {
+    HIP_TRY(hipMemcpyAsync(m->dMps.p, mps, (size_t)M * sizeof(orb_mp_track_t),
+                           hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(m->dMpDesc.p, mp_desc, (size_t)M * 32, hipMemcpyHostToDevice, s));
+  }
+  const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
+                                       F->scale_factors, th, nnratio);
+  HIP_TRY(orb_k_grid_build(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), N, P.minX,
+                           P.minY, P.invW, P.invH, m->dCellStart.as<int32_t>(),
+                           m->dCellIdx.as<int32_t>(), 1, s));
+  HIP_TRY(orb_k_proj_local(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(),
+                           F->u_right ? m->dUr.as<float>() : nullptr,
+                           kp_locked ? m->dLocked.as<uint8_t>() : nullptr,
+                           m->dNKeys.as<int32_t>(), N, m->dMps.as<orb_mp_track_t>(),
+                           m->dMpDesc.as<uint8_t>(), m->dNMps.as<int32_t>(), std::max(M, 1), M,
+                           m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
+                           m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
+                           m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), 1, s));
+  HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+// ------------------------------------------------------------ synthetic input
+void orb_synth_image(uint64_t seed, int frame, int view, int width, int height, uint8_t* out,
+                     size_t stride) {
+  orb_synth::render(seed, frame, view, width, height, out, stride);
+}
+
+void orb_synth_local_map(uint64_t seed, const orb_keypoint_t* keys, const uint8_t* desc,
+                         int n_kp, int n_mp, int width, int height, orb_mp_track_t* mps,
+                         uint8_t* mp_desc, uint8_t* kp_locked) {
+  orb_synth::local_map(seed, keys, desc, n_kp, n_mp, width, height, mps, mp_desc, kp_locked);
+}
+
+}  // extern "C"

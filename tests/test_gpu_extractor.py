@@ -1,0 +1,150 @@
+"""GPU extractor parity: the HIP ORBextractor must reproduce the CPU oracle
+bit-for-bit (keypoints: all 7 cv::KeyPoint fields and their order;
+descriptors: all 256 bits) -- SURVEY.md §8(d) C2/C3/C5 shapes."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [
+    # (width, height, nfeatures, seed)  -- C2 TUM-shaped, C1/C4 KITTI-shaped, C3, C5
+    (640, 480, 1000, 1),
+    (640, 480, 1000, 2),
+    (640, 480, 1000, 3),
+    (1241, 376, 1000, 0),
+    (1241, 376, 2000, 7),
+    (1920, 1080, 4000, 5),
+]
+
+
+def _diff_report(k_gpu, d_gpu, k_ref, d_ref):
+    lines = [f"n gpu={len(k_gpu)} ref={len(k_ref)}"]
+    for lvl in range(8):
+        g = k_gpu[k_gpu["octave"] == lvl]
+        r = k_ref[k_ref["octave"] == lvl]
+        same = len(g) == len(r) and (g.tobytes() == r.tobytes())
+        if not same:
+            gs = set(zip(g["x"].tolist(), g["y"].tolist()))
+            rs = set(zip(r["x"].tolist(), r["y"].tolist()))
+            lines.append(f" level {lvl}: gpu {len(g)} ref {len(r)} only_gpu {len(gs - rs)} only_ref {len(rs - gs)}")
+            n = min(len(g), len(r))
+            for f in ("x", "y", "response", "angle", "size"):
+                bad = np.nonzero(g[f][:n] != r[f][:n])[0]
+                if len(bad):
+                    i = bad[0]
+                    lines.append(f"   field {f}: {len(bad)} diffs, first at {i}: gpu {g[i]} ref {r[i]}")
+    n = min(len(d_gpu), len(d_ref))
+    bad = np.nonzero((d_gpu[:n] != d_ref[:n]).any(1))[0]
+    lines.append(f" descriptor rows differing: {len(bad)}")
+    return "\n".join(lines)
+
+
+@pytest.mark.parametrize("w,h,nf,seed", CONFIGS)
+def test_extract_bit_exact(gpu, oracle, w, h, nf, seed):
+    img = gpu.synth_image(seed, 0, w, h)
+    ext = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    k_gpu, d_gpu = ext(img)
+    k_ref, d_ref, _ = oracle.extract(img, nf, 1.2, 8, 20, 7)
+    ok = len(k_gpu) == len(k_ref) and k_gpu.tobytes() == k_ref.tobytes() and \
+        d_gpu.tobytes() == d_ref.tobytes()
+    assert ok, _diff_report(k_gpu, d_gpu, k_ref, d_ref)
+
+
+@pytest.mark.parametrize("w,h", [(640, 480), (1241, 376), (1920, 1080)])
+def test_pyramid_bit_exact(gpu, oracle, w, h):
+    img = gpu.synth_image(11, 0, w, h)
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    ext(img)
+    pyr = ext.mvImagePyramid
+    ref = oracle.pyramid(img)
+    for l, (a, b) in enumerate(zip(pyr, ref)):
+        assert a.shape == b.shape, (l, a.shape, b.shape)
+        assert np.array_equal(a, b), f"level {l}: {(a != b).sum()} pixels differ"
+
+
+def test_accessors_match_reference_tables(gpu, oracle):
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    p = oracle.params(1000, 1.2, 8)
+    assert ext.GetLevels() == 8
+    assert np.float32(ext.GetScaleFactor()) == np.float32(1.2)
+    assert np.array_equal(np.float32(ext.GetScaleFactors()), p["scale"])
+    assert np.array_equal(np.float32(ext.GetInverseScaleFactors()), p["inv_scale"])
+    assert np.array_equal(np.float32(ext.GetScaleSigmaSquares()), p["sigma2"])
+    assert np.array_equal(np.float32(ext.GetInverseScaleSigmaSquares()), p["inv_sigma2"])
+    assert ext.features_per_level() == p["quota"].tolist()
+
+
+def test_empty_and_invalid(gpu):
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    assert ext(np.zeros((0, 0), np.uint8)) == (None, None)  # src/ORBextractor.cc:1095-1096
+    with pytest.raises(gpu.OrbError):
+        ext(np.zeros((480, 640), np.float32))  # non-8UC1: reference asserts (:1100)
+    with pytest.raises(gpu.OrbError):
+        ext(np.zeros((30, 30), np.uint8))  # too small for an 8-level ORB pyramid
+
+
+def test_flat_image_has_no_keypoints(gpu, oracle):
+    img = np.full((480, 640), 128, np.uint8)
+    k, d = gpu.ORBextractor(1000, 1.2, 8, 20, 7)(img)
+    kr, dr, _ = oracle.extract(img)
+    assert len(k) == 0 and len(kr) == 0 and d.shape == (0, 32)
+
+
+def test_noise_image_heavy_candidates(gpu, oracle):
+    """Uniform noise: every cell is dense with FAST corners, exercising the
+    octree's global-memory key path and the deepest final-phase splits."""
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (480, 640), dtype=np.uint8)
+    k_gpu, d_gpu = gpu.ORBextractor(1000, 1.2, 8, 20, 7)(img)
+    k_ref, d_ref, _ = oracle.extract(img)
+    assert k_gpu.tobytes() == k_ref.tobytes(), _diff_report(k_gpu, d_gpu, k_ref, d_ref)
+    assert d_gpu.tobytes() == d_ref.tobytes()
+
+
+def test_low_contrast_fallback_threshold(gpu, oracle):
+    """Low-contrast image: most cells find nothing at iniThFAST=20 and fall back
+    to minThFAST=7 (src/ORBextractor.cc:846-850)."""
+    rng = np.random.default_rng(4)
+    base = gpu.synth_image(9, 0, 640, 480).astype(np.int32)
+    img = (128 + (base - 128) // 12 + rng.integers(-3, 4, base.shape)).clip(0, 255).astype(np.uint8)
+    k_gpu, d_gpu = gpu.ORBextractor(1000, 1.2, 8, 20, 7)(img)
+    k_ref, d_ref, _ = oracle.extract(img)
+    assert k_gpu.tobytes() == k_ref.tobytes(), _diff_report(k_gpu, d_gpu, k_ref, d_ref)
+    assert d_gpu.tobytes() == d_ref.tobytes()
+
+
+def test_strided_input(gpu):
+    img = gpu.synth_image(2, 0, 640, 480)
+    wide = np.zeros((480, 704), np.uint8)
+    wide[:, :640] = img
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    k1, d1 = ext(img)
+    k2, d2 = ext(wide[:, :640])
+    assert k1.tobytes() == k2.tobytes() and d1.tobytes() == d2.tobytes()
+
+
+def test_batch_matches_single(gpu):
+    torch = pytest.importorskip("torch")
+    w, h, nf, B = 1241, 376, 1000, 5
+    ext = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    imgs = np.stack([gpu.synth_image(20, f, w, h) for f in range(B)])
+    cap = ext.capacity(w, h)
+    d_img = torch.from_numpy(imgs).cuda()
+    d_kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ext.extract_batch(d_img.data_ptr(), B, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(),
+                      cap, d_cnt.data_ptr())
+    torch.cuda.synchronize()
+    import ctypes
+    ctypes.CDLL(None)
+    gpu.lib()  # keep library loaded
+    kps = d_kps.cpu().numpy().view(gpu.KEYPOINT_DTYPE).reshape(B, cap)
+    desc = d_desc.cpu().numpy()
+    cnt = d_cnt.cpu().numpy()
+    for f in range(B):
+        k1, d1 = ext(imgs[f])
+        assert cnt[f] == len(k1)
+        assert kps[f, : cnt[f]].tobytes() == k1.tobytes()
+        assert desc[f, : cnt[f]].tobytes() == d1.tobytes()
