@@ -718,7 +718,7 @@ static int search_by_projection_local(const orb_frame_t* F, const uint8_t* kp_lo
     const orb_mp_track_t& mp = mps[m];
     if (!mp.in_view || mp.bad) continue;
     const int lvl = mp.level;
-    float r = mp.view_cos > 0.998f ? 2.5f : 4.0f;
+    float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;  // float vs double literal (:137)
     if (bFactor) r *= th;
     const float rs = r * F->scale_factors[lvl];
     features_in_area(g, F->keys, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl, idxs);

@@ -68,6 +68,14 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not LIB_PATH.exists():
         raise OrbError(ORB_ENODEV, f"{LIB_PATH} not built (run __graft_entry__.build())")
+    # One HIP runtime per process: torch-ROCm ships its own libamdhip64 (soname
+    # libamdhip64.so.7).  Loading torch first lets liborb_amd.so's DT_NEEDED on
+    # libamdhip64.so.7 bind to that same copy, so device pointers and streams
+    # can be shared with torch (plumbing for device memory / torch.distributed).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(str(LIB_PATH))
     vp, i32, f32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
     sig = {

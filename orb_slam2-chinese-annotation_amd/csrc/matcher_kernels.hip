@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void k_proj_candidates(
     return;
   }
   const int lvl = mp.level;
-  float r = mp.view_cos > 0.998f ? 2.5f : 4.0f;  // RadiusByViewingCos (:135-141)
+  float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:135-141)
   if (P.th != 1.0f) r *= P.th;
   const float rs = r * P.scale[lvl];
   const orb_keypoint_t* K = keys + (size_t)p * kpStride;
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(
       if (lane == 0) {
         const orb_mp_track_t mp = mps[mg];
         const int lvl = mp.level;
-        float r = mp.view_cos > 0.998f ? 2.5f : 4.0f;
+        float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;
         if (P.th != 1.0f) r *= P.th;
         const float rs = r * P.scale[lvl];
         const orb_keypoint_t* K = keys + (size_t)p * kpStride;

@@ -137,9 +137,6 @@ def test_batch_matches_single(gpu):
     ext.extract_batch(d_img.data_ptr(), B, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(),
                       cap, d_cnt.data_ptr())
     torch.cuda.synchronize()
-    import ctypes
-    ctypes.CDLL(None)
-    gpu.lib()  # keep library loaded
     kps = d_kps.cpu().numpy().view(gpu.KEYPOINT_DTYPE).reshape(B, cap)
     desc = d_desc.cpu().numpy()
     cnt = d_cnt.cpu().numpy()
