@@ -121,8 +121,12 @@ orb_status_t orb_extractor_batch_level(orb_extractor_t* h, int image, int level,
 /* Stream the handle launches on (a hipStream_t). */
 void* orb_extractor_stream(orb_extractor_t* h);
 
-/* Timing of the most expensive kernel of the last batch (HIP events on the
- * handle stream): average milliseconds per launch and the kernel's name. */
+/* Kernel timing with HIP events recorded on the stream each stage is launched
+ * on (no synchronisation in the launch path).  profile(h, 1) resets and
+ * enables; profile_read drains the recorded events and returns the summed
+ * milliseconds, launch count and kernel name of `stage`:
+ * 0 k_pyr_resize (nlevels-1 launches per call), 1 k_blur_levels, 2 k_fast_cells,
+ * 3 k_octree, 4 k_orient_desc, 5 = the whole extraction call. */
 orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable);
 orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
                                         int* launches, const char** name);
@@ -156,6 +160,11 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
 orb_status_t orb_matcher_create(int device, orb_matcher_t** out);
 void orb_matcher_destroy(orb_matcher_t* m);
 void* orb_matcher_stream(orb_matcher_t* m);
+/* Same scheme for the batched local-map matcher: stage 0 k_grid_build,
+ * 1 k_proj_candidates, 2 k_proj_resolve, 3 = whole call. */
+orb_status_t orb_matcher_profile(orb_matcher_t* m, int enable);
+orb_status_t orb_matcher_profile_read(orb_matcher_t* m, int stage, double* total_ms,
+                                      int* launches, const char** name);
 
 /* dist[i] = DescriptorDistance(a + 32 i, b + 32 i), device pointers. */
 orb_status_t orb_hamming_batch(orb_matcher_t* m, const uint8_t* d_a, const uint8_t* d_b,

@@ -103,6 +103,8 @@ def lib() -> ctypes.CDLL:
         "orb_matcher_create": (i32, [i32, vp]),
         "orb_matcher_destroy": (None, [vp]),
         "orb_matcher_stream": (vp, [vp]),
+        "orb_matcher_profile": (i32, [vp, i32]),
+        "orb_matcher_profile_read": (i32, [vp, i32, vp, vp, vp]),
         "orb_hamming_batch": (i32, [vp, vp, vp, i32, vp, vp]),
         "orb_match_projection_local": (i32, [vp, vp, vp, i32, vp, vp, f32, f32, vp, vp]),
         "orb_match_projection_local_batch": (
@@ -336,6 +338,32 @@ class ORBmatcher:
         a = np.ascontiguousarray(a, np.uint8)
         b = np.ascontiguousarray(b, np.uint8)
         return lib().orb_descriptor_distance(_ptr(a), _ptr(b))
+
+    def profile(self, enable: bool = True):
+        _check(lib().orb_matcher_profile(self._h, int(enable)), "profile")
+
+    def profile_read(self, stage: int):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int(0)
+        name = ctypes.c_char_p()
+        _check(lib().orb_matcher_profile_read(self._h, stage, ctypes.byref(ms), ctypes.byref(n),
+                                              ctypes.byref(name)), "profile_read")
+        return name.value.decode(), ms.value, n.value
+
+    def stream(self) -> int:
+        return lib().orb_matcher_stream(self._h) or 0
+
+    def search_by_projection_batch(self, n_problems, d_keys, d_desc, d_nkeys, d_locked, kp_stride,
+                                   d_mps, d_mp_desc, d_nmps, mp_stride, width, height,
+                                   scale_factors, th, d_kp_match, d_nmatches, stream: int = 0,
+                                   min_x=0.0, min_y=0.0):
+        """Device-batched SearchByProjection(F, localMap, th) over P problems."""
+        sc = np.ascontiguousarray(scale_factors, np.float32)
+        _check(lib().orb_match_projection_local_batch(
+            self._h, n_problems, d_keys, d_desc, d_nkeys, d_locked or None, kp_stride, d_mps,
+            d_mp_desc, d_nmps, mp_stride, min_x, float(width), min_y, float(height), len(sc),
+            _ptr(sc), th, self.mfNNratio, d_kp_match, d_nmatches, stream or None),
+            "orb_match_projection_local_batch")
 
     def hamming_batch(self, d_a: int, d_b: int, n: int, d_out: int, stream: int = 0):
         _check(lib().orb_hamming_batch(self._h, d_a, d_b, n, d_out, stream or None), "hamming")

@@ -24,30 +24,43 @@
 __global__ __launch_bounds__(256) void k_pyr_resize(
     const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sh,
     uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
-    const int* __restrict__ xofs, const short2* __restrict__ alpha,
-    const int* __restrict__ yofs, const short2* __restrict__ beta, int xmax) {
-  const int dx = blockIdx.x * 64 + threadIdx.x;
+    const int* __restrict__ xofs, const int* __restrict__ alpha,
+    const int* __restrict__ yofs, const int* __restrict__ beta, int xmax) {
+  // 4 consecutive output pixels per thread; blocks of 64 x 4 threads cover 256 x 4.
+  // alpha/beta entries pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
+  const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
   const int dy = blockIdx.y * 4 + threadIdx.y;
-  if (dx >= dw || dy >= dh) return;
+  if (dx0 >= dw || dy >= dh) return;
   const uint8_t* S = src + (long long)blockIdx.z * srcImgPitch;
   const int sy = yofs[dy];
+  const int bw = beta[dy];
+  const int b0 = (int)(short)(bw & 0xFFFF), b1 = bw >> 16;
   const int r0 = min(max(sy, 0), sh - 1), r1 = min(max(sy + 1, 0), sh - 1);
   const uint8_t* p0 = S + (long long)r0 * srcStride;
   const uint8_t* p1 = S + (long long)r1 * srcStride;
-  const int sx = xofs[dx];
-  int h0, h1;
-  if (dx < xmax) {
-    const short2 a = alpha[dx];
-    h0 = p0[sx] * a.x + p0[sx + 1] * a.y;
-    h1 = p1[sx] * a.x + p1[sx + 1] * a.y;
-  } else {
-    h0 = p0[sx] * 2048;
-    h1 = p1[sx] * 2048;
+  uint32_t packed = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int dx = min(dx0 + j, dw - 1);
+    const int sx = xofs[dx];
+    const int aw = alpha[dx];
+    const int a0 = (int)(short)(aw & 0xFFFF), a1 = aw >> 16;
+    const int sx1 = dx < xmax ? sx + 1 : sx;
+    const int h0 = dx < xmax ? p0[sx] * a0 + p0[sx1] * a1 : p0[sx] * 2048;
+    const int h1 = dx < xmax ? p1[sx] * a0 + p1[sx1] * a1 : p1[sx] * 2048;
+    int v = min(max((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 0), 255);
+    // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
+    // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
+    // undefined upper half (observed miscompile on gfx950)
+    __asm__ volatile("" : "+v"(v));
+    packed |= (uint32_t)v << (8 * j);
   }
-  const short2 b = beta[dy];
-  const int v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
-  dst[(long long)blockIdx.z * dstImgPitch + (long long)dy * dstStride + dx] =
-      (uint8_t)min(max(v, 0), 255);
+  uint8_t* out = dst + (long long)blockIdx.z * dstImgPitch + (long long)dy * dstStride + dx0;
+  if (dx0 + 4 <= dw) {
+    *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 64 == 0, dx0 % 4 == 0
+  } else {
+    for (int j = 0; dx0 + j < dw; ++j) out[j] = (uint8_t)(packed >> (8 * j));
+  }
 }
 
 // ============================================================ k_fast_cells
@@ -56,46 +69,34 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
 // min over its 9 pixels of |I(p) - I(q)| on the matching side.  FAST(t) detects
 // the pixel iff m > t, and for a detected corner OpenCV's cornerScore<16> is
 // m - 1 whatever t is.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
   const int v = c[0];
-  int d[16];
-  d[0] = v - c[3 * p];
-  d[1] = v - c[3 * p + 1];
-  d[2] = v - c[2 * p + 2];
-  d[3] = v - c[p + 3];
-  d[4] = v - c[3];
-  d[5] = v - c[-p + 3];
-  d[6] = v - c[-2 * p + 2];
-  d[7] = v - c[-3 * p + 1];
-  d[8] = v - c[-3 * p];
-  d[9] = v - c[-3 * p - 1];
-  d[10] = v - c[-2 * p - 2];
-  d[11] = v - c[-p - 3];
-  d[12] = v - c[-3];
-  d[13] = v - c[p - 3];
-  d[14] = v - c[2 * p - 2];
-  d[15] = v - c[3 * p - 1];
-  int mn2[16], mx2[16];
+  const int off[16] = {3 * p,      3 * p + 1,  2 * p + 2,  p + 3,       3,  -p + 3,
+                       -2 * p + 2, -3 * p + 1, -3 * p,     -3 * p - 1, -2 * p - 2, -p - 3,
+                       -3,         p - 3,      2 * p - 2,  3 * p - 1};
+  // lane .x carries d = v - ring (dark side), .y carries -d (bright side): one
+  // packed 16-bit min/max handles both arcs at once (v_pk_min_i16 / v_pk_max_i16)
+  s16x2 q[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    mn2[k] = min(d[k], d[(k + 1) & 15]);
-    mx2[k] = max(d[k], d[(k + 1) & 15]);
+    const int d = v - (int)c[off[k]];
+    q[k] = s16x2{(short)d, (short)(-d)};
   }
-  int mn4[16], mx4[16];
+  s16x2 m2[16], m4[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m2[k] = __builtin_elementwise_min(q[k], q[(k + 1) & 15]);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+  s16x2 best = s16x2{(short)-1024, (short)-1024};
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    const s16x2 a9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]),
+                                               q[(k + 8) & 15]);
+    best = __builtin_elementwise_max(best, a9);
   }
-  int dark = -1024, brightNeg = 1024;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int a9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-    const int b9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-    dark = max(dark, a9);
-    brightNeg = min(brightNeg, b9);
-  }
-  return max(dark, -brightNeg);
+  return max((int)best.x, (int)best.y);
 }
 
 // One workgroup per (cell, image).  Output: the cell's keypoints (row-major in
@@ -128,16 +129,33 @@ __global__ __launch_bounds__(256) void k_fast_cells(
   }
   uint8_t* roi = smem;  // rows x cols
   const int dh = rows - 6, dw = cols - 6, sp = dw + 2;
-  uint8_t* sc = smem + ((rows * cols + 15) & ~15);  // (dh+2) x (dw+2), zero border
-  for (int i = tid; i < rows * cols; i += 256) {
-    const int y = i / cols, x = i - y * cols;
-    roi[i] = lvl[(long long)(cd.y0 + y) * pitch + cd.x0 + x];
+  uint8_t* sc = smem + ((rows * cols + 15) & ~15);           // (dh+2) x (dw+2), zero border
+  uint8_t* flags = sc + (((dh + 2) * sp + 15) & ~15);        // dh x dw survivors
+  {
+    // all loads in flight before the LDS stores; ROI <= 2048 px (host-checked)
+    const int n = rows * cols;
+    const float invCols = 1.0f / (float)cols;
+    uint8_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = tid + 256 * q;
+      if (i < n) {
+        const int r = (int)(((float)i + 0.5f) * invCols), c = i - r * cols;
+        v[q] = lvl[(long long)(cd.y0 + r) * pitch + cd.x0 + c];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = tid + 256 * q;
+      if (i < n) roi[i] = v[q];
+    }
   }
   for (int i = tid; i < (dh + 2) * sp; i += 256) sc[i] = 0;
   __syncthreads();
   const int npix = dh * dw;
+  const float invDw = 1.0f / (float)dw;
   for (int i = tid; i < npix; i += 256) {
-    const int y = i / dw, x = i - y * dw;
+    const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
     const int s = fast_score(roi + (y + 3) * cols + (x + 3), cols);
     sc[(y + 1) * sp + (x + 1)] = (uint8_t)min(max(s, 0), 255);
   }
@@ -147,32 +165,32 @@ __global__ __launch_bounds__(256) void k_fast_cells(
   // a corner survives iff its score beats all 8 stored neighbour scores.
   const int per = (npix + 255) >> 8;
   const int beg = min(tid * per, npix), end = min(beg + per, npix);
-  auto survives = [&](int i, int t) -> bool {
-    const int y = i / dw, x = i - y * dw;
+  auto survives = [&](int i, int t) -> int {
+    const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
     const uint8_t* c = sc + (y + 1) * sp + (x + 1);
     const int m = c[0];
-    if (m <= t || m < 2) return false;  // not a corner, or score 0 cannot beat a 0 neighbour
+    if (m <= t || m < 2) return 0;  // not a corner, or score 0 cannot beat a 0 neighbour
     const int nb[8] = {c[-sp - 1], c[-sp], c[-sp + 1], c[-1], c[1], c[sp - 1], c[sp], c[sp + 1]};
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      if (nb[k] > t && nb[k] >= m) return false;
-    return true;
+      if (nb[k] > t && nb[k] >= m) return 0;
+    return 1;
   };
   int t = min(max(plan.iniTh, 0), 255);
   int mine = 0;
-  for (int i = beg; i < end; ++i) mine += survives(i, t);
+  for (int i = beg; i < end; ++i) mine += (flags[i] = (uint8_t)survives(i, t));
   int total;
   int off = block_excl_scan(mine, scanTmp, &total);
   if (total == 0) {  // src/ORBextractor.cc:846-850: retry the cell at minThFAST
     t = min(max(plan.minTh, 0), 255);
     mine = 0;
-    for (int i = beg; i < end; ++i) mine += survives(i, t);
+    for (int i = beg; i < end; ++i) mine += (flags[i] = (uint8_t)survives(i, t));
     off = block_excl_scan(mine, scanTmp, &total);
   }
   uint32_t* out = cellKeys + slot * plan.keyCap;
   for (int i = beg; i < end && mine; ++i) {
-    if (survives(i, t)) {
-      const int y = i / dw, x = i - y * dw;
+    if (flags[i]) {
+      const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
       out[off++] = pack_key(cd.x0 + 3 + x, cd.y0 + 3 + y, sc[(y + 1) * sp + (x + 1)] - 1);
     }
   }
@@ -513,12 +531,14 @@ __global__ __launch_bounds__(512) void k_octree(
   if (t == 0) outCount[img * plan.nlevels + l] = alive;
 }
 
-// =========================================================== k_orient_desc
+// ============================================================ k_blur_levels
+// GaussianBlur(level, 7x7, sigma 2, BORDER_REFLECT_101) of every level of every
+// image (src/ORBextractor.cc:1143-1145), 8U integer kernel [18,34,49,55,49,34,18]
+// (SURVEY.md Appendix A.3).  One workgroup per 64x16 output tile (tiles of all
+// levels flattened into one launch); the 70x22 source tile with reflect-101
+// borders is staged in LDS, the row pass is kept as exact u16 sums.
 __constant__ int8_t c_pattern[2 * ORB_PATTERN_POINTS];
 __constant__ int c_umax[16];
-
-#define DESC_TILE 43  // 2 * (18 sample radius + 3 blur radius) + 1
-#define DESC_PITCH 44
 
 __device__ __forceinline__ int reflect101(int i, int n) {
   if (n == 1) return 0;
@@ -529,30 +549,91 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i;
 }
 
-// GaussianBlur 7x7 sigma 2 (8U, integer kernel) of the
-// level evaluated at one tile position; the tile already holds reflect-101
-// extended pixels, so this equals the full-level blur at that pixel.
-__device__ __forceinline__ int blur7_at(const uint8_t* tile, int ty, int tx) {
-  const int k[7] = {18, 34, 49, 55, 49, 34, 18};
-  int acc = 0;
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const uint8_t* r = tile + (ty + j - 3) * DESC_PITCH + tx - 3;
-    const int rs = k[0] * r[0] + k[1] * r[1] + k[2] * r[2] + k[3] * r[3] + k[4] * r[4] +
-                   k[5] * r[5] + k[6] * r[6];
-    acc += k[j] * rs;
-  }
-  return min((acc + (1 << 15)) >> 16, 255);
-}
+#define BLUR_SW (ORB_BLUR_TW + 6)
+#define BLUR_SH (ORB_BLUR_TH + 6)
 
-// One wave per keypoint.  slot -> (level, index) through plan.lv[].outOff.
-__global__ __launch_bounds__(256) void k_orient_desc(
+__global__ __launch_bounds__(256) void k_blur_levels(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
-    const uint32_t* __restrict__ outKeys, const int32_t* __restrict__ outCount,
-    orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc, int capacity,
-    int32_t* __restrict__ counts) {
-  __shared__ __attribute__((aligned(16))) uint8_t tiles[4][DESC_TILE * DESC_PITCH];
+    const OrbTileDesc* __restrict__ tiles, uint8_t* __restrict__ blur, long long blurPitch) {
+  __shared__ uint8_t raw[BLUR_SH][BLUR_SW + 2];
+  __shared__ uint16_t rowp[BLUR_SH][ORB_BLUR_TW];
+  const int tid = threadIdx.x, img = blockIdx.y;
+  const OrbTileDesc td = tiles[blockIdx.x];
+  const int l = td.level;
+  const OrbLevelDesc& L = plan.lv[l];
+  const uint8_t* lvl;
+  int pitch;
+  if (l == 0) {
+    lvl = img0 + (long long)img * img0Pitch;
+    pitch = img0Stride;
+  } else {
+    lvl = arena + (long long)img * arenaPitch + L.arenaOff;
+    pitch = L.pitch;
+  }
+  const bool interior = td.x0 >= 3 && td.y0 >= 3 && td.x0 + ORB_BLUR_TW + 3 <= L.w &&
+                        td.y0 + ORB_BLUR_TH + 3 <= L.h;
+  // issue every global load of the tile before the first LDS store (one memory
+  // latency per workgroup instead of one per loop trip)
+  constexpr int kSlots = (BLUR_SH * BLUR_SW + 255) / 256;
+  uint8_t v[kSlots];
+#pragma unroll
+  for (int q = 0; q < kSlots; ++q) {
+    const int i = tid + 256 * q;
+    if (i < BLUR_SH * BLUR_SW) {
+      const int r = i / BLUR_SW, c = i - r * BLUR_SW;
+      int y = td.y0 - 3 + r, x = td.x0 - 3 + c;
+      if (!interior) {
+        y = reflect101(y, L.h);
+        x = reflect101(x, L.w);
+      }
+      v[q] = lvl[(long long)y * pitch + x];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kSlots; ++q) {
+    const int i = tid + 256 * q;
+    if (i < BLUR_SH * BLUR_SW) {
+      const int r = i / BLUR_SW, c = i - r * BLUR_SW;
+      raw[r][c] = v[q];
+    }
+  }
+  __syncthreads();
+  const int k[7] = {18, 34, 49, 55, 49, 34, 18};
+  for (int i = tid; i < BLUR_SH * ORB_BLUR_TW; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    const uint8_t* p = &raw[r][c];
+    rowp[r][c] = (uint16_t)(k[0] * p[0] + k[1] * p[1] + k[2] * p[2] + k[3] * p[3] + k[4] * p[4] +
+                            k[5] * p[5] + k[6] * p[6]);
+  }
+  __syncthreads();
+  const int c = tid & 63;
+  const int x = td.x0 + c;
+  uint8_t* dst = blur + (long long)img * blurPitch + L.blurOff;
+#pragma unroll
+  for (int rr = 0; rr < ORB_BLUR_TH / 4; ++rr) {
+    const int r = (tid >> 6) + 4 * rr;
+    const int y = td.y0 + r;
+    int acc = 0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) acc += k[j] * (int)rowp[r + j][c];
+    if (x < L.w && y < L.h) dst[(long long)y * L.blurPitch + x] = (uint8_t)min((acc + (1 << 15)) >> 16, 255);
+  }
+}
+
+// =========================================================== k_orient_desc
+// One wave per keypoint.  slot -> (level, index) through plan.lv[].outOff.
+//   IC_Angle (src/ORBextractor.cc:77-113) on the un-blurred level: lanes 0-30
+//   take column u = lane-15 of the centre row and the rows below (+v), lanes
+//   32-62 the rows above (-v); integer moments reduced across the wave.
+//   rBRIEF (:119-164) on the blurred level: lane L evaluates tests L, L+64,
+//   L+128, L+192; one ballot per group of 64 tests is 8 descriptor bytes.
+__global__ __launch_bounds__(256) void k_orient_desc(
+    const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
+    const uint8_t* __restrict__ arena, long long arenaPitch, const uint8_t* __restrict__ blur,
+    long long blurPitch, OrbPlanDesc plan, const uint32_t* __restrict__ outKeys,
+    const int32_t* __restrict__ outCount, orb_keypoint_t* __restrict__ kps,
+    uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int img = blockIdx.y;
   const int slot = blockIdx.x * 4 + w;
@@ -581,34 +662,29 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     lvl = arena + (long long)img * arenaPitch + L.arenaOff;
     pitch = L.pitch;
   }
-  uint8_t* tile = tiles[w];
-  for (int e = lane; e < DESC_TILE * DESC_TILE; e += 64) {
-    const int ty = e / DESC_TILE, tx = e - ty * DESC_TILE;
-    const int yy = reflect101(cy - 21 + ty, L.h), xx = reflect101(cx - 21 + tx, L.w);
-    tile[ty * DESC_PITCH + tx] = lvl[(long long)yy * pitch + xx];
-  }
-  // the tile is private to this wave: a wave-scope fence orders the LDS stores
-  // before other lanes' loads (no block barrier: sibling waves may have exited)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // ---- IC_Angle on the un-blurred level (src/ORBextractor.cc:77-113)
+  // ---- IC_Angle
   int m01 = 0, m10 = 0;
-  if (lane < 31) {
-    const int u = lane - 15;
-    const uint8_t* c = tile + 21 * DESC_PITCH + 21;
-    m10 += u * c[u];
-    for (int v = 1; v <= 15; ++v) {
-      if (u < -c_umax[v] || u > c_umax[v]) continue;
-      const int plus = c[u + v * DESC_PITCH], minus = c[u - v * DESC_PITCH];
-      m01 += v * (plus - minus);
-      m10 += u * (plus + minus);
+  {
+    const int col = lane & 31, below = lane < 32;
+    if (col < 31) {
+      const int u = col - 15;
+      const uint8_t* c = lvl + (long long)cy * pitch + cx + u;
+      const int step = below ? pitch : -pitch;
+      if (below) m10 += u * c[0];
+      int vals[15];
+#pragma unroll
+      for (int v = 1; v <= 15; ++v) vals[v - 1] = (u >= -c_umax[v] && u <= c_umax[v]) ? c[v * step] : 0;
+#pragma unroll
+      for (int v = 1; v <= 15; ++v) {
+        m01 += (below ? v : -v) * vals[v - 1];
+        m10 += u * vals[v - 1];
+      }
     }
   }
   m01 = wave_sum(m01);
   m10 = wave_sum(m10);
   const float angle = fast_atan2_deg((float)m01, (float)m10);
-  // ---- rBRIEF on the blurred level (src/ORBextractor.cc:119-164)
+  // ---- rBRIEF on the blurred level
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float a, b;
   {
@@ -617,21 +693,20 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     a = c;
     b = s;
   }
-  unsigned long long words[4];
+  const uint8_t* bc = blur + (long long)img * blurPitch + L.blurOff + (long long)cy * L.blurPitch + cx;
+  const int bp = L.blurPitch;
+  int v0[4], v1[4];
 #pragma unroll
   for (int kq = 0; kq < 4; ++kq) {
     const int test = lane + 64 * kq;
-    int val[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float px = (float)c_pattern[2 * (2 * test + h)];
-      const float py = (float)c_pattern[2 * (2 * test + h) + 1];
-      const int dy = cv_round(px * b + py * a);
-      const int dx = cv_round(px * a - py * b);
-      val[h] = blur7_at(tile, 21 + dy, 21 + dx);
-    }
-    words[kq] = __ballot(val[0] < val[1]);
+    const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
+    const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
+    v0[kq] = bc[cv_round(px0 * b + py0 * a) * bp + cv_round(px0 * a - py0 * b)];
+    v1[kq] = bc[cv_round(px1 * b + py1 * a) * bp + cv_round(px1 * a - py1 * b)];
   }
+  unsigned long long words[4];
+#pragma unroll
+  for (int kq = 0; kq < 4; ++kq) words[kq] = __ballot(v0[kq] < v1[kq]);
   const long long o = (long long)img * capacity + base + i;
   if (lane == 0) {
     ulonglong4 d;
@@ -673,10 +748,10 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             uint8_t* dst, long long dstImgPitch, int dstStride, int dw, int dh,
                             const int* xofs, const void* alpha, const int* yofs, const void* beta,
                             int xmax, int nimg, hipStream_t s) {
-  dim3 grid((dw + 63) / 64, (dh + 3) / 4, nimg), block(64, 4);
+  dim3 grid((dw + 255) / 256, (dh + 3) / 4, nimg), block(64, 4);
   hipLaunchKernelGGL(k_pyr_resize, grid, block, 0, s, src, srcImgPitch, srcStride, sh, dst,
-                     dstImgPitch, dstStride, dw, dh, xofs, (const short2*)alpha, yofs,
-                     (const short2*)beta, xmax);
+                     dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,
+                     (const int*)beta, xmax);
   return hipGetLastError();
 }
 
@@ -685,7 +760,8 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
                             int nimg, hipStream_t s) {
   const int rows = plan->maxCellRows, cols = plan->maxCellCols;
-  const size_t lds = (size_t)((rows * cols + 15) & ~15) + (size_t)(rows - 4) * (cols - 4);
+  const size_t lds = (size_t)((rows * cols + 15) & ~15) + (size_t)(((rows - 4) * (cols - 4) + 15) & ~15) +
+                     (size_t)(rows - 6) * (cols - 6);
   dim3 grid(plan->ncells, nimg), block(256);
   hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, *plan, cells, cellKeys, cellCount);
@@ -721,14 +797,26 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
   return hipGetLastError();
 }
 
-hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
+hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0Stride,
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                             const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
+                             int nimg, hipStream_t s) {
+  dim3 grid(plan->nBlurTiles, nimg), block(256);
+  hipLaunchKernelGGL(k_blur_levels, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
+                     arenaPitch, *plan, tiles, blur, blurPitch);
+  return hipGetLastError();
+}
+
+hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                             const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
+                             long long blurPitch, const OrbPlanDesc* plan,
                              const uint32_t* outKeys, const int32_t* outCount,
                              orb_keypoint_t* kps, uint8_t* desc, int capacity, int32_t* counts,
                              int nimg, hipStream_t s) {
   dim3 grid((plan->slotsPerImage + 3) / 4, nimg), block(256);
   hipLaunchKernelGGL(k_orient_desc, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, outKeys, outCount, kps, desc, capacity, counts);
+                     arenaPitch, blur, blurPitch, *plan, outKeys, outCount, kps, desc, capacity,
+                     counts);
   return hipGetLastError();
 }
 

@@ -213,6 +213,8 @@ __device__ __forceinline__ bool lock_test(const uint32_t* bm, int idx) {
   return (bm[idx >> 5] >> (idx & 31)) & 1u;
 }
 
+#define RES_CHUNK 256
+
 __global__ __launch_bounds__(64) void k_proj_resolve(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked,
@@ -221,31 +223,52 @@ __global__ __launch_bounds__(64) void k_proj_resolve(
     const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
     const uint32_t* __restrict__ topk, const int32_t* __restrict__ ncand,
     int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t bm[];  // in-call lock bitmap
-  __shared__ int claimArr[64];
+  // LDS: lock bitmap (1 bit / keypoint), earliest claiming lane per keypoint
+  // of the current window, and a prefetched chunk of per-point resolve inputs
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  __shared__ uint4 cTop[RES_CHUNK];
+  __shared__ int cN[RES_CHUNK];
+  __shared__ uint8_t cObs[RES_CHUNK];
   const int p = blockIdx.x, lane = threadIdx.x;
   const int n = nkeys[p], M = nmps[p];
   const int words = (kpStride + 31) >> 5;
+  uint32_t* bm = dyn;
+  int* claimBy = (int*)(dyn + ((words + 3) & ~3));
   for (int i = lane; i < words; i += 64) bm[i] = 0u;
+  for (int i = lane; i < kpStride; i += 64) claimBy[i] = 64;
   int32_t* km = kpMatch + (size_t)p * kpStride;
   for (int i = lane; i < n; i += 64) km[i] = -1;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   const float nnratio = P.nnratio;
+  const size_t pbase = (size_t)p * mpStride;
   int matches = 0;
   int start = 0;
+  int cb = -RES_CHUNK;  // first point held in the LDS chunk
   while (start < M) {
+    if (start + 64 > cb + RES_CHUNK && cb + RES_CHUNK < M) {  // slide the chunk to `start`
+      cb = start;
+      __syncthreads();
+      for (int j = lane; j < RES_CHUNK; j += 64) {
+        const int m = cb + j;
+        if (m < M) {
+          cTop[j] = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
+          cN[j] = ncand[pbase + m];
+          cObs[j] = mps[pbase + m].has_obs;
+        }
+      }
+      __syncthreads();
+    }
     const int m = start + lane;
     const bool active = m < M;
-    const size_t mg = (size_t)p * mpStride + m;
     int nc = -1;
     uint32_t e[TOPK];
     bool hasObs = false;
     if (active) {
-      nc = ncand[mg];
-      for (int j = 0; j < TOPK; ++j) e[j] = topk[mg * TOPK + j];
-      hasObs = mps[mg].has_obs != 0;
+      const int j = m - cb;
+      nc = cN[j];
+      const uint4 t4 = cTop[j];
+      e[0] = t4.x; e[1] = t4.y; e[2] = t4.z; e[3] = t4.w;
+      hasObs = cObs[j] != 0;
     }
     // evaluate against the current locks
     int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
@@ -272,26 +295,24 @@ __global__ __launch_bounds__(64) void k_proj_resolve(
     if (nc > 0 && !slow && bestDist <= 100)
       accept = !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2);
     const bool locks = accept && hasObs;
-    claimArr[lane] = locks ? bestIdx : -1;
+    // conflict: an earlier lane of this window locks a keypoint this lane looked at
+    if (locks) atomicMin(&claimBy[bestIdx], lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     bool conflict = false;
-    if (active && nc > 0) {
-      for (int j = 0; j < lane && !conflict; ++j) {
-        const int c = claimArr[j];
-        if (c < 0) continue;
-        for (int q = 0; q < consumed; ++q)
-          if (cand_idx(e[q]) == c) { conflict = true; break; }
-        if (slow) conflict = true;  // depends on claims beyond its top-K
-      }
-    }
+    for (int q = 0; q < consumed; ++q) conflict |= claimBy[cand_idx(e[q])] < lane;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (locks) claimBy[bestIdx] = 64;
     const unsigned long long bad = __ballot(active && (conflict || (slow && lane > 0)));
     const unsigned long long slowFirst = __ballot(lane == 0 && active && slow);
     int commit = bad ? (int)__builtin_ctzll(bad) : 64;
     if (slowFirst) {
       // exact re-scan of the first point of the window, lane 0, current locks
       if (lane == 0) {
+        const size_t mg = pbase + m;
         const orb_mp_track_t mp = mps[mg];
         const int lvl = mp.level;
         float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;
@@ -320,7 +341,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(
                              });
         if (bd <= 100 && !(bl == bl2 && (float)bd > nnratio * (float)bd2)) {
           atomicMax(&km[bi], m);
-          if (hasObs) bm[bi >> 5] |= 1u << (bi & 31);
+          if (mp.has_obs) bm[bi >> 5] |= 1u << (bi & 31);
           ++matches;
         }
       }
@@ -337,7 +358,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     start += commit;
   }
-  if (lane == 0) nmatches[p] = __shfl(matches, 0, 64);
+  if (lane == 0) nmatches[p] = matches;
 }
 
 // ------------------------------------------------------------ host launchers
@@ -357,22 +378,32 @@ hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, in
   return hipGetLastError();
 }
 
-hipError_t orb_k_proj_local(const orb_keypoint_t* keys, const uint8_t* desc, const float* uright,
-                            const uint8_t* locked, const int32_t* nkeys, int kpStride,
-                            const orb_mp_track_t* mps, const uint8_t* mpDesc,
-                            const int32_t* nmps, int mpStride, int mpMax,
-                            const int32_t* cellStart, const int32_t* cellIdx, const void* params,
-                            uint32_t* topk, int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
-                            int nproblems, hipStream_t s) {
+hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc,
+                                 const float* uright, const uint8_t* locked, int kpStride,
+                                 const orb_mp_track_t* mps, const uint8_t* mpDesc,
+                                 const int32_t* nmps, int mpStride, int mpMax,
+                                 const int32_t* cellStart, const int32_t* cellIdx,
+                                 const void* params, uint32_t* topk, int32_t* ncand,
+                                 int nproblems, hipStream_t s) {
   const ProjParams P = *(const ProjParams*)params;
-  if (mpMax > 0) {
-    hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + 255) / 256, nproblems), dim3(256), 0, s,
-                       keys, desc, uright, locked, kpStride, mps, mpDesc, nmps, mpStride,
-                       cellStart, cellIdx, P, topk, ncand);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  const size_t lds = (size_t)((kpStride + 31) / 32) * 4;
+  if (mpMax <= 0 || nproblems <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + 255) / 256, nproblems), dim3(256), 0, s,
+                     keys, desc, uright, locked, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
+                     cellIdx, P, topk, ncand);
+  return hipGetLastError();
+}
+
+hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
+                              const float* uright, const uint8_t* locked, const int32_t* nkeys,
+                              int kpStride, const orb_mp_track_t* mps, const uint8_t* mpDesc,
+                              const int32_t* nmps, int mpStride, const int32_t* cellStart,
+                              const int32_t* cellIdx, const void* params, const uint32_t* topk,
+                              const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
+                              int nproblems, hipStream_t s) {
+  const ProjParams P = *(const ProjParams*)params;
+  if (nproblems <= 0) return hipSuccess;
+  const size_t words = (size_t)((kpStride + 31) / 32);
+  const size_t lds = ((words + 3) & ~(size_t)3) * 4 + (size_t)kpStride * 4;
   hipLaunchKernelGGL(k_proj_resolve, dim3(nproblems), dim3(64), lds, s, keys, desc, uright,
                      locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, P,
                      topk, ncand, kpMatch, nmatches);

@@ -16,8 +16,9 @@
 struct OrbLevelDesc {
   int w, h;          // level size (cvRound(W * invScale), src/ORBextractor.cc:1180)
   int pitch;         // row pitch of the level in the pyramid arena (level 0: caller stride)
-  int _pad0;
+  int blurPitch;     // row pitch of the level's blurred copy
   long long arenaOff;// byte offset of the level inside one image's pyramid arena (l >= 1)
+  long long blurOff; // byte offset of the blurred level inside one image's blur arena
   int cellBeg, cellEnd;  // range of this level's cells in the cell table
   int quota;         // mnFeaturesPerLevel[l]
   int nodeCap;       // max alive octree nodes == max keypoints this level can emit
@@ -29,7 +30,7 @@ struct OrbLevelDesc {
   float sizeF;       // (float)(int)(31 * scale), src/ORBextractor.cc:874
   int rtabX, rtabY;  // offsets of this level's resize tables (x: xofs/alpha, y: yofs/beta)
   int xmax;          // first dx whose source tap sx+1 falls outside (resize)
-  int _pad1;
+  int tileBeg;       // first blur tile of this level
 };
 
 struct OrbPlanDesc {
@@ -40,6 +41,8 @@ struct OrbPlanDesc {
   int iniTh, minTh;
   int maxCellRows, maxCellCols;  // largest cell ROI (for LDS sizing)
   int srcW, srcH;
+  int nBlurTiles;    // 64x16 blur tiles over all levels of one image
+  int _pad;
   OrbLevelDesc lv[ORB_MAX_LEVELS];
 };
 
@@ -49,3 +52,10 @@ struct OrbPlanDesc {
 struct OrbCellDesc {
   int16_t level, y0, y1, x0, x1, _pad;
 };
+
+// One 64 x 16 output tile of the 7x7 Gaussian pass over level `level`.
+struct OrbTileDesc {
+  int16_t level, x0, y0, _pad;
+};
+#define ORB_BLUR_TW 64
+#define ORB_BLUR_TH 16

@@ -36,8 +36,13 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
                         int nodeCapMax, int maxCellsPerLevel, uint32_t* outKeys,
                         int32_t* outCount, int32_t* errFlag, int nimg, hipStream_t s);
-hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
+hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0Stride,
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                             const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
+                             int nimg, hipStream_t s);
+hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                             const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
+                             long long blurPitch, const OrbPlanDesc* plan,
                              const uint32_t* outKeys, const int32_t* outCount,
                              orb_keypoint_t* kps, uint8_t* desc, int capacity, int32_t* counts,
                              int nimg, hipStream_t s);
@@ -45,13 +50,20 @@ hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
                             int32_t* cellIdx, int nproblems, hipStream_t s);
-hipError_t orb_k_proj_local(const orb_keypoint_t* keys, const uint8_t* desc, const float* uright,
-                            const uint8_t* locked, const int32_t* nkeys, int kpStride,
-                            const orb_mp_track_t* mps, const uint8_t* mpDesc,
-                            const int32_t* nmps, int mpStride, int mpMax,
-                            const int32_t* cellStart, const int32_t* cellIdx, const void* params,
-                            uint32_t* topk, int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
-                            int nproblems, hipStream_t s);
+hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc,
+                                 const float* uright, const uint8_t* locked, int kpStride,
+                                 const orb_mp_track_t* mps, const uint8_t* mpDesc,
+                                 const int32_t* nmps, int mpStride, int mpMax,
+                                 const int32_t* cellStart, const int32_t* cellIdx,
+                                 const void* params, uint32_t* topk, int32_t* ncand,
+                                 int nproblems, hipStream_t s);
+hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
+                              const float* uright, const uint8_t* locked, const int32_t* nkeys,
+                              int kpStride, const orb_mp_track_t* mps, const uint8_t* mpDesc,
+                              const int32_t* nmps, int mpStride, const int32_t* cellStart,
+                              const int32_t* cellIdx, const void* params, const uint32_t* topk,
+                              const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
+                              int nproblems, hipStream_t s);
 size_t orb_k_proj_params_size(void);
 }
 
@@ -93,6 +105,60 @@ struct DevBuf {
   T* as() const { return (T*)p; }
 };
 
+// HIP-event timing of kernel stages on the stream they are launched on.  Each
+// profiled call takes a fresh set of events from a pool (no synchronisation in
+// the launch path); read() drains every recorded set and accumulates per-stage
+// milliseconds, so a timed region of K calls is measured without perturbing it.
+struct StageProfiler {
+  static const int kMaxStages = 6;
+  bool enabled = false;
+  int nStages = 0;
+  const char* names[kMaxStages] = {};
+  std::vector<std::vector<hipEvent_t>> pool;  // each: nStages + 1 events
+  size_t used = 0;
+  double ms[kMaxStages + 1] = {};
+  long launches[kMaxStages + 1] = {};
+  int launchesPerCall[kMaxStages] = {};
+
+  void reset() {
+    used = 0;
+    for (int i = 0; i <= kMaxStages; ++i) { ms[i] = 0; launches[i] = 0; }
+  }
+  std::vector<hipEvent_t>* begin_call() {
+    if (!enabled) return nullptr;
+    if (used == pool.size()) {
+      pool.emplace_back(nStages + 1);
+      for (hipEvent_t& e : pool.back()) hipEventCreate(&e);
+    }
+    return &pool[used++];
+  }
+  void drain() {
+    for (size_t c = 0; c < used; ++c) {
+      std::vector<hipEvent_t>& ev = pool[c];
+      if (hipEventSynchronize(ev[nStages]) != hipSuccess) continue;
+      for (int i = 0; i < nStages; ++i) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, ev[i], ev[i + 1]) == hipSuccess) {
+          ms[i] += t;
+          launches[i] += launchesPerCall[i];
+        }
+      }
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, ev[0], ev[nStages]) == hipSuccess) {
+        ms[nStages] += t;
+        launches[nStages] += 1;
+      }
+    }
+    used = 0;
+  }
+  void destroy() {
+    for (auto& v : pool)
+      for (hipEvent_t e : v) hipEventDestroy(e);
+    pool.clear();
+    used = 0;
+  }
+};
+
 orb_status_t check_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ORB_ENODEV;
@@ -125,13 +191,13 @@ struct orb_extractor {
   int planW = -1, planH = -1;
   OrbPlanDesc plan;
   std::vector<OrbCellDesc> cells;
-  long long arenaBytes = 0;
+  long long arenaBytes = 0, blurBytes = 0;
   int maxCellsPerLevel = 0, nodeCapMax = 0, ldsKeyCap = 0;
-  DevBuf dCells, dRtab;
+  DevBuf dCells, dRtab, dTiles;
 
   // batch scratch
   int batchCap = 0;
-  DevBuf dArena, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
+  DevBuf dArena, dBlur, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
   // single-image API scratch
   DevBuf dImg, dKps, dDesc, dCounts;
   int lastW = 0, lastH = 0;
@@ -140,15 +206,9 @@ struct orb_extractor {
   size_t lastImg0Pitch = 0;
   int lastImg0Stride = 0;
 
-  // profiling
-  bool profile = false;
-  hipEvent_t ev[8] = {};
-  double stageMs[5] = {0, 0, 0, 0, 0};
-  int stageLaunches[5] = {0, 0, 0, 0, 0};
+  // profiling: stages k_pyr_resize (x nlevels-1), k_fast_cells, k_octree, k_orient_desc
+  StageProfiler prof;
 };
-
-static const char* kStageNames[5] = {"k_pyr_resize", "k_fast_cells", "k_octree",
-                                     "k_orient_desc", "extract_total"};
 
 static void compute_tables(orb_extractor* h) {
   const int L = h->nlevels;
@@ -203,7 +263,8 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   P.srcH = H;
   std::vector<OrbCellDesc> cells;
   std::vector<int32_t> rtab;
-  long long arena = 0;
+  std::vector<OrbTileDesc> tiles;
+  long long arena = 0, blurArena = 0;
   int keyCap = 1, maxRows = 7, maxCols = 7, maxCellsPerLevel = 1, nodeCapMax = 1, slots = 0;
   for (int l = 0; l < L; ++l) {
     OrbLevelDesc& d = P.lv[l];
@@ -213,6 +274,19 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     d.pitch = (d.w + 63) & ~63;
     d.arenaOff = l ? arena : 0;
     if (l) arena += (long long)d.pitch * d.h;
+    d.blurPitch = (d.w + 63) & ~63;
+    d.blurOff = blurArena;
+    blurArena += (long long)d.blurPitch * d.h;
+    d.tileBeg = (int)tiles.size();
+    for (int y0 = 0; y0 < d.h; y0 += ORB_BLUR_TH)
+      for (int x0 = 0; x0 < d.w; x0 += ORB_BLUR_TW) {
+        OrbTileDesc t;
+        t.level = (int16_t)l;
+        t.x0 = (int16_t)x0;
+        t.y0 = (int16_t)y0;
+        t._pad = 0;
+        tiles.push_back(t);
+      }
     d.scale = h->scale[l];
     d.sizeF = (float)(int)(31 * h->scale[l]);
     d.quota = h->quota[l];
@@ -293,7 +367,9 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
       }
     }
   }
+  if (maxRows * maxCols > 2048) return ORB_EINVAL;  // k_fast_cells ROI staging limit
   P.ncells = (int)cells.size();
+  P.nBlurTiles = (int)tiles.size();
   P.keyCap = keyCap;
   P.slotsPerImage = slots;
   P.maxCellRows = maxRows;
@@ -310,6 +386,10 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (st) return st;
   st = h->dRtab.ensure(std::max<size_t>(rtab.size(), 1) * 4);
   if (st) return st;
+  st = h->dTiles.ensure(tiles.size() * sizeof(OrbTileDesc));
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(h->dTiles.p, tiles.data(), tiles.size() * sizeof(OrbTileDesc),
+                         hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->dCells.p, cells.data(), cells.size() * sizeof(OrbCellDesc),
                          hipMemcpyHostToDevice, h->stream));
   if (!rtab.empty())
@@ -319,6 +399,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   h->plan = P;
   h->cells.swap(cells);
   h->arenaBytes = (arena + 255) & ~255LL;
+  h->blurBytes = (blurArena + 255) & ~255LL;
   h->maxCellsPerLevel = maxCellsPerLevel;
   h->nodeCapMax = nodeCapMax;
   h->ldsKeyCap = ldsKeyCap;
@@ -334,6 +415,7 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
   const size_t cellSlots = (size_t)B * P.ncells * P.keyCap;
   orb_status_t st;
   if ((st = h->dArena.ensure((size_t)B * h->arenaBytes))) return st;
+  if ((st = h->dBlur.ensure((size_t)B * h->blurBytes))) return st;
   if ((st = h->dCellKeys.ensure(cellSlots * 4))) return st;
   if ((st = h->dGKeys.ensure(cellSlots * 4))) return st;
   if ((st = h->dGNid.ensure(cellSlots * 2))) return st;
@@ -352,7 +434,8 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   const int32_t* rt = h->dRtab.as<int32_t>();
   uint8_t* arena = h->dArena.as<uint8_t>();
   const long long ap = h->arenaBytes;
-  if (h->profile) HIP_TRY(hipEventRecord(h->ev[0], s));
+  std::vector<hipEvent_t>* ev = h->prof.begin_call();
+  if (ev) HIP_TRY(hipEventRecord((*ev)[0], s));
   HIP_TRY(hipMemsetAsync(h->dErr.p, 0, 16, s));
   for (int l = 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
@@ -364,41 +447,28 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                              d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
                              rt + d.rtabY + d.h, d.xmax, B, s));
   }
-  if (h->profile) HIP_TRY(hipEventRecord(h->ev[1], s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[1], s));
+  HIP_TRY(orb_k_blur_levels(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                            h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, B,
+                            s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s));
   HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                            h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
                            h->dCellCount.as<int32_t>(), B, s));
-  if (h->profile) HIP_TRY(hipEventRecord(h->ev[2], s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[3], s));
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                        h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
                        h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), B, s));
-  if (h->profile) HIP_TRY(hipEventRecord(h->ev[3], s));
-  HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                            h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(), d_kps, d_desc,
-                            capacity, d_counts, B, s));
-  if (h->profile) HIP_TRY(hipEventRecord(h->ev[4], s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[4], s));
+  HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap,
+                            h->dBlur.as<uint8_t>(), h->blurBytes, &P, h->dOutKeys.as<uint32_t>(),
+                            h->dOutCount.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[5], s));
   h->lastImg0 = d_images;
   h->lastImg0Pitch = imgPitch;
   h->lastImg0Stride = (int)stride;
   return ORB_OK;
-}
-
-static void profile_collect(orb_extractor* h) {
-  if (!h->profile) return;
-  if (hipEventSynchronize(h->ev[4]) != hipSuccess) return;
-  for (int i = 0; i < 4; ++i) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]) == hipSuccess) {
-      h->stageMs[i] += ms;
-      h->stageLaunches[i] += (i == 0) ? std::max(h->nlevels - 1, 0) : 1;
-    }
-  }
-  float tot = 0.f;
-  if (hipEventElapsedTime(&tot, h->ev[0], h->ev[4]) == hipSuccess) {
-    h->stageMs[4] += tot;
-    h->stageLaunches[4] += 1;
-  }
 }
 
 extern "C" {
@@ -449,7 +519,14 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
     return ORB_EDEVICE;
   }
   h->ownStream = true;
-  for (int i = 0; i < 8; ++i) hipEventCreate(&h->ev[i]);
+  h->prof.nStages = 5;
+  const char* names[5] = {"k_pyr_resize", "k_blur_levels", "k_fast_cells", "k_octree",
+                          "k_orient_desc"};
+  for (int i = 0; i < 5; ++i) {
+    h->prof.names[i] = names[i];
+    h->prof.launchesPerCall[i] = 1;
+  }
+  h->prof.launchesPerCall[0] = std::max(nlevels - 1, 0);
   if (orb_k_upload_constants(h->stream) != hipSuccess ||
       orb_k_upload_umax(h->umax, h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -464,12 +541,11 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   if (!h) return;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  DevBuf* bufs[] = {&h->dCells, &h->dRtab, &h->dArena, &h->dCellKeys, &h->dCellCount,
+  DevBuf* bufs[] = {&h->dCells, &h->dRtab, &h->dTiles, &h->dBlur, &h->dArena, &h->dCellKeys, &h->dCellCount,
                     &h->dGKeys, &h->dGNid, &h->dOutKeys, &h->dOutCount, &h->dErr,
                     &h->dImg, &h->dKps, &h->dDesc, &h->dCounts};
   for (DevBuf* b : bufs) b->release();
-  for (int i = 0; i < 8; ++i)
-    if (h->ev[i]) hipEventDestroy(h->ev[i]);
+  h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
   delete h;
 }
@@ -522,7 +598,6 @@ orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_im
   if (st) return st;
   h->lastW = width;
   h->lastH = height;
-  if (h->profile && s == h->stream) profile_collect(h);
   return ORB_OK;
 }
 
@@ -553,7 +628,6 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   HIP_TRY(hipMemcpyAsync(&n, h->dCounts.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipMemcpyAsync(&err, h->dErr.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  profile_collect(h);
   h->lastW = width;
   h->lastH = height;
   if (err) {
@@ -610,20 +684,24 @@ orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t*
 
 orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable) {
   if (!h) return ORB_EINVAL;
-  h->profile = enable != 0;
-  for (int i = 0; i < 5; ++i) {
-    h->stageMs[i] = 0;
-    h->stageLaunches[i] = 0;
-  }
+  std::lock_guard<std::mutex> g(h->mu);
+  hipSetDevice(h->device);
+  h->prof.drain();
+  h->prof.reset();
+  h->prof.enabled = enable != 0;
   return ORB_OK;
 }
 
+// stage 0..4 = kernels, stage 5 = whole extraction call
 orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
                                         int* launches, const char** name) {
-  if (!h || stage < 0 || stage > 4) return ORB_EINVAL;
-  if (total_ms) *total_ms = h->stageMs[stage];
-  if (launches) *launches = h->stageLaunches[stage];
-  if (name) *name = kStageNames[stage];
+  if (!h || stage < 0 || stage > h->prof.nStages) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  hipSetDevice(h->device);
+  h->prof.drain();
+  if (total_ms) *total_ms = h->prof.ms[stage];
+  if (launches) *launches = (int)h->prof.launches[stage];
+  if (name) *name = stage < h->prof.nStages ? h->prof.names[stage] : "extract_total";
   return ORB_OK;
 }
 
@@ -641,6 +719,8 @@ struct orb_matcher {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // profiling: stages k_grid_build, k_proj_candidates + k_proj_resolve
+  StageProfiler prof;
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
 };
@@ -668,6 +748,11 @@ orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
   if (orb_k_proj_params_size() != sizeof(ProjParamsHost)) return ORB_EINVAL;
   orb_matcher* m = new orb_matcher();
   m->device = device;
+  m->prof.nStages = 3;
+  m->prof.names[0] = "k_grid_build";
+  m->prof.names[1] = "k_proj_candidates";
+  m->prof.names[2] = "k_proj_resolve";
+  for (int i = 0; i < 3; ++i) m->prof.launchesPerCall[i] = 1;
   hipSetDevice(device);
   if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
     delete m;
@@ -685,6 +770,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
                     &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut};
   for (DevBuf* b : bufs) b->release();
+  m->prof.destroy();
   hipStreamDestroy(m->stream);
   delete m;
 }
@@ -738,12 +824,43 @@ orb_status_t orb_match_projection_local_batch(
   if ((st = m->dCellIdx.ensure((size_t)n_problems * kp_stride * 4))) return st;
   if ((st = m->dTopk.ensure((size_t)n_problems * std::max(mp_stride, 1) * 16))) return st;
   if ((st = m->dNcand.ensure((size_t)n_problems * std::max(mp_stride, 1) * 4))) return st;
+  std::vector<hipEvent_t>* ev = m->prof.begin_call();
+  if (ev) HIP_TRY(hipEventRecord((*ev)[0], s));
   HIP_TRY(orb_k_grid_build(d_keys, d_nkeys, kp_stride, P.minX, P.minY, P.invW, P.invH,
                            m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), n_problems, s));
-  HIP_TRY(orb_k_proj_local(d_keys, d_desc, nullptr, d_locked, d_nkeys, kp_stride, d_mps,
-                           d_mp_desc, d_nmps, mp_stride, mp_stride, m->dCellStart.as<int32_t>(),
-                           m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
-                           m->dNcand.as<int32_t>(), d_kp_match, d_nmatches, n_problems, s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[1], s));
+  HIP_TRY(orb_k_proj_candidates(d_keys, d_desc, nullptr, d_locked, kp_stride, d_mps, d_mp_desc,
+                                d_nmps, mp_stride, mp_stride, m->dCellStart.as<int32_t>(),
+                                m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
+                                m->dNcand.as<int32_t>(), n_problems, s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s));
+  HIP_TRY(orb_k_proj_resolve(d_keys, d_desc, nullptr, d_locked, d_nkeys, kp_stride, d_mps,
+                             d_mp_desc, d_nmps, mp_stride, m->dCellStart.as<int32_t>(),
+                             m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
+                             m->dNcand.as<int32_t>(), d_kp_match, d_nmatches, n_problems, s));
+  if (ev) HIP_TRY(hipEventRecord((*ev)[3], s));
+  return ORB_OK;
+}
+
+orb_status_t orb_matcher_profile(orb_matcher_t* m, int enable) {
+  if (!m) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  m->prof.drain();
+  m->prof.reset();
+  m->prof.enabled = enable != 0;
+  return ORB_OK;
+}
+
+orb_status_t orb_matcher_profile_read(orb_matcher_t* m, int stage, double* total_ms,
+                                      int* launches, const char** name) {
+  if (!m || stage < 0 || stage > m->prof.nStages) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  m->prof.drain();
+  if (total_ms) *total_ms = m->prof.ms[stage];
+  if (launches) *launches = (int)m->prof.launches[stage];
+  if (name) *name = stage < m->prof.nStages ? m->prof.names[stage] : "match_total";
   return ORB_OK;
 }
 
@@ -798,14 +915,19 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   HIP_TRY(orb_k_grid_build(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), N, P.minX,
                            P.minY, P.invW, P.invH, m->dCellStart.as<int32_t>(),
                            m->dCellIdx.as<int32_t>(), 1, s));
-  HIP_TRY(orb_k_proj_local(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(),
-                           F->u_right ? m->dUr.as<float>() : nullptr,
-                           kp_locked ? m->dLocked.as<uint8_t>() : nullptr,
-                           m->dNKeys.as<int32_t>(), N, m->dMps.as<orb_mp_track_t>(),
-                           m->dMpDesc.as<uint8_t>(), m->dNMps.as<int32_t>(), std::max(M, 1), M,
-                           m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
-                           m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
-                           m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), 1, s));
+  const float* ur = F->u_right ? m->dUr.as<float>() : nullptr;
+  const uint8_t* lk = kp_locked ? m->dLocked.as<uint8_t>() : nullptr;
+  HIP_TRY(orb_k_proj_candidates(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(), ur, lk, N,
+                                m->dMps.as<orb_mp_track_t>(), m->dMpDesc.as<uint8_t>(),
+                                m->dNMps.as<int32_t>(), std::max(M, 1), M,
+                                m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
+                                m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(), 1, s));
+  HIP_TRY(orb_k_proj_resolve(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(), ur, lk,
+                             m->dNKeys.as<int32_t>(), N, m->dMps.as<orb_mp_track_t>(),
+                             m->dMpDesc.as<uint8_t>(), m->dNMps.as<int32_t>(), std::max(M, 1),
+                             m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
+                             m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
+                             m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), 1, s));
   HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
