@@ -21,33 +21,71 @@
 // fixed-point weights.  The weight tables are computed
 // on the host with the reference's float/double expressions; the kernel only
 // does the integer taps.  One thread per output pixel, 64x4 tiles.
+#define PYR_TW 128  // output tile: 128 columns x 8 rows, 4 columns per thread
+#define PYR_TH 8
+#define PYR_SROWS 12  // >= source rows an 8-row output tile can touch (scale <= 1.25)
+#define PYR_SW 48     // >= dwords of source row one 128-column tile touches
+
+__device__ __forceinline__ int lds_byte(const uint32_t* row, int c) {
+  return (int)((row[c >> 2] >> (8 * (c & 3))) & 0xFFu);
+}
+
 __global__ __launch_bounds__(256) void k_pyr_resize(
-    const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sh,
+    const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sw, int sh,
     uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
     const int* __restrict__ xofs, const int* __restrict__ alpha,
     const int* __restrict__ yofs, const int* __restrict__ beta, int xmax) {
-  // 4 consecutive output pixels per thread; blocks of 64 x 4 threads cover 256 x 4.
-  // alpha/beta entries pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
-  const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-  const int dy = blockIdx.y * 4 + threadIdx.y;
-  if (dx0 >= dw || dy >= dh) return;
+  // The source window of the tile is staged in LDS as aligned dwords; every
+  // output reads its 2x2 taps from there.  alpha/beta pack the two 11-bit
+  // weights as (w1 << 16) | (w0 & 0xFFFF).
+  __shared__ __attribute__((aligned(16))) uint32_t tile[PYR_SROWS][PYR_SW];
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
   const uint8_t* S = src + (long long)blockIdx.z * srcImgPitch;
-  const int sy = yofs[dy];
-  const int bw = beta[dy];
+  const int xl = min(x0 + PYR_TW - 1, dw - 1), yl = min(y0 + PYR_TH - 1, dh - 1);
+  const int sxA = xofs[x0], sxB = min(xofs[xl] + 1, sw - 1);
+  const int syA = min(max(yofs[y0], 0), sh - 1), syB = min(max(yofs[yl] + 1, 0), sh - 1);
+  const int colBase = sxA & ~3;
+  const int nW = ((sxB - colBase) >> 2) + 1, nR = syB - syA + 1;
+  const bool aligned = ((srcStride & 3) == 0) && ((((uintptr_t)S) & 3) == 0);
+  for (int i = tid; i < nR * nW; i += 256) {
+    const int r = i / nW, w = i - r * nW;
+    const uint8_t* p = S + (long long)(syA + r) * srcStride + colBase + 4 * w;
+    uint32_t v;
+    if (aligned && colBase + 4 * w + 3 < sw) {
+      v = *reinterpret_cast<const uint32_t*>(p);
+    } else {
+      v = 0;
+      for (int b = 0; b < 4; ++b)
+        if (colBase + 4 * w + b < sw) v |= (uint32_t)p[b] << (8 * b);
+    }
+    tile[r][w] = v;
+  }
+  __syncthreads();
+  const int ty = tid >> 5, tx = tid & 31;
+  const int y = y0 + ty;
+  const int xs = x0 + 4 * tx;
+  if (y >= dh || xs >= dw) return;
+  const int sy = yofs[y];
+  const int bw = beta[y];
   const int b0 = (int)(short)(bw & 0xFFFF), b1 = bw >> 16;
-  const int r0 = min(max(sy, 0), sh - 1), r1 = min(max(sy + 1, 0), sh - 1);
-  const uint8_t* p0 = S + (long long)r0 * srcStride;
-  const uint8_t* p1 = S + (long long)r1 * srcStride;
+  const uint32_t* R0 = tile[min(max(sy, 0), sh - 1) - syA];
+  const uint32_t* R1 = tile[min(max(sy + 1, 0), sh - 1) - syA];
   uint32_t packed = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int dx = min(dx0 + j, dw - 1);
-    const int sx = xofs[dx];
+    const int dx = min(xs + j, dw - 1);
+    const int c = xofs[dx] - colBase;
     const int aw = alpha[dx];
     const int a0 = (int)(short)(aw & 0xFFFF), a1 = aw >> 16;
-    const int sx1 = dx < xmax ? sx + 1 : sx;
-    const int h0 = dx < xmax ? p0[sx] * a0 + p0[sx1] * a1 : p0[sx] * 2048;
-    const int h1 = dx < xmax ? p1[sx] * a0 + p1[sx1] * a1 : p1[sx] * 2048;
+    int h0, h1;
+    if (dx < xmax) {
+      h0 = lds_byte(R0, c) * a0 + lds_byte(R0, c + 1) * a1;
+      h1 = lds_byte(R1, c) * a0 + lds_byte(R1, c + 1) * a1;
+    } else {
+      h0 = lds_byte(R0, c) * 2048;
+      h1 = lds_byte(R1, c) * 2048;
+    }
     int v = min(max((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 0), 255);
     // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
     // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
@@ -55,11 +93,11 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
     __asm__ volatile("" : "+v"(v));
     packed |= (uint32_t)v << (8 * j);
   }
-  uint8_t* out = dst + (long long)blockIdx.z * dstImgPitch + (long long)dy * dstStride + dx0;
-  if (dx0 + 4 <= dw) {
-    *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 64 == 0, dx0 % 4 == 0
+  uint8_t* out = dst + (long long)blockIdx.z * dstImgPitch + (long long)y * dstStride + xs;
+  if (xs + 4 <= dw) {
+    *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 64 == 0, xs % 4 == 0
   } else {
-    for (int j = 0; dx0 + j < dw; ++j) out[j] = (uint8_t)(packed >> (8 * j));
+    for (int j = 0; xs + j < dw; ++j) out[j] = (uint8_t)(packed >> (8 * j));
   }
 }
 
@@ -109,6 +147,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(
     int32_t* __restrict__ cellCount) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int scanTmp[17];
+  __shared__ int qCount;
   const int cell = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
   const OrbCellDesc cd = cells[cell];
   const int l = cd.level;
@@ -131,6 +170,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(
   const int dh = rows - 6, dw = cols - 6, sp = dw + 2;
   uint8_t* sc = smem + ((rows * cols + 15) & ~15);           // (dh+2) x (dw+2), zero border
   uint8_t* flags = sc + (((dh + 2) * sp + 15) & ~15);        // dh x dw survivors
+  uint16_t* queue = (uint16_t*)(flags + ((dh * dw + 15) & ~15));  // candidate pixel list
   {
     // all loads in flight before the LDS stores; ROI <= 2048 px (host-checked)
     const int n = rows * cols;
@@ -151,10 +191,40 @@ __global__ __launch_bounds__(256) void k_fast_cells(
     }
   }
   for (int i = tid; i < (dh + 2) * sp; i += 256) sc[i] = 0;
+  if (tid == 0) qCount = 0;
   __syncthreads();
   const int npix = dh * dw;
   const float invDw = 1.0f / (float)dw;
-  for (int i = tid; i < npix; i += 256) {
+  // Pixels that cannot be a corner at the lower threshold keep score 0 (what
+  // cv::FAST stores for non-corners).  Necessary condition for a 9-arc: two
+  // circularly adjacent compass pixels (circle positions 0,4,8,12) on the same
+  // side.  Survivors are queued (wave-aggregated LDS append) so the full
+  // arc computation runs on dense lanes.
+  const int tq = min(max(min(plan.iniTh, plan.minTh), 0), 255);
+  const int lane = tid & 63;
+  for (int i0 = 0; i0 < npix; i0 += 256) {
+    const int i = i0 + tid;
+    bool pass = false;
+    if (i < npix) {
+      const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
+      const uint8_t* c = roi + (y + 3) * cols + (x + 3);
+      const int v = c[0];
+      const int q0 = c[3 * cols], q4 = c[3], q8 = c[-3 * cols], q12 = c[-3];
+      const bool d0 = q0 < v - tq, d4 = q4 < v - tq, d8 = q8 < v - tq, d12 = q12 < v - tq;
+      const bool b0 = q0 > v + tq, b4 = q4 > v + tq, b8 = q8 > v + tq, b12 = q12 > v + tq;
+      pass = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) ||
+             (b4 && b8) || (b8 && b12) || (b12 && b0);
+    }
+    const unsigned long long bal = __ballot(pass);
+    int base = 0;
+    if (lane == 0 && bal) base = atomicAdd(&qCount, __popcll(bal));
+    base = __shfl(base, 0, 64);
+    if (pass) queue[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)i;
+  }
+  __syncthreads();
+  const int nq = qCount;
+  for (int j = tid; j < nq; j += 256) {
+    const int i = queue[j];
     const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
     const int s = fast_score(roi + (y + 3) * cols + (x + 3), cols);
     sc[(y + 1) * sp + (x + 1)] = (uint8_t)min(max(s, 0), 255);
@@ -549,15 +619,23 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i;
 }
 
-#define BLUR_SW (ORB_BLUR_TW + 6)
 #define BLUR_SH (ORB_BLUR_TH + 6)
+#define BLUR_WROW 19  // dwords per staged row: bytes x0-4 .. x0+71
+
+__device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
+  const uint32_t w = b < 4 ? w0 : (b < 8 ? w1 : w2);
+  return (int)((w >> (8 * (b & 3))) & 0xFFu);
+}
 
 __global__ __launch_bounds__(256) void k_blur_levels(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbTileDesc* __restrict__ tiles, uint8_t* __restrict__ blur, long long blurPitch) {
-  __shared__ uint8_t raw[BLUR_SH][BLUR_SW + 2];
-  __shared__ uint16_t rowp[BLUR_SH][ORB_BLUR_TW];
+  // staged source rows y0-3 .. y0+18, byte b of a row = level column x0-4+b.
+  // Every LDS access is a naturally aligned dword (or 8 bytes): unaligned
+  // sub-dword LDS reads are replayed by the hardware.
+  __shared__ __attribute__((aligned(16))) uint32_t raw[BLUR_SH][BLUR_WROW + 1];
+  __shared__ __attribute__((aligned(16))) uint32_t rowp[BLUR_SH][ORB_BLUR_TW / 2];
   const int tid = threadIdx.x, img = blockIdx.y;
   const OrbTileDesc td = tiles[blockIdx.x];
   const int l = td.level;
@@ -571,53 +649,96 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     lvl = arena + (long long)img * arenaPitch + L.arenaOff;
     pitch = L.pitch;
   }
-  const bool interior = td.x0 >= 3 && td.y0 >= 3 && td.x0 + ORB_BLUR_TW + 3 <= L.w &&
+  const bool aligned = ((pitch & 3) == 0) && ((((uintptr_t)lvl) & 3) == 0);
+  const bool interior = aligned && td.x0 >= 4 && td.y0 >= 3 && td.x0 + 72 <= L.w &&
                         td.y0 + ORB_BLUR_TH + 3 <= L.h;
-  // issue every global load of the tile before the first LDS store (one memory
-  // latency per workgroup instead of one per loop trip)
-  constexpr int kSlots = (BLUR_SH * BLUR_SW + 255) / 256;
-  uint8_t v[kSlots];
+  if (interior) {
+    constexpr int kN = BLUR_SH * 18;
+    uint32_t v[2];
 #pragma unroll
-  for (int q = 0; q < kSlots; ++q) {
-    const int i = tid + 256 * q;
-    if (i < BLUR_SH * BLUR_SW) {
-      const int r = i / BLUR_SW, c = i - r * BLUR_SW;
-      int y = td.y0 - 3 + r, x = td.x0 - 3 + c;
-      if (!interior) {
-        y = reflect101(y, L.h);
-        x = reflect101(x, L.w);
+    for (int q = 0; q < 2; ++q) {
+      const int i = tid + 256 * q;
+      if (i < kN) {
+        const int r = i / 18, wq = i - r * 18;
+        v[q] = *reinterpret_cast<const uint32_t*>(lvl + (long long)(td.y0 - 3 + r) * pitch +
+                                                  td.x0 - 4 + 4 * wq);
       }
-      v[q] = lvl[(long long)y * pitch + x];
     }
-  }
 #pragma unroll
-  for (int q = 0; q < kSlots; ++q) {
-    const int i = tid + 256 * q;
-    if (i < BLUR_SH * BLUR_SW) {
-      const int r = i / BLUR_SW, c = i - r * BLUR_SW;
-      raw[r][c] = v[q];
+    for (int q = 0; q < 2; ++q) {
+      const int i = tid + 256 * q;
+      if (i < kN) {
+        const int r = i / 18, wq = i - r * 18;
+        raw[r][wq] = v[q];
+      }
+    }
+  } else {
+    // border tile: per-byte reflect-101 gather, assembled into dwords
+    constexpr int kN = BLUR_SH * 18;
+    for (int i = tid; i < kN; i += 256) {
+      const int r = i / 18, wq = i - r * 18;
+      const int y = reflect101(td.y0 - 3 + r, L.h);
+      const uint8_t* row = lvl + (long long)y * pitch;
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int x = reflect101(td.x0 - 4 + 4 * wq + b, L.w);
+        w |= (uint32_t)row[x] << (8 * b);
+      }
+      raw[r][wq] = w;
     }
   }
   __syncthreads();
   const int k[7] = {18, 34, 49, 55, 49, 34, 18};
-  for (int i = tid; i < BLUR_SH * ORB_BLUR_TW; i += 256) {
-    const int r = i >> 6, c = i & 63;
-    const uint8_t* p = &raw[r][c];
-    rowp[r][c] = (uint16_t)(k[0] * p[0] + k[1] * p[1] + k[2] * p[2] + k[3] * p[3] + k[4] * p[4] +
-                            k[5] * p[5] + k[6] * p[6]);
+  // row pass: task (r, g) -> outputs columns 4g..4g+3 from bytes 4g+1 .. 4g+10
+  for (int id = tid; id < BLUR_SH * 16; id += 256) {
+    const int r = id >> 4, g = id & 15;
+    const uint32_t w0 = raw[r][g], w1 = raw[r][g + 1], w2 = raw[r][g + 2];
+    int o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int acc = 0;
+#pragma unroll
+      for (int t = 0; t < 7; ++t) acc += k[t] * byte_of(w0, w1, w2, 1 + i + t);
+      o[i] = acc;
+    }
+    uint2 pk;
+    pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+    pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+    *reinterpret_cast<uint2*>(&rowp[r][2 * g]) = pk;
   }
   __syncthreads();
-  const int c = tid & 63;
-  const int x = td.x0 + c;
+  // column pass: thread -> columns (2q, 2q+1) x rows (2rp, 2rp+1)
+  const int q = tid & 31, rp = tid >> 5;
+  uint32_t cv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cv[j] = rowp[2 * rp + j][q];
+  int out[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    int a0 = 0, a1 = 0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      a0 += k[j] * (int)(cv[j + rr] & 0xFFFFu);
+      a1 += k[j] * (int)(cv[j + rr] >> 16);
+    }
+    out[rr][0] = min((a0 + (1 << 15)) >> 16, 255);
+    out[rr][1] = min((a1 + (1 << 15)) >> 16, 255);
+  }
   uint8_t* dst = blur + (long long)img * blurPitch + L.blurOff;
+  const int x = td.x0 + 2 * q;
 #pragma unroll
-  for (int rr = 0; rr < ORB_BLUR_TH / 4; ++rr) {
-    const int r = (tid >> 6) + 4 * rr;
-    const int y = td.y0 + r;
-    int acc = 0;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) acc += k[j] * (int)rowp[r + j][c];
-    if (x < L.w && y < L.h) dst[(long long)y * L.blurPitch + x] = (uint8_t)min((acc + (1 << 15)) >> 16, 255);
+  for (int rr = 0; rr < 2; ++rr) {
+    const int y = td.y0 + 2 * rp + rr;
+    if (y >= L.h) continue;
+    uint8_t* o = dst + (long long)y * L.blurPitch + x;
+    if (x + 1 < L.w) {
+      int v = out[rr][0] | (out[rr][1] << 8);
+      __asm__ volatile("" : "+v"(v));
+      *reinterpret_cast<uint16_t*>(o) = (uint16_t)v;
+    } else if (x < L.w) {
+      o[0] = (uint8_t)out[rr][0];
+    }
   }
 }
 
@@ -744,12 +865,13 @@ hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s) {
                                 hipMemcpyHostToDevice, s);
 }
 
-hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sh,
-                            uint8_t* dst, long long dstImgPitch, int dstStride, int dw, int dh,
-                            const int* xofs, const void* alpha, const int* yofs, const void* beta,
-                            int xmax, int nimg, hipStream_t s) {
-  dim3 grid((dw + 255) / 256, (dh + 3) / 4, nimg), block(64, 4);
-  hipLaunchKernelGGL(k_pyr_resize, grid, block, 0, s, src, srcImgPitch, srcStride, sh, dst,
+hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sw,
+                            int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
+                            int dh, const int* xofs, const void* alpha, const int* yofs,
+                            const void* beta, int xmax, int nimg, hipStream_t s) {
+  // tile bounds assume a downscale of at most 1.25x per level (checked by the planner)
+  dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, nimg), block(256);
+  hipLaunchKernelGGL(k_pyr_resize, grid, block, 0, s, src, srcImgPitch, srcStride, sw, sh, dst,
                      dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,
                      (const int*)beta, xmax);
   return hipGetLastError();
@@ -761,7 +883,7 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
                             int nimg, hipStream_t s) {
   const int rows = plan->maxCellRows, cols = plan->maxCellCols;
   const size_t lds = (size_t)((rows * cols + 15) & ~15) + (size_t)(((rows - 4) * (cols - 4) + 15) & ~15) +
-                     (size_t)(rows - 6) * (cols - 6);
+                     (size_t)(((rows - 6) * (cols - 6) + 15) & ~15) + 2 * (size_t)(rows - 6) * (cols - 6);
   dim3 grid(plan->ncells, nimg), block(256);
   hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, *plan, cells, cellKeys, cellCount);

@@ -23,10 +23,10 @@
 extern "C" {
 hipError_t orb_k_upload_constants(hipStream_t s);
 hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s);
-hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sh,
-                            uint8_t* dst, long long dstImgPitch, int dstStride, int dw, int dh,
-                            const int* xofs, const void* alpha, const int* yofs, const void* beta,
-                            int xmax, int nimg, hipStream_t s);
+hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sw,
+                            int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
+                            int dh, const int* xofs, const void* alpha, const int* yofs,
+                            const void* beta, int xmax, int nimg, hipStream_t s);
 hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
@@ -443,7 +443,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     const uint8_t* src = l == 1 ? d_images : arena + sd.arenaOff;
     const long long srcPitch = l == 1 ? (long long)imgPitch : ap;
     const int srcStride = l == 1 ? (int)stride : sd.pitch;
-    HIP_TRY(orb_k_pyr_resize(src, srcPitch, srcStride, sd.h, arena + d.arenaOff, ap, d.pitch, d.w,
+    HIP_TRY(orb_k_pyr_resize(src, srcPitch, srcStride, sd.w, sd.h, arena + d.arenaOff, ap, d.pitch, d.w,
                              d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
                              rt + d.rtabY + d.h, d.xmax, B, s));
   }
@@ -499,8 +499,9 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
                                   int min_th_fast, int device, orb_extractor_t** out) {
   if (!out) return ORB_EINVAL;
   *out = nullptr;
+  // k_pyr_resize stages tiles sized for a per-level downscale of at most 1.25
   if (nfeatures < 0 || nlevels < 1 || nlevels > ORB_MAX_LEVELS || !(scale_factor > 1.0f) ||
-      nfeatures > 60000)
+      !(scale_factor <= 1.25f) || nfeatures > 60000)
     return ORB_EINVAL;
   orb_status_t st = check_device(device);
   if (st) return st;

@@ -5,7 +5,7 @@
 #include <stdint.h>
 #include <vector>
 #include <algorithm>
-extern "C" hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sh,
+extern "C" hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sw, int sh,
                             uint8_t* dst, long long dstImgPitch, int dstStride, int dw, int dh,
                             const int* xofs, const void* alpha, const int* yofs, const void* beta,
                             int xmax, int nimg, hipStream_t s);
@@ -36,7 +36,7 @@ int main() {
   hipMemcpy(dsrc, img.data(), sw * sh, hipMemcpyHostToDevice);
   hipMemcpy(drt, rt.data(), rt.size() * 4, hipMemcpyHostToDevice);
   hipMemset(ddst, 0, 576 * dh);
-  hipError_t e = orb_k_pyr_resize(dsrc, sw * sh, sw, sh, ddst, 576 * dh, 576, dw, dh, drt, drt + dw, drt + 2 * dw, drt + 2 * dw + dh, xmax, 1, 0);
+  hipError_t e = orb_k_pyr_resize(dsrc, sw * sh, sw, sw, sh, ddst, 576 * dh, 576, dw, dh, drt, drt + dw, drt + 2 * dw, drt + 2 * dw + dh, xmax, 1, 0);
   hipDeviceSynchronize();
   hipMemcpy2D(got.data(), dw, ddst, 576, dw, dh, hipMemcpyDeviceToHost);
   int bad = 0;
