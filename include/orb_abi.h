@@ -218,10 +218,26 @@ typedef struct orb_stereo_input {
 orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in,
                               float* u_right, float* depth);
 
+/* Device-batched ComputeStereoMatches for n_pairs rectified pairs whose left
+ * and right images went through orb_extractor_extract_batch on left_ext and
+ * right_ext (pyramids are read from those handles).  Keypoints/descriptors as
+ * written by the two batches (pair i at i*kp_stride), counts d_left_n/d_right_n.
+ * Writes d_u_right / d_depth (-1 = none) and d_sad (SAD of kept matches, -1). */
+orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor_t* left_ext,
+                                    orb_extractor_t* right_ext, const orb_keypoint_t* d_left_keys,
+                                    const uint8_t* d_left_desc, const int32_t* d_left_n,
+                                    const orb_keypoint_t* d_right_keys,
+                                    const uint8_t* d_right_desc, const int32_t* d_right_n,
+                                    int kp_stride, float bf, float fx, float* d_u_right,
+                                    float* d_depth, int32_t* d_sad, void* stream);
+
 /* SearchByProjection(CurrentFrame, LastFrame, th, bMono) with ORBmatcher(nnratio, checkOri).
  * The last frame's map points are given already projected with the current
  * pose (the float camera-space coordinates xc, yc and invzc computed exactly
- * as src/ORBmatcher.cc:1500-1505).  valid[i]=0 for NULL or outlier entries. */
+ * as src/ORBmatcher.cc:1500-1505).  valid[i]=0 for NULL or outlier entries.
+ * kp_match[i] (out) = MapPoint id assigned to current keypoint i by this call,
+ * -1 untouched, -2 reset to NULL by the rotation-consistency filter
+ * (src/ORBmatcher.cc:1597-1616). */
 typedef struct orb_last_mp {
   float xc, yc, invzc;          /* Rcw*x3Dw + tcw, 1/z */
   int32_t last_octave;          /* LastFrame.mvKeys[i].octave */

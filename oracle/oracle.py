@@ -229,3 +229,109 @@ def synth_local_map(seed, keys, desc, n_mp, width, height):
     lib().oracle_synth_local_map(seed, _p(keys), _p(desc), len(keys), n_mp, width, height,
                                  _p(mps), _p(mpd), _p(lk))
     return mps, mpd, lk
+
+
+# ------------------------------------------------------------ stereo / frame / BoW
+class _StereoInput(ctypes.Structure):
+    _fields_ = [
+        ("left", ctypes.c_void_p), ("n_right", ctypes.c_int32), ("right_keys", ctypes.c_void_p),
+        ("right_desc", ctypes.c_void_p), ("n_levels", ctypes.c_int32),
+        ("left_levels", ctypes.c_void_p), ("right_levels", ctypes.c_void_p),
+        ("level_width", ctypes.c_void_p), ("level_height", ctypes.c_void_p),
+        ("level_stride", ctypes.c_void_p), ("inv_scale_factors", ctypes.c_void_p),
+        ("bf", ctypes.c_float), ("fx", ctypes.c_float),
+    ]
+
+
+class _Camera(ctypes.Structure):
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float),
+                ("cy", ctypes.c_float), ("bf", ctypes.c_float), ("mb", ctypes.c_float)]
+
+
+LAST_MP_DTYPE = np.dtype([("xc", "<f4"), ("yc", "<f4"), ("invzc", "<f4"), ("last_octave", "<i4"),
+                          ("last_angle", "<f4"), ("valid", "u1"), ("has_obs", "u1"),
+                          ("_pad", "u1", 2), ("mp_id", "<i4")])
+assert LAST_MP_DTYPE.itemsize == 28
+
+
+def stereo_struct(lkeys, ldesc, scale, rkeys, rdesc, lpyr, rpyr, inv_scale, bf, fx, width, height):
+    """Build an orb_stereo_input_t (shared by the oracle and the product wrappers)."""
+    f, keep = frame_struct(lkeys, ldesc, scale, width, height)
+    rkeys = np.ascontiguousarray(rkeys, KEYPOINT_DTYPE)
+    rdesc = np.ascontiguousarray(rdesc, np.uint8)
+    L = len(lpyr)
+    lp = [np.ascontiguousarray(a) for a in lpyr]
+    rp = [np.ascontiguousarray(a) for a in rpyr]
+    lptr = (ctypes.c_void_p * L)(*[a.ctypes.data for a in lp])
+    rptr = (ctypes.c_void_p * L)(*[a.ctypes.data for a in rp])
+    w = np.array([a.shape[1] for a in lp], np.int32)
+    h = np.array([a.shape[0] for a in lp], np.int32)
+    st = np.array([a.strides[0] for a in lp], np.int64)
+    inv = np.ascontiguousarray(inv_scale, np.float32)
+    s = _StereoInput()
+    s.left = ctypes.addressof(f)
+    s.n_right = len(rkeys)
+    s.right_keys, s.right_desc = _p(rkeys), _p(rdesc)
+    s.n_levels = L
+    s.left_levels = ctypes.addressof(lptr)
+    s.right_levels = ctypes.addressof(rptr)
+    s.level_width, s.level_height, s.level_stride = _p(w), _p(h), _p(st)
+    s.inv_scale_factors = _p(inv)
+    s.bf, s.fx = bf, fx
+    return s, (f, keep, rkeys, rdesc, lp, rp, lptr, rptr, w, h, st, inv)
+
+
+def stereo_match(*args):
+    s, keep = stereo_struct(*args)
+    n = keep[0].n
+    ur = np.full(n, -1, np.float32)
+    dp = np.full(n, -1, np.float32)
+    lib().oracle_stereo_match.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib().oracle_stereo_match(ctypes.byref(s), _p(ur), _p(dp))
+    return ur, dp
+
+
+def match_projection_frame(keys, desc, scale, width, height, last, last_desc, cam, tlc_z, th,
+                           mono, check_ori, kp_locked=None, u_right=None):
+    f, keep = frame_struct(keys, desc, scale, width, height, u_right)
+    last = np.ascontiguousarray(last, LAST_MP_DTYPE)
+    last_desc = np.ascontiguousarray(last_desc, np.uint8)
+    c = _Camera(*cam)
+    km = np.full(len(keys), -1, np.int32)
+    lk = None if kp_locked is None else np.ascontiguousarray(kp_locked, np.uint8)
+    fn = lib().oracle_match_projection_frame
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    n = fn(ctypes.byref(f), _p(lk) if lk is not None else None, len(last), _p(last),
+           _p(last_desc), ctypes.byref(c), tlc_z, th, int(mono), int(check_ori), _p(km))
+    return n, km
+
+
+def feature_vector(node_of):
+    """DBoW2 FeatureVector as CSR: (sorted node ids, offsets, feature indices ascending)."""
+    node_of = np.asarray(node_of, np.int64)
+    order = np.argsort(node_of, kind="stable")
+    ids, counts = np.unique(node_of, return_counts=True)
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    return ids.astype(np.uint32), offs, order.astype(np.uint32)
+
+
+def match_bow(kf_desc, kf_angle, kf_mp, kf_bad, kf_fv, f_desc, f_angle, f_fv, nnratio, check_ori):
+    kf_desc = np.ascontiguousarray(kf_desc, np.uint8)
+    f_desc = np.ascontiguousarray(f_desc, np.uint8)
+    kf_angle = np.ascontiguousarray(kf_angle, np.float32)
+    f_angle = np.ascontiguousarray(f_angle, np.float32)
+    kf_mp = np.ascontiguousarray(kf_mp, np.int32)
+    kf_bad = None if kf_bad is None else np.ascontiguousarray(kf_bad, np.uint8)
+    fm = np.full(len(f_desc), -1, np.int32)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fn = lib().oracle_match_bow
+    fn.argtypes = [i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, i32, vp]
+    fn.restype = i32
+    n = fn(len(kf_desc), _p(kf_desc), _p(kf_angle), _p(kf_mp),
+           _p(kf_bad) if kf_bad is not None else None, len(kf_fv[0]), _p(kf_fv[0]), _p(kf_fv[1]),
+           _p(kf_fv[2]), len(f_desc), _p(f_desc), _p(f_angle), len(f_fv[0]), _p(f_fv[0]),
+           _p(f_fv[1]), _p(f_fv[2]), nnratio, int(check_ori), _p(fm))
+    return n, fm

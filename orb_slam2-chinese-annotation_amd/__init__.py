@@ -34,7 +34,11 @@ MP_TRACK_DTYPE = np.dtype(
     [("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
      ("level", "<i4"), ("in_view", "u1"), ("bad", "u1"), ("has_obs", "u1"), ("_pad", "u1")]
 )
+LAST_MP_DTYPE = np.dtype([("xc", "<f4"), ("yc", "<f4"), ("invzc", "<f4"), ("last_octave", "<i4"),
+                          ("last_angle", "<f4"), ("valid", "u1"), ("has_obs", "u1"),
+                          ("_pad", "u1", 2), ("mp_id", "<i4")])
 assert KEYPOINT_DTYPE.itemsize == 28 and MP_TRACK_DTYPE.itemsize == 24
+assert LAST_MP_DTYPE.itemsize == 28
 
 
 class OrbError(RuntimeError):
@@ -110,6 +114,13 @@ def lib() -> ctypes.CDLL:
         "orb_match_projection_local_batch": (
             i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, f32, f32, f32, f32, i32, vp,
                   f32, f32, vp, vp, vp]),
+        "orb_stereo_match": (i32, [vp, vp, vp, vp]),
+        "orb_stereo_match_batch": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32,
+                                         vp, vp, vp, vp]),
+        "orb_match_projection_frame": (i32, [vp, vp, vp, i32, vp, vp, vp, f32, f32, i32, i32, vp,
+                                             vp]),
+        "orb_match_bow": (i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp,
+                                vp, vp, f32, i32, vp, vp]),
         "orb_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
         "orb_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     }
@@ -306,6 +317,22 @@ class Frame:
         return f
 
 
+class _StereoInput(ctypes.Structure):
+    _fields_ = [
+        ("left", ctypes.c_void_p), ("n_right", ctypes.c_int32), ("right_keys", ctypes.c_void_p),
+        ("right_desc", ctypes.c_void_p), ("n_levels", ctypes.c_int32),
+        ("left_levels", ctypes.c_void_p), ("right_levels", ctypes.c_void_p),
+        ("level_width", ctypes.c_void_p), ("level_height", ctypes.c_void_p),
+        ("level_stride", ctypes.c_void_p), ("inv_scale_factors", ctypes.c_void_p),
+        ("bf", ctypes.c_float), ("fx", ctypes.c_float),
+    ]
+
+
+class _Camera(ctypes.Structure):
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float),
+                ("cy", ctypes.c_float), ("bf", ctypes.c_float), ("mb", ctypes.c_float)]
+
+
 class ORBmatcher:
     """ORB_SLAM2::ORBmatcher(nnratio=0.6, checkOri=true)."""
 
@@ -385,3 +412,88 @@ class ORBmatcher:
             _ptr(mps) if len(mps) else None, _ptr(mp_desc) if len(mps) else None, th,
             self.mfNNratio, _ptr(kp_match), ctypes.byref(nm)), "SearchByProjection")
         return nm.value, kp_match
+
+
+    # ---------------------------------------------------- Frame::ComputeStereoMatches
+    def ComputeStereoMatches(self, left: Frame, right_keys, right_desc, left_pyramid,
+                             right_pyramid, inv_scale_factors, bf: float, fx: float):
+        """Frame::ComputeStereoMatches (src/Frame.cc:516-704): (mvuRight, mvDepth)."""
+        rk = np.ascontiguousarray(right_keys, KEYPOINT_DTYPE)
+        rd = np.ascontiguousarray(right_desc, np.uint8).reshape(-1, 32)
+        L = len(left_pyramid)
+        lp = [np.ascontiguousarray(a, np.uint8) for a in left_pyramid]
+        rp = [np.ascontiguousarray(a, np.uint8) for a in right_pyramid]
+        for a, b in zip(lp, rp):
+            if a.shape != b.shape:
+                raise OrbError(ORB_EINVAL, "left/right pyramid level shapes differ")
+        lptr = (ctypes.c_void_p * L)(*[a.ctypes.data for a in lp])
+        rptr = (ctypes.c_void_p * L)(*[a.ctypes.data for a in rp])
+        w = np.array([a.shape[1] for a in lp], np.int32)
+        h = np.array([a.shape[0] for a in lp], np.int32)
+        st = np.array([a.strides[0] for a in lp], np.int64)
+        inv = np.ascontiguousarray(inv_scale_factors, np.float32)
+        f = left._c()
+        s = _StereoInput()
+        s.left = ctypes.addressof(f)
+        s.n_right = len(rk)
+        s.right_keys = _ptr(rk) if len(rk) else None
+        s.right_desc = _ptr(rd) if len(rk) else None
+        s.n_levels = L
+        s.left_levels, s.right_levels = ctypes.addressof(lptr), ctypes.addressof(rptr)
+        s.level_width, s.level_height, s.level_stride = _ptr(w), _ptr(h), _ptr(st)
+        s.inv_scale_factors = _ptr(inv)
+        s.bf, s.fx = bf, fx
+        ur = np.full(left.N, -1, np.float32)
+        dp = np.full(left.N, -1, np.float32)
+        _check(lib().orb_stereo_match(self._h, ctypes.byref(s), _ptr(ur), _ptr(dp)),
+               "ComputeStereoMatches")
+        return ur, dp
+
+    def stereo_match_batch(self, n_pairs, left_ext, right_ext, d_lk, d_ld, d_ln, d_rk, d_rd,
+                           d_rn, kp_stride, bf, fx, d_ur, d_depth, d_sad, stream: int = 0):
+        _check(lib().orb_stereo_match_batch(self._h, n_pairs, left_ext.handle, right_ext.handle,
+                                            d_lk, d_ld, d_ln, d_rk, d_rd, d_rn, kp_stride, bf, fx,
+                                            d_ur, d_depth, d_sad, stream or None),
+               "orb_stereo_match_batch")
+
+    # -------------------------------------------- SearchByProjection(F, LastFrame)
+    def SearchByProjectionFrame(self, current: Frame, last, last_desc, cam, tlc_z: float,
+                                th: float, bMono: bool, kp_locked=None):
+        """SearchByProjection(CurrentFrame, LastFrame, th, bMono): (nmatches, kp_match).
+        kp_match: MapPoint id assigned, -1 untouched, -2 reset by the rotation filter."""
+        last = np.ascontiguousarray(last, LAST_MP_DTYPE)
+        last_desc = np.ascontiguousarray(last_desc, np.uint8).reshape(-1, 32)
+        locked = None if kp_locked is None else np.ascontiguousarray(kp_locked, np.uint8)
+        c = _Camera(*cam)
+        km = np.full(current.N, -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f = current._c()
+        _check(lib().orb_match_projection_frame(
+            self._h, ctypes.byref(f), _ptr(locked) if locked is not None else None, len(last),
+            _ptr(last) if len(last) else None, _ptr(last_desc) if len(last) else None,
+            ctypes.byref(c), tlc_z, th, int(bMono), int(self.mbCheckOrientation), _ptr(km),
+            ctypes.byref(nm)), "SearchByProjection(F, LastFrame)")
+        return nm.value, km
+
+    # ------------------------------------------------------------- SearchByBoW
+    def SearchByBoW(self, kf_desc, kf_angle, kf_mp, kf_bad, kf_fv, f_desc, f_angle, f_fv):
+        """SearchByBoW(pKF, F, vpMapPointMatches): (nmatches, f_match).
+        *_fv = DBoW2 FeatureVector as (node ids ascending, offsets, feature indices)."""
+        kd = np.ascontiguousarray(kf_desc, np.uint8)
+        ka = np.ascontiguousarray(kf_angle, np.float32)
+        km = np.ascontiguousarray(kf_mp, np.int32)
+        kb = None if kf_bad is None else np.ascontiguousarray(kf_bad, np.uint8)
+        fd = np.ascontiguousarray(f_desc, np.uint8)
+        fa = np.ascontiguousarray(f_angle, np.float32)
+        kfv = [np.ascontiguousarray(kf_fv[0], np.uint32), np.ascontiguousarray(kf_fv[1], np.int32),
+               np.ascontiguousarray(kf_fv[2], np.uint32)]
+        ffv = [np.ascontiguousarray(f_fv[0], np.uint32), np.ascontiguousarray(f_fv[1], np.int32),
+               np.ascontiguousarray(f_fv[2], np.uint32)]
+        fm = np.full(len(fd), -1, np.int32)
+        nm = ctypes.c_int32(0)
+        _check(lib().orb_match_bow(
+            self._h, len(kd), _ptr(kd), _ptr(ka), _ptr(km), _ptr(kb) if kb is not None else None,
+            len(kfv[0]), _ptr(kfv[0]), _ptr(kfv[1]), _ptr(kfv[2]), len(fd), _ptr(fd), _ptr(fa),
+            len(ffv[0]), _ptr(ffv[0]), _ptr(ffv[1]), _ptr(ffv[2]), self.mfNNratio,
+            int(self.mbCheckOrientation), _ptr(fm), ctypes.byref(nm)), "SearchByBoW")
+        return nm.value, fm

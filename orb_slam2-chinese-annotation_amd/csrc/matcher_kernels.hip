@@ -8,6 +8,7 @@
 // stage that replays the sequential semantics exactly.
 #include "orb_device.h"
 #include "../../include/orb_abi.h"
+#include <algorithm>
 
 #define GRID_CELLS (ORB_GRID_COLS * ORB_GRID_ROWS)
 #define TOPK 4
@@ -413,3 +414,594 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
 size_t orb_k_proj_params_size(void) { return sizeof(ProjParams); }
 
 }  // extern "C"
+
+// ==================================================== Frame::ComputeStereoMatches
+// src/Frame.cc:516-704.  One wave per left keypoint:
+//  1. candidates = right keypoints whose row band [floor(y-2s), ceil(y+2s)]
+//     contains int(vL), octave within +-1, uR in [uL - maxD, uL]; the lanes
+//     scan the right keypoints strided and reduce (dist, iR) -> first minimum
+//     (the reference scans vRowIndices[vL] in ascending iR, strict <).
+//  2. 11x11 SAD (patch minus its centre) at the left octave for the 11 shifts,
+//     parabola sub-pixel, disparity window, depth = bf / disparity.
+// k_stereo_prune then drops matches whose SAD >= 1.5*1.4*median (:690-703).
+struct StereoParams {
+  int nLevels;
+  float bf, fx;
+  int w[ORB_MAX_LEVELS], h[ORB_MAX_LEVELS];
+  int strideL[ORB_MAX_LEVELS], strideR[ORB_MAX_LEVELS];
+  float scale[ORB_MAX_LEVELS], invScale[ORB_MAX_LEVELS];
+};
+
+struct StereoPairLevels {
+  const uint8_t* L[ORB_MAX_LEVELS];
+  const uint8_t* R[ORB_MAX_LEVELS];
+};
+
+__global__ __launch_bounds__(256) void k_stereo_match(
+    const orb_keypoint_t* __restrict__ lkeys, const uint8_t* __restrict__ ldesc,
+    const int32_t* __restrict__ nleft, const orb_keypoint_t* __restrict__ rkeys,
+    const uint8_t* __restrict__ rdesc, const int32_t* __restrict__ nright, int kpStride,
+    const StereoPairLevels* __restrict__ pyr, StereoParams P, float* __restrict__ uRight,
+    float* __restrict__ depth, int32_t* __restrict__ sad) {
+  const int pair = blockIdx.y, lane = threadIdx.x & 63;
+  const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int NL = nleft[pair], NR = nright[pair];
+  if (iL >= NL) return;
+  const size_t base = (size_t)pair * kpStride;
+  const orb_keypoint_t kpL = lkeys[base + iL];
+  float ur = -1.0f, dp = -1.0f;
+  int sadOut = -1;
+  const float mb = P.bf / P.fx;
+  const float minZ = mb, minD = 0.f, maxD = P.bf / minZ;
+  const int levelL = kpL.octave;
+  const float vL = kpL.y, uL = kpL.x;
+  const int row = (int)vL;  // vRowIndices[vL]: float -> size_t truncation
+  const float minU = uL - maxD, maxU = uL - minD;
+  int bestDist = 1 << 30, bestIdx = 1 << 30;
+  if (maxU >= 0) {
+    const ulonglong4 dL = load_desc(ldesc + (base + iL) * 32);
+    for (int iR = lane; iR < NR; iR += 64) {
+      const orb_keypoint_t kpR = rkeys[base + iR];
+      const float r = 2.0f * P.scale[kpR.octave];
+      const int maxr = (int)ceilf(kpR.y + r), minr = (int)floorf(kpR.y - r);
+      if (row < minr || row > maxr) continue;
+      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+      const float uR = kpR.x;
+      if (!(uR >= minU && uR <= maxU)) continue;
+      const int dist = hamming256(dL, load_desc(rdesc + (base + iR) * 32));
+      if (dist < bestDist) { bestDist = dist; bestIdx = iR; }  // lane's iR ascend
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int od = __shfl_xor(bestDist, o, 64), oi = __shfl_xor(bestIdx, o, 64);
+    if (od < bestDist || (od == bestDist && oi < bestIdx)) { bestDist = od; bestIdx = oi; }
+  }
+  // bestDist starts at TH_HIGH=100 in the reference; accept below (100+50)/2
+  if (maxU >= 0 && bestDist < 75) {
+    const float uR0 = rkeys[base + bestIdx].x;
+    const float sf = P.invScale[levelL];
+    const float scaleduL = round_half_away(kpL.x * sf);
+    const float scaledvL = round_half_away(kpL.y * sf);
+    const float scaleduR0 = round_half_away(uR0 * sf);
+    const int w = 5, L = 5;
+    const float iniu = scaleduR0 + L - w;
+    const float endu = scaleduR0 + L + w + 1;
+    if (!(iniu < 0 || endu >= P.w[levelL])) {
+      const uint8_t* IL = pyr[pair].L[levelL];
+      const uint8_t* IR = pyr[pair].R[levelL];
+      const int sL = P.strideL[levelL], sR = P.strideR[levelL];
+      const int y0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
+      const int cL = IL[(long long)(y0 + w) * sL + xl0 + w];
+      int dists[11];
+#pragma unroll
+      for (int inc = -L; inc <= L; ++inc) {
+        const int xr0 = (int)scaleduR0 + inc - w;
+        const int cR = IR[(long long)(y0 + w) * sR + xr0 + w];
+        int acc = 0;
+        for (int p = lane; p < 121; p += 64) {
+          const int yy = p / 11, xx = p - yy * 11;
+          const int a = (int)IL[(long long)(y0 + yy) * sL + xl0 + xx] - cL;
+          const int b = (int)IR[(long long)(y0 + yy) * sR + xr0 + xx] - cR;
+          acc += abs(a - b);
+        }
+        dists[inc + L] = wave_sum(acc);
+      }
+      int bestSad = 2147483647, bestinc = 0;
+#pragma unroll
+      for (int inc = -L; inc <= L; ++inc)
+        if ((float)dists[inc + L] < (float)bestSad) { bestSad = dists[inc + L]; bestinc = inc; }
+      if (bestinc != -L && bestinc != L) {
+        const float dist1 = (float)dists[L + bestinc - 1], dist2 = (float)dists[L + bestinc],
+                    dist3 = (float)dists[L + bestinc + 1];
+        const float deltaR = __fdiv_rn(dist1 - dist3, 2.0f * (dist1 + dist3 - 2.0f * dist2));
+        if (!(deltaR < -1 || deltaR > 1)) {
+          float bestuR = P.scale[levelL] * ((float)scaleduR0 + (float)bestinc + deltaR);
+          float disparity = uL - bestuR;
+          if (disparity >= minD && disparity < maxD) {
+            if (disparity <= 0) {
+              disparity = 0.01f;
+              bestuR = (float)((double)uL - 0.01);
+            }
+            dp = __fdiv_rn(P.bf, disparity);
+            ur = bestuR;
+            sadOut = bestSad;
+          }
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    uRight[base + iL] = ur;
+    depth[base + iL] = dp;
+    sad[base + iL] = sadOut;
+  }
+}
+
+// Median-based outlier rejection: k-th smallest SAD by bisection on the value
+// (k = V/2 of the V valid matches, == vDistIdx[size/2] after the sort), then
+// every match with SAD >= 1.5*1.4*median is reset to -1.  One block per pair.
+__global__ __launch_bounds__(256) void k_stereo_prune(const int32_t* __restrict__ nleft,
+                                                      int kpStride, float* __restrict__ uRight,
+                                                      float* __restrict__ depth,
+                                                      const int32_t* __restrict__ sad) {
+  __shared__ int tmp[17];
+  const int pair = blockIdx.x, t = threadIdx.x;
+  const int NL = nleft[pair];
+  const size_t base = (size_t)pair * kpStride;
+  int c = 0;
+  for (int i = t; i < NL; i += 256) c += sad[base + i] >= 0;
+  int V;
+  block_excl_scan(c, tmp, &V);
+  if (V == 0) return;  // the reference indexes an empty vector here (undefined)
+  const int k = V / 2;
+  int lo = 0, hi = 1 << 20;  // smallest v with count(sad <= v) > k
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    int cnt = 0;
+    for (int i = t; i < NL; i += 256) {
+      const int s = sad[base + i];
+      cnt += (s >= 0 && s <= mid);
+    }
+    int tot;
+    block_excl_scan(cnt, tmp, &tot);
+    if (tot > k) hi = mid; else lo = mid + 1;
+  }
+  const float median = (float)lo;
+  const float thDist = 1.5f * 1.4f * median;
+  for (int i = t; i < NL; i += 256) {
+    const int s = sad[base + i];
+    if (s >= 0 && !((float)s < thDist)) {
+      uRight[base + i] = -1.0f;
+      depth[base + i] = -1.0f;
+    }
+  }
+}
+
+extern "C" size_t orb_k_stereo_params_size(void) { return sizeof(StereoParams); }
+
+extern "C" hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc,
+                                   const int32_t* nleft, const orb_keypoint_t* rkeys,
+                                   const uint8_t* rdesc, const int32_t* nright, int kpStride,
+                                   int maxLeft, const void* pyr, const void* params,
+                                   float* uRight, float* depth, int32_t* sad, int npairs,
+                                   hipStream_t s) {
+  if (npairs <= 0 || maxLeft <= 0) return hipSuccess;
+  const StereoParams P = *(const StereoParams*)params;
+  hipLaunchKernelGGL(k_stereo_match, dim3((maxLeft + 3) / 4, npairs), dim3(256), 0, s, lkeys,
+                     ldesc, nleft, rkeys, rdesc, nright, kpStride,
+                     (const StereoPairLevels*)pyr, P, uRight, depth, sad);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_stereo_prune, dim3(npairs), dim3(256), 0, s, nleft, kpStride, uRight,
+                     depth, sad);
+  return hipGetLastError();
+}
+
+// ========================================== rotation consistency (shared)
+// src/ORBmatcher.cc:1582-1588: bin = round(rot * (1/30)) with rot in [0,360)
+// -> only bins 0..12 are ever used (upstream quirk, kept).
+__device__ __forceinline__ int rot_bin(float rot) {
+  const float factor = 1.0f / 30;
+  if (rot < 0.0f) rot += 360.0f;
+  int bin = (int)round_half_away(rot * factor);
+  if (bin == 30) bin = 0;
+  return bin;
+}
+
+// ComputeThreeMaxima (src/ORBmatcher.cc:1765-1809) over 30 bin counts.
+__device__ __forceinline__ void three_maxima(const int* h, int& ind1, int& ind2, int& ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  ind1 = ind2 = ind3 = -1;
+  for (int i = 0; i < 30; ++i) {
+    const int s = h[i];
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s; ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+  else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+// ============================== SearchByProjection(CurrentFrame, LastFrame)
+// src/ORBmatcher.cc:1460-1619.  k_frame_candidates: per last-frame point, the
+// first K candidates in (distance, scan order).  k_frame_resolve: one wave per
+// problem replays the sequential loop (first-come locks by points with
+// observations), then the rotation histogram filter.
+struct FrameProjParams {
+  float minX, maxX, minY, maxY, invW, invH;
+  float fx, fy, cx, cy, bf;
+  float th;
+  int fwd, bwd, checkOri;
+  float scale[ORB_MAX_LEVELS];
+};
+
+__global__ __launch_bounds__(256) void k_frame_candidates(
+    const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
+    const float* __restrict__ uright, const uint8_t* __restrict__ locked,
+    const orb_last_mp_t* __restrict__ last, const uint8_t* __restrict__ lastDesc, int nlast,
+    const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, FrameProjParams F,
+    uint32_t* __restrict__ topk, int32_t* __restrict__ ncand) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nlast) return;
+  const orb_last_mp_t L = last[i];
+  ncand[i] = -1;
+  if (!L.valid) return;
+  const float invzc = L.invzc;
+  if (invzc < 0) return;
+  const float u = F.fx * L.xc * invzc + F.cx;
+  const float v = F.fy * L.yc * invzc + F.cy;
+  if (u < F.minX || u > F.maxX) return;
+  if (v < F.minY || v > F.maxY) return;
+  const int o = L.last_octave;
+  const float radius = F.th * F.scale[o];
+  ProjParams P;
+  P.minX = F.minX; P.minY = F.minY; P.invW = F.invW; P.invH = F.invH;
+  int minL, maxL;
+  if (F.fwd) { minL = o; maxL = -1; }
+  else if (F.bwd) { minL = 0; maxL = o; }
+  else { minL = o - 1; maxL = o + 1; }
+  const ulonglong4 q = load_desc(lastDesc + (size_t)i * 32);
+  uint32_t top[TOPK];
+  int ntop = 0, count = 0;
+  for_features_in_area(keys, cellStart, cellIdx, P, u, v, radius, minL, maxL,
+                       [&](int idx, const orb_keypoint_t& kp) {
+                         if (locked && locked[idx]) return;
+                         if (uright && uright[idx] > 0) {
+                           const float ur = u - F.bf * invzc;
+                           const float er = fabsf(ur - uright[idx]);
+                           if (er > radius) return;
+                         }
+                         const int dist = hamming256(q, load_desc(desc + (size_t)idx * 32));
+                         if (dist >= 256) return;
+                         ++count;
+                         int pos = ntop;
+                         while (pos > 0 && cand_dist(top[pos - 1]) > dist) --pos;
+                         if (pos >= TOPK) return;
+                         const int lastj = ntop < TOPK ? ntop : TOPK - 1;
+                         for (int j = lastj; j > pos; --j) top[j] = top[j - 1];
+                         top[pos] = pack_cand(idx, dist, kp.octave);
+                         if (ntop < TOPK) ++ntop;
+                       });
+  for (int j = 0; j < TOPK; ++j) topk[(size_t)i * TOPK + j] = j < ntop ? top[j] : 0xFFFFFFFFu;
+  ncand[i] = count;
+}
+
+__global__ __launch_bounds__(64) void k_frame_resolve(
+    const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
+    const float* __restrict__ uright, const uint8_t* __restrict__ locked, int nkeys,
+    const orb_last_mp_t* __restrict__ last, const uint8_t* __restrict__ lastDesc, int nlast,
+    const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, FrameProjParams F,
+    const uint32_t* __restrict__ topk, const int32_t* __restrict__ ncand,
+    int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches) {
+  // LDS: in-call lock bits, earliest claiming lane of the window, the last
+  // point assigned to each keypoint, the accepted keypoint of each point
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  __shared__ int hist[32];
+  const int lane = threadIdx.x;
+  const int words = (nkeys + 31) >> 5;
+  const int wpad = (words + 3) & ~3, npad = (nkeys + 3) & ~3;
+  uint32_t* bm = dyn;
+  int* claimBy = (int*)(dyn + wpad);
+  int* lastWriter = claimBy + npad;
+  int* accIdx = lastWriter + npad;
+  for (int i = lane; i < words; i += 64) bm[i] = 0u;
+  for (int i = lane; i < nkeys; i += 64) { claimBy[i] = 64; lastWriter[i] = -1; }
+  if (lane < 32) hist[lane] = 0;
+  __syncthreads();
+  int start = 0;
+  while (start < nlast) {
+    const int m = start + lane;
+    const bool active = m < nlast;
+    int nc = -1;
+    uint32_t e[TOPK];
+    bool hasObs = false;
+    if (active) {
+      nc = ncand[m];
+      for (int j = 0; j < TOPK; ++j) e[j] = topk[(size_t)m * TOPK + j];
+      hasObs = last[m].has_obs != 0;
+    }
+    int best = -1, bestDist = 256, consumed = 0;
+    if (nc > 0) {
+      const int avail = nc < TOPK ? nc : TOPK;
+      for (int j = 0; j < avail; ++j) {
+        ++consumed;
+        if (lock_test(bm, cand_idx(e[j]))) continue;
+        best = cand_idx(e[j]);
+        bestDist = cand_dist(e[j]);
+        break;
+      }
+    }
+    const bool slow = nc > TOPK && best < 0;
+    const bool accept = !slow && best >= 0 && bestDist <= 100;
+    const bool locks = accept && hasObs;
+    if (locks) atomicMin(&claimBy[best], lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bool conflict = false;
+    for (int q = 0; q < consumed; ++q) conflict |= claimBy[cand_idx(e[q])] < lane;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (locks) claimBy[best] = 64;
+    const unsigned long long bad = __ballot(active && (conflict || (slow && lane > 0)));
+    const unsigned long long slowFirst = __ballot(lane == 0 && active && slow);
+    int commit = bad ? (int)__builtin_ctzll(bad) : 64;
+    if (slowFirst) {
+      if (lane == 0) {  // exact re-scan against the current locks
+        const orb_last_mp_t L = last[m];
+        const float invzc = L.invzc;
+        const float u = F.fx * L.xc * invzc + F.cx;
+        const float v = F.fy * L.yc * invzc + F.cy;
+        const int o = L.last_octave;
+        const float radius = F.th * F.scale[o];
+        ProjParams P;
+        P.minX = F.minX; P.minY = F.minY; P.invW = F.invW; P.invH = F.invH;
+        int minL, maxL;
+        if (F.fwd) { minL = o; maxL = -1; }
+        else if (F.bwd) { minL = 0; maxL = o; }
+        else { minL = o - 1; maxL = o + 1; }
+        const ulonglong4 q = load_desc(lastDesc + (size_t)m * 32);
+        int bd = 256, bi = -1;
+        for_features_in_area(keys, cellStart, cellIdx, P, u, v, radius, minL, maxL,
+                             [&](int idx, const orb_keypoint_t& kp) {
+                               if ((locked && locked[idx]) || lock_test(bm, idx)) return;
+                               if (uright && uright[idx] > 0) {
+                                 const float ur = u - F.bf * invzc;
+                                 if (fabsf(ur - uright[idx]) > radius) return;
+                               }
+                               const int dist = hamming256(q, load_desc(desc + (size_t)idx * 32));
+                               if (dist < bd) { bd = dist; bi = idx; }
+                             });
+        accIdx[m] = -1;
+        if (bd <= 100) {
+          accIdx[m] = bi;
+          atomicMax(&lastWriter[bi], m);
+          if (hasObs) bm[bi >> 5] |= 1u << (bi & 31);
+          if (F.checkOri) atomicAdd(&hist[rot_bin(L.last_angle - keys[bi].angle)], 1);
+        }
+      }
+      commit = 1;
+    } else {
+      if (active && lane < commit) {
+        accIdx[m] = accept ? best : -1;
+        if (accept) {
+          atomicMax(&lastWriter[best], m);
+          if (locks) atomicOr(&bm[best >> 5], 1u << (best & 31));
+          if (F.checkOri) atomicAdd(&hist[rot_bin(last[m].last_angle - keys[best].angle)], 1);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    start += commit;
+  }
+  // rotation filter: records of the bins outside the top 3 are undone
+  int ind1 = -1, ind2 = -1, ind3 = -1;
+  if (F.checkOri) three_maxima(hist, ind1, ind2, ind3);
+  uint32_t* cleared = bm;  // reuse: bit set = keypoint reset to NULL by the filter
+  for (int i = lane; i < words; i += 64) cleared[i] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int removed = 0, accepted = 0;
+  for (int m = lane; m < nlast; m += 64) {
+    const int bi = accIdx[m];
+    if (bi < 0) continue;
+    ++accepted;
+    if (!F.checkOri) continue;
+    const int b = rot_bin(last[m].last_angle - keys[bi].angle);
+    if (b != ind1 && b != ind2 && b != ind3) {
+      ++removed;
+      atomicOr(&cleared[bi >> 5], 1u << (bi & 31));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // kpMatch: MapPoint id assigned by this call, -1 untouched, -2 reset to NULL
+  for (int i = lane; i < nkeys; i += 64) {
+    const int wr = lastWriter[i];
+    if ((cleared[i >> 5] >> (i & 31)) & 1u) kpMatch[i] = -2;
+    else kpMatch[i] = wr >= 0 ? last[wr].mp_id : -1;
+  }
+  const int acc = wave_sum(accepted), rem = wave_sum(removed);
+  if (lane == 0) *nmatches = acc - rem;
+}
+
+extern "C" size_t orb_k_frame_params_size(void) { return sizeof(FrameProjParams); }
+
+extern "C" hipError_t orb_k_frame_proj(const orb_keypoint_t* keys, const uint8_t* desc,
+                                       const float* uright, const uint8_t* locked, int nkeys,
+                                       const orb_last_mp_t* last, const uint8_t* lastDesc,
+                                       int nlast, const int32_t* cellStart,
+                                       const int32_t* cellIdx, const void* params,
+                                       uint32_t* topk, int32_t* ncand, int32_t* kpMatch,
+                                       int32_t* nmatches, hipStream_t s) {
+  const FrameProjParams F = *(const FrameProjParams*)params;
+  if (nlast > 0) {
+    hipLaunchKernelGGL(k_frame_candidates, dim3((nlast + 255) / 256), dim3(256), 0, s, keys,
+                       desc, uright, locked, last, lastDesc, nlast, cellStart, cellIdx, F, topk,
+                       ncand);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const size_t words = (size_t)((nkeys + 31) / 32);
+  const size_t lds = (((words + 3) & ~(size_t)3) + 2 * (((size_t)nkeys + 3) & ~(size_t)3) +
+                      (size_t)std::max(nlast, 1)) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_frame_resolve,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_frame_resolve, dim3(1), dim3(64), lds, s, keys, desc, uright, locked,
+                     nkeys, last, lastDesc, nlast, cellStart, cellIdx, F, topk, ncand, kpMatch,
+                     nmatches);
+  return hipGetLastError();
+}
+
+// ====================================== SearchByBoW(KeyFrame*, Frame&, ...)
+// src/ORBmatcher.cc:164-306.  A frame feature belongs to exactly one vocabulary
+// node, and claims (vpMapPointMatches[realIdxF]) only ever involve features of
+// the node being matched, so nodes are independent: one wave per KeyFrame
+// node finds its Frame node by binary search and replays the node's loop
+// sequentially, lanes sharing the brute-force distance scan.  k_bow_finish
+// applies the rotation histogram filter.
+__global__ __launch_bounds__(256) void k_bow_match(
+    const uint8_t* __restrict__ kfDesc, const float* __restrict__ kfAngle,
+    const int32_t* __restrict__ kfMp, const uint8_t* __restrict__ kfBad, int kfNodes,
+    const uint32_t* __restrict__ kfNodeIds, const int32_t* __restrict__ kfOffs,
+    const uint32_t* __restrict__ kfFeats, const uint8_t* __restrict__ fDesc,
+    const float* __restrict__ fAngle, int fNodes, const uint32_t* __restrict__ fNodeIds,
+    const int32_t* __restrict__ fOffs, const uint32_t* __restrict__ fFeats, float nnratio,
+    int nF, int32_t* __restrict__ fMatch, int32_t* __restrict__ accF) {
+  // per-wave LDS bitmap of the frame features this wave's node has claimed
+  extern __shared__ __attribute__((aligned(16))) uint32_t claimBits[];
+  const int lane = threadIdx.x & 63;
+  const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int words = (nF + 31) >> 5;
+  uint32_t* claimed = claimBits + (threadIdx.x >> 6) * words;
+  for (int i = lane; i < words; i += 64) claimed[i] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (a >= kfNodes) return;
+  const uint32_t id = kfNodeIds[a];
+  int lo = 0, hi = fNodes;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (fNodeIds[mid] < id) lo = mid + 1; else hi = mid;
+  }
+  const bool found = lo < fNodes && fNodeIds[lo] == id;
+  for (int p = kfOffs[a]; p < kfOffs[a + 1]; ++p) {
+    accF[p] = -1;
+    if (!found) continue;
+    const int realIdxKF = (int)kfFeats[p];
+    if (kfMp[realIdxKF] < 0) continue;
+    if (kfBad && kfBad[realIdxKF]) continue;
+    const ulonglong4 dKF = load_desc(kfDesc + (size_t)realIdxKF * 32);
+    const int fb = fOffs[lo], fe = fOffs[lo + 1];
+    // per-lane first-two in (dist, position) order, then a wave merge
+    int d1 = 256, q1 = 1 << 30, d2 = 256, q2 = 1 << 30;
+    for (int q = fb + lane; q < fe; q += 64) {
+      const int realIdxF = (int)fFeats[q];
+      if ((claimed[realIdxF >> 5] >> (realIdxF & 31)) & 1u) continue;
+      const int dist = hamming256(dKF, load_desc(fDesc + (size_t)realIdxF * 32));
+      if (dist < d1) { d2 = d1; q2 = q1; d1 = dist; q1 = q; }
+      else if (dist < d2) { d2 = dist; q2 = q; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int od1 = __shfl_xor(d1, o, 64), oq1 = __shfl_xor(q1, o, 64);
+      const int od2 = __shfl_xor(d2, o, 64), oq2 = __shfl_xor(q2, o, 64);
+      // merge two sorted pairs by (dist, position)
+      const bool mineFirst = d1 < od1 || (d1 == od1 && q1 < oq1);
+      int n1d, n1q, c1d, c1q, c2d, c2q;
+      if (mineFirst) { n1d = d1; n1q = q1; c1d = d2; c1q = q2; c2d = od1; c2q = oq1; }
+      else { n1d = od1; n1q = oq1; c1d = od2; c1q = oq2; c2d = d1; c2q = q1; }
+      const bool c1First = c1d < c2d || (c1d == c2d && c1q < c2q);
+      d1 = n1d; q1 = n1q;
+      d2 = c1First ? c1d : c2d;
+      q2 = c1First ? c1q : c2q;
+    }
+    if (d1 <= 50 && (float)d1 < nnratio * (float)d2) {  // TH_LOW, ratio (:239-242)
+      const int realIdxF = (int)fFeats[q1];
+      if (lane == 0) {
+        claimed[realIdxF >> 5] |= 1u << (realIdxF & 31);
+        fMatch[realIdxF] = kfMp[realIdxKF];
+        accF[p] = realIdxF;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bow_finish(
+    int nKfFeats, const uint32_t* __restrict__ kfFeats, const float* __restrict__ kfAngle,
+    const float* __restrict__ fAngle, int checkOri, const int32_t* __restrict__ accF,
+    int32_t* __restrict__ fMatch, int32_t* __restrict__ nmatches) {
+  __shared__ int hist[32];
+  __shared__ int tmp[17];
+  const int t = threadIdx.x;
+  if (t < 32) hist[t] = 0;
+  __syncthreads();
+  int acc = 0;
+  for (int p = t; p < nKfFeats; p += 256) {
+    const int f = accF[p];
+    if (f < 0) continue;
+    ++acc;
+    if (checkOri) atomicAdd(&hist[rot_bin(kfAngle[kfFeats[p]] - fAngle[f])], 1);
+  }
+  __syncthreads();
+  int ind1 = -1, ind2 = -1, ind3 = -1;
+  if (checkOri) three_maxima(hist, ind1, ind2, ind3);
+  int removed = 0;
+  if (checkOri) {
+    for (int p = t; p < nKfFeats; p += 256) {
+      const int f = accF[p];
+      if (f < 0) continue;
+      const int b = rot_bin(kfAngle[kfFeats[p]] - fAngle[f]);
+      if (b != ind1 && b != ind2 && b != ind3) {
+        fMatch[f] = -1;
+        ++removed;
+      }
+    }
+  }
+  int totA, totR;
+  block_excl_scan(acc, tmp, &totA);
+  block_excl_scan(removed, tmp, &totR);
+  if (t == 0) *nmatches = totA - totR;
+}
+
+extern "C" hipError_t orb_k_bow(const uint8_t* kfDesc, const float* kfAngle, const int32_t* kfMp,
+                                const uint8_t* kfBad, int kfNodes, const uint32_t* kfNodeIds,
+                                const int32_t* kfOffs, const uint32_t* kfFeats, int nKfFeats,
+                                const uint8_t* fDesc, const float* fAngle, int fNodes,
+                                const uint32_t* fNodeIds, const int32_t* fOffs,
+                                const uint32_t* fFeats, int nF, float nnratio, int checkOri,
+                                int32_t* fMatch, int32_t* accF, int32_t* nmatches,
+                                hipStream_t s) {
+  if (kfNodes > 0) {
+    const size_t lds = 4 * (size_t)((nF + 31) / 32) * 4;
+    if (lds > 65536) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bow_match, dim3((kfNodes + 3) / 4), dim3(256), lds, s, kfDesc, kfAngle,
+                       kfMp, kfBad, kfNodes, kfNodeIds, kfOffs, kfFeats, fDesc, fAngle, fNodes,
+                       fNodeIds, fOffs, fFeats, nnratio, nF, fMatch, accF);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_bow_finish, dim3(1), dim3(256), 0, s, nKfFeats, kfFeats, kfAngle, fAngle,
+                     checkOri, accF, fMatch, nmatches);
+  return hipGetLastError();
+}

@@ -65,6 +65,24 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
                               const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
                               int nproblems, hipStream_t s);
 size_t orb_k_proj_params_size(void);
+size_t orb_k_stereo_params_size(void);
+hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc, const int32_t* nleft,
+                        const orb_keypoint_t* rkeys, const uint8_t* rdesc, const int32_t* nright,
+                        int kpStride, int maxLeft, const void* pyr, const void* params,
+                        float* uRight, float* depth, int32_t* sad, int npairs, hipStream_t s);
+size_t orb_k_frame_params_size(void);
+hipError_t orb_k_frame_proj(const orb_keypoint_t* keys, const uint8_t* desc, const float* uright,
+                            const uint8_t* locked, int nkeys, const orb_last_mp_t* last,
+                            const uint8_t* lastDesc, int nlast, const int32_t* cellStart,
+                            const int32_t* cellIdx, const void* params, uint32_t* topk,
+                            int32_t* ncand, int32_t* kpMatch, int32_t* nmatches, hipStream_t s);
+hipError_t orb_k_bow(const uint8_t* kfDesc, const float* kfAngle, const int32_t* kfMp,
+                     const uint8_t* kfBad, int kfNodes, const uint32_t* kfNodeIds,
+                     const int32_t* kfOffs, const uint32_t* kfFeats, int nKfFeats,
+                     const uint8_t* fDesc, const float* fAngle, int fNodes,
+                     const uint32_t* fNodeIds, const int32_t* fOffs, const uint32_t* fFeats,
+                     int nF, float nnratio, int checkOri, int32_t* fMatch, int32_t* accF,
+                     int32_t* nmatches, hipStream_t s);
 }
 
 namespace {
@@ -716,6 +734,25 @@ struct ProjParamsHost {  // mirrors ProjParams in matcher_kernels.hip
   float scale[ORB_MAX_LEVELS];
 };
 
+struct StereoParamsHost {  // mirrors StereoParams in matcher_kernels.hip
+  int nLevels;
+  float bf, fx;
+  int w[ORB_MAX_LEVELS], h[ORB_MAX_LEVELS];
+  int strideL[ORB_MAX_LEVELS], strideR[ORB_MAX_LEVELS];
+  float scale[ORB_MAX_LEVELS], invScale[ORB_MAX_LEVELS];
+};
+struct StereoPairLevelsHost {
+  const uint8_t* L[ORB_MAX_LEVELS];
+  const uint8_t* R[ORB_MAX_LEVELS];
+};
+struct FrameProjParamsHost {  // mirrors FrameProjParams
+  float minX, maxX, minY, maxY, invW, invH;
+  float fx, fy, cx, cy, bf;
+  float th;
+  int fwd, bwd, checkOri;
+  float scale[ORB_MAX_LEVELS];
+};
+
 struct orb_matcher {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -724,6 +761,10 @@ struct orb_matcher {
   StageProfiler prof;
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
+  // stereo / frame / BoW scratch
+  DevBuf dRKeys, dRDesc, dNR, dPyr, dPairLv, dDepth, dSad, dBowA, dBowB, dBowC, dBowD, dBowE,
+      dBowF, dBowG, dBowH, dBowI, dBowJ, dBowK;
+  std::vector<uint8_t> hostScratch;
 };
 
 extern "C" {
@@ -746,7 +787,10 @@ orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
   *out = nullptr;
   orb_status_t st = check_device(device);
   if (st) return st;
-  if (orb_k_proj_params_size() != sizeof(ProjParamsHost)) return ORB_EINVAL;
+  if (orb_k_proj_params_size() != sizeof(ProjParamsHost) ||
+      orb_k_stereo_params_size() != sizeof(StereoParamsHost) ||
+      orb_k_frame_params_size() != sizeof(FrameProjParamsHost))
+    return ORB_EINVAL;
   orb_matcher* m = new orb_matcher();
   m->device = device;
   m->prof.nStages = 3;
@@ -769,7 +813,10 @@ void orb_matcher_destroy(orb_matcher_t* m) {
   hipStreamSynchronize(m->stream);
   DevBuf* bufs[] = {&m->dKeys, &m->dDesc, &m->dUr, &m->dLocked, &m->dNKeys, &m->dMps,
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
-                    &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut};
+                    &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut,
+                    &m->dRKeys, &m->dRDesc, &m->dNR, &m->dPyr, &m->dPairLv, &m->dDepth,
+                    &m->dSad, &m->dBowA, &m->dBowB, &m->dBowC, &m->dBowD, &m->dBowE,
+                    &m->dBowF, &m->dBowG, &m->dBowH, &m->dBowI, &m->dBowJ, &m->dBowK};
   for (DevBuf* b : bufs) b->release();
   m->prof.destroy();
   hipStreamDestroy(m->stream);
@@ -930,6 +977,244 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
                              m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
                              m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), 1, s));
   HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+// ------------------------------------------------------------------ stereo
+static orb_status_t upload(DevBuf& b, const void* src, size_t n, hipStream_t s) {
+  orb_status_t st = b.ensure(std::max<size_t>(n, 16));
+  if (st) return st;
+  if (n) HIP_TRY(hipMemcpyAsync(b.p, src, n, hipMemcpyHostToDevice, s));
+  return ORB_OK;
+}
+
+orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in, float* u_right,
+                              float* depth) {
+  if (!m || !in || !in->left || !u_right || !depth) return ORB_EINVAL;
+  const orb_frame_t* F = in->left;
+  const int NL = F->n, NR = in->n_right, L = in->n_levels;
+  if (NL < 0 || NR < 0 || L <= 0 || L > ORB_MAX_LEVELS || !F->scale_factors ||
+      !in->inv_scale_factors || !in->left_levels || !in->right_levels || !in->level_width ||
+      !in->level_height || !in->level_stride || !(in->fx > 0))
+    return ORB_EINVAL;
+  for (int i = 0; i < NL; ++i) { u_right[i] = -1.0f; depth[i] = -1.0f; }
+  if (NL == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  const int stride = std::max(NL, std::max(NR, 1));
+  orb_status_t st;
+  if ((st = upload(m->dKeys, F->keys, (size_t)NL * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(m->dDesc, F->descriptors, (size_t)NL * 32, s))) return st;
+  if ((st = upload(m->dRKeys, in->right_keys, (size_t)NR * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(m->dRDesc, in->right_desc, (size_t)NR * 32, s))) return st;
+  const int32_t nl = NL, nr = NR;
+  if ((st = upload(m->dNKeys, &nl, 4, s))) return st;
+  if ((st = upload(m->dNR, &nr, 4, s))) return st;
+  // both pyramids, packed with 64-byte pitches
+  StereoParamsHost P;
+  memset(&P, 0, sizeof(P));
+  P.nLevels = L;
+  P.bf = in->bf;
+  P.fx = in->fx;
+  size_t total = 0;
+  std::vector<size_t> off(L);
+  for (int l = 0; l < L; ++l) {
+    P.w[l] = in->level_width[l];
+    P.h[l] = in->level_height[l];
+    P.strideL[l] = P.strideR[l] = (P.w[l] + 63) & ~63;
+    P.scale[l] = F->scale_factors[l];
+    P.invScale[l] = in->inv_scale_factors[l];
+    off[l] = total;
+    total += 2 * (size_t)P.strideL[l] * P.h[l];
+  }
+  if ((st = m->dPyr.ensure(total))) return st;
+  StereoPairLevelsHost lv;
+  memset(&lv, 0, sizeof(lv));
+  uint8_t* base = m->dPyr.as<uint8_t>();
+  for (int l = 0; l < L; ++l) {
+    uint8_t* dl = base + off[l];
+    uint8_t* dr = dl + (size_t)P.strideL[l] * P.h[l];
+    HIP_TRY(hipMemcpy2DAsync(dl, P.strideL[l], in->left_levels[l], (size_t)in->level_stride[l],
+                             P.w[l], P.h[l], hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpy2DAsync(dr, P.strideR[l], in->right_levels[l], (size_t)in->level_stride[l],
+                             P.w[l], P.h[l], hipMemcpyHostToDevice, s));
+    lv.L[l] = dl;
+    lv.R[l] = dr;
+  }
+  if ((st = upload(m->dPairLv, &lv, sizeof(lv), s))) return st;
+  if ((st = m->dUr.ensure((size_t)stride * 4))) return st;
+  if ((st = m->dDepth.ensure((size_t)stride * 4))) return st;
+  if ((st = m->dSad.ensure((size_t)stride * 4))) return st;
+  HIP_TRY(orb_k_stereo(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(),
+                       m->dNKeys.as<int32_t>(), m->dRKeys.as<orb_keypoint_t>(),
+                       m->dRDesc.as<uint8_t>(), m->dNR.as<int32_t>(), stride, NL, m->dPairLv.p, &P,
+                       m->dUr.as<float>(), m->dDepth.as<float>(), m->dSad.as<int32_t>(), 1, s));
+  HIP_TRY(hipMemcpyAsync(u_right, m->dUr.p, (size_t)NL * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(depth, m->dDepth.p, (size_t)NL * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor_t* left_ext,
+                                    orb_extractor_t* right_ext, const orb_keypoint_t* d_left_keys,
+                                    const uint8_t* d_left_desc, const int32_t* d_left_n,
+                                    const orb_keypoint_t* d_right_keys,
+                                    const uint8_t* d_right_desc, const int32_t* d_right_n,
+                                    int kp_stride, float bf, float fx, float* d_u_right,
+                                    float* d_depth, int32_t* d_sad, void* stream) {
+  if (!m || !left_ext || !right_ext || n_pairs < 0 || kp_stride <= 0 || !(fx > 0) ||
+      !d_u_right || !d_depth || !d_sad)
+    return ORB_EINVAL;
+  if (n_pairs == 0) return ORB_OK;
+  const int L = orb_extractor_get_levels(left_ext);
+  if (L != orb_extractor_get_levels(right_ext)) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  StereoParamsHost P;
+  memset(&P, 0, sizeof(P));
+  P.nLevels = L;
+  P.bf = bf;
+  P.fx = fx;
+  orb_extractor_get_scale_factors(left_ext, P.scale);
+  orb_extractor_get_inverse_scale_factors(left_ext, P.invScale);
+  std::vector<StereoPairLevelsHost> lv(n_pairs);
+  for (int i = 0; i < n_pairs; ++i) {
+    memset(&lv[i], 0, sizeof(StereoPairLevelsHost));
+    for (int l = 0; l < L; ++l) {
+      int wl, hl, wr, hr;
+      size_t sl, sr;
+      orb_status_t st = orb_extractor_batch_level(left_ext, i, l, &lv[i].L[l], &wl, &hl, &sl);
+      if (st) return st;
+      st = orb_extractor_batch_level(right_ext, i, l, &lv[i].R[l], &wr, &hr, &sr);
+      if (st) return st;
+      if (wl != wr || hl != hr) return ORB_EINVAL;
+      P.w[l] = wl;
+      P.h[l] = hl;
+      P.strideL[l] = (int)sl;
+      P.strideR[l] = (int)sr;
+    }
+  }
+  orb_status_t st = m->dPairLv.ensure(lv.size() * sizeof(StereoPairLevelsHost));
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(m->dPairLv.p, lv.data(), lv.size() * sizeof(StereoPairLevelsHost),
+                         hipMemcpyHostToDevice, s));
+  HIP_TRY(orb_k_stereo(d_left_keys, d_left_desc, d_left_n, d_right_keys, d_right_desc, d_right_n,
+                       kp_stride, kp_stride, m->dPairLv.p, &P, d_u_right, d_depth, d_sad,
+                       n_pairs, s));
+  // the pair-level pointer table must outlive the asynchronous launch
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+// -------------------------------------------------- SearchByProjection(F, LastF)
+orb_status_t orb_match_projection_frame(orb_matcher_t* m, const orb_frame_t* C,
+                                        const uint8_t* kp_locked, int n_last,
+                                        const orb_last_mp_t* last, const uint8_t* last_desc,
+                                        const orb_camera_t* cam, float tlc_z, float th,
+                                        int mono, int check_orientation, int32_t* kp_match,
+                                        int32_t* nmatches) {
+  if (!m || !C || !cam || n_last < 0 || (n_last > 0 && (!last || !last_desc)) || !kp_match ||
+      !nmatches || C->n < 0 || (C->n > 0 && (!C->keys || !C->descriptors)) ||
+      !C->scale_factors || C->n_levels <= 0 || C->n_levels > ORB_MAX_LEVELS ||
+      C->n >= (1 << 19))
+    return ORB_EINVAL;
+  *nmatches = 0;
+  for (int i = 0; i < C->n; ++i) kp_match[i] = -1;
+  if (C->n == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  const int N = C->n, M = n_last;
+  orb_status_t st;
+  if ((st = upload(m->dKeys, C->keys, (size_t)N * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(m->dDesc, C->descriptors, (size_t)N * 32, s))) return st;
+  if (C->u_right && (st = upload(m->dUr, C->u_right, (size_t)N * 4, s))) return st;
+  if (kp_locked && (st = upload(m->dLocked, kp_locked, (size_t)N, s))) return st;
+  const int32_t nk = N;
+  if ((st = upload(m->dNKeys, &nk, 4, s))) return st;
+  if ((st = upload(m->dA, last, (size_t)M * sizeof(orb_last_mp_t), s))) return st;
+  if ((st = upload(m->dB, last_desc, (size_t)M * 32, s))) return st;
+  if ((st = m->dCellStart.ensure((size_t)(ORB_GRID_COLS * ORB_GRID_ROWS + 1) * 4))) return st;
+  if ((st = m->dCellIdx.ensure((size_t)N * 4))) return st;
+  if ((st = m->dTopk.ensure((size_t)std::max(M, 1) * 16))) return st;
+  if ((st = m->dNcand.ensure((size_t)std::max(M, 1) * 4))) return st;
+  if ((st = m->dKpMatch.ensure((size_t)N * 4))) return st;
+  if ((st = m->dNMatch.ensure(16))) return st;
+  FrameProjParamsHost P;
+  memset(&P, 0, sizeof(P));
+  P.minX = C->min_x; P.maxX = C->max_x; P.minY = C->min_y; P.maxY = C->max_y;
+  P.invW = (float)ORB_GRID_COLS / (C->max_x - C->min_x);
+  P.invH = (float)ORB_GRID_ROWS / (C->max_y - C->min_y);
+  P.fx = cam->fx; P.fy = cam->fy; P.cx = cam->cx; P.cy = cam->cy; P.bf = cam->bf;
+  P.th = th;
+  P.fwd = (tlc_z > cam->mb && !mono) ? 1 : 0;   // src/ORBmatcher.cc:1482-1484
+  P.bwd = (-tlc_z > cam->mb && !mono) ? 1 : 0;
+  P.checkOri = check_orientation ? 1 : 0;
+  for (int i = 0; i < C->n_levels; ++i) P.scale[i] = C->scale_factors[i];
+  HIP_TRY(orb_k_grid_build(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), N, P.minX,
+                           P.minY, P.invW, P.invH, m->dCellStart.as<int32_t>(),
+                           m->dCellIdx.as<int32_t>(), 1, s));
+  HIP_TRY(orb_k_frame_proj(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(),
+                           C->u_right ? m->dUr.as<float>() : nullptr,
+                           kp_locked ? m->dLocked.as<uint8_t>() : nullptr, N,
+                           m->dA.as<orb_last_mp_t>(), m->dB.as<uint8_t>(), M,
+                           m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
+                           m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
+                           m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), s));
+  HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+// ------------------------------------------------------------- SearchByBoW
+orb_status_t orb_match_bow(orb_matcher_t* m, int n_kf, const uint8_t* kf_desc,
+                           const float* kf_angle, const int32_t* kf_mp,
+                           const uint8_t* kf_mp_bad, int kf_nodes, const uint32_t* kf_node_ids,
+                           const int32_t* kf_offs, const uint32_t* kf_feats, int n_f,
+                           const uint8_t* f_desc, const float* f_angle, int f_nodes,
+                           const uint32_t* f_node_ids, const int32_t* f_offs,
+                           const uint32_t* f_feats, float nnratio, int check_orientation,
+                           int32_t* f_match, int32_t* nmatches) {
+  if (!m || n_kf < 0 || n_f < 0 || kf_nodes < 0 || f_nodes < 0 || !f_match || !nmatches ||
+      (kf_nodes > 0 && (!kf_node_ids || !kf_offs)) || (f_nodes > 0 && (!f_node_ids || !f_offs)))
+    return ORB_EINVAL;
+  *nmatches = 0;
+  for (int j = 0; j < n_f; ++j) f_match[j] = -1;
+  if (n_kf == 0 || n_f == 0 || kf_nodes == 0 || f_nodes == 0) return ORB_OK;
+  const int nKfFeats = kf_offs[kf_nodes], nFFeats = f_offs[f_nodes];
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  orb_status_t st;
+  if ((st = upload(m->dBowA, kf_desc, (size_t)n_kf * 32, s))) return st;
+  if ((st = upload(m->dBowB, kf_angle, (size_t)n_kf * 4, s))) return st;
+  if ((st = upload(m->dBowC, kf_mp, (size_t)n_kf * 4, s))) return st;
+  if (kf_mp_bad && (st = upload(m->dBowD, kf_mp_bad, (size_t)n_kf, s))) return st;
+  if ((st = upload(m->dBowE, kf_node_ids, (size_t)kf_nodes * 4, s))) return st;
+  if ((st = upload(m->dBowF, kf_offs, (size_t)(kf_nodes + 1) * 4, s))) return st;
+  if ((st = upload(m->dBowG, kf_feats, (size_t)nKfFeats * 4, s))) return st;
+  if ((st = upload(m->dDesc, f_desc, (size_t)n_f * 32, s))) return st;
+  if ((st = upload(m->dBowH, f_angle, (size_t)n_f * 4, s))) return st;
+  if ((st = upload(m->dBowI, f_node_ids, (size_t)f_nodes * 4, s))) return st;
+  if ((st = upload(m->dBowJ, f_offs, (size_t)(f_nodes + 1) * 4, s))) return st;
+  if ((st = upload(m->dBowK, f_feats, (size_t)nFFeats * 4, s))) return st;
+  if ((st = m->dKpMatch.ensure((size_t)n_f * 4))) return st;
+  if ((st = m->dTopk.ensure((size_t)std::max(nKfFeats, 1) * 4))) return st;
+  if ((st = m->dNMatch.ensure(16))) return st;
+  HIP_TRY(hipMemsetAsync(m->dKpMatch.p, 0xFF, (size_t)n_f * 4, s));
+  HIP_TRY(orb_k_bow(m->dBowA.as<uint8_t>(), m->dBowB.as<float>(), m->dBowC.as<int32_t>(),
+                    kf_mp_bad ? m->dBowD.as<uint8_t>() : nullptr, kf_nodes,
+                    m->dBowE.as<uint32_t>(), m->dBowF.as<int32_t>(), m->dBowG.as<uint32_t>(),
+                    nKfFeats, m->dDesc.as<uint8_t>(), m->dBowH.as<float>(), f_nodes,
+                    m->dBowI.as<uint32_t>(), m->dBowJ.as<int32_t>(), m->dBowK.as<uint32_t>(), n_f,
+                    nnratio, check_orientation, m->dKpMatch.as<int32_t>(),
+                    m->dTopk.as<int32_t>(), m->dNMatch.as<int32_t>(), s));
+  HIP_TRY(hipMemcpyAsync(f_match, m->dKpMatch.p, (size_t)n_f * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return ORB_OK;

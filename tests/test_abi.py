@@ -1,0 +1,80 @@
+"""The C-ABI library: builds, loads without a GPU, exports exactly what
+include/orb_abi.h declares, and refuses to compute without a gfx950 device."""
+import ctypes
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG_DIR, ROOT
+
+HEADER = ROOT / "include" / "orb_abi.h"
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", " ", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(orb_[a-z0-9_]+)\s*\(", text)))
+
+
+def exported(lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib_path)], check=True,
+                         capture_output=True, text=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+
+
+def test_header_declares_the_drop_in_surface():
+    fns = declared_functions()
+    for must in ["orb_extractor_create", "orb_extractor_extract", "orb_extractor_extract_batch",
+                 "orb_extractor_pyramid_level", "orb_descriptor_distance", "orb_hamming_batch",
+                 "orb_match_projection_local", "orb_match_projection_local_batch",
+                 "orb_stereo_match", "orb_match_projection_frame", "orb_match_bow"]:
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol(orb):
+    orb.lib()
+    missing = set(declared_functions()) - exported(orb.LIB_PATH)
+    assert not missing, f"declared in orb_abi.h but not exported: {sorted(missing)}"
+
+
+def test_library_has_gfx950_code_object(orb):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list",
+                          "--type=o", f"--input={PKG_DIR / 'build' / 'extractor_kernels.o'}"],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("offload bundler unavailable")
+    assert "gfx950" in out.stdout
+
+
+def test_abi_version_and_status_strings(orb):
+    L = orb.lib()
+    assert L.orb_abi_version() == 1
+    assert L.orb_status_string(0) == b"ok"
+    assert L.orb_status_string(-5) == b"no gfx950 device"
+
+
+def test_host_descriptor_distance(orb):
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, (200, 32), dtype=np.uint8)
+    b = rng.integers(0, 256, (200, 32), dtype=np.uint8)
+    for i in range(200):
+        assert orb.ORBmatcher.DescriptorDistance(a[i], b[i]) == int(np.unpackbits(a[i] ^ b[i]).sum())
+
+
+def test_no_cpu_fallback_without_gpu(orb):
+    """Without a gfx950 device the product refuses to compute (fails loudly)."""
+    if orb.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(orb.OrbError) as e:
+        orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    assert e.value.status == orb.ORB_ENODEV
+    with pytest.raises(orb.OrbError):
+        orb.ORBmatcher(0.8)
+
+
+def test_product_does_not_link_the_oracle(orb):
+    out = subprocess.run(["ldd", str(orb.LIB_PATH)], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+    syms = exported(orb.LIB_PATH)
+    assert not any(s.startswith("oracle_") for s in syms)

@@ -1,0 +1,102 @@
+"""GPU ComputeStereoMatches, SearchByProjection(F, LastFrame) and SearchByBoW
+against the CPU oracle: float outputs bit-exact, assignments index-exact."""
+import numpy as np
+import pytest
+
+import scenarios
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_stereo_matches(gpu, oracle, seed):
+    sp = scenarios.stereo_pair(oracle, seed)
+    args = (sp["kl"], sp["dl"], sp["scale"], sp["kr"], sp["dr"], sp["lpyr"], sp["rpyr"],
+            sp["inv"], scenarios.BF, scenarios.FX, sp["w"], sp["h"])
+    ur_ref, dp_ref = oracle.stereo_match(*args)
+    F = gpu.Frame(sp["kl"], sp["dl"], sp["scale"], sp["w"], sp["h"])
+    ur, dp = gpu.ORBmatcher().ComputeStereoMatches(F, sp["kr"], sp["dr"], sp["lpyr"], sp["rpyr"],
+                                                   sp["inv"], scenarios.BF, scenarios.FX)
+    assert (ur_ref > 0).sum() > 50
+    assert ur.tobytes() == ur_ref.tobytes(), np.nonzero(ur != ur_ref)[0][:10]
+    assert dp.tobytes() == dp_ref.tobytes()
+
+
+def test_stereo_batch_from_extractors(gpu, oracle):
+    """C3 path: both images of each pair through extract_batch, stereo on device."""
+    torch = pytest.importorskip("torch")
+    w, h, nf, P = 1241, 376, 2000, 3
+    L = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    R = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    cap = L.capacity(w, h)
+    imgs_l = np.stack([oracle.synth_image(30 + i, 0, w, h, 0) for i in range(P)])
+    imgs_r = np.stack([oracle.synth_image(30 + i, 0, w, h, 1) for i in range(P)])
+    dev = "cuda"
+    dl, dr = torch.from_numpy(imgs_l).to(dev), torch.from_numpy(imgs_r).to(dev)
+    out = {}
+    for name, ext, d in (("l", L, dl), ("r", R, dr)):
+        k = torch.zeros((P, cap, 7), dtype=torch.int32, device=dev)
+        de = torch.zeros((P, cap, 32), dtype=torch.uint8, device=dev)
+        n = torch.zeros(P, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        ext.extract_batch(d.data_ptr(), P, w, h, w, w * h, k.data_ptr(), de.data_ptr(), cap,
+                          n.data_ptr())
+        torch.cuda.synchronize()
+        out[name] = (k, de, n)
+    ur = torch.zeros((P, cap), dtype=torch.float32, device=dev)
+    dp = torch.zeros((P, cap), dtype=torch.float32, device=dev)
+    sad = torch.zeros((P, cap), dtype=torch.int32, device=dev)
+    m = gpu.ORBmatcher()
+    (kl, dlsc, nl), (kr, drsc, nr) = out["l"], out["r"]
+    m.stereo_match_batch(P, L, R, kl.data_ptr(), dlsc.data_ptr(), nl.data_ptr(), kr.data_ptr(),
+                         drsc.data_ptr(), nr.data_ptr(), cap, scenarios.BF, scenarios.FX,
+                         ur.data_ptr(), dp.data_ptr(), sad.data_ptr())
+    torch.cuda.synchronize()
+    p = oracle.params(nf)
+    for i in range(P):
+        klh, dlh, _ = oracle.extract(imgs_l[i], nf)
+        krh, drh, _ = oracle.extract(imgs_r[i], nf)
+        ur_ref, dp_ref = oracle.stereo_match(klh, dlh, p["scale"], krh, drh,
+                                             oracle.pyramid(imgs_l[i]), oracle.pyramid(imgs_r[i]),
+                                             p["inv_scale"], scenarios.BF, scenarios.FX, w, h)
+        n = int(nl[i].item())
+        assert n == len(klh)
+        assert ur[i, :n].cpu().numpy().tobytes() == ur_ref.tobytes()
+        assert dp[i, :n].cpu().numpy().tobytes() == dp_ref.tobytes()
+
+
+@pytest.mark.parametrize("mono,tlc,th", [(1, 0.0, 15.0), (0, 1.0, 7.0), (0, -1.0, 7.0),
+                                         (0, 0.0, 14.0)])
+@pytest.mark.parametrize("check_ori", [1, 0])
+def test_search_by_projection_frame(gpu, oracle, mono, tlc, th, check_ori):
+    fp = scenarios.frame_pair(oracle, 2, rng_seed=int(th))
+    rng = np.random.default_rng(7)
+    n = len(fp["kb"])
+    ur = None if mono else np.where(rng.random(n) < 0.6,
+                                    fp["kb"]["x"] - rng.uniform(3, 60, n), -1).astype(np.float32)
+    locked = (rng.random(n) < 0.1).astype(np.uint8)
+    n_ref, km_ref = oracle.match_projection_frame(
+        fp["kb"], fp["db"], fp["scale"], fp["w"], fp["h"], fp["last"], fp["last_desc"],
+        scenarios.camera(), tlc, th, mono, check_ori, locked, ur)
+    F = gpu.Frame(fp["kb"], fp["db"], fp["scale"], fp["w"], fp["h"], u_right=ur)
+    m = gpu.ORBmatcher(0.9, bool(check_ori))
+    n_gpu, km = m.SearchByProjectionFrame(F, fp["last"], fp["last_desc"], scenarios.camera(), tlc,
+                                          th, bool(mono), locked)
+    assert n_ref > 100
+    assert n_gpu == n_ref
+    assert np.array_equal(km, km_ref), np.nonzero(km != km_ref)[0][:10]
+
+
+@pytest.mark.parametrize("seed,nnratio", [(4, 0.75), (5, 0.7), (6, 0.9)])
+@pytest.mark.parametrize("check_ori", [1, 0])
+def test_search_by_bow(gpu, oracle, seed, nnratio, check_ori):
+    bp = scenarios.bow_pair(oracle, seed)
+    n_ref, fm_ref = oracle.match_bow(bp["kf_desc"], bp["kf_angle"], bp["kf_mp"], bp["kf_bad"],
+                                     bp["kf_fv"], bp["f_desc"], bp["f_angle"], bp["f_fv"], nnratio,
+                                     check_ori)
+    m = gpu.ORBmatcher(nnratio, bool(check_ori))
+    n_gpu, fm = m.SearchByBoW(bp["kf_desc"], bp["kf_angle"], bp["kf_mp"], bp["kf_bad"],
+                              bp["kf_fv"], bp["f_desc"], bp["f_angle"], bp["f_fv"])
+    assert n_ref > 50
+    assert n_gpu == n_ref
+    assert np.array_equal(fm, fm_ref)
