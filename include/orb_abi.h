@@ -30,7 +30,7 @@
  * Error behaviour: the reference has no status codes (an empty image returns
  * silently with outputs untouched, src/ORBextractor.cc:1095-1096; a non-8UC1
  * image asserts, :1100).  Here every call returns an orb_status_t; the C++
- * wrapper (orb_slam2-chinese-annotation_amd/host/ORBextractor.h) maps
+ * wrapper (orb_slam2-chinese-annotation_amd/host/orb_amd.hpp) maps
  * ORB_EEMPTY to "return, outputs untouched" and ORB_EINVAL to an assert.
  */
 #ifndef ORB_ABI_H
