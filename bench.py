@@ -68,6 +68,40 @@ def algorithmic_bytes(w, h, scale, nlevels, n_kp, n_mp):
             "frame_total_survey": (2 * sum(P) - P[0]) + 60 * n_kp + match}
 
 
+def shard_frames(rank, batch):
+    """Frame ids this rank processes in each step: a contiguous block of the
+    synthetic sequence per rank (weak scaling, no data-path collective)."""
+    return [rank * batch + i for i in range(batch)]
+
+
+def gather_counts(dist, counts, out):
+    """RCCL all-gather of every frame's keypoint count (int32 per frame)."""
+    dist.all_gather_into_tensor(out, counts)
+    return out
+
+
+def max_over_ranks(dist, elapsed, device):
+    """The job's time = the slowest rank's time."""
+    import torch
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def measured_traffic(kernel, batch):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_hbm_traffic.json, tools/pmc_summary.py), scaled to this batch."""
+    files = sorted((ROOT / "profiles").glob("r*_hbm_traffic.json"))
+    if not files:
+        return None, None
+    t = json.loads(files[-1].read_text())
+    k = t["kernels"].get(kernel)
+    if k is None:
+        return None, files[-1].name
+    return k["traffic_bytes"] * batch / t["batch"], files[-1].name
+
+
 def cpu_baseline(imgs_host, maps, args, scale):
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # CPU oracle: checker / baseline only
@@ -95,7 +129,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=512, help="frames per GPU per step")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--features", type=int, default=1000)
@@ -120,7 +154,7 @@ def main():
     W, H, B, NF, M = args.width, args.height, args.batch, args.features, args.mappoints
 
     # ---------------- inputs: this rank's shard of the synthetic sequence, in HBM
-    frames = [rank * B + i for i in range(B)]
+    frames = shard_frames(rank, B)
     imgs = np.stack([orb.synth_image(args.seed, f, W, H) for f in frames])
     ext = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=local)
     scale = np.float32(ext.GetScaleFactors())
@@ -168,7 +202,7 @@ def main():
                                            d_mpd.data_ptr(), d_nmps.data_ptr(), M, W, H, scale, 1.0,
                                            d_match.data_ptr(), d_nmatch.data_ptr(), stream)
         if dist is not None:  # RCCL: gather every frame's keypoint count
-            dist.all_gather_into_tensor(gathered, d_cnt)
+            gather_counts(dist, d_cnt, gathered)
 
     for _ in range(args.warmup):
         step()
@@ -186,9 +220,7 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = max_over_ranks(dist, elapsed, dev)
 
     # per-kernel HIP-event times over the timed region
     kern = {}
@@ -210,6 +242,7 @@ def main():
     dom_bytes = alg[dom] * B / launches_per_step
     achieved = dom_bytes / (dom_ms_per_launch * 1e-3) / 1e9
 
+    traffic, traffic_src = measured_traffic(dom, B)
     total_frames = B * args.steps * world
     result = {
         "metric": METRIC,
@@ -239,7 +272,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": f"profiles/{traffic_src} (rocprofv3 FETCH_SIZE+WRITE_SIZE, "
+                              "separate passes, raw KiB x 1024)" if traffic_src else None,
             "bytes_per_launch": dom_bytes,
             "ms_per_launch": dom_ms_per_launch,
         },
