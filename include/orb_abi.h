@@ -155,6 +155,31 @@ typedef struct orb_mp_track {
   uint8_t _pad;
 } orb_mp_track_t;
 
+/* MapPoint state read by Frame::isInFrustum and Tracking::SearchLocalPoints
+ * (src/Frame.cc:303-366, src/Tracking.cc:1360-1377, src/MapPoint.cc:404-450). */
+typedef struct orb_map_point {
+  float pos[3];        /* GetWorldPos() */
+  float normal[3];     /* GetNormal() */
+  float min_distance;  /* mfMinDistance (GetMinDistanceInvariance = 0.8f * it) */
+  float max_distance;  /* mfMaxDistance (GetMaxDistanceInvariance = 1.2f * it) */
+  uint8_t bad;         /* isBad() */
+  uint8_t seen;        /* mnLastFrameSeen == mCurrentFrame.mnId (already matched) */
+  uint8_t has_obs;     /* Observations() > 0 */
+  uint8_t _pad;
+} orb_map_point_t;     /* 36 bytes */
+
+/* Pinhole camera (Frame::fx, fy, cx, cy, mbf, mb). */
+typedef struct orb_camera {
+  float fx, fy, cx, cy, bf, mb;
+} orb_camera_t;
+
+/* Frame pose (Frame::UpdatePoseMatrices, src/Frame.cc:294-300). */
+typedef struct orb_pose {
+  float rcw[9];        /* mRcw, row-major */
+  float tcw[3];        /* mtcw */
+  float ow[3];         /* mOw = -mRcw^T * mtcw (camera centre) */
+} orb_pose_t;
+
 int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
 orb_status_t orb_matcher_create(int device, orb_matcher_t** out);
@@ -194,6 +219,29 @@ orb_status_t orb_match_projection_local_batch(
     int mp_stride, float min_x, float max_x, float min_y, float max_y, int n_levels,
     const float* scale_factors, float th, float nnratio, int32_t* d_kp_match,
     int32_t* d_nmatches, void* stream);
+
+/* Tracking::SearchLocalPoints' frustum pass: for each local MapPoint in order,
+ * skip it if seen or bad, else Frame::isInFrustum(pMP, viewing_cos_limit)
+ * (src/Tracking.cc:1360-1377, src/Frame.cc:303-366, MapPoint::PredictScale
+ * src/MapPoint.cc:435-450).  Writes tracks[i] (proj_x, proj_y, proj_xr,
+ * view_cos, level, in_view; bad and has_obs copied through; all-zero
+ * projection fields when not in view) and n_in_view = nToMatch.  The tracks
+ * feed orb_match_projection_local unchanged.  log_scale_factor =
+ * Frame::mfLogScaleFactor.  Host buffers. */
+orb_status_t orb_frustum(orb_matcher_t* m, int n_mp, const orb_map_point_t* mps,
+                         const orb_pose_t* pose, const orb_camera_t* cam, float min_x,
+                         float max_x, float min_y, float max_y, float viewing_cos_limit,
+                         float log_scale_factor, int n_levels, orb_mp_track_t* tracks,
+                         int32_t* n_in_view);
+
+/* Device-batched form: problem p uses d_poses[p], map points d_mps + p*mp_stride
+ * (count d_nmps[p]); writes d_tracks + p*mp_stride and d_n_in_view[p]. */
+orb_status_t orb_frustum_batch(orb_matcher_t* m, int n_problems, const orb_map_point_t* d_mps,
+                               const int32_t* d_nmps, int mp_stride, const orb_pose_t* d_poses,
+                               const orb_camera_t* cam, float min_x, float max_x, float min_y,
+                               float max_y, float viewing_cos_limit, float log_scale_factor,
+                               int n_levels, orb_mp_track_t* d_tracks, int32_t* d_n_in_view,
+                               void* stream);
 
 /* Frame::ComputeStereoMatches for one rectified pair.  Left/right keypoints
  * and descriptors as produced by the two extractors, plus both pyramids
@@ -248,9 +296,6 @@ typedef struct orb_last_mp {
   int32_t mp_id;                /* identity of pMP (same id => same MapPoint) */
 } orb_last_mp_t;
 
-typedef struct orb_camera {
-  float fx, fy, cx, cy, bf, mb;
-} orb_camera_t;
 
 orb_status_t orb_match_projection_frame(orb_matcher_t* m, const orb_frame_t* current,
                                         const uint8_t* kp_locked, int n_last,

@@ -335,3 +335,33 @@ def match_bow(kf_desc, kf_angle, kf_mp, kf_bad, kf_fv, f_desc, f_angle, f_fv, nn
            _p(kf_fv[2]), len(f_desc), _p(f_desc), _p(f_angle), len(f_fv[0]), _p(f_fv[0]),
            _p(f_fv[1]), _p(f_fv[2]), nnratio, int(check_ori), _p(fm))
     return n, fm
+
+
+MAP_POINT_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_distance", "<f4"),
+                            ("max_distance", "<f4"), ("bad", "u1"), ("seen", "u1"),
+                            ("has_obs", "u1"), ("_pad", "u1")])
+POSE_DTYPE = np.dtype([("rcw", "<f4", (9,)), ("tcw", "<f4", (3,)), ("ow", "<f4", (3,))])
+
+
+def pinned_log(x):
+    fn = lib().oracle_log
+    fn.restype, fn.argtypes = ctypes.c_double, [ctypes.c_double]
+    return fn(float(x))
+
+
+def frustum(mps, pose, cam, width, height, cos_limit=0.5, log_scale=None, n_levels=8,
+            min_x=0.0, min_y=0.0):
+    """Tracking::SearchLocalPoints' isInFrustum loop on the CPU: (n_in_view, tracks)."""
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    pose = np.ascontiguousarray(pose, POSE_DTYPE).reshape(1)
+    if log_scale is None:
+        log_scale = np.float32(pinned_log(np.float32(1.2)))
+    tracks = np.zeros(len(mps), MP_TRACK_DTYPE)
+    c = _Camera(*cam)
+    fn = lib().oracle_frustum
+    vp, f32 = ctypes.c_void_p, ctypes.c_float
+    fn.argtypes = [ctypes.c_int, vp, vp, vp, f32, f32, f32, f32, f32, f32, ctypes.c_int, vp]
+    fn.restype = ctypes.c_int
+    n = fn(len(mps), _p(mps), _p(pose), ctypes.byref(c), min_x, float(width), min_y, float(height),
+           cos_limit, float(log_scale), n_levels, _p(tracks))
+    return n, tracks

@@ -754,6 +754,118 @@ static int search_by_projection_local(const orb_frame_t* F, const uint8_t* kp_lo
 }
 
 // a18: ComputeThreeMaxima, src/ORBmatcher.cc:1765-1809
+// ---------------------------------------------------------------- frustum
+// A.7 pinned log: the fdlibm e_log scheme in double (x = 2^k (1+f),
+// s = f/(2+f), R = degree-14 polynomial in s^2).  MapPoint::PredictScale's
+// log(float) is pinned to (float)pinned_log((double)ratio).
+static double pinned_log(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01,
+               L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01,
+               L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (!(x > 0.0)) return x == 0.0 ? -INFINITY : NAN;
+  if (isinf(x)) return x;
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  int32_t hi = (int32_t)(bits >> 32);
+  const uint32_t lo = (uint32_t)bits;
+  int k = (hi >> 20) - 1023;
+  hi &= 0x000fffff;
+  const int32_t up = (hi + 0x95f64) & 0x100000;  // mantissa >= sqrt(2): halve it
+  const uint64_t mb = ((uint64_t)(uint32_t)(hi | (up ^ 0x3ff00000)) << 32) | lo;
+  double mant;
+  memcpy(&mant, &mb, 8);
+  k += up >> 20;
+  const double f = mant - 1.0, dk = (double)k;
+  if ((0x000fffff & (2 + hi)) < 3) {
+    if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+    const double R = f * f * (0.5 - 0.33333333333333333 * f);
+    return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  const double sv = f / (2.0 + f), z = sv * sv, w = z * z;
+  const double R = z * (L1 + w * (L3 + w * (L5 + w * L7))) + w * (L2 + w * (L4 + w * L6));
+  if (((hi - 0x6147a) | (0x6b851 - hi)) > 0) {
+    const double hf = 0.5 * f * f;
+    return k == 0 ? f - (hf - sv * (hf + R))
+                  : dk * ln2_hi - ((hf - (sv * (hf + R) + dk * ln2_lo)) - f);
+  }
+  return k == 0 ? f - sv * (f - R) : dk * ln2_hi - ((sv * (f - R) - dk * ln2_lo) - f);
+}
+
+struct FrustumCfg {
+  orb_camera_t cam;
+  float minX, maxX, minY, maxY, cosLimit, logScale;
+  int nLevels;
+};
+
+// Frame::isInFrustum (src/Frame.cc:303-366) for one MapPoint; true = in view.
+// Pinned arithmetic: Pc = Rcw*P + tcw as float dot products left to right
+// then + t (cv::gemm's 3x3 float path); cv::norm(PO) = sqrt of a double sum
+// of squares (normL2Sqr<float,double>), returned as double and stored as float
+// (:339); PO.dot(Pn) accumulates in double (dotProd_32f), divided in double by
+// the float dist (:351); PredictScale (src/MapPoint.cc:435-450) in float with
+// logf pinned above.
+static bool frustum_one(const orb_map_point_t& mp, const orb_pose_t& T, const FrustumCfg& c,
+                        orb_mp_track_t& tr) {
+  const float P0 = mp.pos[0], P1 = mp.pos[1], P2 = mp.pos[2];
+  const float X = ((T.rcw[0] * P0 + T.rcw[1] * P1) + T.rcw[2] * P2) + T.tcw[0];
+  const float Y = ((T.rcw[3] * P0 + T.rcw[4] * P1) + T.rcw[5] * P2) + T.tcw[1];
+  const float Z = ((T.rcw[6] * P0 + T.rcw[7] * P1) + T.rcw[8] * P2) + T.tcw[2];
+  if (Z < 0.0f) return false;                                   // :320-321
+  const float invz = 1.0f / Z;                                  // :325
+  const float u = c.cam.fx * X * invz + c.cam.cx;
+  const float v = c.cam.fy * Y * invz + c.cam.cy;
+  if (u < c.minX || u > c.maxX) return false;                   // :329-332
+  if (v < c.minY || v > c.maxY) return false;
+  const float maxDistance = 1.2f * mp.max_distance;             // src/MapPoint.cc:410-414
+  const float minDistance = 0.8f * mp.min_distance;             // src/MapPoint.cc:404-408
+  const float O0 = P0 - T.ow[0], O1 = P1 - T.ow[1], O2 = P2 - T.ow[2];
+  double ss = 0.0;
+  ss += (double)O0 * O0;
+  ss += (double)O1 * O1;
+  ss += (double)O2 * O2;
+  const float dist = (float)sqrt(ss);                           // :339
+  if (dist < minDistance || dist > maxDistance) return false;   // :341-342
+  double dot = 0.0;
+  dot += (double)O0 * mp.normal[0];
+  dot += (double)O1 * mp.normal[1];
+  dot += (double)O2 * mp.normal[2];
+  const float viewCos = (float)(dot / (double)dist);            // :351
+  if (viewCos < c.cosLimit) return false;                       // :353-354
+  const float ratio = mp.max_distance / dist;                   // PredictScale
+  const float lr = (float)pinned_log((double)ratio);
+  const float q = ceilf(lr / c.logScale);
+  int level;
+  if (q < 0.f) level = 0;
+  else if (q >= (float)c.nLevels) level = c.nLevels - 1;
+  else level = (int)q;
+  tr.proj_x = u;                                                // :362-368
+  tr.proj_xr = u - c.cam.bf * invz;
+  tr.proj_y = v;
+  tr.level = level;
+  tr.view_cos = viewCos;
+  return true;
+}
+
+// Tracking::SearchLocalPoints' frustum loop (src/Tracking.cc:1360-1377).
+static int frustum_all(int n, const orb_map_point_t* mps, const orb_pose_t& T,
+                       const FrustumCfg& c, orb_mp_track_t* tracks) {
+  int nToMatch = 0;
+  for (int i = 0; i < n; ++i) {
+    orb_mp_track_t tr;
+    memset(&tr, 0, sizeof(tr));
+    tr.bad = mps[i].bad;
+    tr.has_obs = mps[i].has_obs;
+    if (!mps[i].seen && !mps[i].bad && frustum_one(mps[i], T, c, tr)) {
+      tr.in_view = 1;
+      ++nToMatch;
+    }
+    tracks[i] = tr;
+  }
+  return nToMatch;
+}
+
 static void three_maxima(const std::vector<int>* histo, int L, int& ind1, int& ind2, int& ind3) {
   int max1 = 0, max2 = 0, max3 = 0;
   for (int i = 0; i < L; ++i) {
@@ -1121,6 +1233,23 @@ int oracle_match_projection_local(const orb_frame_t* F, const uint8_t* kp_locked
                                   const orb_mp_track_t* mps, const uint8_t* mp_desc, float th,
                                   float nnratio, int32_t* kp_match) {
   return search_by_projection_local(F, kp_locked, nmp, mps, mp_desc, th, nnratio, kp_match);
+}
+
+double oracle_log(double x) { return pinned_log(x); }
+
+int oracle_frustum(int n, const orb_map_point_t* mps, const orb_pose_t* pose,
+                   const orb_camera_t* cam, float minX, float maxX, float minY, float maxY,
+                   float cosLimit, float logScale, int nLevels, orb_mp_track_t* tracks) {
+  FrustumCfg c;
+  c.cam = *cam;
+  c.minX = minX;
+  c.maxX = maxX;
+  c.minY = minY;
+  c.maxY = maxY;
+  c.cosLimit = cosLimit;
+  c.logScale = logScale;
+  c.nLevels = nLevels;
+  return frustum_all(n, mps, *pose, c, tracks);
 }
 
 int oracle_match_projection_frame(const orb_frame_t* C, const uint8_t* kp_locked, int nlast,

@@ -41,6 +41,12 @@ assert KEYPOINT_DTYPE.itemsize == 28 and MP_TRACK_DTYPE.itemsize == 24
 assert LAST_MP_DTYPE.itemsize == 28
 
 
+MAP_POINT_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_distance", "<f4"),
+                            ("max_distance", "<f4"), ("bad", "u1"), ("seen", "u1"),
+                            ("has_obs", "u1"), ("_pad", "u1")])
+POSE_DTYPE = np.dtype([("rcw", "<f4", (9,)), ("tcw", "<f4", (3,)), ("ow", "<f4", (3,))])
+
+
 class OrbError(RuntimeError):
     def __init__(self, status: int, what: str):
         self.status = status
@@ -121,6 +127,9 @@ def lib() -> ctypes.CDLL:
                                              vp]),
         "orb_match_bow": (i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp,
                                 vp, vp, f32, i32, vp, vp]),
+        "orb_frustum": (i32, [vp, i32, vp, vp, vp, f32, f32, f32, f32, f32, f32, i32, vp, vp]),
+        "orb_frustum_batch": (i32, [vp, i32, vp, vp, i32, vp, vp, f32, f32, f32, f32, f32, f32,
+                                    i32, vp, vp, vp]),
         "orb_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
         "orb_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     }
@@ -474,6 +483,31 @@ class ORBmatcher:
             ctypes.byref(c), tlc_z, th, int(bMono), int(self.mbCheckOrientation), _ptr(km),
             ctypes.byref(nm)), "SearchByProjection(F, LastFrame)")
         return nm.value, km
+
+    # ------------------------------------------------------------ isInFrustum
+    def isInFrustum(self, mps, pose, cam, min_x: float, max_x: float, min_y: float, max_y: float,
+                    viewingCosLimit: float, logScaleFactor: float, nLevels: int):
+        """Tracking::SearchLocalPoints' loop of Frame::isInFrustum over the local map
+        (src/Tracking.cc:1360-1377): (nToMatch, tracks as MP_TRACK_DTYPE)."""
+        mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+        pose = np.ascontiguousarray(pose, POSE_DTYPE).reshape(1)
+        tracks = np.zeros(len(mps), MP_TRACK_DTYPE)
+        n = ctypes.c_int32(0)
+        c = _Camera(*cam)
+        _check(lib().orb_frustum(self._h, len(mps), _ptr(mps) if len(mps) else None, _ptr(pose),
+                                 ctypes.byref(c), min_x, max_x, min_y, max_y, viewingCosLimit,
+                                 logScaleFactor, nLevels, _ptr(tracks) if len(mps) else None,
+                                 ctypes.byref(n)), "isInFrustum")
+        return n.value, tracks
+
+    def frustum_batch(self, n_problems, d_mps, d_nmps, mp_stride, d_poses, cam, min_x, max_x,
+                      min_y, max_y, viewingCosLimit, logScaleFactor, nLevels, d_tracks,
+                      d_n_in_view, stream: int = 0):
+        c = _Camera(*cam)
+        _check(lib().orb_frustum_batch(self._h, n_problems, d_mps, d_nmps, mp_stride, d_poses,
+                                       ctypes.byref(c), min_x, max_x, min_y, max_y,
+                                       viewingCosLimit, logScaleFactor, nLevels, d_tracks,
+                                       d_n_in_view, stream or None), "frustum_batch")
 
     # ------------------------------------------------------------- SearchByBoW
     def SearchByBoW(self, kf_desc, kf_angle, kf_mp, kf_bad, kf_fv, f_desc, f_angle, f_fv):

@@ -1005,3 +1005,96 @@ extern "C" hipError_t orb_k_bow(const uint8_t* kfDesc, const float* kfAngle, con
                      checkOri, accF, fMatch, nmatches);
   return hipGetLastError();
 }
+
+// ================================================================ k_frustum
+// Tracking::SearchLocalPoints' frustum pass (src/Tracking.cc:1360-1377):
+// Frame::isInFrustum (src/Frame.cc:303-366) + MapPoint::PredictScale
+// (src/MapPoint.cc:435-450), one thread per map point, one grid row per
+// problem.  Pinned arithmetic (oracle/orb_oracle.cpp frustum_one):
+//   Pc = Rcw*P + tcw       float, left-to-right dot, then + t (cv::gemm 3x3 path)
+//   dist = cv::norm(P-Ow)  double sum of squares, double sqrt, to float
+//   viewCos = PO.dot(Pn)/dist   double dot / double(dist), to float
+//   level = ceil(logf(maxDist/dist) / logScale) with logf pinned to pinned_log
+struct FrustumParams {
+  float fx, fy, cx, cy, bf;
+  float minX, maxX, minY, maxY;
+  float cosLimit, logScale;
+  int nLevels;
+};
+
+__global__ __launch_bounds__(256) void k_frustum(const orb_map_point_t* __restrict__ mps,
+                                                 const int32_t* __restrict__ nmps, int mpStride,
+                                                 const orb_pose_t* __restrict__ poses,
+                                                 FrustumParams fp,
+                                                 orb_mp_track_t* __restrict__ tracks,
+                                                 int32_t* __restrict__ nInView) {
+  const int p = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int M = nmps[p];
+  bool in = false;
+  if (i < M) {
+    const orb_map_point_t mp = mps[(long long)p * mpStride + i];
+    const orb_pose_t& T = poses[p];
+    orb_mp_track_t tr;
+    tr.proj_x = tr.proj_y = tr.proj_xr = tr.view_cos = 0.f;
+    tr.level = 0;
+    tr.bad = mp.bad;
+    tr.has_obs = mp.has_obs;
+    tr._pad = 0;
+    if (!mp.seen && !mp.bad) {
+      const float P0 = mp.pos[0], P1 = mp.pos[1], P2 = mp.pos[2];
+      const float X = ((T.rcw[0] * P0 + T.rcw[1] * P1) + T.rcw[2] * P2) + T.tcw[0];
+      const float Y = ((T.rcw[3] * P0 + T.rcw[4] * P1) + T.rcw[5] * P2) + T.tcw[1];
+      const float Z = ((T.rcw[6] * P0 + T.rcw[7] * P1) + T.rcw[8] * P2) + T.tcw[2];
+      if (!(Z < 0.0f)) {
+        const float invz = __fdiv_rn(1.0f, Z);
+        const float u = fp.fx * X * invz + fp.cx;
+        const float v = fp.fy * Y * invz + fp.cy;
+        if (!(u < fp.minX || u > fp.maxX) && !(v < fp.minY || v > fp.maxY)) {
+          const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
+          const float O0 = P0 - T.ow[0], O1 = P1 - T.ow[1], O2 = P2 - T.ow[2];
+          const double ss = (((double)O0 * O0) + (double)O1 * O1) + (double)O2 * O2;
+          const float dist = (float)__dsqrt_rn(ss);
+          if (!(dist < minD || dist > maxD)) {
+            const double dot = (((double)O0 * mp.normal[0]) + (double)O1 * mp.normal[1]) +
+                               (double)O2 * mp.normal[2];
+            const float viewCos = (float)(dot / (double)dist);
+            if (!(viewCos < fp.cosLimit)) {
+              const float ratio = __fdiv_rn(mp.max_distance, dist);
+              const float lr = (float)pinned_log((double)ratio);
+              const float q = ceilf(__fdiv_rn(lr, fp.logScale));
+              int lvl;
+              if (q < 0.f) lvl = 0;
+              else if (q >= (float)fp.nLevels) lvl = fp.nLevels - 1;
+              else lvl = (int)q;
+              tr.proj_x = u;
+              tr.proj_y = v;
+              tr.proj_xr = u - fp.bf * invz;
+              tr.view_cos = viewCos;
+              tr.level = lvl;
+              in = true;
+            }
+          }
+        }
+      }
+    }
+    tr.in_view = in ? 1 : 0;
+    tracks[(long long)p * mpStride + i] = tr;
+  }
+  const int c = __popcll(__ballot(in));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&nInView[p], c);
+}
+
+extern "C" size_t orb_k_frustum_params_size(void) { return sizeof(FrustumParams); }
+
+extern "C" hipError_t orb_k_frustum(const orb_map_point_t* mps, const int32_t* nmps, int mpStride,
+                         int mpMax, const orb_pose_t* poses, const void* params,
+                         orb_mp_track_t* tracks, int32_t* nInView, int nproblems, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(nInView, 0, sizeof(int32_t) * nproblems, s);
+  if (e != hipSuccess) return e;
+  if (mpMax <= 0) return hipSuccess;
+  const FrustumParams fp = *static_cast<const FrustumParams*>(params);
+  hipLaunchKernelGGL(k_frustum, dim3((mpMax + 255) / 256, nproblems), dim3(256), 0, s, mps, nmps,
+                     mpStride, poses, fp, tracks, nInView);
+  return hipGetLastError();
+}

@@ -70,6 +70,47 @@ __device__ __forceinline__ void pinned_sincos(float angle, float* s_out, float* 
   *c_out = (float)c;
 }
 
+// ------------------------------------------------ A.7 pinned log (double)
+// Natural log by the classic fdlibm scheme: x = 2^k (1+f) with 1+f in
+// [sqrt(2)/2, sqrt(2)), s = f/(2+f), log(1+f) = f - (hf - s (hf + R(s^2)))
+// with a degree-14 even polynomial R; all in double, same operation sequence
+// as the oracle.  MapPoint::PredictScale's logf(ratio) is pinned to
+// (float)pinned_log((double)ratio).  Inputs are floats widened to double, so
+// no subnormal double ever reaches it.
+__device__ __forceinline__ double pinned_log(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01,
+               L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01,
+               L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (!(x > 0.0)) return x == 0.0 ? -__builtin_inf() : __builtin_nan("");
+  if (x == __builtin_inf()) return x;
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
+  int hx = (int)(bits >> 32);
+  const unsigned int lx = (unsigned int)bits;
+  int k = (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int i = (hx + 0x95f64) & 0x100000;  // 1 when the mantissa is >= sqrt(2)
+  const double m = __longlong_as_double(
+      (long long)(((unsigned long long)(unsigned int)(hx | (i ^ 0x3ff00000)) << 32) | lx));
+  k += i >> 20;
+  const double f = m - 1.0, dk = (double)k;
+  if ((0x000fffff & (2 + hx)) < 3) {  // |f| < 2^-20
+    if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+    const double R = f * f * (0.5 - 0.33333333333333333 * f);
+    return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  const double s = f / (2.0 + f), z = s * s, w = z * z;
+  const double t1 = w * (L2 + w * (L4 + w * L6));
+  const double t2 = z * (L1 + w * (L3 + w * (L5 + w * L7)));
+  const double R = t2 + t1;
+  if (((hx - 0x6147a) | (0x6b851 - hx)) > 0) {
+    const double hf = 0.5 * f * f;
+    return k == 0 ? f - (hf - s * (hf + R)) : dk * ln2_hi - ((hf - (s * (hf + R) + dk * ln2_lo)) - f);
+  }
+  return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
 // ------------------------------------------------------------- Hamming
 // DescriptorDistance (src/ORBmatcher.cc:1814-1830) == popcount(a ^ b) over 256 bits.
 __device__ __forceinline__ int hamming256(const ulonglong4 a, const ulonglong4 b) {

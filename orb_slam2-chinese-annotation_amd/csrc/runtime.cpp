@@ -71,6 +71,10 @@ hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc, const
                         int kpStride, int maxLeft, const void* pyr, const void* params,
                         float* uRight, float* depth, int32_t* sad, int npairs, hipStream_t s);
 size_t orb_k_frame_params_size(void);
+size_t orb_k_frustum_params_size(void);
+hipError_t orb_k_frustum(const orb_map_point_t* mps, const int32_t* nmps, int mpStride,
+                         int mpMax, const orb_pose_t* poses, const void* params,
+                         orb_mp_track_t* tracks, int32_t* nInView, int nproblems, hipStream_t s);
 hipError_t orb_k_frame_proj(const orb_keypoint_t* keys, const uint8_t* desc, const float* uright,
                             const uint8_t* locked, int nkeys, const orb_last_mp_t* last,
                             const uint8_t* lastDesc, int nlast, const int32_t* cellStart,
@@ -727,6 +731,32 @@ orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* t
 }  // extern "C"
 
 // ================================================================== matcher
+struct FrustumParamsHost {  // mirrors FrustumParams in matcher_kernels.hip
+  float fx, fy, cx, cy, bf;
+  float minX, maxX, minY, maxY;
+  float cosLimit, logScale;
+  int nLevels;
+};
+
+static FrustumParamsHost frustum_params(const orb_camera_t* cam, float min_x, float max_x,
+                                        float min_y, float max_y, float cos_limit,
+                                        float log_scale, int n_levels) {
+  FrustumParamsHost f;
+  f.fx = cam->fx;
+  f.fy = cam->fy;
+  f.cx = cam->cx;
+  f.cy = cam->cy;
+  f.bf = cam->bf;
+  f.minX = min_x;
+  f.maxX = max_x;
+  f.minY = min_y;
+  f.maxY = max_y;
+  f.cosLimit = cos_limit;
+  f.logScale = log_scale;
+  f.nLevels = n_levels;
+  return f;
+}
+
 struct ProjParamsHost {  // mirrors ProjParams in matcher_kernels.hip
   float minX, minY, invW, invH;
   float th, nnratio;
@@ -764,6 +794,8 @@ struct orb_matcher {
   // stereo / frame / BoW scratch
   DevBuf dRKeys, dRDesc, dNR, dPyr, dPairLv, dDepth, dSad, dBowA, dBowB, dBowC, dBowD, dBowE,
       dBowF, dBowG, dBowH, dBowI, dBowJ, dBowK;
+  // frustum scratch
+  DevBuf dMapPts, dPose, dTracks, dNInView;
   std::vector<uint8_t> hostScratch;
 };
 
@@ -789,7 +821,8 @@ orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
   if (st) return st;
   if (orb_k_proj_params_size() != sizeof(ProjParamsHost) ||
       orb_k_stereo_params_size() != sizeof(StereoParamsHost) ||
-      orb_k_frame_params_size() != sizeof(FrameProjParamsHost))
+      orb_k_frame_params_size() != sizeof(FrameProjParamsHost) ||
+      orb_k_frustum_params_size() != sizeof(FrustumParamsHost))
     return ORB_EINVAL;
   orb_matcher* m = new orb_matcher();
   m->device = device;
@@ -979,6 +1012,64 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+// ----------------------------------------------------------------- frustum
+orb_status_t orb_frustum(orb_matcher_t* m, int n_mp, const orb_map_point_t* mps,
+                         const orb_pose_t* pose, const orb_camera_t* cam, float min_x,
+                         float max_x, float min_y, float max_y, float viewing_cos_limit,
+                         float log_scale_factor, int n_levels, orb_mp_track_t* tracks,
+                         int32_t* n_in_view) {
+  if (!m || n_mp < 0 || (n_mp > 0 && (!mps || !tracks)) || !pose || !cam || !n_in_view ||
+      n_levels <= 0 || n_levels > ORB_MAX_LEVELS)
+    return ORB_EINVAL;
+  *n_in_view = 0;
+  if (n_mp == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  orb_status_t st;
+  if ((st = m->dMapPts.ensure((size_t)n_mp * sizeof(orb_map_point_t)))) return st;
+  if ((st = m->dPose.ensure(sizeof(orb_pose_t)))) return st;
+  if ((st = m->dTracks.ensure((size_t)n_mp * sizeof(orb_mp_track_t)))) return st;
+  if ((st = m->dNInView.ensure(16))) return st;
+  if ((st = m->dNMps.ensure(16))) return st;
+  hipStream_t s = m->stream;
+  HIP_TRY(hipMemcpyAsync(m->dMapPts.p, mps, (size_t)n_mp * sizeof(orb_map_point_t),
+                         hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(m->dPose.p, pose, sizeof(orb_pose_t), hipMemcpyHostToDevice, s));
+  const int32_t nm = n_mp;
+  HIP_TRY(hipMemcpyAsync(m->dNMps.p, &nm, 4, hipMemcpyHostToDevice, s));
+  const FrustumParamsHost fp = frustum_params(cam, min_x, max_x, min_y, max_y, viewing_cos_limit,
+                                              log_scale_factor, n_levels);
+  HIP_TRY(orb_k_frustum(m->dMapPts.as<orb_map_point_t>(), m->dNMps.as<int32_t>(), n_mp, n_mp,
+                        m->dPose.as<orb_pose_t>(), &fp, m->dTracks.as<orb_mp_track_t>(),
+                        m->dNInView.as<int32_t>(), 1, s));
+  HIP_TRY(hipMemcpyAsync(tracks, m->dTracks.p, (size_t)n_mp * sizeof(orb_mp_track_t),
+                         hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(n_in_view, m->dNInView.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_frustum_batch(orb_matcher_t* m, int n_problems, const orb_map_point_t* d_mps,
+                               const int32_t* d_nmps, int mp_stride, const orb_pose_t* d_poses,
+                               const orb_camera_t* cam, float min_x, float max_x, float min_y,
+                               float max_y, float viewing_cos_limit, float log_scale_factor,
+                               int n_levels, orb_mp_track_t* d_tracks, int32_t* d_n_in_view,
+                               void* stream) {
+  if (!m || n_problems < 0 || mp_stride < 0 || !cam || n_levels <= 0 ||
+      n_levels > ORB_MAX_LEVELS)
+    return ORB_EINVAL;
+  if (n_problems == 0) return ORB_OK;
+  if (!d_mps || !d_nmps || !d_poses || !d_tracks || !d_n_in_view || n_problems > 65535)
+    return ORB_EINVAL;
+  hipSetDevice(m->device);
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  const FrustumParamsHost fp = frustum_params(cam, min_x, max_x, min_y, max_y, viewing_cos_limit,
+                                              log_scale_factor, n_levels);
+  HIP_TRY(orb_k_frustum(d_mps, d_nmps, mp_stride, mp_stride, d_poses, &fp, d_tracks, d_n_in_view,
+                        n_problems, s));
   return ORB_OK;
 }
 

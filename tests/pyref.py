@@ -325,3 +325,39 @@ def search_by_projection_local(keys, desc, scale, width, height, mps, mp_desc, t
                 lock[bi] = True
             n += 1
     return n, km
+
+
+def frustum(mps, rcw, tcw, ow, cam, width, height, cos_limit, log_scale, n_levels):
+    """Vectorised numpy restatement of Frame::isInFrustum + MapPoint::PredictScale
+    (src/Frame.cc:303-366, src/MapPoint.cc:435-450) with the oracle's pinned
+    arithmetic: float32 Pc / projection, float64 norm and dot.  log via numpy
+    float64 (the oracle pins fdlibm's scheme; both agree after rounding to float)."""
+    f32 = np.float32
+    fx, fy, cx, cy, bf, _ = (f32(c) for c in cam)
+    R = np.asarray(rcw, f32).reshape(3, 3)
+    t = np.asarray(tcw, f32)
+    P = mps["pos"].astype(f32)
+    pc = [((R[i, 0] * P[:, 0] + R[i, 1] * P[:, 1]) + R[i, 2] * P[:, 2]) + t[i] for i in range(3)]
+    X, Y, Z = pc
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        invz = f32(1.0) / Z
+        u = fx * X * invz + cx
+        v = fy * Y * invz + cy
+        O = P - np.asarray(ow, f32)
+        dist = np.sqrt(((O[:, 0].astype(np.float64) ** 2) + O[:, 1].astype(np.float64) ** 2)
+                       + O[:, 2].astype(np.float64) ** 2).astype(f32)
+        N = mps["normal"].astype(np.float64)
+        dot = ((O[:, 0] * N[:, 0]) + O[:, 1] * N[:, 1]) + O[:, 2] * N[:, 2]
+        view_cos = (dot / dist.astype(np.float64)).astype(f32)
+        maxd = f32(1.2) * mps["max_distance"]
+        mind = f32(0.8) * mps["min_distance"]
+        ok = (mps["seen"] == 0) & (mps["bad"] == 0) & ~(Z < 0)
+        ok &= ~((u < 0) | (u > f32(width)) | (v < 0) | (v > f32(height)))
+        ok &= ~((dist < mind) | (dist > maxd))
+        ok &= ~(view_cos < f32(cos_limit))
+        ratio = mps["max_distance"] / dist
+        lr = np.log(ratio.astype(np.float64)).astype(f32)
+        q = np.ceil(lr / f32(log_scale))
+        level = np.where(q < 0, 0, np.where(q >= n_levels, n_levels - 1,
+                                            np.nan_to_num(q).astype(np.int64)))
+    return ok, u, v, u - bf * invz, view_cos, level

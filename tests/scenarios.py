@@ -83,3 +83,71 @@ def bow_pair(oracle, seed, nf=1000, rng_seed=0):
     f_fv = oracle.feature_vector(vocab_nodes(fp["db"]))
     return dict(kf_desc=kf_desc, kf_angle=kf_angle, kf_mp=kf_mp, kf_bad=kf_bad, kf_fv=kf_fv,
                 f_desc=fp["db"], f_angle=fp["kb"]["angle"], f_fv=f_fv)
+
+
+def _rot(ax, ay, az):
+    cx, sx, cy, sy, cz, sz = np.cos(ax), np.sin(ax), np.cos(ay), np.sin(ay), np.cos(az), np.sin(az)
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def pose(rng):
+    """A camera pose Tcw with mOw computed as Frame::UpdatePoseMatrices does (float)."""
+    R = _rot(*rng.uniform(-0.1, 0.1, 3)).astype(np.float32)
+    t = rng.uniform(-2, 2, 3).astype(np.float32)
+    ow = np.zeros(3, np.float32)
+    for i in range(3):  # -Rcw^T * tcw, float dot left to right
+        ow[i] = -((R[0, i] * t[0] + R[1, i] * t[1]) + R[2, i] * t[2])
+    return R, t, ow
+
+
+def local_map_3d(oracle, keys, desc, n_mp, width, height, rng_seed=0, scale_factor=1.2):
+    """Local MapPoints in world coordinates for Frame::isInFrustum + SearchByProjection.
+    70 % are back-projections of frame keypoints at random depth (descriptor = the
+    keypoint's with ~8 % bit flips, distance range consistent with the keypoint's
+    octave), 30 % random points (some behind the camera or out of the image).
+    Normals are mostly towards the camera; ~10 % are tilted past the 0.5 cos limit.
+    Returns (pose record, map points, map-point descriptors)."""
+    rng = np.random.default_rng(rng_seed)
+    R, t, ow = pose(rng)
+    P = np.zeros(n_mp, oracle.MAP_POINT_DTYPE)
+    mpd = rng.integers(0, 256, (n_mp, 32), dtype=np.uint8)
+    n_kp = len(keys)
+    from_kp = (rng.random(n_mp) < 0.7) & (n_kp > 0)
+    kidx = rng.integers(0, max(n_kp, 1), n_mp)
+    z = rng.uniform(2.0, 50.0, n_mp)
+    u = np.where(from_kp, keys["x"][kidx % max(n_kp, 1)] + rng.uniform(-1, 1, n_mp),
+                 rng.uniform(-100, width + 100, n_mp))
+    v = np.where(from_kp, keys["y"][kidx % max(n_kp, 1)] + rng.uniform(-1, 1, n_mp),
+                 rng.uniform(-100, height + 100, n_mp))
+    z = np.where(~from_kp & (rng.random(n_mp) < 0.1), -z, z)
+    pc = np.stack([(u - CX) / FX * z, (v - CY) / FY * z, z], 1)
+    pw = (pc - t.astype(np.float64)) @ R.astype(np.float64)  # R^T (pc - t)
+    P["pos"] = pw.astype(np.float32)
+    d = pw - ow.astype(np.float64)
+    dist = np.linalg.norm(d, axis=1)
+    nrm = d / dist[:, None] + rng.normal(0, 0.15, (n_mp, 3))
+    tilt = rng.random(n_mp) < 0.1
+    nrm[tilt] = rng.normal(0, 1, (tilt.sum(), 3))
+    P["normal"] = (nrm / np.linalg.norm(nrm, axis=1)[:, None]).astype(np.float32)
+    octv = np.where(from_kp, keys["octave"][kidx % max(n_kp, 1)], rng.integers(0, 8, n_mp))
+    maxd = dist * scale_factor ** octv * rng.uniform(0.9, 1.1, n_mp)
+    maxd[rng.random(n_mp) < 0.05] *= 0.5  # out of the scale-invariance range
+    P["max_distance"] = maxd.astype(np.float32)
+    P["min_distance"] = (maxd / scale_factor ** 7).astype(np.float32)
+    P["bad"] = rng.random(n_mp) < 0.03
+    P["seen"] = rng.random(n_mp) < 0.05
+    P["has_obs"] = rng.random(n_mp) < 0.9
+    if n_kp:
+        src = desc[kidx % n_kp]
+        flips = rng.random((n_mp, 256)) < 0.08
+        bits = np.unpackbits(src, axis=1, bitorder="little") ^ flips
+        mpd = np.where(from_kp[:, None], np.packbits(bits.astype(np.uint8), axis=1,
+                                                      bitorder="little"), mpd)
+    rec = np.zeros(1, oracle.POSE_DTYPE)
+    rec["rcw"] = R.reshape(1, 9)
+    rec["tcw"] = t
+    rec["ow"] = ow
+    return rec, P, np.ascontiguousarray(mpd, np.uint8)
