@@ -26,6 +26,10 @@
  *                                  src/ORBmatcher.cc:1460-1619
  *   orb_match_bow                  ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
  *                                  src/ORBmatcher.cc:164-306
+ *   orb_frustum(_batch)            Frame::isInFrustum src/Frame.cc:303-366 over the local map
+ *                                  (Tracking::SearchLocalPoints src/Tracking.cc:1360-1377,
+ *                                  MapPoint::PredictScale src/MapPoint.cc:435-450)
+ *   orb_stereo_match_batch         device-batched ComputeStereoMatches (pairs from two extractors)
  *
  * Error behaviour: the reference has no status codes (an empty image returns
  * silently with outputs untouched, src/ORBextractor.cc:1095-1096; a non-8UC1
