@@ -3,8 +3,8 @@
 // Pipeline for a batch of B images (one launch per stage, every launch covers
 // all B images; HBM layout in DESIGN.md §3):
 //   k_pyr_resize   x (nlevels-1)  bilinear level l from level l-1   src/ORBextractor.cc:1172-1207
-//   k_fast_cells   x 1            FAST-9/16 score, cell-local NMS,    src/ORBextractor.cc:816-865
-//                                 iniTh -> minTh fallback, ordered compaction
+//   k_fast_band    x 1            FAST-9/16 score over a band of      src/ORBextractor.cc:816-865
+//                                 cells, cell-local NMS, iniTh -> minTh fallback, ordered compaction
 //   k_octree       x 1            DistributeOctTree, one workgroup   src/ORBextractor.cc:558-782
 //                                 per (image, level), list order emulated exactly
 //   k_orient_desc  x 1            IC_Angle + 7x7 blur + rBRIEF-256,   src/ORBextractor.cc:77-164,
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   }
 }
 
-// ============================================================ k_fast_cells
+// ============================================================ k_fast_band
 // FAST arc strength at the pixel `c` points to (LDS tile, row pitch `p`):
 // m = max(best dark 9-arc, best bright 9-arc), where an arc's strength is the
 // min over its 9 pixels of |I(p) - I(q)| on the matching side.  FAST(t) detects
@@ -137,24 +137,43 @@ __device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
   return max((int)best.x, (int)best.y);
 }
 
-// One workgroup per (cell, image).  Output: the cell's keypoints (row-major in
-// the cell's detection window, exactly cv::FAST's order) packed as
-// x | y<<12 | score<<24 in level coordinates, and their count.
-__global__ __launch_bounds__(256) void k_fast_cells(
+// One workgroup per (band, image).  A band is a run of cells of one cell row
+// of one level (OrbBandDesc).  Cell detection windows (ROI shrunk by 3,
+// src/ORBextractor.cc:819-843) tile the band interior without overlap, so
+// every pixel's FAST arc strength is computed once for the whole band.  NMS
+// stays per cell: a cell window's edge acts as cv::FAST's zero border (column
+// edge flags), survivors at iniTh and at minTh are set in two interior
+// bitmaps, and one wave per cell compacts its window row by row (lane = row),
+// falling back to the minTh bitmap when the cell has no iniTh survivor
+// (src/ORBextractor.cc:846-850).  Output per cell: its keypoints in row-major
+// window order (cv::FAST's order), packed x | y<<12 | score<<24 in level
+// coordinates, and their count.
+#define FAST_ROUND 2048    // pixels pretested per round (8 per thread)
+#define FAST_CORNERS 2048  // corner list capacity; beyond it NMS runs densely
+
+__device__ __forceinline__ unsigned long long bit_run(const uint32_t* bits, int start, int n) {
+  // bits [start, start + n) of a little-endian bit array, n <= 64
+  const int w = start >> 5, sh = start & 31;
+  unsigned long long v = (unsigned long long)bits[w] | ((unsigned long long)bits[w + 1] << 32);
+  v >>= sh;
+  if (sh) v |= (unsigned long long)bits[w + 2] << (64 - sh);
+  return n >= 64 ? v : (v & ((1ull << n) - 1ull));
+}
+
+__global__ __launch_bounds__(256) void k_fast_band(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
-    const OrbCellDesc* __restrict__ cells, uint32_t* __restrict__ cellKeys,
-    int32_t* __restrict__ cellCount) {
+    const OrbBandDesc* __restrict__ bands, const OrbCellDesc* __restrict__ cells,
+    uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int scanTmp[17];
-  __shared__ int qCount;
-  const int cell = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
-  const OrbCellDesc cd = cells[cell];
-  const int l = cd.level;
-  const int rows = cd.y1 - cd.y0, cols = cd.x1 - cd.x0;
-  const long long slot = (long long)img * plan.ncells + cell;
-  if (rows < 7 || cols < 7) {
-    if (tid == 0) cellCount[slot] = 0;
+  __shared__ int qCount, cCount;
+  const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const OrbBandDesc bd = bands[blockIdx.x];
+  const int l = bd.level;
+  const int R = bd.y1 - bd.y0, C = bd.x1 - bd.x0;
+  const long long slot0 = (long long)img * plan.ncells + bd.cellBeg;
+  if (R < 7 || C < 7) {
+    for (int c = tid; c < bd.nCells; c += 256) cellCount[slot0 + c] = 0;
     return;
   }
   const uint8_t* lvl;
@@ -166,105 +185,183 @@ __global__ __launch_bounds__(256) void k_fast_cells(
     lvl = arena + (long long)img * arenaPitch + plan.lv[l].arenaOff;
     pitch = plan.lv[l].pitch;
   }
-  uint8_t* roi = smem;  // rows x cols
-  const int dh = rows - 6, dw = cols - 6, sp = dw + 2;
-  uint8_t* sc = smem + ((rows * cols + 15) & ~15);           // (dh+2) x (dw+2), zero border
-  uint8_t* flags = sc + (((dh + 2) * sp + 15) & ~15);        // dh x dw survivors
-  uint16_t* queue = (uint16_t*)(flags + ((dh * dw + 15) & ~15));  // candidate pixel list
+  const int P = (C + 3) & ~3;  // LDS row pitch (bytes)
+  const int nD = P >> 2;       // dwords per LDS row
+  const int iw = C - 6, ih = R - 6, ni = iw * ih;
+  const int nBitWords = (ni >> 5) + 3;
+  const int bandBytes = plan.maxBandBytes;
+  uint8_t* roi = smem;                                        // R x P band pixels
+  uint8_t* sc = smem + bandBytes;                             // R x P arc strengths
+  uint16_t* queue = (uint16_t*)(smem + 2 * bandBytes);        // FAST_ROUND candidates
+  uint16_t* corners = queue + FAST_ROUND;                     // FAST_CORNERS corners
+  uint32_t* bitsIni = (uint32_t*)(corners + FAST_CORNERS);    // interior survivors, iniTh
+  uint32_t* bitsMin = bitsIni + ((bandBytes >> 5) + 3);       // interior survivors, minTh
+  uint8_t* colf = (uint8_t*)(bitsMin + ((bandBytes >> 5) + 3));  // window edge flags per column
   {
-    // all loads in flight before the LDS stores; ROI <= 2048 px (host-checked)
-    const int n = rows * cols;
-    const float invCols = 1.0f / (float)cols;
-    uint8_t v[8];
+    // Realigning copy: LDS dword k of row r = bytes [x0 + 4k, x0 + 4k + 4) of
+    // the row, assembled with alignbyte from the two aligned dwords covering it
+    // (level 0 rows can start at any byte: caller stride).
+    uint32_t* roi32 = (uint32_t*)roi;
+    const int n = R * nD;
+    const float invN = 1.0f / (float)nD;
+    for (int i0 = 0; i0 < n; i0 += 4 * 256) {
+      uint32_t w0[4], w1[4];
+      int sh[4];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int i = tid + 256 * q;
-      if (i < n) {
-        const int r = (int)(((float)i + 0.5f) * invCols), c = i - r * cols;
-        v[q] = lvl[(long long)(cd.y0 + r) * pitch + cd.x0 + c];
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + q * 256 + tid;
+        w0[q] = w1[q] = 0;
+        sh[q] = 0;
+        if (i < n) {
+          const int r = (int)(((float)i + 0.5f) * invN), k = i - r * nD;
+          const uint8_t* a = lvl + (long long)(bd.y0 + r) * pitch + bd.x0 + 4 * k;
+          sh[q] = (int)((uintptr_t)a & 3);
+          const uint32_t* al = (const uint32_t*)(a - sh[q]);
+          w0[q] = al[0];
+          if (sh[q] && 4 * k + 4 - sh[q] < C) w1[q] = al[1];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + q * 256 + tid;
+        if (i < n) roi32[i] = __builtin_amdgcn_alignbyte(w1[q], w0[q], (uint32_t)sh[q]);
       }
     }
+  }
+  for (int i = tid; i < nBitWords; i += 256) bitsIni[i] = bitsMin[i] = 0;
+  for (int i = tid; i < iw; i += 256) colf[i] = 0;
+  if (tid == 0) qCount = cCount = 0;
+  __syncthreads();
+  for (int ci = tid; ci < bd.nCells; ci += 256) {
+    const OrbCellDesc cd = cells[bd.cellBeg + ci];
+    const int cx0 = cd.x0 - bd.x0, ww = cd.x1 - cd.x0 - 6;
+    if (ww > 0) {
+      colf[cx0] |= 1;           // left window edge: x-1 is outside
+      colf[cx0 + ww - 1] |= 2;  // right window edge: x+1 is outside
+    }
+  }
+  // Arc strengths of the band interior.  Pixels that cannot be a corner at the
+  // lower threshold store 0 (what cv::FAST stores for non-corners); the
+  // necessary condition is two circularly adjacent compass pixels (circle
+  // positions 0,4,8,12) on the same side.  Survivors are queued so the full
+  // arc computation runs on dense lanes; scored pixels above the lower
+  // threshold go to the corner list.
+  const float invIw = 1.0f / (float)iw;
+  const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
+  const int tq = min(ti, tm);
+  for (int base = 0; base < ni; base += FAST_ROUND) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int i = tid + 256 * q;
-      if (i < n) roi[i] = v[q];
+    for (int q = 0; q < FAST_ROUND / 256; ++q) {
+      const int i = base + q * 256 + tid;
+      bool pass = false;
+      int off = 0;
+      if (i < ni) {
+        const int y = (int)(((float)i + 0.5f) * invIw), x = i - y * iw;
+        off = (y + 3) * P + (x + 3);
+        const uint8_t* c = roi + off;
+        const int v = c[0];
+        const int q0 = c[3 * P], q4 = c[3], q8 = c[-3 * P], q12 = c[-3];
+        const bool d0 = q0 < v - tq, d4 = q4 < v - tq, d8 = q8 < v - tq, d12 = q12 < v - tq;
+        const bool b0 = q0 > v + tq, b4 = q4 > v + tq, b8 = q8 > v + tq, b12 = q12 > v + tq;
+        pass = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) ||
+               (b4 && b8) || (b8 && b12) || (b12 && b0);
+        if (!pass) sc[off] = 0;
+      }
+      const unsigned long long bal = __ballot(pass);
+      int qb = 0;
+      if (lane == 0 && bal) qb = atomicAdd(&qCount, __popcll(bal));
+      qb = __shfl(qb, 0, 64);
+      if (pass) queue[qb + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)off;
     }
-  }
-  for (int i = tid; i < (dh + 2) * sp; i += 256) sc[i] = 0;
-  if (tid == 0) qCount = 0;
-  __syncthreads();
-  const int npix = dh * dw;
-  const float invDw = 1.0f / (float)dw;
-  // Pixels that cannot be a corner at the lower threshold keep score 0 (what
-  // cv::FAST stores for non-corners).  Necessary condition for a 9-arc: two
-  // circularly adjacent compass pixels (circle positions 0,4,8,12) on the same
-  // side.  Survivors are queued (wave-aggregated LDS append) so the full
-  // arc computation runs on dense lanes.
-  const int tq = min(max(min(plan.iniTh, plan.minTh), 0), 255);
-  const int lane = tid & 63;
-  for (int i0 = 0; i0 < npix; i0 += 256) {
-    const int i = i0 + tid;
-    bool pass = false;
-    if (i < npix) {
-      const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
-      const uint8_t* c = roi + (y + 3) * cols + (x + 3);
-      const int v = c[0];
-      const int q0 = c[3 * cols], q4 = c[3], q8 = c[-3 * cols], q12 = c[-3];
-      const bool d0 = q0 < v - tq, d4 = q4 < v - tq, d8 = q8 < v - tq, d12 = q12 < v - tq;
-      const bool b0 = q0 > v + tq, b4 = q4 > v + tq, b8 = q8 > v + tq, b12 = q12 > v + tq;
-      pass = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) ||
-             (b4 && b8) || (b8 && b12) || (b12 && b0);
+    __syncthreads();
+    const int nq = qCount;
+    for (int j0 = 0; j0 < nq; j0 += 256) {
+      const int j = j0 + tid;
+      bool corner = false;
+      int off = 0;
+      if (j < nq) {
+        off = queue[j];
+        const int m = min(max(fast_score(roi + off, P), 0), 255);
+        sc[off] = (uint8_t)m;
+        corner = m > tq && m >= 2;
+      }
+      const unsigned long long bal = __ballot(corner);
+      int cb = 0;
+      if (lane == 0 && bal) cb = atomicAdd(&cCount, __popcll(bal));
+      cb = __shfl(cb, 0, 64) + __popcll(bal & ((1ull << lane) - 1ull));
+      if (corner && cb < FAST_CORNERS) corners[cb] = (uint16_t)off;
     }
-    const unsigned long long bal = __ballot(pass);
-    int base = 0;
-    if (lane == 0 && bal) base = atomicAdd(&qCount, __popcll(bal));
-    base = __shfl(base, 0, 64);
-    if (pass) queue[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)i;
+    __syncthreads();
+    if (tid == 0) qCount = 0;
+    __syncthreads();
   }
-  __syncthreads();
-  const int nq = qCount;
-  for (int j = tid; j < nq; j += 256) {
-    const int i = queue[j];
-    const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
-    const int s = fast_score(roi + (y + 3) * cols + (x + 3), cols);
-    sc[(y + 1) * sp + (x + 1)] = (uint8_t)min(max(s, 0), 255);
-  }
-  __syncthreads();
-  // cell-local NMS at threshold t (OpenCV FAST_t with nonmax_suppression):
-  // corners store score m-1, everything else (incl. outside the window) 0, and
-  // a corner survives iff its score beats all 8 stored neighbour scores.
-  const int per = (npix + 255) >> 8;
-  const int beg = min(tid * per, npix), end = min(beg + per, npix);
-  auto survives = [&](int i, int t) -> int {
-    const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
-    const uint8_t* c = sc + (y + 1) * sp + (x + 1);
+  // NMS of every corner at both thresholds (OpenCV FAST_t with
+  // nonmax_suppression inside the cell window): a corner (m > t) survives iff
+  // no neighbour inside its window has nb > t && nb >= m.
+  const int nc = cCount;
+  const bool dense = nc > FAST_CORNERS;
+  const int nItems = dense ? ni : nc;
+  for (int j = tid; j < nItems; j += 256) {
+    int x, y, off;
+    if (dense) {
+      y = (int)(((float)j + 0.5f) * invIw);
+      x = j - y * iw;
+      off = (y + 3) * P + (x + 3);
+    } else {
+      off = corners[j];
+      const int ry = (int)(((float)off + 0.5f) / (float)P);
+      y = ry - 3;
+      x = off - ry * P - 3;
+    }
+    const uint8_t* c = sc + off;
     const int m = c[0];
-    if (m <= t || m < 2) return 0;  // not a corner, or score 0 cannot beat a 0 neighbour
-    const int nb[8] = {c[-sp - 1], c[-sp], c[-sp + 1], c[-1], c[1], c[sp - 1], c[sp], c[sp + 1]};
+    if (m <= tq || m < 2) continue;
+    const int cf = colf[x];
+    const bool L = !(cf & 1), Rt = !(cf & 2), U = y > 0, D = y < ih - 1;
+    const int nb[8] = {(U && L) ? c[-P - 1] : 0, U ? c[-P] : 0, (U && Rt) ? c[-P + 1] : 0,
+                       L ? c[-1] : 0, Rt ? c[1] : 0, (D && L) ? c[P - 1] : 0,
+                       D ? c[P] : 0, (D && Rt) ? c[P + 1] : 0};
+    bool si = m > ti, sm = m > tm;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (nb[k] > t && nb[k] >= m) return 0;
-    return 1;
-  };
-  int t = min(max(plan.iniTh, 0), 255);
-  int mine = 0;
-  for (int i = beg; i < end; ++i) mine += (flags[i] = (uint8_t)survives(i, t));
-  int total;
-  int off = block_excl_scan(mine, scanTmp, &total);
-  if (total == 0) {  // src/ORBextractor.cc:846-850: retry the cell at minThFAST
-    t = min(max(plan.minTh, 0), 255);
-    mine = 0;
-    for (int i = beg; i < end; ++i) mine += (flags[i] = (uint8_t)survives(i, t));
-    off = block_excl_scan(mine, scanTmp, &total);
-  }
-  uint32_t* out = cellKeys + slot * plan.keyCap;
-  for (int i = beg; i < end && mine; ++i) {
-    if (flags[i]) {
-      const int y = (int)(((float)i + 0.5f) * invDw), x = i - y * dw;
-      out[off++] = pack_key(cd.x0 + 3 + x, cd.y0 + 3 + y, sc[(y + 1) * sp + (x + 1)] - 1);
+    for (int k = 0; k < 8; ++k) {
+      if (nb[k] >= m) {
+        si = si && !(nb[k] > ti);
+        sm = sm && !(nb[k] > tm);
+      }
     }
+    const int bit = y * iw + x;
+    if (si) atomicOr(&bitsIni[bit >> 5], 1u << (bit & 31));
+    if (sm) atomicOr(&bitsMin[bit >> 5], 1u << (bit & 31));
   }
-  if (tid == 0) cellCount[slot] = total;
+  __syncthreads();
+  // Per-cell compaction, one wave per cell, lane = window row (ih <= 64,
+  // host-checked): prefix over rows gives each row's first output slot.
+  const int nw = blockDim.x >> 6;
+  for (int ci = wave; ci < bd.nCells; ci += nw) {
+    const OrbCellDesc cd = cells[bd.cellBeg + ci];
+    const int cx0 = cd.x0 - bd.x0, ww = cd.x1 - cd.x0 - 6;
+    const long long slot = slot0 + ci;
+    uint32_t* out = cellKeys + slot * plan.keyCap;
+    int total = 0;
+    if (ww > 0) {
+      for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1 && (total > 0 || tm == ti)) break;
+        const uint32_t* bits = pass == 0 ? bitsIni : bitsMin;
+        unsigned long long row = lane < ih ? bit_run(bits, lane * iw + cx0, ww) : 0ull;
+        const int cnt = __popcll(row);
+        const int incl = wave_incl_scan(cnt);
+        total = __shfl(incl, 63, 64);
+        int o = incl - cnt;
+        while (row) {
+          const int x = __builtin_ctzll(row);
+          row &= row - 1;
+          const int m = sc[(lane + 3) * P + cx0 + x + 3];
+          out[o++] = pack_key(bd.x0 + 3 + cx0 + x, bd.y0 + 3 + lane, m - 1);
+        }
+      }
+    }
+    if (lane == 0) cellCount[slot] = total;
+  }
 }
 
 // ================================================================ k_octree
@@ -877,16 +974,16 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   return hipGetLastError();
 }
 
-hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
-                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
-                            const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
-                            int nimg, hipStream_t s) {
-  const int rows = plan->maxCellRows, cols = plan->maxCellCols;
-  const size_t lds = (size_t)((rows * cols + 15) & ~15) + (size_t)(((rows - 4) * (cols - 4) + 15) & ~15) +
-                     (size_t)(((rows - 6) * (cols - 6) + 15) & ~15) + 2 * (size_t)(rows - 6) * (cols - 6);
-  dim3 grid(plan->ncells, nimg), block(256);
-  hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, cells, cellKeys, cellCount);
+hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                           const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                           const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
+                           uint32_t* cellKeys, int32_t* cellCount, int nimg, hipStream_t s) {
+  const size_t bitBytes = 4 * (size_t)((plan->maxBandBytes >> 5) + 3);
+  const size_t lds = (size_t)plan->maxBandBytes * 2 + FAST_ROUND * 2 + FAST_CORNERS * 2 +
+                     2 * bitBytes + (size_t)plan->maxBandBytes / 7 + 16;
+  dim3 grid(nbands, nimg), block(256);
+  hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
+                     arenaPitch, *plan, bands, cells, cellKeys, cellCount);
   return hipGetLastError();
 }
 

@@ -42,7 +42,8 @@ struct OrbPlanDesc {
   int maxCellRows, maxCellCols;  // largest cell ROI (for LDS sizing)
   int srcW, srcH;
   int nBlurTiles;    // 64x16 blur tiles over all levels of one image
-  int _pad;
+  int nBands;        // FAST bands over all levels
+  int maxBandBytes;  // largest band's LDS footprint: rows x (cols rounded up to 4)
   OrbLevelDesc lv[ORB_MAX_LEVELS];
 };
 
@@ -52,6 +53,15 @@ struct OrbPlanDesc {
 struct OrbCellDesc {
   int16_t level, y0, y1, x0, x1, _pad;
 };
+
+// One FAST band: cells [cellBeg, cellBeg + nCells) of one cell row of one
+// level (consecutive in the cell table); rows [y0,y1) x cols [x0,x1) is the
+// union of their ROIs.
+struct OrbBandDesc {
+  int16_t level, y0, y1, x0, x1, nCells;
+  int32_t cellBeg;
+};
+#define ORB_BAND_BYTES 10240  // LDS budget for one band's pixels (and again for scores)
 
 // One 64 x 16 output tile of the 7x7 Gaussian pass over level `level`.
 struct OrbTileDesc {

@@ -27,10 +27,10 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
                             int dh, const int* xofs, const void* alpha, const int* yofs,
                             const void* beta, int xmax, int nimg, hipStream_t s);
-hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
-                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
-                            const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
-                            int nimg, hipStream_t s);
+hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                           const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                           const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
+                           uint32_t* cellKeys, int32_t* cellCount, int nimg, hipStream_t s);
 size_t orb_k_octree_lds(int nodeCapMax, int maxCellsPerLevel, int ldsKeyCap);
 hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
@@ -215,7 +215,7 @@ struct orb_extractor {
   std::vector<OrbCellDesc> cells;
   long long arenaBytes = 0, blurBytes = 0;
   int maxCellsPerLevel = 0, nodeCapMax = 0, ldsKeyCap = 0;
-  DevBuf dCells, dRtab, dTiles;
+  DevBuf dCells, dRtab, dTiles, dBands;
 
   // batch scratch
   int batchCap = 0;
@@ -228,7 +228,8 @@ struct orb_extractor {
   size_t lastImg0Pitch = 0;
   int lastImg0Stride = 0;
 
-  // profiling: stages k_pyr_resize (x nlevels-1), k_fast_cells, k_octree, k_orient_desc
+  // profiling: stages k_pyr_resize (x nlevels-1), k_blur_levels, k_fast_band, k_octree,
+  // k_orient_desc
   StageProfiler prof;
 };
 
@@ -286,6 +287,8 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   std::vector<OrbCellDesc> cells;
   std::vector<int32_t> rtab;
   std::vector<OrbTileDesc> tiles;
+  std::vector<OrbBandDesc> bands;
+  int maxBandBytes = 0;
   long long arena = 0, blurArena = 0;
   int keyCap = 1, maxRows = 7, maxCols = 7, maxCellsPerLevel = 1, nodeCapMax = 1, slots = 0;
   for (int l = 0; l < L; ++l) {
@@ -345,6 +348,33 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
       }
     }
     d.cellEnd = (int)cells.size();
+    // FAST bands: runs of consecutive cells of one cell row whose union ROI
+    // fits ORB_BAND_BYTES of LDS (k_fast_band)
+    for (int c = d.cellBeg; c < d.cellEnd;) {
+      OrbBandDesc b;
+      b.level = (int16_t)l;
+      b.y0 = cells[c].y0;
+      b.y1 = cells[c].y1;
+      b.x0 = cells[c].x0;
+      b.x1 = cells[c].x1;
+      b.cellBeg = c;
+      int e = c + 1;
+      while (e < d.cellEnd && cells[e].y0 == b.y0) {
+        const int x1 = std::max<int>(b.x1, cells[e].x1);
+        if ((b.y1 - b.y0) * ((x1 - b.x0 + 3) & ~3) > ORB_BAND_BYTES) break;
+        b.x1 = (int16_t)x1;
+        ++e;
+      }
+      b.nCells = (int16_t)(e - c);
+      // k_fast_band compacts a cell window with one lane per row and one
+      // 64-bit word per row segment
+      if (b.y1 - b.y0 - 6 > 64) return ORB_EINVAL;
+      for (int k = c; k < e; ++k)
+        if (cells[k].x1 - cells[k].x0 - 6 > 64) return ORB_EINVAL;
+      maxBandBytes = std::max(maxBandBytes, (b.y1 - b.y0) * ((b.x1 - b.x0 + 3) & ~3));
+      bands.push_back(b);
+      c = e;
+    }
     maxCellsPerLevel = std::max(maxCellsPerLevel, d.cellEnd - d.cellBeg);
     // octree roots, src/ORBextractor.cc:562-564
     d.Wr = maxBX - minBX;
@@ -389,9 +419,13 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
       }
     }
   }
-  if (maxRows * maxCols > 2048) return ORB_EINVAL;  // k_fast_cells ROI staging limit
+  // k_fast_band: one band = at least one cell; its pixels and scores + the
+  // candidate queue must fit the 64 KiB a workgroup may allocate
+  if (2 * (size_t)maxBandBytes + 4096 > 64 * 1024) return ORB_EINVAL;
   P.ncells = (int)cells.size();
   P.nBlurTiles = (int)tiles.size();
+  P.nBands = (int)bands.size();
+  P.maxBandBytes = maxBandBytes;
   P.keyCap = keyCap;
   P.slotsPerImage = slots;
   P.maxCellRows = maxRows;
@@ -410,6 +444,10 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (st) return st;
   st = h->dTiles.ensure(tiles.size() * sizeof(OrbTileDesc));
   if (st) return st;
+  st = h->dBands.ensure(bands.size() * sizeof(OrbBandDesc));
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(h->dBands.p, bands.data(), bands.size() * sizeof(OrbBandDesc),
+                         hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->dTiles.p, tiles.data(), tiles.size() * sizeof(OrbTileDesc),
                          hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->dCells.p, cells.data(), cells.size() * sizeof(OrbCellDesc),
@@ -474,9 +512,9 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                             h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, B,
                             s));
   if (ev) HIP_TRY(hipEventRecord((*ev)[2], s));
-  HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                           h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                           h->dCellCount.as<int32_t>(), B, s));
+  HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                          h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
+                          h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
   if (ev) HIP_TRY(hipEventRecord((*ev)[3], s));
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
@@ -543,7 +581,7 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   }
   h->ownStream = true;
   h->prof.nStages = 5;
-  const char* names[5] = {"k_pyr_resize", "k_blur_levels", "k_fast_cells", "k_octree",
+  const char* names[5] = {"k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree",
                           "k_orient_desc"};
   for (int i = 0; i < 5; ++i) {
     h->prof.names[i] = names[i];

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(orb):
 def test_library_has_gfx950_code_object(orb):
     blob = orb.LIB_PATH.read_bytes()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle entry for gfx950
-    for k in (b"k_fast_cells", b"k_octree", b"k_orient_desc", b"k_proj_resolve", b"k_stereo_match"):
+    for k in (b"k_fast_band", b"k_octree", b"k_orient_desc", b"k_proj_resolve", b"k_stereo_match"):
         assert k in blob
 
 
