@@ -20,24 +20,21 @@
 // cv::resize(prev, level, sz, 0, 0, INTER_LINEAR) on 8U with OpenCV's 11-bit
 // fixed-point weights.  The weight tables are computed
 // on the host with the reference's float/double expressions; the kernel only
-// does the integer taps.  One thread per output pixel, 64x4 tiles.
-#define PYR_TW 128  // output tile: 128 columns x 8 rows, 4 columns per thread
-#define PYR_TH 8
-#define PYR_SROWS 12  // >= source rows an 8-row output tile can touch (scale <= 1.25)
-#define PYR_SW 48     // >= dwords of source row one 128-column tile touches
-
-__device__ __forceinline__ int lds_byte(const uint32_t* row, int c) {
-  return (int)((row[c >> 2] >> (8 * (c & 3))) & 0xFFu);
-}
+// does the integer taps.  One workgroup per 128 x 32 output tile: the source
+// window is staged in LDS as aligned dwords (realigned from any source stride),
+// each thread produces 4 columns x 4 rows and stores whole dwords, so a wave
+// writes two full 128-byte rows per store.
+#define PYR_TW 128
+#define PYR_TH 32
+#define PYR_SROWS 44  // >= source rows a 32-row output tile can touch (scale <= 1.25)
+#define PYR_SW 44     // >= dwords of source row a 128-column tile touches (+2 read-ahead)
 
 __global__ __launch_bounds__(256) void k_pyr_resize(
     const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sw, int sh,
     uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
     const int* __restrict__ xofs, const int* __restrict__ alpha,
     const int* __restrict__ yofs, const int* __restrict__ beta, int xmax) {
-  // The source window of the tile is staged in LDS as aligned dwords; every
-  // output reads its 2x2 taps from there.  alpha/beta pack the two 11-bit
-  // weights as (w1 << 16) | (w0 & 0xFFFF).
+  // alpha/beta pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
   __shared__ __attribute__((aligned(16))) uint32_t tile[PYR_SROWS][PYR_SW];
   const int tid = threadIdx.x;
   const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
@@ -47,57 +44,84 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   const int syA = min(max(yofs[y0], 0), sh - 1), syB = min(max(yofs[yl] + 1, 0), sh - 1);
   const int colBase = sxA & ~3;
   const int nW = ((sxB - colBase) >> 2) + 1, nR = syB - syA + 1;
-  const bool aligned = ((srcStride & 3) == 0) && ((((uintptr_t)S) & 3) == 0);
-  for (int i = tid; i < nR * nW; i += 256) {
-    const int r = i / nW, w = i - r * nW;
-    const uint8_t* p = S + (long long)(syA + r) * srcStride + colBase + 4 * w;
-    uint32_t v;
-    if (aligned && colBase + 4 * w + 3 < sw) {
-      v = *reinterpret_cast<const uint32_t*>(p);
-    } else {
-      v = 0;
-      for (int b = 0; b < 4; ++b)
-        if (colBase + 4 * w + b < sw) v |= (uint32_t)p[b] << (8 * b);
+  const int n = nR * nW;
+  const float invW = 1.0f / (float)nW;
+  for (int i0 = 0; i0 < n; i0 += 8 * 256) {
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = i0 + q * 256 + tid;
+      v[q] = 0;
+      if (i < n) {
+        const int r = (int)(((float)i + 0.5f) * invW), w = i - r * nW;
+        const uint8_t* row = S + (long long)(syA + r) * srcStride;
+        v[q] = load_u32_any(row + colBase + 4 * w, row + sw - 1);
+      }
     }
-    tile[r][w] = v;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = i0 + q * 256 + tid;
+      if (i < n) {
+        const int r = (int)(((float)i + 0.5f) * invW), w = i - r * nW;
+        tile[r][w] = v[q];
+      }
+    }
   }
   __syncthreads();
-  const int ty = tid >> 5, tx = tid & 31;
-  const int y = y0 + ty;
+  const int tx = tid & 31, ty = tid >> 5;
   const int xs = x0 + 4 * tx;
-  if (y >= dh || xs >= dw) return;
-  const int sy = yofs[y];
-  const int bw = beta[y];
-  const int b0 = (int)(short)(bw & 0xFFFF), b1 = bw >> 16;
-  const uint32_t* R0 = tile[min(max(sy, 0), sh - 1) - syA];
-  const uint32_t* R1 = tile[min(max(sy + 1, 0), sh - 1) - syA];
-  uint32_t packed = 0;
+  if (xs >= dw) return;
+  int cb[4], a0[4], a1[4];
+  bool inner[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int dx = min(xs + j, dw - 1);
-    const int c = xofs[dx] - colBase;
+    cb[j] = xofs[dx] - colBase;
     const int aw = alpha[dx];
-    const int a0 = (int)(short)(aw & 0xFFFF), a1 = aw >> 16;
-    int h0, h1;
-    if (dx < xmax) {
-      h0 = lds_byte(R0, c) * a0 + lds_byte(R0, c + 1) * a1;
-      h1 = lds_byte(R1, c) * a0 + lds_byte(R1, c + 1) * a1;
-    } else {
-      h0 = lds_byte(R0, c) * 2048;
-      h1 = lds_byte(R1, c) * 2048;
-    }
-    int v = min(max((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 0), 255);
-    // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
-    // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
-    // undefined upper half (observed miscompile on gfx950)
-    __asm__ volatile("" : "+v"(v));
-    packed |= (uint32_t)v << (8 * j);
+    a0[j] = (int)(short)(aw & 0xFFFF);
+    a1[j] = aw >> 16;
+    inner[j] = dx < xmax;
   }
-  uint8_t* out = dst + (long long)blockIdx.z * dstImgPitch + (long long)y * dstStride + xs;
-  if (xs + 4 <= dw) {
-    *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 64 == 0, xs % 4 == 0
-  } else {
-    for (int j = 0; xs + j < dw; ++j) out[j] = (uint8_t)(packed >> (8 * j));
+  const int k0 = cb[0] >> 2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cb[j] -= 4 * k0;
+  uint8_t* outImg = dst + (long long)blockIdx.z * dstImgPitch;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int y = y0 + 4 * ty + rr;
+    if (y >= dh) break;
+    const int sy = yofs[y];
+    const int bw = beta[y];
+    const int b0 = (int)(short)(bw & 0xFFFF), b1 = bw >> 16;
+    const uint32_t* R0 = tile[min(max(sy, 0), sh - 1) - syA] + k0;
+    const uint32_t* R1 = tile[min(max(sy + 1, 0), sh - 1) - syA] + k0;
+    const uint32_t p0 = R0[0], p1 = R0[1], p2 = R0[2];
+    const uint32_t q0 = R1[0], q1 = R1[1], q2 = R1[2];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t t0 = byte_pair(p0, p1, p2, cb[j]), t1 = byte_pair(q0, q1, q2, cb[j]);
+      int h0, h1;
+      if (inner[j]) {
+        h0 = (int)(t0 & 0xFFu) * a0[j] + (int)((t0 >> 8) & 0xFFu) * a1[j];
+        h1 = (int)(t1 & 0xFFu) * a0[j] + (int)((t1 >> 8) & 0xFFu) * a1[j];
+      } else {
+        h0 = (int)(t0 & 0xFFu) * 2048;
+        h1 = (int)(t1 & 0xFFu) * 2048;
+      }
+      int v = min(max((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 0), 255);
+      // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
+      // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
+      // undefined upper half (observed miscompile on gfx950)
+      __asm__ volatile("" : "+v"(v));
+      packed |= (uint32_t)v << (8 * j);
+    }
+    uint8_t* out = outImg + (long long)y * dstStride + xs;
+    if (xs + 4 <= dw) {
+      *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 64 == 0, xs % 4 == 0
+    } else {
+      for (int j = 0; xs + j < dw; ++j) out[j] = (uint8_t)(packed >> (8 * j));
+    }
   }
 }
 
@@ -716,8 +740,9 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i;
 }
 
-#define BLUR_SH (ORB_BLUR_TH + 6)
-#define BLUR_WROW 19  // dwords per staged row: bytes x0-4 .. x0+71
+#define BLUR_SH (ORB_BLUR_TH + 6)  // staged source rows y0-3 .. y0+TH+2
+#define BLUR_WROW (ORB_BLUR_TW / 4 + 2)  // dwords per staged row: bytes x0-4 .. x0+TW+3
+#define BLUR_RP (ORB_BLUR_TW / 2 + 2)    // row-pass pitch in dwords (u16 pairs), padded
 
 __device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
   const uint32_t w = b < 4 ? w0 : (b < 8 ? w1 : w2);
@@ -728,11 +753,11 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbTileDesc* __restrict__ tiles, uint8_t* __restrict__ blur, long long blurPitch) {
-  // staged source rows y0-3 .. y0+18, byte b of a row = level column x0-4+b.
-  // Every LDS access is a naturally aligned dword (or 8 bytes): unaligned
-  // sub-dword LDS reads are replayed by the hardware.
+  // Source tile staged as aligned dwords, byte b of a row = level column
+  // x0-4+b (realigned from any stride); every LDS access is an aligned dword
+  // or 8 bytes (unaligned sub-dword LDS reads are replayed by the hardware).
   __shared__ __attribute__((aligned(16))) uint32_t raw[BLUR_SH][BLUR_WROW + 1];
-  __shared__ __attribute__((aligned(16))) uint32_t rowp[BLUR_SH][ORB_BLUR_TW / 2];
+  __shared__ __attribute__((aligned(16))) uint32_t rowp[BLUR_SH][BLUR_RP];
   const int tid = threadIdx.x, img = blockIdx.y;
   const OrbTileDesc td = tiles[blockIdx.x];
   const int l = td.level;
@@ -746,34 +771,33 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     lvl = arena + (long long)img * arenaPitch + L.arenaOff;
     pitch = L.pitch;
   }
-  const bool aligned = ((pitch & 3) == 0) && ((((uintptr_t)lvl) & 3) == 0);
-  const bool interior = aligned && td.x0 >= 4 && td.y0 >= 3 && td.x0 + 72 <= L.w &&
+  constexpr int kN = BLUR_SH * BLUR_WROW;
+  const bool interior = td.x0 >= 4 && td.y0 >= 3 && td.x0 + ORB_BLUR_TW + 4 <= L.w &&
                         td.y0 + ORB_BLUR_TH + 3 <= L.h;
   if (interior) {
-    constexpr int kN = BLUR_SH * 18;
-    uint32_t v[2];
+    uint32_t v[(kN + 255) / 256];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < (kN + 255) / 256; ++q) {
       const int i = tid + 256 * q;
+      v[q] = 0;
       if (i < kN) {
-        const int r = i / 18, wq = i - r * 18;
-        v[q] = *reinterpret_cast<const uint32_t*>(lvl + (long long)(td.y0 - 3 + r) * pitch +
-                                                  td.x0 - 4 + 4 * wq);
+        const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
+        const uint8_t* row = lvl + (long long)(td.y0 - 3 + r) * pitch;
+        v[q] = load_u32_any(row + td.x0 - 4 + 4 * wq, row + L.w - 1);
       }
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < (kN + 255) / 256; ++q) {
       const int i = tid + 256 * q;
       if (i < kN) {
-        const int r = i / 18, wq = i - r * 18;
+        const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
         raw[r][wq] = v[q];
       }
     }
   } else {
     // border tile: per-byte reflect-101 gather, assembled into dwords
-    constexpr int kN = BLUR_SH * 18;
     for (int i = tid; i < kN; i += 256) {
-      const int r = i / 18, wq = i - r * 18;
+      const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
       const int y = reflect101(td.y0 - 3 + r, L.h);
       const uint8_t* row = lvl + (long long)y * pitch;
       uint32_t w = 0;
@@ -787,9 +811,10 @@ __global__ __launch_bounds__(256) void k_blur_levels(
   }
   __syncthreads();
   const int k[7] = {18, 34, 49, 55, 49, 34, 18};
-  // row pass: task (r, g) -> outputs columns 4g..4g+3 from bytes 4g+1 .. 4g+10
-  for (int id = tid; id < BLUR_SH * 16; id += 256) {
-    const int r = id >> 4, g = id & 15;
+  // row pass: task (r, g) -> u16 sums of columns 4g..4g+3 from bytes 4g+1 .. 4g+10
+  constexpr int G = ORB_BLUR_TW / 4;
+  for (int id = tid; id < BLUR_SH * G; id += 256) {
+    const int r = id / G, g = id - r * G;
     const uint32_t w0 = raw[r][g], w1 = raw[r][g + 1], w2 = raw[r][g + 2];
     int o[4];
 #pragma unroll
@@ -805,36 +830,38 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     *reinterpret_cast<uint2*>(&rowp[r][2 * g]) = pk;
   }
   __syncthreads();
-  // column pass: thread -> columns (2q, 2q+1) x rows (2rp, 2rp+1)
-  const int q = tid & 31, rp = tid >> 5;
-  uint32_t cv[8];
+  // column pass: thread -> columns 4qx..4qx+3 x rows 4qy..4qy+3, dword stores
+  // (a wave writes two whole 128-byte rows per store)
+  const int qx = tid & (G - 1), qy = tid / G;
+  uint8_t* dst = blur + (long long)img * blurPitch + L.blurOff;
+  const int x = td.x0 + 4 * qx;
+  uint2 cv[10];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) cv[j] = rowp[2 * rp + j][q];
-  int out[2][2];
+  for (int j = 0; j < 10; ++j) cv[j] = *reinterpret_cast<const uint2*>(&rowp[4 * qy + j][2 * qx]);
 #pragma unroll
-  for (int rr = 0; rr < 2; ++rr) {
-    int a0 = 0, a1 = 0;
+  for (int rr = 0; rr < 4; ++rr) {
+    int a[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
-      a0 += k[j] * (int)(cv[j + rr] & 0xFFFFu);
-      a1 += k[j] * (int)(cv[j + rr] >> 16);
+      a[0] += k[j] * (int)(cv[j + rr].x & 0xFFFFu);
+      a[1] += k[j] * (int)(cv[j + rr].x >> 16);
+      a[2] += k[j] * (int)(cv[j + rr].y & 0xFFFFu);
+      a[3] += k[j] * (int)(cv[j + rr].y >> 16);
     }
-    out[rr][0] = min((a0 + (1 << 15)) >> 16, 255);
-    out[rr][1] = min((a1 + (1 << 15)) >> 16, 255);
-  }
-  uint8_t* dst = blur + (long long)img * blurPitch + L.blurOff;
-  const int x = td.x0 + 2 * q;
+    uint32_t packed = 0;
 #pragma unroll
-  for (int rr = 0; rr < 2; ++rr) {
-    const int y = td.y0 + 2 * rp + rr;
-    if (y >= L.h) continue;
+    for (int c = 0; c < 4; ++c) {
+      int v = min((a[c] + (1 << 15)) >> 16, 255);
+      __asm__ volatile("" : "+v"(v));  // see k_pyr_resize: keep the byte pack opaque
+      packed |= (uint32_t)v << (8 * c);
+    }
+    const int y = td.y0 + 4 * qy + rr;
+    if (y >= L.h || x >= L.w) continue;
     uint8_t* o = dst + (long long)y * L.blurPitch + x;
-    if (x + 1 < L.w) {
-      int v = out[rr][0] | (out[rr][1] << 8);
-      __asm__ volatile("" : "+v"(v));
-      *reinterpret_cast<uint16_t*>(o) = (uint16_t)v;
-    } else if (x < L.w) {
-      o[0] = (uint8_t)out[rr][0];
+    if (x + 4 <= L.w) {
+      *reinterpret_cast<uint32_t*>(o) = packed;  // blurPitch % 64 == 0, x % 4 == 0
+    } else {
+      for (int c = 0; x + c < L.w; ++c) o[c] = (uint8_t)(packed >> (8 * c));
     }
   }
 }

@@ -111,6 +111,27 @@ __device__ __forceinline__ double pinned_log(double x) {
   return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
 }
 
+// --------------------------------------------------- realigning byte loads
+// Bytes [p, p+4) as one dword for any alignment of p, from the aligned dwords
+// covering them.  `last` = the last byte that may be read (the second aligned
+// dword is only touched if it starts at or before it, so no read leaves the
+// page of a valid byte).
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p, const uint8_t* last) {
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+  const uint32_t* a = (const uint32_t*)(p - sh);
+  const uint32_t lo = a[0];
+  const uint32_t hi = (sh && (const uint8_t*)(a + 1) <= last) ? a[1] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// Bytes b and b+1 (b < 11) of the 12-byte little-endian window (w0, w1, w2),
+// as the low 16 bits of the result.
+__device__ __forceinline__ uint32_t byte_pair(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
+  const uint32_t lo = b < 4 ? w0 : (b < 8 ? w1 : w2);
+  const uint32_t hi = b < 4 ? w1 : (b < 8 ? w2 : 0u);
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(b & 3));
+}
+
 // ------------------------------------------------------------- Hamming
 // DescriptorDistance (src/ORBmatcher.cc:1814-1830) == popcount(a ^ b) over 256 bits.
 __device__ __forceinline__ int hamming256(const ulonglong4 a, const ulonglong4 b) {

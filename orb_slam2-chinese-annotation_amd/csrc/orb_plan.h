@@ -41,7 +41,7 @@ struct OrbPlanDesc {
   int iniTh, minTh;
   int maxCellRows, maxCellCols;  // largest cell ROI (for LDS sizing)
   int srcW, srcH;
-  int nBlurTiles;    // 64x16 blur tiles over all levels of one image
+  int nBlurTiles;    // blur tiles over all levels of one image
   int nBands;        // FAST bands over all levels
   int maxBandBytes;  // largest band's LDS footprint: rows x (cols rounded up to 4)
   OrbLevelDesc lv[ORB_MAX_LEVELS];
@@ -63,9 +63,9 @@ struct OrbBandDesc {
 };
 #define ORB_BAND_BYTES 10240  // LDS budget for one band's pixels (and again for scores)
 
-// One 64 x 16 output tile of the 7x7 Gaussian pass over level `level`.
+// One ORB_BLUR_TW x ORB_BLUR_TH output tile of the 7x7 Gaussian pass over level `level`.
 struct OrbTileDesc {
   int16_t level, x0, y0, _pad;
 };
-#define ORB_BLUR_TW 64
-#define ORB_BLUR_TH 16
+#define ORB_BLUR_TW 128
+#define ORB_BLUR_TH 32
