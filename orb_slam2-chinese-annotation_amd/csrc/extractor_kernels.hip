@@ -11,6 +11,9 @@
 //                                 one wave per keypoint, rescale       1131-1167
 // Bit-exactness contract: every output byte equals the CPU oracle
 // (oracle/orb_oracle.cpp) on the same image.
+#include <stdlib.h>
+#include <type_traits>
+#include <algorithm>
 #include "orb_device.h"
 #include "orb_plan.h"
 #include "orb_pattern_data.h"
@@ -164,16 +167,21 @@ __device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
 // One workgroup per (band, image).  A band is a run of cells of one cell row
 // of one level (OrbBandDesc).  Cell detection windows (ROI shrunk by 3,
 // src/ORBextractor.cc:819-843) tile the band interior without overlap, so
-// every pixel's FAST arc strength is computed once for the whole band.  NMS
-// stays per cell: a cell window's edge acts as cv::FAST's zero border (column
-// edge flags), survivors at iniTh and at minTh are set in two interior
-// bitmaps, and one wave per cell compacts its window row by row (lane = row),
-// falling back to the minTh bitmap when the cell has no iniTh survivor
-// (src/ORBextractor.cc:846-850).  Output per cell: its keypoints in row-major
-// window order (cv::FAST's order), packed x | y<<12 | score<<24 in level
-// coordinates, and their count.
-#define FAST_ROUND 2048    // pixels pretested per round (8 per thread)
+// every pixel's FAST arc strength is computed at most once for the whole band.
+//
+// Phase A (every cell, FAST at iniThFAST): packed compass pretest on 4 pixels
+// per lane, arc strengths of the survivors, NMS of pixels with m > iniTh.
+// Phase B (only cells with no phase-A keypoint, src/ORBextractor.cc:846-850):
+// the same at minThFAST over those cells' windows, reusing phase-A strengths.
+// NMS is per cell: a window's edge acts as cv::FAST's zero border (column
+// edge flags); survivors go to an interior bitmap and one wave per cell
+// compacts its window row by row (lane = row).  Output per cell: keypoints
+// in row-major window order (cv::FAST's order), packed x | y<<12 | score<<24
+// in level coordinates, and their count.
+#define FAST_GROUPS 512    // 4-pixel groups pretested per round (2 per thread)
+#define FAST_QUEUE (4 * FAST_GROUPS)
 #define FAST_CORNERS 2048  // corner list capacity; beyond it NMS runs densely
+#define FAST_LOADS 10      // dwords per thread in flight while staging a band (10 KB)
 
 __device__ __forceinline__ unsigned long long bit_run(const uint32_t* bits, int start, int n) {
   // bits [start, start + n) of a little-endian bit array, n <= 64
@@ -184,14 +192,51 @@ __device__ __forceinline__ unsigned long long bit_run(const uint32_t* bits, int 
   return n >= 64 ? v : (v & ((1ull << n) - 1ull));
 }
 
+// Compass pretest of one parity (two pixels as u16 halves): a pixel can be a
+// FAST(t) corner only if two circularly adjacent compass pixels (circle
+// positions 0,4,8,12) are both darker than v - t or both brighter than v + t.
+// Sign bits (15, 31) of the result are set for passing pixels.
+__device__ __forceinline__ uint32_t pretest_half(uint32_t v, uint32_t q0, uint32_t q4, uint32_t q8,
+                                                 uint32_t q12, s16x2 t1, s16x2 nt1) {
+  const s16x2 V = __builtin_bit_cast(s16x2, v);
+  const s16x2 d0 = V - __builtin_bit_cast(s16x2, q0), d4 = V - __builtin_bit_cast(s16x2, q4);
+  const s16x2 d8 = V - __builtin_bit_cast(s16x2, q8), d12 = V - __builtin_bit_cast(s16x2, q12);
+  // (v - q) - (t+1) >= 0  <=>  dark;  -(t+1) - (v - q) >= 0  <=>  bright
+  const uint32_t nd0 = __builtin_bit_cast(uint32_t, d0 - t1), nd4 = __builtin_bit_cast(uint32_t, d4 - t1);
+  const uint32_t nd8 = __builtin_bit_cast(uint32_t, d8 - t1), nd12 = __builtin_bit_cast(uint32_t, d12 - t1);
+  const uint32_t nb0 = __builtin_bit_cast(uint32_t, nt1 - d0), nb4 = __builtin_bit_cast(uint32_t, nt1 - d4);
+  const uint32_t nb8 = __builtin_bit_cast(uint32_t, nt1 - d8), nb12 = __builtin_bit_cast(uint32_t, nt1 - d12);
+  const uint32_t failD = (nd0 | nd4) & (nd4 | nd8) & (nd8 | nd12) & (nd12 | nd0);
+  const uint32_t failB = (nb0 | nb4) & (nb4 | nb8) & (nb8 | nb12) & (nb12 | nb0);
+  return ~(failD & failB) & 0x80008000u;
+}
+
+// Pretest of the 4 pixels at region columns 4k..4k+3 of region row r (r in
+// [3, R-3)); bit j of the result = pixel 4k+j passes.
+__device__ __forceinline__ uint32_t pretest4(const uint32_t* roi32, int nD, int r, int k, s16x2 t1,
+                                             s16x2 nt1) {
+  const uint32_t* row = roi32 + r * nD + k;
+  const uint32_t A = row[-1], B = row[0], Cn = row[1];  // row[-1]: only bytes of valid pixels are used
+  const uint32_t Q0 = row[3 * nD], Q8 = row[-3 * nD];
+  const uint32_t Q4 = __builtin_amdgcn_alignbyte(Cn, B, 3);   // columns 4k+3 .. 4k+6
+  const uint32_t Q12 = __builtin_amdgcn_alignbyte(B, A, 1);   // columns 4k-3 .. 4k
+  const uint32_t M = 0x00FF00FFu;
+  const uint32_t e = pretest_half(B & M, Q0 & M, Q4 & M, Q8 & M, Q12 & M, t1, nt1);
+  const uint32_t o = pretest_half((B >> 8) & M, (Q0 >> 8) & M, (Q4 >> 8) & M, (Q8 >> 8) & M,
+                                  (Q12 >> 8) & M, t1, nt1);
+  return ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
+}
+
 __global__ __launch_bounds__(256) void k_fast_band(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbBandDesc* __restrict__ bands, const OrbCellDesc* __restrict__ cells,
-    uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount) {
+    uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount, int dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qCount, cCount;
+  __shared__ uint32_t fbMask[2];  // cells (of this band) that fall back to minThFAST
   const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nw = blockDim.x >> 6;
   const OrbBandDesc bd = bands[blockIdx.x];
   const int l = bd.level;
   const int R = bd.y1 - bd.y0, C = bd.x1 - bd.x0;
@@ -214,47 +259,47 @@ __global__ __launch_bounds__(256) void k_fast_band(
   const int iw = C - 6, ih = R - 6, ni = iw * ih;
   const int nBitWords = (ni >> 5) + 3;
   const int bandBytes = plan.maxBandBytes;
+  const int bitStride = (bandBytes >> 5) + 3;
   uint8_t* roi = smem;                                        // R x P band pixels
+  uint32_t* roi32 = (uint32_t*)roi;
   uint8_t* sc = smem + bandBytes;                             // R x P arc strengths
-  uint16_t* queue = (uint16_t*)(smem + 2 * bandBytes);        // FAST_ROUND candidates
-  uint16_t* corners = queue + FAST_ROUND;                     // FAST_CORNERS corners
+  uint16_t* queue = (uint16_t*)(smem + 2 * bandBytes);        // FAST_QUEUE candidates
+  uint16_t* corners = queue + FAST_QUEUE;                     // FAST_CORNERS corners
   uint32_t* bitsIni = (uint32_t*)(corners + FAST_CORNERS);    // interior survivors, iniTh
-  uint32_t* bitsMin = bitsIni + ((bandBytes >> 5) + 3);       // interior survivors, minTh
-  uint8_t* colf = (uint8_t*)(bitsMin + ((bandBytes >> 5) + 3));  // window edge flags per column
+  uint32_t* bitsMin = bitsIni + bitStride;                    // interior survivors, minTh
+  uint8_t* colf = (uint8_t*)(bitsMin + bitStride);            // window edge flags per column
+  uint8_t* cellOf = colf + bandBytes / 7 + 8;                 // cell of each interior column
   {
     // Realigning copy: LDS dword k of row r = bytes [x0 + 4k, x0 + 4k + 4) of
-    // the row, assembled with alignbyte from the two aligned dwords covering it
-    // (level 0 rows can start at any byte: caller stride).
-    uint32_t* roi32 = (uint32_t*)roi;
+    // the row (level 0 rows can start at any byte: caller stride).  All of a
+    // thread's loads are issued before the first LDS store (one HBM round trip).
     const int n = R * nD;
     const float invN = 1.0f / (float)nD;
-    for (int i0 = 0; i0 < n; i0 += 4 * 256) {
-      uint32_t w0[4], w1[4];
-      int sh[4];
+    for (int i0 = 0; i0 < n; i0 += FAST_LOADS * 256) {
+      uint32_t v[FAST_LOADS];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < FAST_LOADS; ++q) {
         const int i = i0 + q * 256 + tid;
-        w0[q] = w1[q] = 0;
-        sh[q] = 0;
+        v[q] = 0;
         if (i < n) {
           const int r = (int)(((float)i + 0.5f) * invN), k = i - r * nD;
-          const uint8_t* a = lvl + (long long)(bd.y0 + r) * pitch + bd.x0 + 4 * k;
-          sh[q] = (int)((uintptr_t)a & 3);
-          const uint32_t* al = (const uint32_t*)(a - sh[q]);
-          w0[q] = al[0];
-          if (sh[q] && 4 * k + 4 - sh[q] < C) w1[q] = al[1];
+          const uint8_t* row = lvl + (long long)(bd.y0 + r) * pitch + bd.x0;
+          v[q] = load_u32_any(row + 4 * k, row + C - 1);
         }
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < FAST_LOADS; ++q) {
         const int i = i0 + q * 256 + tid;
-        if (i < n) roi32[i] = __builtin_amdgcn_alignbyte(w1[q], w0[q], (uint32_t)sh[q]);
+        if (i < n) roi32[i] = v[q];
       }
     }
   }
   for (int i = tid; i < nBitWords; i += 256) bitsIni[i] = bitsMin[i] = 0;
   for (int i = tid; i < iw; i += 256) colf[i] = 0;
-  if (tid == 0) qCount = cCount = 0;
+  if (tid == 0) {
+    qCount = cCount = 0;
+    fbMask[0] = fbMask[1] = 0;
+  }
   __syncthreads();
   for (int ci = tid; ci < bd.nCells; ci += 256) {
     const OrbCellDesc cd = cells[bd.cellBeg + ci];
@@ -262,129 +307,204 @@ __global__ __launch_bounds__(256) void k_fast_band(
     if (ww > 0) {
       colf[cx0] |= 1;           // left window edge: x-1 is outside
       colf[cx0 + ww - 1] |= 2;  // right window edge: x+1 is outside
+      for (int x = 0; x < ww; ++x) cellOf[cx0 + x] = (uint8_t)ci;
     }
   }
-  // Arc strengths of the band interior.  Pixels that cannot be a corner at the
-  // lower threshold store 0 (what cv::FAST stores for non-corners); the
-  // necessary condition is two circularly adjacent compass pixels (circle
-  // positions 0,4,8,12) on the same side.  Survivors are queued so the full
-  // arc computation runs on dense lanes; scored pixels above the lower
-  // threshold go to the corner list.
-  const float invIw = 1.0f / (float)iw;
+  if (dbg == 1) return;
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
-  const int tq = min(ti, tm);
-  for (int base = 0; base < ni; base += FAST_ROUND) {
+  const unsigned long long ltMask = (1ull << lane) - 1ull;
+  const int nGroups = ih * nD;
+  const float invND = 1.0f / (float)nD;
+
+  // Group columns pretested by a pass: all of them in phase A, only those
+  // touching a fallback cell in phase B (fbK, built before phase B).
+  __shared__ int nFbK;
+  uint16_t* fbK = (uint16_t*)(cellOf + bandBytes / 7 + 8);
+
+  // One FAST pass at threshold t: pretest, arc strengths, corner list (m > t).
+  // In phase B (FB) only pixels of fallback cells, and strengths already known
+  // from phase A are kept.
+  auto fast_pass = [&](int t, auto fbTag) {
+    constexpr bool FB = decltype(fbTag)::value;
+    s16x2 t1, nt1;
+    t1.x = t1.y = (short)(t + 1);
+    nt1.x = nt1.y = (short)(-(t + 1));
+    const int nK = FB ? nFbK : nD;
+    const int nG = ih * nK;
+    const float invK = 1.0f / (float)nK;
+    for (int g0 = 0; g0 < nG; g0 += FAST_GROUPS) {
 #pragma unroll
-    for (int q = 0; q < FAST_ROUND / 256; ++q) {
-      const int i = base + q * 256 + tid;
-      bool pass = false;
-      int off = 0;
-      if (i < ni) {
-        const int y = (int)(((float)i + 0.5f) * invIw), x = i - y * iw;
+      for (int q = 0; q < FAST_GROUPS / 256; ++q) {
+        const int gi = g0 + q * 256 + tid;
+        uint32_t m4 = 0;
+        int off = 0;
+        if (gi < nG) {
+          const int rr = (int)(((float)gi + 0.5f) * invK), kk = gi - rr * nK;
+          const int k = FB ? (int)fbK[kk] : kk;
+          const int r = rr + 3;
+          off = r * P + 4 * k;
+          // valid columns 3 <= 4k+j < C-3 (and, in phase B, in a fallback cell)
+          uint32_t cm = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int col = 4 * k + j;
+            bool ok = col >= 3 && col < C - 3;
+            if (FB && ok) {
+              const int c = cellOf[col - 3];
+              ok = (fbMask[c >> 5] >> (c & 31)) & 1u;
+            }
+            cm |= (uint32_t)ok << j;
+          }
+          if (cm) m4 = pretest4(roi32, nD, r, k, t1, nt1) & cm;
+          if (!FB) ((uint32_t*)sc)[r * nD + k] = 0;  // non-corners store 0
+        }
+        const unsigned long long b0 = __ballot(m4 & 1u), b1 = __ballot(m4 & 2u);
+        const unsigned long long b2 = __ballot(m4 & 4u), b3 = __ballot(m4 & 8u);
+        const int n0 = __popcll(b0), n1 = __popcll(b1), n2 = __popcll(b2), n3 = __popcll(b3);
+        const int tot = n0 + n1 + n2 + n3;
+        int base = 0;
+        if (lane == 0 && tot) base = atomicAdd(&qCount, tot);
+        base = __shfl(base, 0, 64);
+        if (m4 & 1u) queue[base + __popcll(b0 & ltMask)] = (uint16_t)off;
+        if (m4 & 2u) queue[base + n0 + __popcll(b1 & ltMask)] = (uint16_t)(off + 1);
+        if (m4 & 4u) queue[base + n0 + n1 + __popcll(b2 & ltMask)] = (uint16_t)(off + 2);
+        if (m4 & 8u) queue[base + n0 + n1 + n2 + __popcll(b3 & ltMask)] = (uint16_t)(off + 3);
+      }
+      __syncthreads();
+      const int nq = dbg == 3 ? 0 : qCount;
+      for (int j0 = 0; j0 < nq; j0 += 256) {
+        const int j = j0 + tid;
+        bool corner = false;
+        int off = 0;
+        if (j < nq) {
+          off = queue[j];
+          int m = FB ? sc[off] : 0;
+          if (m == 0) {
+            m = min(max(fast_score(roi + off, P), 0), 255);
+            sc[off] = (uint8_t)m;
+          }
+          corner = m > t && m >= 2;
+        }
+        const unsigned long long bal = __ballot(corner);
+        int cb = 0;
+        if (lane == 0 && bal) cb = atomicAdd(&cCount, __popcll(bal));
+        cb = __shfl(cb, 0, 64) + __popcll(bal & ltMask);
+        if (corner && cb < FAST_CORNERS) corners[cb] = (uint16_t)off;
+      }
+      __syncthreads();
+      if (tid == 0) qCount = 0;
+      __syncthreads();
+    }
+  };
+
+  // NMS at threshold t of every corner (m > t) into `bits`: a corner survives
+  // iff no neighbour inside its window has nb > t && nb >= m.  Dense over the
+  // (fallback-)interior when the corner list overflowed.
+  auto nms_pass = [&](int t, uint32_t* bits, bool fallbackOnly) {
+    const int nc = cCount;
+    const bool dense = nc > FAST_CORNERS;
+    const int nItems = dense ? ni : nc;
+    for (int j = tid; j < nItems; j += 256) {
+      int x, y, off;
+      if (dense) {
+        y = (int)(((float)j + 0.5f) / (float)iw);
+        x = j - y * iw;
         off = (y + 3) * P + (x + 3);
-        const uint8_t* c = roi + off;
-        const int v = c[0];
-        const int q0 = c[3 * P], q4 = c[3], q8 = c[-3 * P], q12 = c[-3];
-        const bool d0 = q0 < v - tq, d4 = q4 < v - tq, d8 = q8 < v - tq, d12 = q12 < v - tq;
-        const bool b0 = q0 > v + tq, b4 = q4 > v + tq, b8 = q8 > v + tq, b12 = q12 > v + tq;
-        pass = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) ||
-               (b4 && b8) || (b8 && b12) || (b12 && b0);
-        if (!pass) sc[off] = 0;
+        if (fallbackOnly) {
+          const int c = cellOf[x];
+          if (!((fbMask[c >> 5] >> (c & 31)) & 1u)) continue;
+        }
+      } else {
+        off = corners[j];
+        const int ry = (int)(((float)off + 0.5f) / (float)P);
+        y = ry - 3;
+        x = off - ry * P - 3;
       }
-      const unsigned long long bal = __ballot(pass);
-      int qb = 0;
-      if (lane == 0 && bal) qb = atomicAdd(&qCount, __popcll(bal));
-      qb = __shfl(qb, 0, 64);
-      if (pass) queue[qb + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)off;
-    }
-    __syncthreads();
-    const int nq = qCount;
-    for (int j0 = 0; j0 < nq; j0 += 256) {
-      const int j = j0 + tid;
-      bool corner = false;
-      int off = 0;
-      if (j < nq) {
-        off = queue[j];
-        const int m = min(max(fast_score(roi + off, P), 0), 255);
-        sc[off] = (uint8_t)m;
-        corner = m > tq && m >= 2;
-      }
-      const unsigned long long bal = __ballot(corner);
-      int cb = 0;
-      if (lane == 0 && bal) cb = atomicAdd(&cCount, __popcll(bal));
-      cb = __shfl(cb, 0, 64) + __popcll(bal & ((1ull << lane) - 1ull));
-      if (corner && cb < FAST_CORNERS) corners[cb] = (uint16_t)off;
-    }
-    __syncthreads();
-    if (tid == 0) qCount = 0;
-    __syncthreads();
-  }
-  // NMS of every corner at both thresholds (OpenCV FAST_t with
-  // nonmax_suppression inside the cell window): a corner (m > t) survives iff
-  // no neighbour inside its window has nb > t && nb >= m.
-  const int nc = cCount;
-  const bool dense = nc > FAST_CORNERS;
-  const int nItems = dense ? ni : nc;
-  for (int j = tid; j < nItems; j += 256) {
-    int x, y, off;
-    if (dense) {
-      y = (int)(((float)j + 0.5f) * invIw);
-      x = j - y * iw;
-      off = (y + 3) * P + (x + 3);
-    } else {
-      off = corners[j];
-      const int ry = (int)(((float)off + 0.5f) / (float)P);
-      y = ry - 3;
-      x = off - ry * P - 3;
-    }
-    const uint8_t* c = sc + off;
-    const int m = c[0];
-    if (m <= tq || m < 2) continue;
-    const int cf = colf[x];
-    const bool L = !(cf & 1), Rt = !(cf & 2), U = y > 0, D = y < ih - 1;
-    const int nb[8] = {(U && L) ? c[-P - 1] : 0, U ? c[-P] : 0, (U && Rt) ? c[-P + 1] : 0,
-                       L ? c[-1] : 0, Rt ? c[1] : 0, (D && L) ? c[P - 1] : 0,
-                       D ? c[P] : 0, (D && Rt) ? c[P + 1] : 0};
-    bool si = m > ti, sm = m > tm;
+      const uint8_t* c = sc + off;
+      const int m = c[0];
+      if (m <= t || m < 2) continue;
+      const int cf = colf[x];
+      const bool L = !(cf & 1), Rt = !(cf & 2), U = y > 0, D = y < ih - 1;
+      const int nb[8] = {(U && L) ? c[-P - 1] : 0, U ? c[-P] : 0, (U && Rt) ? c[-P + 1] : 0,
+                         L ? c[-1] : 0, Rt ? c[1] : 0, (D && L) ? c[P - 1] : 0,
+                         D ? c[P] : 0, (D && Rt) ? c[P + 1] : 0};
+      bool ok = true;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (nb[k] >= m) {
-        si = si && !(nb[k] > ti);
-        sm = sm && !(nb[k] > tm);
+      for (int k = 0; k < 8; ++k) ok = ok && !(nb[k] > t && nb[k] >= m);
+      if (ok) {
+        const int bit = y * iw + x;
+        atomicOr(&bits[bit >> 5], 1u << (bit & 31));
       }
     }
-    const int bit = y * iw + x;
-    if (si) atomicOr(&bitsIni[bit >> 5], 1u << (bit & 31));
-    if (sm) atomicOr(&bitsMin[bit >> 5], 1u << (bit & 31));
-  }
-  __syncthreads();
-  // Per-cell compaction, one wave per cell, lane = window row (ih <= 64,
-  // host-checked): prefix over rows gives each row's first output slot.
-  const int nw = blockDim.x >> 6;
-  for (int ci = wave; ci < bd.nCells; ci += nw) {
+  };
+
+  // Compaction of cell ci from `bits`, one wave, lane = window row (ih <= 64,
+  // host-checked).  Returns the cell's key count (wave-uniform).
+  auto compact = [&](int ci, const uint32_t* bits) -> int {
     const OrbCellDesc cd = cells[bd.cellBeg + ci];
     const int cx0 = cd.x0 - bd.x0, ww = cd.x1 - cd.x0 - 6;
-    const long long slot = slot0 + ci;
-    uint32_t* out = cellKeys + slot * plan.keyCap;
-    int total = 0;
-    if (ww > 0) {
-      for (int pass = 0; pass < 2; ++pass) {
-        if (pass == 1 && (total > 0 || tm == ti)) break;
-        const uint32_t* bits = pass == 0 ? bitsIni : bitsMin;
-        unsigned long long row = lane < ih ? bit_run(bits, lane * iw + cx0, ww) : 0ull;
-        const int cnt = __popcll(row);
-        const int incl = wave_incl_scan(cnt);
-        total = __shfl(incl, 63, 64);
-        int o = incl - cnt;
-        while (row) {
-          const int x = __builtin_ctzll(row);
-          row &= row - 1;
-          const int m = sc[(lane + 3) * P + cx0 + x + 3];
-          out[o++] = pack_key(bd.x0 + 3 + cx0 + x, bd.y0 + 3 + lane, m - 1);
+    if (ww <= 0) return 0;
+    uint32_t* out = cellKeys + (slot0 + ci) * plan.keyCap;
+    unsigned long long row = lane < ih ? bit_run(bits, lane * iw + cx0, ww) : 0ull;
+    const int cnt = __popcll(row);
+    const int incl = wave_incl_scan(cnt);
+    const int total = __shfl(incl, 63, 64);
+    int o = incl - cnt;
+    while (row) {
+      const int x = __builtin_ctzll(row);
+      row &= row - 1;
+      const int m = sc[(lane + 3) * P + cx0 + x + 3];
+      out[o++] = pack_key(bd.x0 + 3 + cx0 + x, bd.y0 + 3 + lane, m - 1);
+    }
+    return total;
+  };
+
+  // ---- phase A: every cell at iniThFAST
+  fast_pass(ti, std::false_type{});
+  if (dbg == 3 || dbg == 4) return;
+  nms_pass(ti, bitsIni, false);
+  __syncthreads();
+  for (int ci = wave; ci < bd.nCells; ci += nw) {
+    const int n = compact(ci, bitsIni);
+    if (lane == 0) {
+      if (n == 0 && tm != ti) atomicOr(&fbMask[ci >> 5], 1u << (ci & 31));
+      else cellCount[slot0 + ci] = n;
+    }
+  }
+  if (tid == 0) cCount = 0;
+  __syncthreads();
+  if ((fbMask[0] | fbMask[1]) == 0 || dbg == 2) return;
+  // ---- phase B: cells without an iniThFAST keypoint, at minThFAST, over the
+  // group columns that touch one (wave 0 lists them in order with ballots)
+  if (wave == 0) {
+    int cnt = 0;
+    for (int k0 = 0; k0 < nD; k0 += 64) {
+      const int k = k0 + lane;
+      bool hit = false;
+      if (k < nD) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = 4 * k + j;
+          if (col >= 3 && col < C - 3) {
+            const int c = cellOf[col - 3];
+            hit = hit || ((fbMask[c >> 5] >> (c & 31)) & 1u);
+          }
         }
       }
+      const unsigned long long b = __ballot(hit);
+      if (hit) fbK[cnt + __popcll(b & ltMask)] = (uint16_t)k;
+      cnt += __popcll(b);
     }
-    if (lane == 0) cellCount[slot] = total;
+    if (lane == 0) nFbK = cnt;
+  }
+  __syncthreads();
+  fast_pass(tm, std::true_type{});
+  nms_pass(tm, bitsMin, true);
+  __syncthreads();
+  for (int ci = wave; ci < bd.nCells; ci += nw) {
+    if (!((fbMask[ci >> 5] >> (ci & 31)) & 1u)) continue;
+    const int n = compact(ci, bitsMin);
+    if (lane == 0) cellCount[slot0 + ci] = n;
   }
 }
 
@@ -1006,11 +1126,13 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
                            uint32_t* cellKeys, int32_t* cellCount, int nimg, hipStream_t s) {
   const size_t bitBytes = 4 * (size_t)((plan->maxBandBytes >> 5) + 3);
-  const size_t lds = (size_t)plan->maxBandBytes * 2 + FAST_ROUND * 2 + FAST_CORNERS * 2 +
-                     2 * bitBytes + (size_t)plan->maxBandBytes / 7 + 16;
+  const size_t lds = (size_t)plan->maxBandBytes * 2 + FAST_QUEUE * 2 + FAST_CORNERS * 2 +
+                     2 * bitBytes + 2 * ((size_t)plan->maxBandBytes / 7 + 8) +
+                     2 * ((size_t)plan->maxBandBytes / 28 + 8);
   dim3 grid(nbands, nimg), block(256);
+  static const int dbg = getenv("ORB_FAST_DBG") ? atoi(getenv("ORB_FAST_DBG")) : 0;
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, bands, cells, cellKeys, cellCount);
+                     arenaPitch, *plan, bands, cells, cellKeys, cellCount, dbg);
   return hipGetLastError();
 }
 

@@ -296,10 +296,10 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     d.w = l ? cvRoundF((float)W * h->invScale[l]) : W;  // src/ORBextractor.cc:1180
     d.h = l ? cvRoundF((float)H * h->invScale[l]) : H;
     if (d.w < 40 || d.h < 40 || d.w > 4095 || d.h > 4095) return ORB_EINVAL;
-    d.pitch = (d.w + 63) & ~63;
+    d.pitch = ((d.w + 127) & ~127) | 128;  // odd multiple of 128 B: whole-line rows, channel spread
     d.arenaOff = l ? arena : 0;
     if (l) arena += (long long)d.pitch * d.h;
-    d.blurPitch = (d.w + 63) & ~63;
+    d.blurPitch = ((d.w + 127) & ~127) | 128;
     d.blurOff = blurArena;
     blurArena += (long long)d.blurPitch * d.h;
     d.tileBeg = (int)tiles.size();
@@ -359,7 +359,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
       b.x1 = cells[c].x1;
       b.cellBeg = c;
       int e = c + 1;
-      while (e < d.cellEnd && cells[e].y0 == b.y0) {
+      while (e < d.cellEnd && cells[e].y0 == b.y0 && e - c < 64) {  // k_fast_band: <= 64 cells
         const int x1 = std::max<int>(b.x1, cells[e].x1);
         if ((b.y1 - b.y0) * ((x1 - b.x0 + 3) & ~3) > ORB_BAND_BYTES) break;
         b.x1 = (int16_t)x1;
