@@ -23,13 +23,13 @@
 // cv::resize(prev, level, sz, 0, 0, INTER_LINEAR) on 8U with OpenCV's 11-bit
 // fixed-point weights.  The weight tables are computed
 // on the host with the reference's float/double expressions; the kernel only
-// does the integer taps.  One workgroup per 128 x 32 output tile: the source
+// does the integer taps.  One workgroup per 128 x 64 output tile: the source
 // window is staged in LDS as aligned dwords (realigned from any source stride),
-// each thread produces 4 columns x 4 rows and stores whole dwords, so a wave
+// each thread produces 4 columns x 8 rows and stores whole dwords, so a wave
 // writes two full 128-byte rows per store.
 #define PYR_TW 128
-#define PYR_TH 32
-#define PYR_SROWS 44  // >= source rows a 32-row output tile can touch (scale <= 1.25)
+#define PYR_TH 64
+#define PYR_SROWS 84  // >= source rows a 64-row output tile can touch (scale <= 1.25)
 #define PYR_SW 44     // >= dwords of source row a 128-column tile touches (+2 read-ahead)
 
 __global__ __launch_bounds__(256) void k_pyr_resize(
@@ -40,7 +40,24 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   // alpha/beta pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
   __shared__ __attribute__((aligned(16))) uint32_t tile[PYR_SROWS][PYR_SW];
   const int tid = threadIdx.x;
+  const int tx = tid & 31, ty = tid >> 5;
   const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
+  const int xs = x0 + 4 * tx;
+  // this thread's weight tables, issued together with the source loads so the
+  // workgroup pays one memory round trip before its compute
+  int xo[4], al[4], yo[PYR_TH / 8], be[PYR_TH / 8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int dx = min(xs + j, dw - 1);
+    xo[j] = xofs[dx];
+    al[j] = alpha[dx];
+  }
+#pragma unroll
+  for (int rr = 0; rr < PYR_TH / 8; ++rr) {
+    const int y = min(y0 + (PYR_TH / 8) * ty + rr, dh - 1);
+    yo[rr] = yofs[y];
+    be[rr] = beta[y];
+  }
   const uint8_t* S = src + (long long)blockIdx.z * srcImgPitch;
   const int xl = min(x0 + PYR_TW - 1, dw - 1), yl = min(y0 + PYR_TH - 1, dh - 1);
   const int sxA = xofs[x0], sxB = min(xofs[xl] + 1, sw - 1);
@@ -49,55 +66,48 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   const int nW = ((sxB - colBase) >> 2) + 1, nR = syB - syA + 1;
   const int n = nR * nW;
   const float invW = 1.0f / (float)nW;
-  for (int i0 = 0; i0 < n; i0 += 8 * 256) {
-    uint32_t v[8];
+  // every load of the window is issued before the first use (branch-free:
+  // out-of-range lanes re-read the window's last dword)
+  for (int i0 = 0; i0 < n; i0 += 16 * 256) {
+    RawDw v[16];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int i = i0 + q * 256 + tid;
-      v[q] = 0;
-      if (i < n) {
-        const int r = (int)(((float)i + 0.5f) * invW), w = i - r * nW;
-        const uint8_t* row = S + (long long)(syA + r) * srcStride;
-        v[q] = load_u32_any(row + colBase + 4 * w, row + sw - 1);
-      }
+    for (int q = 0; q < 16; ++q) {
+      const int i = min(i0 + q * 256 + tid, n - 1);
+      const int r = (int)(((float)i + 0.5f) * invW), w = i - r * nW;
+      const uint8_t* row = S + (long long)(syA + r) * srcStride;
+      v[q] = raw_u32_any(row + colBase + 4 * w, row + sw - 1);
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < 16; ++q) {
       const int i = i0 + q * 256 + tid;
       if (i < n) {
         const int r = (int)(((float)i + 0.5f) * invW), w = i - r * nW;
-        tile[r][w] = v[q];
+        tile[r][w] = v[q].get();
       }
     }
   }
   __syncthreads();
-  const int tx = tid & 31, ty = tid >> 5;
-  const int xs = x0 + 4 * tx;
   if (xs >= dw) return;
   int cb[4], a0[4], a1[4];
   bool inner[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int dx = min(xs + j, dw - 1);
-    cb[j] = xofs[dx] - colBase;
-    const int aw = alpha[dx];
-    a0[j] = (int)(short)(aw & 0xFFFF);
-    a1[j] = aw >> 16;
-    inner[j] = dx < xmax;
+    cb[j] = xo[j] - colBase;
+    a0[j] = (int)(short)(al[j] & 0xFFFF);
+    a1[j] = al[j] >> 16;
+    inner[j] = min(xs + j, dw - 1) < xmax;
   }
   const int k0 = cb[0] >> 2;
 #pragma unroll
   for (int j = 0; j < 4; ++j) cb[j] -= 4 * k0;
   uint8_t* outImg = dst + (long long)blockIdx.z * dstImgPitch;
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int y = y0 + 4 * ty + rr;
+  for (int rr = 0; rr < PYR_TH / 8; ++rr) {
+    const int y = y0 + (PYR_TH / 8) * ty + rr;
     if (y >= dh) break;
-    const int sy = yofs[y];
-    const int bw = beta[y];
-    const int b0 = (int)(short)(bw & 0xFFFF), b1 = bw >> 16;
-    const uint32_t* R0 = tile[min(max(sy, 0), sh - 1) - syA] + k0;
-    const uint32_t* R1 = tile[min(max(sy + 1, 0), sh - 1) - syA] + k0;
+    const int b0 = (int)(short)(be[rr] & 0xFFFF), b1 = be[rr] >> 16;
+    const uint32_t* R0 = tile[min(max(yo[rr], 0), sh - 1) - syA] + k0;
+    const uint32_t* R1 = tile[min(max(yo[rr] + 1, 0), sh - 1) - syA] + k0;
     const uint32_t p0 = R0[0], p1 = R0[1], p2 = R0[2];
     const uint32_t q0 = R1[0], q1 = R1[1], q2 = R1[2];
     uint32_t packed = 0;
@@ -121,7 +131,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
     }
     uint8_t* out = outImg + (long long)y * dstStride + xs;
     if (xs + 4 <= dw) {
-      *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 64 == 0, xs % 4 == 0
+      *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 128 == 0, xs % 4 == 0
     } else {
       for (int j = 0; xs + j < dw; ++j) out[j] = (uint8_t)(packed >> (8 * j));
     }
@@ -276,21 +286,18 @@ __global__ __launch_bounds__(256) void k_fast_band(
     const int n = R * nD;
     const float invN = 1.0f / (float)nD;
     for (int i0 = 0; i0 < n; i0 += FAST_LOADS * 256) {
-      uint32_t v[FAST_LOADS];
+      RawDw v[FAST_LOADS];
 #pragma unroll
       for (int q = 0; q < FAST_LOADS; ++q) {
-        const int i = i0 + q * 256 + tid;
-        v[q] = 0;
-        if (i < n) {
-          const int r = (int)(((float)i + 0.5f) * invN), k = i - r * nD;
-          const uint8_t* row = lvl + (long long)(bd.y0 + r) * pitch + bd.x0;
-          v[q] = load_u32_any(row + 4 * k, row + C - 1);
-        }
+        const int i = min(i0 + q * 256 + tid, n - 1);  // branch-free loads
+        const int r = (int)(((float)i + 0.5f) * invN), k = i - r * nD;
+        const uint8_t* row = lvl + (long long)(bd.y0 + r) * pitch + bd.x0;
+        v[q] = raw_u32_any(row + 4 * k, row + C - 1);
       }
 #pragma unroll
       for (int q = 0; q < FAST_LOADS; ++q) {
         const int i = i0 + q * 256 + tid;
-        if (i < n) roi32[i] = v[q];
+        if (i < n) roi32[i] = v[q].get();
       }
     }
   }
@@ -895,23 +902,20 @@ __global__ __launch_bounds__(256) void k_blur_levels(
   const bool interior = td.x0 >= 4 && td.y0 >= 3 && td.x0 + ORB_BLUR_TW + 4 <= L.w &&
                         td.y0 + ORB_BLUR_TH + 3 <= L.h;
   if (interior) {
-    uint32_t v[(kN + 255) / 256];
+    RawDw v[(kN + 255) / 256];
 #pragma unroll
     for (int q = 0; q < (kN + 255) / 256; ++q) {
-      const int i = tid + 256 * q;
-      v[q] = 0;
-      if (i < kN) {
-        const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
-        const uint8_t* row = lvl + (long long)(td.y0 - 3 + r) * pitch;
-        v[q] = load_u32_any(row + td.x0 - 4 + 4 * wq, row + L.w - 1);
-      }
+      const int i = min(tid + 256 * q, kN - 1);  // branch-free: every load in flight at once
+      const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
+      const uint8_t* row = lvl + (long long)(td.y0 - 3 + r) * pitch;
+      v[q] = raw_u32_any(row + td.x0 - 4 + 4 * wq, row + L.w - 1);
     }
 #pragma unroll
     for (int q = 0; q < (kN + 255) / 256; ++q) {
       const int i = tid + 256 * q;
       if (i < kN) {
         const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
-        raw[r][wq] = v[q];
+        raw[r][wq] = v[q].get();
       }
     }
   } else {

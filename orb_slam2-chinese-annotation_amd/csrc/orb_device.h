@@ -113,15 +113,27 @@ __device__ __forceinline__ double pinned_log(double x) {
 
 // --------------------------------------------------- realigning byte loads
 // Bytes [p, p+4) as one dword for any alignment of p, from the aligned dwords
-// covering them.  `last` = the last byte that may be read (the second aligned
-// dword is only touched if it starts at or before it, so no read leaves the
-// page of a valid byte).
-__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p, const uint8_t* last) {
+// covering them.  `last` = the last byte that may be read: the second aligned
+// dword is replaced by the first when it starts past `last`, so no read
+// leaves the page of a valid byte.  Split in two halves so that a loop can
+// issue every load (branch-free, no wait) before assembling any dword:
+//   RawDw r = raw_u32_any(p, last);  ...  uint32_t v = r.get();
+struct RawDw {
+  uint32_t lo, hi, sh;
+  __device__ __forceinline__ uint32_t get() const { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
+};
+__device__ __forceinline__ RawDw raw_u32_any(const uint8_t* p, const uint8_t* last) {
   const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
   const uint32_t* a = (const uint32_t*)(p - sh);
-  const uint32_t lo = a[0];
-  const uint32_t hi = (sh && (const uint8_t*)(a + 1) <= last) ? a[1] : 0u;
-  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+  const uint32_t* b = ((const uint8_t*)(a + 1) <= last) ? a + 1 : a;
+  RawDw r;
+  r.lo = a[0];
+  r.hi = b[0];
+  r.sh = sh;
+  return r;
+}
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p, const uint8_t* last) {
+  return raw_u32_any(p, last).get();
 }
 
 // Bytes b and b+1 (b < 11) of the 12-byte little-endian window (w0, w1, w2),
