@@ -105,6 +105,11 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
  * dst may be NULL to query the size. */
 orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t* dst,
                                          size_t dst_stride, int* width, int* height);
+/* The 7x7 Gaussian-blurred copy of level `level` of the first image of the
+ * last call (the image computeDescriptors samples, src/ORBextractor.cc:1143-1145);
+ * same conventions as orb_extractor_pyramid_level. */
+orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t* dst,
+                                         size_t dst_stride, int* width, int* height);
 
 /* Throughput form: n_images device-resident images (image i at
  * d_images + i*image_pitch, rows `stride` apart), all width x height.

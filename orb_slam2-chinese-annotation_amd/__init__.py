@@ -104,6 +104,7 @@ def lib() -> ctypes.CDLL:
         "orb_extractor_capacity": (i32, [vp, i32, i32]),
         "orb_extractor_extract": (i32, [vp, vp, i32, i32, sz, vp, vp, i32, vp]),
         "orb_extractor_pyramid_level": (i32, [vp, i32, vp, sz, vp, vp]),
+        "orb_extractor_blurred_level": (i32, [vp, i32, vp, sz, vp, vp]),
         "orb_extractor_extract_batch": (i32, [vp, vp, i32, i32, i32, sz, sz, vp, vp, i32, vp, vp]),
         "orb_extractor_batch_level": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "orb_extractor_stream": (vp, [vp]),
@@ -273,6 +274,20 @@ class ORBextractor:
             a = np.zeros((h.value, w.value), np.uint8)
             _check(L.orb_extractor_pyramid_level(self._h, l, _ptr(a), w.value, None, None),
                    "pyramid_level")
+            out.append(a)
+        return out
+
+    def blurred_levels(self) -> list:
+        """Host copies of the last image's 7x7-blurred levels (what rBRIEF samples)."""
+        L = lib()
+        out = []
+        for l in range(self.nlevels):
+            w, h = ctypes.c_int(0), ctypes.c_int(0)
+            _check(L.orb_extractor_blurred_level(self._h, l, None, 0, ctypes.byref(w),
+                                                 ctypes.byref(h)), "blurred_level")
+            a = np.zeros((h.value, w.value), np.uint8)
+            _check(L.orb_extractor_blurred_level(self._h, l, _ptr(a), w.value, None, None),
+                   "blurred_level")
             out.append(a)
         return out
 

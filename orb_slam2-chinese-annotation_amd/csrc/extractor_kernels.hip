@@ -869,12 +869,8 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 
 #define BLUR_SH (ORB_BLUR_TH + 6)  // staged source rows y0-3 .. y0+TH+2
 #define BLUR_WROW (ORB_BLUR_TW / 4 + 2)  // dwords per staged row: bytes x0-4 .. x0+TW+3
-#define BLUR_RP (ORB_BLUR_TW / 2 + 2)    // row-pass pitch in dwords (u16 pairs), padded
+#define BLUR_RP2 (ORB_BLUR_TW + 4)       // row-pass pitch in dwords (one column per dword), padded
 
-__device__ __forceinline__ int byte_of(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
-  const uint32_t w = b < 4 ? w0 : (b < 8 ? w1 : w2);
-  return (int)((w >> (8 * (b & 3))) & 0xFFu);
-}
 
 __global__ __launch_bounds__(256) void k_blur_levels(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
@@ -884,7 +880,8 @@ __global__ __launch_bounds__(256) void k_blur_levels(
   // x0-4+b (realigned from any stride); every LDS access is an aligned dword
   // or 8 bytes (unaligned sub-dword LDS reads are replayed by the hardware).
   __shared__ __attribute__((aligned(16))) uint32_t raw[BLUR_SH][BLUR_WROW + 1];
-  __shared__ __attribute__((aligned(16))) uint32_t rowp[BLUR_SH][BLUR_RP];
+  // row-pass sums, two staged rows per dword: rowp2[p][c] = sum(2p, c) | sum(2p+1, c) << 16
+  __shared__ __attribute__((aligned(16))) uint32_t rowp2[BLUR_SH / 2][BLUR_RP2];
   const int tid = threadIdx.x, img = blockIdx.y;
   const OrbTileDesc td = tiles[blockIdx.x];
   const int l = td.level;
@@ -934,58 +931,81 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     }
   }
   __syncthreads();
-  const int k[7] = {18, 34, 49, 55, 49, 34, 18};
-  // row pass: task (r, g) -> u16 sums of columns 4g..4g+3 from bytes 4g+1 .. 4g+10
+  // Integer 7-tap kernel [18,34,49,55,49,34,18] (sums to 257 per axis).  Row
+  // pass: a 7-tap sum is two v_dot4_u32_u8 on the byte window realigned with
+  // v_alignbyte; column pass: four v_dot2_u32_u16 over row pairs.
+  constexpr uint32_t K0123 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
+  constexpr uint32_t K456 = 49u | (34u << 8) | (18u << 16);
+  // row pass: task (row pair p, group g) -> sums of columns 4g..4g+3 of staged
+  // rows 2p, 2p+1 (output column x0+4g+i reads staged bytes 4g+i+1 .. 4g+i+7)
   constexpr int G = ORB_BLUR_TW / 4;
-  for (int id = tid; id < BLUR_SH * G; id += 256) {
-    const int r = id / G, g = id - r * G;
-    const uint32_t w0 = raw[r][g], w1 = raw[r][g + 1], w2 = raw[r][g + 2];
-    int o[4];
+  for (int id = tid; id < (BLUR_SH / 2) * G; id += 256) {
+    const int pr = id / G, g = id - pr * G;
+    uint32_t o[2][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int acc = 0;
-#pragma unroll
-      for (int t = 0; t < 7; ++t) acc += k[t] * byte_of(w0, w1, w2, 1 + i + t);
-      o[i] = acc;
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t* rw = raw[2 * pr + h] + g;
+      const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
+      o[h][0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), K0123,
+                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), K456, 0u, false), false);
+      o[h][1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), K0123,
+                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), K456, 0u, false), false);
+      o[h][2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), K0123,
+                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), K456, 0u, false), false);
+      o[h][3] = __builtin_amdgcn_udot4(w1, K0123, __builtin_amdgcn_udot4(w2, K456, 0u, false), false);
     }
-    uint2 pk;
-    pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-    pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-    *reinterpret_cast<uint2*>(&rowp[r][2 * g]) = pk;
+    uint4 pk;
+    pk.x = o[0][0] | (o[1][0] << 16);
+    pk.y = o[0][1] | (o[1][1] << 16);
+    pk.z = o[0][2] | (o[1][2] << 16);
+    pk.w = o[0][3] | (o[1][3] << 16);
+    *reinterpret_cast<uint4*>(&rowp2[pr][4 * g]) = pk;
   }
   __syncthreads();
-  // column pass: thread -> columns 4qx..4qx+3 x rows 4qy..4qy+3, dword stores
-  // (a wave writes two whole 128-byte rows per store)
-  const int qx = tid & (G - 1), qy = tid / G;
+  // column pass: thread -> columns 4qx..4qx+3 x output rows 2p, 2p+1 for
+  // p = qp and qp + 8; output row y reads staged rows y..y+6 = pairs
+  // y/2 .. y/2+3 with weights (k0,k1)(k2,k3)(k4,k5)(k6,0) for even y and
+  // (0,k0)(k1,k2)(k3,k4)(k5,k6) for odd y.
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 E0 = {18, 34}, E1 = {49, 55}, E2 = {49, 34}, E3 = {18, 0};
+  const u16x2 O0 = {0, 18}, O1 = {34, 49}, O2 = {55, 49}, O3 = {34, 18};
+  const int qx = tid & (G - 1), qp = tid / G;
   uint8_t* dst = blur + (long long)img * blurPitch + L.blurOff;
   const int x = td.x0 + 4 * qx;
-  uint2 cv[10];
 #pragma unroll
-  for (int j = 0; j < 10; ++j) cv[j] = *reinterpret_cast<const uint2*>(&rowp[4 * qy + j][2 * qx]);
+  for (int half = 0; half < 2; ++half) {
+    const int pp = qp + 8 * half;
+    uint4 pv[4];
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    int a[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      a[0] += k[j] * (int)(cv[j + rr].x & 0xFFFFu);
-      a[1] += k[j] * (int)(cv[j + rr].x >> 16);
-      a[2] += k[j] * (int)(cv[j + rr].y & 0xFFFFu);
-      a[3] += k[j] * (int)(cv[j + rr].y >> 16);
-    }
-    uint32_t packed = 0;
+    for (int k = 0; k < 4; ++k) pv[k] = *reinterpret_cast<const uint4*>(&rowp2[pp + k][4 * qx]);
+    uint32_t packedE = 0, packedO = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      int v = min((a[c] + (1 << 15)) >> 16, 255);
-      __asm__ volatile("" : "+v"(v));  // see k_pyr_resize: keep the byte pack opaque
-      packed |= (uint32_t)v << (8 * c);
+      uint32_t se = 0, so = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t w = c == 0 ? pv[k].x : (c == 1 ? pv[k].y : (c == 2 ? pv[k].z : pv[k].w));
+        const u16x2 v = __builtin_bit_cast(u16x2, w);
+        se = __builtin_amdgcn_udot2(v, k == 0 ? E0 : (k == 1 ? E1 : (k == 2 ? E2 : E3)), se, false);
+        so = __builtin_amdgcn_udot2(v, k == 0 ? O0 : (k == 1 ? O1 : (k == 2 ? O2 : O3)), so, false);
+      }
+      // the pinned kernel sums to 257 per axis: saturate (row sums <= 255*257 fit u16)
+      int ve = min((int)((se + (1u << 15)) >> 16), 255), vo = min((int)((so + (1u << 15)) >> 16), 255);
+      __asm__ volatile("" : "+v"(ve), "+v"(vo));  // see k_pyr_resize: keep the byte pack opaque
+      packedE |= (uint32_t)ve << (8 * c);
+      packedO |= (uint32_t)vo << (8 * c);
     }
-    const int y = td.y0 + 4 * qy + rr;
-    if (y >= L.h || x >= L.w) continue;
-    uint8_t* o = dst + (long long)y * L.blurPitch + x;
-    if (x + 4 <= L.w) {
-      *reinterpret_cast<uint32_t*>(o) = packed;  // blurPitch % 64 == 0, x % 4 == 0
-    } else {
-      for (int c = 0; x + c < L.w; ++c) o[c] = (uint8_t)(packed >> (8 * c));
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int y = td.y0 + 2 * pp + rr;
+      if (y >= L.h || x >= L.w) continue;
+      const uint32_t packed = rr ? packedO : packedE;
+      uint8_t* o = dst + (long long)y * L.blurPitch + x;
+      if (x + 4 <= L.w) {
+        *reinterpret_cast<uint32_t*>(o) = packed;  // blurPitch % 128 == 0, x % 4 == 0
+      } else {
+        for (int c = 0; x + c < L.w; ++c) o[c] = (uint8_t)(packed >> (8 * c));
+      }
     }
   }
 }

@@ -743,6 +743,23 @@ orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t*
   return ORB_OK;
 }
 
+orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t* dst,
+                                         size_t dst_stride, int* width, int* height) {
+  if (!h) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (h->planW < 0 || h->batchCap <= 0 || level < 0 || level >= h->plan.nlevels) return ORB_EINVAL;
+  const OrbLevelDesc& L = h->plan.lv[level];
+  if (width) *width = L.w;
+  if (height) *height = L.h;
+  if (!dst) return ORB_OK;
+  if (dst_stride < (size_t)L.w) return ORB_EINVAL;
+  hipSetDevice(h->device);
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy2D(dst, dst_stride, h->dBlur.as<uint8_t>() + L.blurOff, L.blurPitch, L.w, L.h,
+                      hipMemcpyDeviceToHost));
+  return ORB_OK;
+}
+
 orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable) {
   if (!h) return ORB_EINVAL;
   std::lock_guard<std::mutex> g(h->mu);

@@ -62,6 +62,19 @@ def test_pyramid_bit_exact(gpu, oracle, w, h):
         assert np.array_equal(a, b), f"level {l}: {(a != b).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("w,h", [(640, 480), (1241, 376), (1920, 1080), (403, 301)])
+def test_blurred_levels_bit_exact(gpu, oracle, w, h):
+    """GaussianBlur(7x7, sigma 2, REFLECT_101) of every level (src/ORBextractor.cc:1143-1145)."""
+    img = gpu.synth_image(12, 0, w, h)
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    ext(img)
+    for l, (a, lv) in enumerate(zip(ext.blurred_levels(), oracle.pyramid(img))):
+        b = oracle.blur7(lv)
+        assert a.shape == b.shape
+        bad = np.argwhere(a != b)
+        assert len(bad) == 0, f"level {l}: {len(bad)} px differ, first {bad[:5].tolist()}"
+
+
 def test_accessors_match_reference_tables(gpu, oracle):
     ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
     p = oracle.params(1000, 1.2, 8)
