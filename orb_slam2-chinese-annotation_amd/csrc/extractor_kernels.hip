@@ -896,16 +896,20 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     pitch = L.pitch;
   }
   constexpr int kN = BLUR_SH * BLUR_WROW;
-  const bool interior = td.x0 >= 4 && td.y0 >= 3 && td.x0 + ORB_BLUR_TW + 4 <= L.w &&
-                        td.y0 + ORB_BLUR_TH + 3 <= L.h;
-  if (interior) {
+  // Staging (all loads in flight at once).  Rows outside the level are
+  // reflected (REFLECT_101) when addressed; columns are loaded with the dword
+  // start clamped into the row, and the few bytes a border tile needs outside
+  // [0, w) are patched from their reflected columns afterwards.
+  const int colA = td.x0 - 4;  // level column of staged byte 0
+  {
     RawDw v[(kN + 255) / 256];
 #pragma unroll
     for (int q = 0; q < (kN + 255) / 256; ++q) {
-      const int i = min(tid + 256 * q, kN - 1);  // branch-free: every load in flight at once
+      const int i = min(tid + 256 * q, kN - 1);
       const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
-      const uint8_t* row = lvl + (long long)(td.y0 - 3 + r) * pitch;
-      v[q] = raw_u32_any(row + td.x0 - 4 + 4 * wq, row + L.w - 1);
+      const uint8_t* row = lvl + (long long)reflect101(td.y0 - 3 + r, L.h) * pitch;
+      const int c = min(max(colA + 4 * wq, 0), L.w - 1);
+      v[q] = raw_u32_any(row + c, row + L.w - 1);
     }
 #pragma unroll
     for (int q = 0; q < (kN + 255) / 256; ++q) {
@@ -915,19 +919,22 @@ __global__ __launch_bounds__(256) void k_blur_levels(
         raw[r][wq] = v[q].get();
       }
     }
-  } else {
-    // border tile: per-byte reflect-101 gather, assembled into dwords
-    for (int i = tid; i < kN; i += 256) {
-      const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
-      const int y = reflect101(td.y0 - 3 + r, L.h);
-      const uint8_t* row = lvl + (long long)y * pitch;
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int x = reflect101(td.x0 - 4 + 4 * wq + b, L.w);
-        w |= (uint32_t)row[x] << (8 * b);
+  }
+  const bool leftB = colA < 0, rightB = td.x0 + ORB_BLUR_TW + 3 > L.w;
+  if (leftB || rightB) {  // uniform per workgroup
+    __syncthreads();
+    uint8_t* rb = reinterpret_cast<uint8_t*>(&raw[0][0]);
+    constexpr int RB = (BLUR_WROW + 1) * 4;  // staged row pitch in bytes
+    // byte (r, b) holds column colA + b; fix columns -4..-1 and w..w+2 (the
+    // only out-of-range columns an in-range output reads)
+    for (int i = tid; i < BLUR_SH * 7; i += 256) {
+      const int r = i / 7, j = i - r * 7;
+      const int x = j < 4 ? -4 + j : L.w + (j - 4);
+      const int b = x - colA;
+      if (b >= 0 && b < 4 * BLUR_WROW) {
+        const int bs = reflect101(x, L.w) - colA;
+        rb[r * RB + b] = (bs >= 0 && bs < 4 * BLUR_WROW) ? rb[r * RB + bs] : 0;
       }
-      raw[r][wq] = w;
     }
   }
   __syncthreads();
