@@ -88,41 +88,47 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   }
   __syncthreads();
   if (xs >= dw) return;
-  int cb[4], a0[4], a1[4];
-  bool inner[4];
+  // Horizontal taps with v_perm + v_dot2: the thread's 4 columns read source
+  // bytes sx0 .. sx0+6 (scale <= 1.25), realigned once per source row into
+  // (W0, W1); column j's pair (S[sx], S[sx+1]) is one v_perm into u16 lanes
+  // and h = a0*S[sx] + a1*S[sx+1] one v_dot2_u32_u16.  Columns past xmax carry
+  // weights (2048, 0) from the host table, which is exactly OpenCV's
+  // S[sx]*2048 there.
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const int rel0 = xo[0] - colBase;
+  const int k0 = rel0 >> 2, sh0 = rel0 & 3;
+  uint32_t sel[4];
+  u16x2 wts[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    cb[j] = xo[j] - colBase;
-    a0[j] = (int)(short)(al[j] & 0xFFFF);
-    a1[j] = al[j] >> 16;
-    inner[j] = min(xs + j, dw - 1) < xmax;
+    const uint32_t bj = (uint32_t)(xo[j] - xo[0]);
+    sel[j] = bj | (0x0Cu << 8) | ((bj + 1) << 16) | (0x0Cu << 24);
+    wts[j] = __builtin_bit_cast(u16x2, (uint32_t)al[j]);
   }
-  const int k0 = cb[0] >> 2;
+  auto hrow = [&](int srow, uint32_t* h) {
+    const uint32_t* R = tile[srow] + k0;
+    const uint32_t w0 = R[0], w1 = R[1], w2 = R[2];
+    const uint32_t W0 = __builtin_amdgcn_alignbyte(w1, w0, sh0);
+    const uint32_t W1 = __builtin_amdgcn_alignbyte(w2, w1, sh0);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) cb[j] -= 4 * k0;
+    for (int j = 0; j < 4; ++j)
+      h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(W1, W0, sel[j])),
+                                    wts[j], 0u, false);
+  };
   uint8_t* outImg = dst + (long long)blockIdx.z * dstImgPitch;
 #pragma unroll
   for (int rr = 0; rr < PYR_TH / 8; ++rr) {
     const int y = y0 + (PYR_TH / 8) * ty + rr;
     if (y >= dh) break;
-    const int b0 = (int)(short)(be[rr] & 0xFFFF), b1 = be[rr] >> 16;
-    const uint32_t* R0 = tile[min(max(yo[rr], 0), sh - 1) - syA] + k0;
-    const uint32_t* R1 = tile[min(max(yo[rr] + 1, 0), sh - 1) - syA] + k0;
-    const uint32_t p0 = R0[0], p1 = R0[1], p2 = R0[2];
-    const uint32_t q0 = R1[0], q1 = R1[1], q2 = R1[2];
+    const uint32_t b0 = (uint32_t)be[rr] & 0xFFFFu, b1 = (uint32_t)be[rr] >> 16;
+    uint32_t h0[4], h1[4];
+    hrow(min(max(yo[rr], 0), sh - 1) - syA, h0);
+    hrow(min(max(yo[rr] + 1, 0), sh - 1) - syA, h1);
     uint32_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t t0 = byte_pair(p0, p1, p2, cb[j]), t1 = byte_pair(q0, q1, q2, cb[j]);
-      int h0, h1;
-      if (inner[j]) {
-        h0 = (int)(t0 & 0xFFu) * a0[j] + (int)((t0 >> 8) & 0xFFu) * a1[j];
-        h1 = (int)(t1 & 0xFFu) * a0[j] + (int)((t1 >> 8) & 0xFFu) * a1[j];
-      } else {
-        h0 = (int)(t0 & 0xFFu) * 2048;
-        h1 = (int)(t1 & 0xFFu) * 2048;
-      }
-      int v = min(max((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 0), 255);
+      // h <= 255*2048 and b <= 2048: 24-bit multiplies, sum < 2^31
+      int v = min((int)((h0[j] * b0 + h1[j] * b1 + (1u << 21)) >> 22), 255);
       // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
       // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
       // undefined upper half (observed miscompile on gfx950)
@@ -320,8 +326,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
   if (dbg == 1) return;
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
   const unsigned long long ltMask = (1ull << lane) - 1ull;
-  const int nGroups = ih * nD;
-  const float invND = 1.0f / (float)nD;
 
   // Group columns pretested by a pass: all of them in phase A, only those
   // touching a fallback cell in phase B (fbK, built before phase B).
