@@ -23,23 +23,24 @@
 // cv::resize(prev, level, sz, 0, 0, INTER_LINEAR) on 8U with OpenCV's 11-bit
 // fixed-point weights.  The weight tables are computed
 // on the host with the reference's float/double expressions; the kernel only
-// does the integer taps.  One workgroup per 128 x 64 output tile: the source
+// does the integer taps.  One workgroup per 128 x 32 output tile: the source
 // window is staged in LDS as aligned dwords (realigned from any source stride),
-// each thread produces 4 columns x 8 rows and stores whole dwords, so a wave
+// each thread produces 4 columns x 4 rows and stores whole dwords, so a wave
 // writes two full 128-byte rows per store.
 #define PYR_TW 128
-#define PYR_TH 64
-#define PYR_SROWS 84  // >= source rows a 64-row output tile can touch (scale <= 1.25)
+#define PYR_TH 32
+#define PYR_SROWS 44  // >= source rows a 32-row output tile can touch (scale <= 1.25), multiple of 4
 #define PYR_SW 44     // >= dwords of source row a 128-column tile touches (+2 read-ahead)
 
+template <bool ALIGNED>
 __global__ __launch_bounds__(256) void k_pyr_resize(
     const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sw, int sh,
     uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
     const int* __restrict__ xofs, const int* __restrict__ alpha,
-    const int* __restrict__ yofs, const int* __restrict__ beta, int xmax) {
+    const int* __restrict__ yofs, const int* __restrict__ beta) {
   // alpha/beta pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
   __shared__ __attribute__((aligned(16))) uint32_t tile[PYR_SROWS][PYR_SW];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int tx = tid & 31, ty = tid >> 5;
   const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
   const int xs = x0 + 4 * tx;
@@ -58,32 +59,36 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
     yo[rr] = yofs[y];
     be[rr] = beta[y];
   }
-  const uint8_t* S = src + (long long)blockIdx.z * srcImgPitch;
   const int xl = min(x0 + PYR_TW - 1, dw - 1), yl = min(y0 + PYR_TH - 1, dh - 1);
   const int sxA = xofs[x0], sxB = min(xofs[xl] + 1, sw - 1);
   const int syA = min(max(yofs[y0], 0), sh - 1), syB = min(max(yofs[yl] + 1, 0), sh - 1);
   const int colBase = sxA & ~3;
   const int nW = ((sxB - colBase) >> 2) + 1, nR = syB - syA + 1;
-  const int n = nR * nW;
-  const float invW = 1.0f / (float)nW;
-  // every load of the window is issued before the first use (branch-free:
-  // out-of-range lanes re-read the window's last dword)
-  for (int i0 = 0; i0 < n; i0 += 16 * 256) {
-    RawDw v[16];
+  // staging: lane = dword column, wave = row (stride 4); ALIGNED sources need
+  // one dword per LDS dword, others two (realigned with v_alignbyte)
+  {
+    const __amdgpu_buffer_rsrc_t rs =
+        make_rsrc(src + (long long)blockIdx.z * srcImgPitch,
+                  (uint32_t)(((sh - 1) * srcStride + sw + 3) & ~3));  // range check is per dword
+    uint32_t off = (uint32_t)((syA + wv) * srcStride + colBase + 4 * lane);
+    const uint32_t step = 4u * (uint32_t)srcStride;
+    constexpr int RPW = PYR_SROWS / 4;  // rows per wave
+    uint32_t lo[RPW], hi[RPW];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = min(i0 + q * 256 + tid, n - 1);
-      const int r = (int)(((float)i + 0.5f) * invW), w = i - r * nW;
-      const uint8_t* row = S + (long long)(syA + r) * srcStride;
-      v[q] = raw_u32_any(row + colBase + 4 * w, row + sw - 1);
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = i0 + q * 256 + tid;
-      if (i < n) {
-        const int r = (int)(((float)i + 0.5f) * invW), w = i - r * nW;
-        tile[r][w] = v[q].get();
+    for (int q = 0; q < RPW; ++q, off += step) {
+      if (ALIGNED) {
+        lo[q] = buf_ld32(rs, off);
+      } else {
+        lo[q] = buf_ld32(rs, off & ~3u);
+        hi[q] = buf_ld32(rs, (off & ~3u) + 4);
       }
+    }
+    uint32_t sh0 = (uint32_t)((syA + wv) * srcStride + colBase + 4 * lane);
+#pragma unroll
+    for (int q = 0; q < RPW; ++q, sh0 += step) {
+      const int r = wv + 4 * q;
+      if (lane < nW && r < nR)
+        tile[r][lane] = ALIGNED ? lo[q] : __builtin_amdgcn_alignbyte(hi[q], lo[q], sh0 & 3u);
     }
   }
   __syncthreads();
@@ -115,7 +120,10 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
       h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(W1, W0, sel[j])),
                                     wts[j], 0u, false);
   };
-  uint8_t* outImg = dst + (long long)blockIdx.z * dstImgPitch;
+  // destination: arena level, pitch a multiple of 128 >= dw rounded to 4, so a
+  // whole dword store at xs < dw stays inside the row (padding bytes unused)
+  const __amdgpu_buffer_rsrc_t rd =
+      make_rsrc(dst + (long long)blockIdx.z * dstImgPitch, (uint32_t)(dh * dstStride));
 #pragma unroll
   for (int rr = 0; rr < PYR_TH / 8; ++rr) {
     const int y = y0 + (PYR_TH / 8) * ty + rr;
@@ -128,19 +136,14 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       // h <= 255*2048 and b <= 2048: 24-bit multiplies, sum < 2^31
-      int v = min((int)((h0[j] * b0 + h1[j] * b1 + (1u << 21)) >> 22), 255);
+      int v = min((int)((__umul24(h0[j], b0) + __umul24(h1[j], b1) + (1u << 21)) >> 22), 255);
       // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
       // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
       // undefined upper half (observed miscompile on gfx950)
       __asm__ volatile("" : "+v"(v));
       packed |= (uint32_t)v << (8 * j);
     }
-    uint8_t* out = outImg + (long long)y * dstStride + xs;
-    if (xs + 4 <= dw) {
-      *reinterpret_cast<uint32_t*>(out) = packed;  // dstStride % 128 == 0, xs % 4 == 0
-    } else {
-      for (int j = 0; xs + j < dw; ++j) out[j] = (uint8_t)(packed >> (8 * j));
-    }
+    buf_st32(rd, (uint32_t)(y * dstStride + xs), packed);
   }
 }
 
@@ -1148,11 +1151,18 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
                             int dh, const int* xofs, const void* alpha, const int* yofs,
                             const void* beta, int xmax, int nimg, hipStream_t s) {
+  (void)xmax;  // folded into the alpha table: (2048, 0) past xmax
   // tile bounds assume a downscale of at most 1.25x per level (checked by the planner)
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, nimg), block(256);
-  hipLaunchKernelGGL(k_pyr_resize, grid, block, 0, s, src, srcImgPitch, srcStride, sw, sh, dst,
-                     dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,
-                     (const int*)beta, xmax);
+  const bool aligned = (srcStride & 3) == 0 && (((uintptr_t)src) & 3) == 0 && (srcImgPitch & 3) == 0;
+  if (aligned)
+    hipLaunchKernelGGL(k_pyr_resize<true>, grid, block, 0, s, src, srcImgPitch, srcStride, sw, sh,
+                       dst, dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,
+                       (const int*)beta);
+  else
+    hipLaunchKernelGGL(k_pyr_resize<false>, grid, block, 0, s, src, srcImgPitch, srcStride, sw, sh,
+                       dst, dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,
+                       (const int*)beta);
   return hipGetLastError();
 }
 

@@ -136,6 +136,19 @@ __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p, const uint8_t
   return raw_u32_any(p, last).get();
 }
 
+// Buffer resources: 32-bit per-lane offsets (no 64-bit address VALU) and a
+// hardware range check per dword (a dword load that ends past `bytes` reads
+// as 0, a store past it is dropped).  Build only from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_st32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
+}
+
 // Bytes b and b+1 (b < 11) of the 12-byte little-endian window (w0, w1, w2),
 // as the low 16 bits of the result.
 __device__ __forceinline__ uint32_t byte_pair(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
