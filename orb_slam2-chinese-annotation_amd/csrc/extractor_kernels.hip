@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
     const int* __restrict__ yofs, const int* __restrict__ beta) {
   // alpha/beta pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
   __shared__ __attribute__((aligned(16))) uint32_t tile[PYR_SROWS][PYR_SW];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int tx = tid & 31, ty = tid >> 5;
   const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
   const int xs = x0 + 4 * tx;
@@ -64,32 +64,13 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   const int syA = min(max(yofs[y0], 0), sh - 1), syB = min(max(yofs[yl] + 1, 0), sh - 1);
   const int colBase = sxA & ~3;
   const int nW = ((sxB - colBase) >> 2) + 1, nR = syB - syA + 1;
-  // staging: lane = dword column, wave = row (stride 4); ALIGNED sources need
-  // one dword per LDS dword, others two (realigned with v_alignbyte)
+  // staging: lane = dword column, wave = row; ALIGNED sources need one dword
+  // load per LDS dword, others two (realigned with v_alignbyte)
   {
-    const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(src + (long long)blockIdx.z * srcImgPitch,
-                  (uint32_t)(((sh - 1) * srcStride + sw + 3) & ~3));  // range check is per dword
-    uint32_t off = (uint32_t)((syA + wv) * srcStride + colBase + 4 * lane);
-    const uint32_t step = 4u * (uint32_t)srcStride;
-    constexpr int RPW = PYR_SROWS / 4;  // rows per wave
-    uint32_t lo[RPW], hi[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q, off += step) {
-      if (ALIGNED) {
-        lo[q] = buf_ld32(rs, off);
-      } else {
-        lo[q] = buf_ld32(rs, off & ~3u);
-        hi[q] = buf_ld32(rs, (off & ~3u) + 4);
-      }
-    }
-    uint32_t sh0 = (uint32_t)((syA + wv) * srcStride + colBase + 4 * lane);
-#pragma unroll
-    for (int q = 0; q < RPW; ++q, sh0 += step) {
-      const int r = wv + 4 * q;
-      if (lane < nW && r < nR)
-        tile[r][lane] = ALIGNED ? lo[q] : __builtin_amdgcn_alignbyte(hi[q], lo[q], sh0 & 3u);
-    }
+    const ImgRsrc im = img_rsrc(src + (long long)blockIdx.z * srcImgPitch,
+                                (uint32_t)((sh - 1) * srcStride + sw));
+    stage_rows<ALIGNED, PYR_SROWS / 4>(im, nR, nW, (uint32_t)(colBase + 4 * lane), &tile[0][0], PYR_SW,
+                        [&](int r) { return (uint32_t)((syA + r) * srcStride); });
   }
   __syncthreads();
   if (xs >= dw) return;
@@ -902,30 +883,22 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     lvl = arena + (long long)img * arenaPitch + L.arenaOff;
     pitch = L.pitch;
   }
-  constexpr int kN = BLUR_SH * BLUR_WROW;
   // Staging (all loads in flight at once).  Rows outside the level are
   // reflected (REFLECT_101) when addressed; columns are loaded with the dword
   // start clamped into the row, and the few bytes a border tile needs outside
   // [0, w) are patched from their reflected columns afterwards.
   const int colA = td.x0 - 4;  // level column of staged byte 0
   {
-    RawDw v[(kN + 255) / 256];
-#pragma unroll
-    for (int q = 0; q < (kN + 255) / 256; ++q) {
-      const int i = min(tid + 256 * q, kN - 1);
-      const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
-      const uint8_t* row = lvl + (long long)reflect101(td.y0 - 3 + r, L.h) * pitch;
-      const int c = min(max(colA + 4 * wq, 0), L.w - 1);
-      v[q] = raw_u32_any(row + c, row + L.w - 1);
-    }
-#pragma unroll
-    for (int q = 0; q < (kN + 255) / 256; ++q) {
-      const int i = tid + 256 * q;
-      if (i < kN) {
-        const int r = i / BLUR_WROW, wq = i - r * BLUR_WROW;
-        raw[r][wq] = v[q].get();
-      }
-    }
+    const bool aligned = l > 0 || ((pitch & 3) == 0 && (((uintptr_t)lvl) & 3) == 0);
+    const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
+    const int lane = tid & 63;
+    // dword start clamped into the row (keeping 4-alignment on aligned levels)
+    const int c = min(max(colA + 4 * lane, 0), aligned ? ((L.w - 1) & ~3) : L.w - 1);
+    auto rowOff = [&](int r) { return (uint32_t)(reflect101(td.y0 - 3 + r, L.h) * pitch); };
+    if (aligned)
+      stage_rows<true, (BLUR_SH + 3) / 4>(im, BLUR_SH, BLUR_WROW, (uint32_t)c, &raw[0][0], BLUR_WROW + 1, rowOff);
+    else
+      stage_rows<false, (BLUR_SH + 3) / 4>(im, BLUR_SH, BLUR_WROW, (uint32_t)c, &raw[0][0], BLUR_WROW + 1, rowOff);
   }
   const bool leftB = colA < 0, rightB = td.x0 + ORB_BLUR_TW + 3 > L.w;
   if (leftB || rightB) {  // uniform per workgroup
@@ -1154,6 +1127,7 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   (void)xmax;  // folded into the alpha table: (2048, 0) past xmax
   // tile bounds assume a downscale of at most 1.25x per level (checked by the planner)
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, nimg), block(256);
+  // every image base and row start 4-aligned: one load per staged dword
   const bool aligned = (srcStride & 3) == 0 && (((uintptr_t)src) & 3) == 0 && (srcImgPitch & 3) == 0;
   if (aligned)
     hipLaunchKernelGGL(k_pyr_resize<true>, grid, block, 0, s, src, srcImgPitch, srcStride, sw, sh,

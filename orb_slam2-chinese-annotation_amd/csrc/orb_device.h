@@ -149,6 +149,52 @@ __device__ __forceinline__ void buf_st32(__amdgpu_buffer_rsrc_t r, uint32_t off,
   __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
 }
 
+// A byte image behind a buffer resource built from its 4-aligned-down base:
+// image byte o lives at resource offset o + sh.
+struct ImgRsrc {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t sh;
+};
+__device__ __forceinline__ ImgRsrc img_rsrc(const uint8_t* p, uint32_t bytes) {
+  ImgRsrc ir;
+  ir.sh = (uint32_t)((uintptr_t)p & 3);
+  ir.r = make_rsrc(p - ir.sh, (bytes + ir.sh + 3) & ~3u);
+  return ir;
+}
+
+// Stage image rows into LDS, lane = dword column, wave = row (4 waves, B rows
+// per wave in flight per batch): lds[r * ldsPitch + lane] = image bytes
+// [rowOff(r) + colOff, +4) for r < nR and lane < nW (nW <= 64; colOff is this
+// lane's column byte offset).  ALIGNED: every such offset (plus the base
+// misalignment) is a multiple of 4 -- one load per dword; otherwise two,
+// realigned with v_alignbyte.  Bytes past the image read as 0.
+template <bool ALIGNED, int B, class RowOff>
+__device__ __forceinline__ void stage_rows(const ImgRsrc& im, int nR, int nW, uint32_t colOff,
+                                           uint32_t* lds, int ldsPitch, RowOff rowOff) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int r0 = 0; r0 < nR; r0 += 4 * B) {
+    uint32_t lo[B], hi[B], sh[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int r = min(r0 + wv + 4 * q, nR - 1);
+      const uint32_t o = rowOff(r) + colOff + im.sh;
+      if (ALIGNED) {
+        lo[q] = buf_ld32(im.r, o);
+      } else {
+        sh[q] = o & 3u;
+        lo[q] = buf_ld32(im.r, o & ~3u);
+        hi[q] = buf_ld32(im.r, (o & ~3u) + 4);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int r = r0 + wv + 4 * q;
+      if (r < nR && lane < nW)
+        lds[r * ldsPitch + lane] = ALIGNED ? lo[q] : __builtin_amdgcn_alignbyte(hi[q], lo[q], sh[q]);
+    }
+  }
+}
+
 // Bytes b and b+1 (b < 11) of the 12-byte little-endian window (w0, w1, w2),
 // as the low 16 bits of the result.
 __device__ __forceinline__ uint32_t byte_pair(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
