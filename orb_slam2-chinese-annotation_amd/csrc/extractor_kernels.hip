@@ -206,8 +206,9 @@ __device__ __forceinline__ uint32_t pretest_half(uint32_t v, uint32_t q0, uint32
   const uint32_t nd8 = __builtin_bit_cast(uint32_t, d8 - t1), nd12 = __builtin_bit_cast(uint32_t, d12 - t1);
   const uint32_t nb0 = __builtin_bit_cast(uint32_t, nt1 - d0), nb4 = __builtin_bit_cast(uint32_t, nt1 - d4);
   const uint32_t nb8 = __builtin_bit_cast(uint32_t, nt1 - d8), nb12 = __builtin_bit_cast(uint32_t, nt1 - d12);
-  const uint32_t failD = (nd0 | nd4) & (nd4 | nd8) & (nd8 | nd12) & (nd12 | nd0);
-  const uint32_t failB = (nb0 | nb4) & (nb4 | nb8) & (nb8 | nb12) & (nb12 | nb0);
+  // some adjacent pair (0,4)(4,8)(8,12)(12,0) both dark  <=>  (d0|d8) & (d4|d12)
+  const uint32_t failD = (nd0 & nd8) | (nd4 & nd12);
+  const uint32_t failB = (nb0 & nb8) | (nb4 & nb12);
   return ~(failD & failB) & 0x80008000u;
 }
 
@@ -220,10 +221,14 @@ __device__ __forceinline__ uint32_t pretest4(const uint32_t* roi32, int nD, int 
   const uint32_t Q0 = row[3 * nD], Q8 = row[-3 * nD];
   const uint32_t Q4 = __builtin_amdgcn_alignbyte(Cn, B, 3);   // columns 4k+3 .. 4k+6
   const uint32_t Q12 = __builtin_amdgcn_alignbyte(B, A, 1);   // columns 4k-3 .. 4k
-  const uint32_t M = 0x00FF00FFu;
-  const uint32_t e = pretest_half(B & M, Q0 & M, Q4 & M, Q8 & M, Q12 & M, t1, nt1);
-  const uint32_t o = pretest_half((B >> 8) & M, (Q0 >> 8) & M, (Q4 >> 8) & M, (Q8 >> 8) & M,
-                                  (Q12 >> 8) & M, t1, nt1);
+  // even bytes (0, 2) and odd bytes (1, 3) as u16 lanes, one v_perm each
+  constexpr uint32_t SE = 0x0C020C00u, SO = 0x0C030C01u;
+#define ORB_PK(x, sel) __builtin_amdgcn_perm(0u, (x), (sel))
+  const uint32_t e = pretest_half(ORB_PK(B, SE), ORB_PK(Q0, SE), ORB_PK(Q4, SE), ORB_PK(Q8, SE),
+                                  ORB_PK(Q12, SE), t1, nt1);
+  const uint32_t o = pretest_half(ORB_PK(B, SO), ORB_PK(Q0, SO), ORB_PK(Q4, SO), ORB_PK(Q8, SO),
+                                  ORB_PK(Q12, SO), t1, nt1);
+#undef ORB_PK
   return ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
 }
 
