@@ -113,6 +113,24 @@ __device__ __forceinline__ int cand_idx(uint32_t e) { return (int)(e & 0x7FFFFu)
 __device__ __forceinline__ int cand_dist(uint32_t e) { return (int)((e >> 19) & 0x1FFu); }
 __device__ __forceinline__ int cand_oct(uint32_t e) { return (int)(e >> 28); }
 
+// First TOPK (= 4) candidates in (dist, scan order), kept in registers: a
+// stable sorted insertion (after equal distances) as a branch-free network.
+// Empty slots are 0xFFFFFFFF, whose distance field (511) exceeds any real one.
+struct Top4 {
+  uint32_t t0 = 0xFFFFFFFFu, t1 = 0xFFFFFFFFu, t2 = 0xFFFFFFFFu, t3 = 0xFFFFFFFFu;
+  __device__ __forceinline__ void insert(uint32_t e, int d) {
+    const bool b0 = cand_dist(t0) > d, b1 = cand_dist(t1) > d, b2 = cand_dist(t2) > d,
+               b3 = cand_dist(t3) > d;
+    t3 = b2 ? t2 : (b3 ? e : t3);
+    t2 = b1 ? t1 : (b2 ? e : t2);
+    t1 = b0 ? t0 : (b1 ? e : t1);
+    t0 = b0 ? e : t0;
+  }
+  __device__ __forceinline__ void store(uint32_t* dst) const {
+    *reinterpret_cast<uint4*>(dst) = make_uint4(t0, t1, t2, t3);
+  }
+};
+
 // Visit, in GetFeaturesInArea order (src/Frame.cc:368-424), every keypoint of
 // the window that passes the level and |dx|,|dy| < r tests.
 template <typename F>
@@ -178,28 +196,21 @@ __global__ __launch_bounds__(256) void k_proj_candidates(
   const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
   const int32_t* ci = cellIdx + (size_t)p * kpStride;
   const ulonglong4 q = load_desc(mpDesc + mg * 32);
-  uint32_t top[TOPK];
-  int ntop = 0, count = 0;
+  Top4 top;
+  int count = 0;
   for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
                        [&](int idx, const orb_keypoint_t& kp) {
                          if (LK && LK[idx]) return;
                          if (UR && UR[idx] > 0) {
                            const float er = fabsf(mp.proj_xr - UR[idx]);
-                           if (er > r * P.scale[lvl]) return;
+                           if (er > rs) return;
                          }
                          const int dist = hamming256(q, load_desc(D + (size_t)idx * 32));
                          if (dist >= 256) return;  // can never become best or second
                          ++count;
-                         // stable insertion: after existing entries with equal distance
-                         int pos = ntop;
-                         while (pos > 0 && cand_dist(top[pos - 1]) > dist) --pos;
-                         if (pos >= TOPK) return;
-                         const int last = ntop < TOPK ? ntop : TOPK - 1;
-                         for (int j = last; j > pos; --j) top[j] = top[j - 1];
-                         top[pos] = pack_cand(idx, dist, kp.octave);
-                         if (ntop < TOPK) ++ntop;
+                         top.insert(pack_cand(idx, dist, kp.octave), dist);
                        });
-  for (int j = 0; j < TOPK; ++j) topk[mg * TOPK + j] = j < ntop ? top[j] : 0xFFFFFFFFu;
+  top.store(topk + mg * TOPK);
   ncand[mg] = count;
 }
 
@@ -668,8 +679,8 @@ __global__ __launch_bounds__(256) void k_frame_candidates(
   else if (F.bwd) { minL = 0; maxL = o; }
   else { minL = o - 1; maxL = o + 1; }
   const ulonglong4 q = load_desc(lastDesc + (size_t)i * 32);
-  uint32_t top[TOPK];
-  int ntop = 0, count = 0;
+  Top4 top;
+  int count = 0;
   for_features_in_area(keys, cellStart, cellIdx, P, u, v, radius, minL, maxL,
                        [&](int idx, const orb_keypoint_t& kp) {
                          if (locked && locked[idx]) return;
@@ -681,15 +692,9 @@ __global__ __launch_bounds__(256) void k_frame_candidates(
                          const int dist = hamming256(q, load_desc(desc + (size_t)idx * 32));
                          if (dist >= 256) return;
                          ++count;
-                         int pos = ntop;
-                         while (pos > 0 && cand_dist(top[pos - 1]) > dist) --pos;
-                         if (pos >= TOPK) return;
-                         const int lastj = ntop < TOPK ? ntop : TOPK - 1;
-                         for (int j = lastj; j > pos; --j) top[j] = top[j - 1];
-                         top[pos] = pack_cand(idx, dist, kp.octave);
-                         if (ntop < TOPK) ++ntop;
+                         top.insert(pack_cand(idx, dist, kp.octave), dist);
                        });
-  for (int j = 0; j < TOPK; ++j) topk[(size_t)i * TOPK + j] = j < ntop ? top[j] : 0xFFFFFFFFu;
+  top.store(topk + (size_t)i * TOPK);
   ncand[i] = count;
 }
 
