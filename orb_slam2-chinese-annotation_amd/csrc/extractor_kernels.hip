@@ -850,6 +850,9 @@ __global__ __launch_bounds__(512) void k_octree(
 // borders is staged in LDS, the row pass is kept as exact u16 sums.
 __constant__ int8_t c_pattern[2 * ORB_PATTERN_POINTS];
 __constant__ int c_umax[16];
+// IC_Angle byte masks: row v+15 (v in [-15, 15]), dword k of the 32 bytes at
+// columns -16..15: 0xFF where |u| <= umax[|v|] (built from umax on upload)
+__constant__ uint32_t c_icmask[32][8];
 
 __device__ __forceinline__ int reflect101(int i, int n) {
   if (n == 1) return 0;
@@ -1015,7 +1018,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     long long blurPitch, OrbPlanDesc plan, const uint32_t* __restrict__ outKeys,
     const int32_t* __restrict__ outCount, orb_keypoint_t* __restrict__ kps,
     uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave id through readfirstlane: everything derived from it (level, key,
+  // buffer descriptors) is then provably wave-uniform -> SGPRs, no waterfall
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int img = blockIdx.y;
   const int slot = blockIdx.x * 4 + w;
   const int32_t* cnts = outCount + img * plan.nlevels;
@@ -1043,23 +1048,31 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     lvl = arena + (long long)img * arenaPitch + L.arenaOff;
     pitch = L.pitch;
   }
-  // ---- IC_Angle
+  // ---- IC_Angle (src/ORBextractor.cc:77-113), exact integer moments.
+  // Lane = (row v = (lane & 31) - 15, half = lane >> 5): 16 bytes at columns
+  // 16*half-16 .. 16*half-1 of row cy+v, masked to |u| <= umax[|v|].  Row sum
+  // and u-moment are v_dot4 products: m10 = sum (u+16)*I - 16*sum I,
+  // m01 = sum v * rowsum.
   int m01 = 0, m10 = 0;
   {
-    const int col = lane & 31, below = lane < 32;
-    if (col < 31) {
-      const int u = col - 15;
-      const uint8_t* c = lvl + (long long)cy * pitch + cx + u;
-      const int step = below ? pitch : -pitch;
-      if (below) m10 += u * c[0];
-      int vals[15];
+    const int ri = lane & 31, half = lane >> 5;
+    if (ri < 31) {
+      const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
+      const uint32_t o0 = (uint32_t)((cy + ri - 15) * pitch + cx - 16 + 16 * half) + im.sh;
+      const uint32_t sh = o0 & 3u, a0 = o0 & ~3u;
+      uint32_t w[5];
 #pragma unroll
-      for (int v = 1; v <= 15; ++v) vals[v - 1] = (u >= -c_umax[v] && u <= c_umax[v]) ? c[v * step] : 0;
+      for (int k = 0; k < 5; ++k) w[k] = buf_ld32(im.r, a0 + 4 * k);
+      uint32_t rs = 0, rm = 0;
 #pragma unroll
-      for (int v = 1; v <= 15; ++v) {
-        m01 += (below ? v : -v) * vals[v - 1];
-        m10 += u * vals[v - 1];
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t d = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh) & c_icmask[ri][4 * half + k];
+        const uint32_t wt = (uint32_t)(16 * half + 4 * k) * 0x01010101u + 0x03020100u;  // u + 16
+        rs = __builtin_amdgcn_udot4(d, 0x01010101u, rs, false);
+        rm = __builtin_amdgcn_udot4(d, wt, rm, false);
       }
+      m10 = (int)rm - 16 * (int)rs;
+      m01 = (ri - 15) * (int)rs;
     }
   }
   m01 = wave_sum(m01);
@@ -1074,16 +1087,22 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     a = c;
     b = s;
   }
-  const uint8_t* bc = blur + (long long)img * blurPitch + L.blurOff + (long long)cy * L.blurPitch + cx;
+  // 512 samples of the blurred level around (cx, cy): byte loads through a
+  // buffer resource (32-bit offsets)
   const int bp = L.blurPitch;
+  const __amdgpu_buffer_rsrc_t rb =
+      make_rsrc(blur + (long long)img * blurPitch + L.blurOff, (uint32_t)(L.h * bp));
+  const int cofs = cy * bp + cx;
   int v0[4], v1[4];
 #pragma unroll
   for (int kq = 0; kq < 4; ++kq) {
     const int test = lane + 64 * kq;
     const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
     const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
-    v0[kq] = bc[cv_round(px0 * b + py0 * a) * bp + cv_round(px0 * a - py0 * b)];
-    v1[kq] = bc[cv_round(px1 * b + py1 * a) * bp + cv_round(px1 * a - py1 * b)];
+    const int o0 = cofs + cv_round(px0 * b + py0 * a) * bp + cv_round(px0 * a - py0 * b);
+    const int o1 = cofs + cv_round(px1 * b + py1 * a) * bp + cv_round(px1 * a - py1 * b);
+    v0[kq] = __builtin_amdgcn_raw_buffer_load_b8(rb, o0, 0, 0);
+    v1[kq] = __builtin_amdgcn_raw_buffer_load_b8(rb, o1, 0, 0);
   }
   unsigned long long words[4];
 #pragma unroll
@@ -1121,8 +1140,23 @@ hipError_t orb_k_upload_constants(hipStream_t s) {
 }
 
 hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s) {
-  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_umax), umax16, 16 * sizeof(int), 0,
-                                hipMemcpyHostToDevice, s);
+  static uint32_t mask[32][8];
+  for (int r = 0; r < 32; ++r)
+    for (int k = 0; k < 8; ++k) {
+      uint32_t m = 0;
+      for (int j = 0; j < 4; ++j) {
+        const int u = 4 * k + j - 16, v = r - 15;
+        if (r < 31 && u >= -umax16[v < 0 ? -v : v] && u <= umax16[v < 0 ? -v : v]) m |= 0xFFu << (8 * j);
+      }
+      mask[r][k] = m;
+    }
+  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_icmask), mask, sizeof(mask), 0,
+                                        hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_umax), umax16, 16 * sizeof(int), 0,
+                             hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(s);  // the static staging array is reused
 }
 
 hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sw,
