@@ -17,11 +17,18 @@ import sys
 from pathlib import Path
 
 
+def kname(full):
+    """'void k_pyr_resize<true>(...)' -> 'k_pyr_resize'"""
+    n = full.split("(")[0]
+    n = n[5:] if n.startswith("void ") else n
+    return n.split("<")[0]
+
+
 def per_kernel(d, counter):
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(Path(d) / "run_counter_collection.csv")):
         if r["Counter_Name"] == counter:
-            vals[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024.0)
+            vals[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
     return vals
 
 

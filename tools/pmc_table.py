@@ -6,11 +6,18 @@ import csv
 import sys
 from pathlib import Path
 
+
+def kname(full):
+    """'void k_pyr_resize<true>(...)' -> 'k_pyr_resize'"""
+    n = full.split("(")[0]
+    n = n[5:] if n.startswith("void ") else n
+    return n.split("<")[0]
+
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for d in sys.argv[1:]:
     for f in Path(d).glob("*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0]
+            k = kname(r["Kernel_Name"])
             if k.startswith("k_"):
                 vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 names = sorted({c for k in vals for c in vals[k]})
