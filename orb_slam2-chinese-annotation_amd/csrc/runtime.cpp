@@ -430,9 +430,12 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   P.slotsPerImage = slots;
   P.maxCellRows = maxRows;
   P.maxCellCols = maxCols;
-  // octree LDS: node tables + as many keys as fit in ~150 KiB
+  // octree LDS: node tables + keys within ~52 KiB (three workgroups per CU
+  // overlap their latency-bound passes); a level with more candidate keys
+  // keeps them in global scratch instead (ORB_OCTREE_LDS_KB overrides)
   const size_t nodeBytes = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, 0);
-  const size_t budget = 150 * 1024;
+  const char* lk = getenv("ORB_OCTREE_LDS_KB");
+  const size_t budget = (size_t)(lk ? std::max(16, std::min(150, atoi(lk))) : 52) * 1024;
   int ldsKeyCap = nodeBytes < budget ? (int)((budget - nodeBytes) / 6) : 0;
   ldsKeyCap &= ~7;
   if (nodeBytes + (size_t)ldsKeyCap * 6 > 160 * 1024) return ORB_EINVAL;
