@@ -169,16 +169,55 @@ __device__ __forceinline__ void for_features_in_area(const orb_keypoint_t* K,
 // Per map point: candidate scan + first-K in (dist, scan order); counts every
 // candidate that could ever be best/second (dist < 256, not pre-locked, passes
 // the stereo gate).  ncand = -1 marks a point the reference skips outright.
+//
+// The frame's grid is staged in LDS once per workgroup: cellStart, and the
+// keypoints in cell order as {x, y, idx | octave << 24 | locked << 31, uR}
+// (the order GetFeaturesInArea visits them), so the scan is LDS-latency bound;
+// only the descriptors of window candidates come from global memory.  Frames
+// with more than PROJ_STAGE keypoints scan the global grid instead.
+#define PROJ_STAGE 2048
+
 __global__ __launch_bounds__(256) void k_proj_candidates(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked, int kpStride,
-    const orb_mp_track_t* __restrict__ mps, const uint8_t* __restrict__ mpDesc,
-    const int32_t* __restrict__ nmps, int mpStride, const int32_t* __restrict__ cellStart,
-    const int32_t* __restrict__ cellIdx, ProjParams P, uint32_t* __restrict__ topk,
-    int32_t* __restrict__ ncand) {
+    const int32_t* __restrict__ nkeys, const orb_mp_track_t* __restrict__ mps,
+    const uint8_t* __restrict__ mpDesc, const int32_t* __restrict__ nmps, int mpStride,
+    const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
+    uint32_t* __restrict__ topk, int32_t* __restrict__ ncand) {
+  __shared__ int sCS[GRID_CELLS + 1];
+  __shared__ __attribute__((aligned(16))) uint4 sKp[PROJ_STAGE];
+  __shared__ float sScale[ORB_MAX_LEVELS];
   const int p = blockIdx.y;
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= nmps[p]) return;
+  const int tid = threadIdx.x;
+  const int m = blockIdx.x * blockDim.x + tid;
+  const int M = nmps[p], N = nkeys[p];
+  if ((int)(blockIdx.x * blockDim.x) >= M) return;  // whole workgroup idle (uniform)
+  const orb_keypoint_t* K = keys + (size_t)p * kpStride;
+  const uint8_t* D = desc + (size_t)p * kpStride * 32;
+  const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
+  const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
+  const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
+  const int32_t* ci = cellIdx + (size_t)p * kpStride;
+  const bool staged = N <= PROJ_STAGE;
+#pragma unroll
+  for (int i = 0; i < ORB_MAX_LEVELS; ++i)
+    if (tid == i) sScale[i] = P.scale[i];
+  if (staged) {
+    for (int i = tid; i <= GRID_CELLS; i += 256) sCS[i] = cs[i];
+    const int nInGrid = cs[GRID_CELLS];
+    for (int j = tid; j < nInGrid; j += 256) {
+      const int idx = ci[j];
+      const orb_keypoint_t kp = K[idx];
+      uint4 e;
+      e.x = __float_as_uint(kp.x);
+      e.y = __float_as_uint(kp.y);
+      e.z = (uint32_t)idx | ((uint32_t)kp.octave << 24) | ((LK && LK[idx]) ? 0x80000000u : 0u);
+      e.w = __float_as_uint(UR ? UR[idx] : -1.0f);
+      sKp[j] = e;
+    }
+  }
+  __syncthreads();
+  if (m >= M) return;
   const size_t mg = (size_t)p * mpStride + m;
   const orb_mp_track_t mp = mps[mg];
   if (!mp.in_view || mp.bad) {
@@ -188,28 +227,52 @@ __global__ __launch_bounds__(256) void k_proj_candidates(
   const int lvl = mp.level;
   float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:135-141)
   if (P.th != 1.0f) r *= P.th;
-  const float rs = r * P.scale[lvl];
-  const orb_keypoint_t* K = keys + (size_t)p * kpStride;
-  const uint8_t* D = desc + (size_t)p * kpStride * 32;
-  const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
-  const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
-  const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
-  const int32_t* ci = cellIdx + (size_t)p * kpStride;
+  const float rs = r * sScale[lvl];
   const ulonglong4 q = load_desc(mpDesc + mg * 32);
   Top4 top;
   int count = 0;
-  for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
-                       [&](int idx, const orb_keypoint_t& kp) {
-                         if (LK && LK[idx]) return;
-                         if (UR && UR[idx] > 0) {
-                           const float er = fabsf(mp.proj_xr - UR[idx]);
-                           if (er > rs) return;
-                         }
-                         const int dist = hamming256(q, load_desc(D + (size_t)idx * 32));
-                         if (dist >= 256) return;  // can never become best or second
-                         ++count;
-                         top.insert(pack_cand(idx, dist, kp.octave), dist);
-                       });
+  auto visit = [&](int idx, int oct, bool lockd, float ur) {
+    if (lockd) return;
+    if (ur > 0) {
+      const float er = fabsf(mp.proj_xr - ur);
+      if (er > rs) return;
+    }
+    const int dist = hamming256(q, load_desc(D + (size_t)idx * 32));
+    if (dist >= 256) return;  // can never become best or second
+    ++count;
+    top.insert(pack_cand(idx, dist, oct), dist);
+  };
+  if (staged) {
+    // GetFeaturesInArea (src/Frame.cc:368-424) over the staged grid
+    const float x = mp.proj_x, y = mp.proj_y;
+    const int nMinCellX = max(0, (int)floorf((x - P.minX - rs) * P.invW));
+    const int nMaxCellX = min(ORB_GRID_COLS - 1, (int)ceilf((x - P.minX + rs) * P.invW));
+    const int nMinCellY = max(0, (int)floorf((y - P.minY - rs) * P.invH));
+    const int nMaxCellY = min(ORB_GRID_ROWS - 1, (int)ceilf((y - P.minY + rs) * P.invH));
+    if (nMinCellX < ORB_GRID_COLS && nMaxCellX >= 0 && nMinCellY < ORB_GRID_ROWS &&
+        nMaxCellY >= 0) {
+      const int minL = lvl - 1, maxL = lvl;
+      for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
+          const int c = ix * ORB_GRID_ROWS + iy;
+          const int e = sCS[c + 1];
+          for (int j = sCS[c]; j < e; ++j) {
+            const uint4 E = sKp[j];
+            const int oct = (int)((E.z >> 24) & 0x7Fu);
+            if (oct < minL || oct > maxL) continue;
+            const float dx = __uint_as_float(E.x) - x, dy = __uint_as_float(E.y) - y;
+            if (fabsf(dx) < rs && fabsf(dy) < rs)
+              visit((int)(E.z & 0xFFFFFFu), oct, (E.z >> 31) != 0, __uint_as_float(E.w));
+          }
+        }
+      }
+    }
+  } else {
+    for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
+                         [&](int idx, const orb_keypoint_t& kp) {
+                           visit(idx, kp.octave, LK && LK[idx], UR ? UR[idx] : -1.0f);
+                         });
+  }
   top.store(topk + mg * TOPK);
   ncand[mg] = count;
 }
@@ -392,7 +455,8 @@ hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, in
 
 hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc,
                                  const float* uright, const uint8_t* locked, int kpStride,
-                                 const orb_mp_track_t* mps, const uint8_t* mpDesc,
+                                 const int32_t* nkeys, const orb_mp_track_t* mps,
+                                 const uint8_t* mpDesc,
                                  const int32_t* nmps, int mpStride, int mpMax,
                                  const int32_t* cellStart, const int32_t* cellIdx,
                                  const void* params, uint32_t* topk, int32_t* ncand,
@@ -400,8 +464,8 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
   const ProjParams P = *(const ProjParams*)params;
   if (mpMax <= 0 || nproblems <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + 255) / 256, nproblems), dim3(256), 0, s,
-                     keys, desc, uright, locked, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                     cellIdx, P, topk, ncand);
+                     keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
+                     cellStart, cellIdx, P, topk, ncand);
   return hipGetLastError();
 }
 

@@ -52,7 +52,8 @@ hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, in
                             int32_t* cellIdx, int nproblems, hipStream_t s);
 hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc,
                                  const float* uright, const uint8_t* locked, int kpStride,
-                                 const orb_mp_track_t* mps, const uint8_t* mpDesc,
+                                 const int32_t* nkeys, const orb_mp_track_t* mps,
+                                 const uint8_t* mpDesc,
                                  const int32_t* nmps, int mpStride, int mpMax,
                                  const int32_t* cellStart, const int32_t* cellIdx,
                                  const void* params, uint32_t* topk, int32_t* ncand,
@@ -968,7 +969,7 @@ orb_status_t orb_match_projection_local_batch(
   HIP_TRY(orb_k_grid_build(d_keys, d_nkeys, kp_stride, P.minX, P.minY, P.invW, P.invH,
                            m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), n_problems, s));
   if (ev) HIP_TRY(hipEventRecord((*ev)[1], s));
-  HIP_TRY(orb_k_proj_candidates(d_keys, d_desc, nullptr, d_locked, kp_stride, d_mps, d_mp_desc,
+  HIP_TRY(orb_k_proj_candidates(d_keys, d_desc, nullptr, d_locked, kp_stride, d_nkeys, d_mps, d_mp_desc,
                                 d_nmps, mp_stride, mp_stride, m->dCellStart.as<int32_t>(),
                                 m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
                                 m->dNcand.as<int32_t>(), n_problems, s));
@@ -1057,6 +1058,7 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   const float* ur = F->u_right ? m->dUr.as<float>() : nullptr;
   const uint8_t* lk = kp_locked ? m->dLocked.as<uint8_t>() : nullptr;
   HIP_TRY(orb_k_proj_candidates(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(), ur, lk, N,
+                                m->dNKeys.as<int32_t>(),
                                 m->dMps.as<orb_mp_track_t>(), m->dMpDesc.as<uint8_t>(),
                                 m->dNMps.as<int32_t>(), std::max(M, 1), M,
                                 m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
