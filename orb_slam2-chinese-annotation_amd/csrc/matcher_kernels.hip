@@ -177,7 +177,8 @@ __device__ __forceinline__ void for_features_in_area(const orb_keypoint_t* K,
 // with more than PROJ_STAGE keypoints scan the global grid instead.
 #define PROJ_STAGE 2048
 
-__global__ __launch_bounds__(256) void k_proj_candidates(
+#define PROJ_WG 1024
+__global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked, int kpStride,
     const int32_t* __restrict__ nkeys, const orb_mp_track_t* __restrict__ mps,
@@ -203,9 +204,9 @@ __global__ __launch_bounds__(256) void k_proj_candidates(
   for (int i = 0; i < ORB_MAX_LEVELS; ++i)
     if (tid == i) sScale[i] = P.scale[i];
   if (staged) {
-    for (int i = tid; i <= GRID_CELLS; i += 256) sCS[i] = cs[i];
+    for (int i = tid; i <= GRID_CELLS; i += PROJ_WG) sCS[i] = cs[i];
     const int nInGrid = cs[GRID_CELLS];
-    for (int j = tid; j < nInGrid; j += 256) {
+    for (int j = tid; j < nInGrid; j += PROJ_WG) {
       const int idx = ci[j];
       const orb_keypoint_t kp = K[idx];
       uint4 e;
@@ -463,7 +464,8 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
                                  int nproblems, hipStream_t s) {
   const ProjParams P = *(const ProjParams*)params;
   if (mpMax <= 0 || nproblems <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + 255) / 256, nproblems), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems),
+                     dim3(PROJ_WG), 0, s,
                      keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
                      cellStart, cellIdx, P, topk, ncand);
   return hipGetLastError();
