@@ -192,8 +192,8 @@ __device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
 // compacts its window row by row (lane = row).  Output per cell: keypoints
 // in row-major window order (cv::FAST's order), packed x | y<<12 | score<<24
 // in level coordinates, and their count.
-#define FAST_GROUPS 512    // 4-pixel groups pretested per round (2 per thread)
-#define FAST_QUEUE (4 * FAST_GROUPS)
+#define FAST_GROUPS 256    // 8-pixel groups pretested per round (one per thread)
+#define FAST_QUEUE (8 * FAST_GROUPS)
 #define FAST_CORNERS 2048  // corner list capacity; beyond it NMS runs densely
 #define FAST_LOADS 10      // dwords per thread in flight while staging a band (10 KB)
 
@@ -244,6 +244,32 @@ __device__ __forceinline__ uint32_t pretest4(const uint32_t* roi32, int nD, int 
                                   ORB_PK(Q12, SO), t1, nt1);
 #undef ORB_PK
   return ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
+}
+
+// Pretest of the 8 pixels at region columns 8k..8k+7 of region row r: bit j
+// of the result = pixel 8k+j passes.  (Dwords past the row end are read but
+// only feed masked-off pixels.)
+__device__ __forceinline__ uint32_t pretest8(const uint32_t* roi32, int nD, int r, int k, s16x2 t1,
+                                             s16x2 nt1) {
+  const uint32_t* row = roi32 + r * nD + 2 * k;
+  const uint32_t A = row[-1], B0 = row[0], B1 = row[1], Cn = row[2];
+  const uint32_t Q0a = row[3 * nD], Q0b = row[3 * nD + 1];
+  const uint32_t Q8a = row[-3 * nD], Q8b = row[-3 * nD + 1];
+  const uint32_t Q4a = __builtin_amdgcn_alignbyte(B1, B0, 3), Q4b = __builtin_amdgcn_alignbyte(Cn, B1, 3);
+  const uint32_t Q12a = __builtin_amdgcn_alignbyte(B0, A, 1), Q12b = __builtin_amdgcn_alignbyte(B1, B0, 1);
+  constexpr uint32_t SE = 0x0C020C00u, SO = 0x0C030C01u;
+#define ORB_PK(x, sel) __builtin_amdgcn_perm(0u, (x), (sel))
+  const uint32_t ea = pretest_half(ORB_PK(B0, SE), ORB_PK(Q0a, SE), ORB_PK(Q4a, SE),
+                                   ORB_PK(Q8a, SE), ORB_PK(Q12a, SE), t1, nt1);
+  const uint32_t oa = pretest_half(ORB_PK(B0, SO), ORB_PK(Q0a, SO), ORB_PK(Q4a, SO),
+                                   ORB_PK(Q8a, SO), ORB_PK(Q12a, SO), t1, nt1);
+  const uint32_t eb = pretest_half(ORB_PK(B1, SE), ORB_PK(Q0b, SE), ORB_PK(Q4b, SE),
+                                   ORB_PK(Q8b, SE), ORB_PK(Q12b, SE), t1, nt1);
+  const uint32_t ob = pretest_half(ORB_PK(B1, SO), ORB_PK(Q0b, SO), ORB_PK(Q4b, SO),
+                                   ORB_PK(Q8b, SO), ORB_PK(Q12b, SO), t1, nt1);
+#undef ORB_PK
+  return ((ea >> 15) & 1u) | ((oa >> 14) & 2u) | ((ea >> 29) & 4u) | ((oa >> 28) & 8u) |
+         ((eb >> 11) & 16u) | ((ob >> 10) & 32u) | ((eb >> 25) & 64u) | ((ob >> 24) & 128u);
 }
 
 __global__ __launch_bounds__(256) void k_fast_band(
@@ -343,46 +369,55 @@ __global__ __launch_bounds__(256) void k_fast_band(
     s16x2 t1, nt1;
     t1.x = t1.y = (short)(t + 1);
     nt1.x = nt1.y = (short)(-(t + 1));
-    const int nK = FB ? nFbK : nD;
+    // 8-pixel groups (two LDS dwords): phase A covers every group column of
+    // the band, phase B only those listed in fbK
+    const int nK = FB ? nFbK : (nD + 1) >> 1;
     const int nG = ih * nK;
     const float invK = 1.0f / (float)nK;
     for (int g0 = 0; g0 < nG; g0 += FAST_GROUPS) {
+      const int gi = g0 + tid;
+      uint32_t m8 = 0;
+      int off = 0;
+      if (gi < nG) {
+        const int rr = (int)(((float)gi + 0.5f) * invK), kk = gi - rr * nK;
+        const int k = FB ? (int)fbK[kk] : kk;
+        const int r = rr + 3;
+        off = r * P + 8 * k;
+        // valid columns 3 <= 8k+j < C-3 (and, in phase B, in a fallback cell)
+        const int lo = max(3 - 8 * k, 0), hi = min(C - 3 - 8 * k, 8);
+        uint32_t cm = hi > lo ? ((1u << hi) - (1u << lo)) : 0u;
+        if (FB) {
 #pragma unroll
-      for (int q = 0; q < FAST_GROUPS / 256; ++q) {
-        const int gi = g0 + q * 256 + tid;
-        uint32_t m4 = 0;
-        int off = 0;
-        if (gi < nG) {
-          const int rr = (int)(((float)gi + 0.5f) * invK), kk = gi - rr * nK;
-          const int k = FB ? (int)fbK[kk] : kk;
-          const int r = rr + 3;
-          off = r * P + 4 * k;
-          // valid columns 3 <= 4k+j < C-3 (and, in phase B, in a fallback cell)
-          uint32_t cm = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int col = 4 * k + j;
-            bool ok = col >= 3 && col < C - 3;
-            if (FB && ok) {
-              const int c = cellOf[col - 3];
-              ok = (fbMask[c >> 5] >> (c & 31)) & 1u;
+          for (int j = 0; j < 8; ++j) {
+            if ((cm >> j) & 1u) {
+              const int c = cellOf[8 * k + j - 3];
+              if (!((fbMask[c >> 5] >> (c & 31)) & 1u)) cm &= ~(1u << j);
             }
-            cm |= (uint32_t)ok << j;
           }
-          if (cm) m4 = pretest4(roi32, nD, r, k, t1, nt1) & cm;
-          if (!FB) ((uint32_t*)sc)[r * nD + k] = 0;  // non-corners store 0
         }
-        const unsigned long long b0 = __ballot(m4 & 1u), b1 = __ballot(m4 & 2u);
-        const unsigned long long b2 = __ballot(m4 & 4u), b3 = __ballot(m4 & 8u);
-        const int n0 = __popcll(b0), n1 = __popcll(b1), n2 = __popcll(b2), n3 = __popcll(b3);
-        const int tot = n0 + n1 + n2 + n3;
-        int base = 0;
-        if (lane == 0 && tot) base = atomicAdd(&qCount, tot);
-        base = __shfl(base, 0, 64);
-        if (m4 & 1u) queue[base + __popcll(b0 & ltMask)] = (uint16_t)off;
-        if (m4 & 2u) queue[base + n0 + __popcll(b1 & ltMask)] = (uint16_t)(off + 1);
-        if (m4 & 4u) queue[base + n0 + n1 + __popcll(b2 & ltMask)] = (uint16_t)(off + 2);
-        if (m4 & 8u) queue[base + n0 + n1 + n2 + __popcll(b3 & ltMask)] = (uint16_t)(off + 3);
+        if (cm) m8 = pretest8(roi32, nD, r, k, t1, nt1) & cm;
+        if (!FB) {  // non-corners store 0 (two dwords; the second may be the row's pad)
+          uint32_t* z = (uint32_t*)sc + r * nD + 2 * k;
+          z[0] = 0;
+          if (2 * k + 1 < nD) z[1] = 0;
+        }
+      }
+      // wave-aggregated append: one LDS atomic per wave, lane offsets by mbcnt
+      unsigned long long bj[8];
+      int nj[8], tot = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bj[j] = __ballot((m8 >> j) & 1u);
+        nj[j] = __popcll(bj[j]);
+        tot += nj[j];
+      }
+      int base = 0;
+      if (lane == 0 && tot) base = atomicAdd(&qCount, tot);
+      base = __shfl(base, 0, 64);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if ((m8 >> j) & 1u) queue[base + __popcll(bj[j] & ltMask)] = (uint16_t)(off + j);
+        base += nj[j];
       }
       __syncthreads();
       const int nq = dbg == 3 ? 0 : qCount;
@@ -492,13 +527,14 @@ __global__ __launch_bounds__(256) void k_fast_band(
   // group columns that touch one (wave 0 lists them in order with ballots)
   if (wave == 0) {
     int cnt = 0;
-    for (int k0 = 0; k0 < nD; k0 += 64) {
+    const int nK8 = (nD + 1) >> 1;
+    for (int k0 = 0; k0 < nK8; k0 += 64) {
       const int k = k0 + lane;
       bool hit = false;
-      if (k < nD) {
+      if (k < nK8) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = 4 * k + j;
+        for (int j = 0; j < 8; ++j) {
+          const int col = 8 * k + j;
           if (col >= 3 && col < C - 3) {
             const int c = cellOf[col - 3];
             hit = hit || ((fbMask[c >> 5] >> (c & 31)) & 1u);
