@@ -133,11 +133,14 @@ struct DevBuf {
 // the launch path); read() drains every recorded set and accumulates per-stage
 // milliseconds, so a timed region of K calls is measured without perturbing it.
 struct StageProfiler {
+  // Per call: a (begin, end) event pair per stage, recorded on whichever stream
+  // runs that stage (stages may overlap), plus a (begin, end) pair for the
+  // whole call on the caller's stream.
   static const int kMaxStages = 6;
   bool enabled = false;
   int nStages = 0;
   const char* names[kMaxStages] = {};
-  std::vector<std::vector<hipEvent_t>> pool;  // each: nStages + 1 events
+  std::vector<std::vector<hipEvent_t>> pool;  // each: 2 * nStages + 2 events
   size_t used = 0;
   double ms[kMaxStages + 1] = {};
   long launches[kMaxStages + 1] = {};
@@ -150,24 +153,28 @@ struct StageProfiler {
   std::vector<hipEvent_t>* begin_call() {
     if (!enabled) return nullptr;
     if (used == pool.size()) {
-      pool.emplace_back(nStages + 1);
+      pool.emplace_back(2 * nStages + 2);
       for (hipEvent_t& e : pool.back()) hipEventCreate(&e);
     }
     return &pool[used++];
   }
+  hipEvent_t b(std::vector<hipEvent_t>* ev, int stage) const { return (*ev)[2 * stage]; }
+  hipEvent_t e(std::vector<hipEvent_t>* ev, int stage) const { return (*ev)[2 * stage + 1]; }
+  hipEvent_t t0(std::vector<hipEvent_t>* ev) const { return (*ev)[2 * nStages]; }
+  hipEvent_t t1(std::vector<hipEvent_t>* ev) const { return (*ev)[2 * nStages + 1]; }
   void drain() {
     for (size_t c = 0; c < used; ++c) {
       std::vector<hipEvent_t>& ev = pool[c];
-      if (hipEventSynchronize(ev[nStages]) != hipSuccess) continue;
+      if (hipEventSynchronize(ev[2 * nStages + 1]) != hipSuccess) continue;
       for (int i = 0; i < nStages; ++i) {
         float t = 0.f;
-        if (hipEventElapsedTime(&t, ev[i], ev[i + 1]) == hipSuccess) {
+        if (hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]) == hipSuccess) {
           ms[i] += t;
           launches[i] += launchesPerCall[i];
         }
       }
       float t = 0.f;
-      if (hipEventElapsedTime(&t, ev[0], ev[nStages]) == hipSuccess) {
+      if (hipEventElapsedTime(&t, ev[2 * nStages], ev[2 * nStages + 1]) == hipSuccess) {
         ms[nStages] += t;
         launches[nStages] += 1;
       }
@@ -176,11 +183,16 @@ struct StageProfiler {
   }
   void destroy() {
     for (auto& v : pool)
-      for (hipEvent_t e : v) hipEventDestroy(e);
+      for (hipEvent_t ev : v) hipEventDestroy(ev);
     pool.clear();
     used = 0;
   }
 };
+
+#define PROF_REC(ev, evt, strm) \
+  do {                                            \
+    if (ev) HIP_TRY(hipEventRecord((evt), (strm))); \
+  } while (0)
 
 orb_status_t check_device(int device) {
   int n = 0;
@@ -207,6 +219,8 @@ struct orb_extractor {
   std::vector<int> quota;
   int umax[16];
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // side stream: blur runs beside FAST + octree
+  hipEvent_t evFork = nullptr, evJoin = nullptr;
   bool ownStream = false;
   std::mutex mu;
 
@@ -494,13 +508,22 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
 static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, size_t stride,
                               size_t imgPitch, orb_keypoint_t* d_kps, uint8_t* d_desc,
                               int capacity, int32_t* d_counts, hipStream_t s) {
+  // Stage DAG: pyramid -> { blur || FAST -> octree } -> orient+desc.  The blur
+  // may run on a side stream beside FAST + octree (ORB_EXTRACT_STREAMS=2;
+  // fork/join by events, graph-capturable).  Both are VALU-bound at batch
+  // sizes that fill the GPU, so by default they run in order on one stream
+  // (measured: no gain from the overlap at B = 512).
   const OrbPlanDesc& P = h->plan;
   const int32_t* rt = h->dRtab.as<int32_t>();
   uint8_t* arena = h->dArena.as<uint8_t>();
   const long long ap = h->arenaBytes;
-  std::vector<hipEvent_t>* ev = h->prof.begin_call();
-  if (ev) HIP_TRY(hipEventRecord((*ev)[0], s));
+  static const bool sideStream = getenv("ORB_EXTRACT_STREAMS") && atoi(getenv("ORB_EXTRACT_STREAMS")) > 1;
+  hipStream_t s2 = sideStream ? h->stream2 : s;
+  StageProfiler& pf = h->prof;
+  std::vector<hipEvent_t>* ev = pf.begin_call();
+  PROF_REC(ev, pf.t0(ev), s);
   HIP_TRY(hipMemsetAsync(h->dErr.p, 0, 16, s));
+  PROF_REC(ev, pf.b(ev, 0), s);
   for (int l = 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
     const OrbLevelDesc& sd = P.lv[l - 1];
@@ -511,24 +534,35 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                              d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
                              rt + d.rtabY + d.h, d.xmax, B, s));
   }
-  if (ev) HIP_TRY(hipEventRecord((*ev)[1], s));
+  PROF_REC(ev, pf.e(ev, 0), s);
+  if (s2 != s) {
+    HIP_TRY(hipEventRecord(h->evFork, s));
+    HIP_TRY(hipStreamWaitEvent(s2, h->evFork, 0));
+  }
+  PROF_REC(ev, pf.b(ev, 1), s2);
   HIP_TRY(orb_k_blur_levels(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                             h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, B,
-                            s));
-  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s));
+                            s2));
+  PROF_REC(ev, pf.e(ev, 1), s2);
+  if (s2 != s) HIP_TRY(hipEventRecord(h->evJoin, s2));
+  PROF_REC(ev, pf.b(ev, 2), s);
   HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                           h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
                           h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
-  if (ev) HIP_TRY(hipEventRecord((*ev)[3], s));
+  PROF_REC(ev, pf.e(ev, 2), s);
+  PROF_REC(ev, pf.b(ev, 3), s);
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                        h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
                        h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), B, s));
-  if (ev) HIP_TRY(hipEventRecord((*ev)[4], s));
+  PROF_REC(ev, pf.e(ev, 3), s);
+  if (s2 != s) HIP_TRY(hipStreamWaitEvent(s, h->evJoin, 0));
+  PROF_REC(ev, pf.b(ev, 4), s);
   HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap,
                             h->dBlur.as<uint8_t>(), h->blurBytes, &P, h->dOutKeys.as<uint32_t>(),
                             h->dOutCount.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
-  if (ev) HIP_TRY(hipEventRecord((*ev)[5], s));
+  PROF_REC(ev, pf.e(ev, 4), s);
+  PROF_REC(ev, pf.t1(ev), s);
   h->lastImg0 = d_images;
   h->lastImg0Pitch = imgPitch;
   h->lastImg0Stride = (int)stride;
@@ -579,7 +613,14 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   h->minTh = min_th_fast;
   compute_tables(h);
   hipSetDevice(device);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess) {
+    if (h->stream) hipStreamDestroy(h->stream);
+    if (h->stream2) hipStreamDestroy(h->stream2);
+    if (h->evFork) hipEventDestroy(h->evFork);
+    if (h->evJoin) hipEventDestroy(h->evJoin);
     delete h;
     return ORB_EDEVICE;
   }
@@ -612,6 +653,9 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   for (DevBuf* b : bufs) b->release();
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
+  if (h->stream2) hipStreamDestroy(h->stream2);
+  if (h->evFork) hipEventDestroy(h->evFork);
+  if (h->evJoin) hipEventDestroy(h->evJoin);
   delete h;
 }
 
@@ -964,21 +1008,26 @@ orb_status_t orb_match_projection_local_batch(
   if ((st = m->dCellIdx.ensure((size_t)n_problems * kp_stride * 4))) return st;
   if ((st = m->dTopk.ensure((size_t)n_problems * std::max(mp_stride, 1) * 16))) return st;
   if ((st = m->dNcand.ensure((size_t)n_problems * std::max(mp_stride, 1) * 4))) return st;
-  std::vector<hipEvent_t>* ev = m->prof.begin_call();
-  if (ev) HIP_TRY(hipEventRecord((*ev)[0], s));
+  StageProfiler& pf = m->prof;
+  std::vector<hipEvent_t>* ev = pf.begin_call();
+  PROF_REC(ev, pf.t0(ev), s);
+  PROF_REC(ev, pf.b(ev, 0), s);
   HIP_TRY(orb_k_grid_build(d_keys, d_nkeys, kp_stride, P.minX, P.minY, P.invW, P.invH,
                            m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), n_problems, s));
-  if (ev) HIP_TRY(hipEventRecord((*ev)[1], s));
+  PROF_REC(ev, pf.e(ev, 0), s);
+  PROF_REC(ev, pf.b(ev, 1), s);
   HIP_TRY(orb_k_proj_candidates(d_keys, d_desc, nullptr, d_locked, kp_stride, d_nkeys, d_mps, d_mp_desc,
                                 d_nmps, mp_stride, mp_stride, m->dCellStart.as<int32_t>(),
                                 m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
                                 m->dNcand.as<int32_t>(), n_problems, s));
-  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s));
+  PROF_REC(ev, pf.e(ev, 1), s);
+  PROF_REC(ev, pf.b(ev, 2), s);
   HIP_TRY(orb_k_proj_resolve(d_keys, d_desc, nullptr, d_locked, d_nkeys, kp_stride, d_mps,
                              d_mp_desc, d_nmps, mp_stride, m->dCellStart.as<int32_t>(),
                              m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
                              m->dNcand.as<int32_t>(), d_kp_match, d_nmatches, n_problems, s));
-  if (ev) HIP_TRY(hipEventRecord((*ev)[3], s));
+  PROF_REC(ev, pf.e(ev, 2), s);
+  PROF_REC(ev, pf.t1(ev), s);
   return ORB_OK;
 }
 
