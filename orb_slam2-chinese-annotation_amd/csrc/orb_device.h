@@ -215,20 +215,22 @@ __device__ __forceinline__ ulonglong4 load_desc(const uint8_t* p) {
 // ------------------------------------------------------ wave primitives
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
+// each 16-lane row, then row_bcast 15 and 31 across rows): six VALU ops, no
+// LDS round trips.  All 64 lanes must be active.
 __device__ __forceinline__ int wave_incl_scan(int v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o, 64);
-    if (l >= o) v += t;
-  }
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
   return v;
 }
 
+// Sum over the 64 lanes, returned (wave-uniform) in every lane.
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return __builtin_amdgcn_readlane(wave_incl_scan(v), 63);
 }
 
 // Block-wide exclusive scan of one value per thread; returns the exclusive
