@@ -899,6 +899,7 @@ __global__ __launch_bounds__(512) void k_octree(
 // levels flattened into one launch); the 70x22 source tile with reflect-101
 // borders is staged in LDS, the row pass is kept as exact u16 sums.
 __constant__ int8_t c_pattern[2 * ORB_PATTERN_POINTS];
+#define ORB_PATCH_DW 12  // LDS row pitch (dwords) of the staged 37 x 37 descriptor patch
 __constant__ int c_umax[16];
 // IC_Angle byte masks: row v+15 (v in [-15, 15]), dword k of the 32 bytes at
 // columns -16..15: 0xFF where |u| <= umax[|v|] (built from umax on upload)
@@ -1137,22 +1138,46 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     a = c;
     b = s;
   }
-  // 512 samples of the blurred level around (cx, cy): byte loads through a
-  // buffer resource (32-bit offsets)
+  // 512 samples of the blurred level around (cx, cy).  The rotated pattern
+  // stays within +-18 px (max pattern radius 18.38), so the wave first stages
+  // the 37 x 37 patch into LDS with row-contiguous loads (11 aligned dwords
+  // per row, shared by the whole wave), then gathers bytes from LDS: scattered
+  // byte loads from global memory cost one L1 tag lookup per distinct line.
+  __shared__ __attribute__((aligned(16))) uint32_t patch[4][37][ORB_PATCH_DW];
   const int bp = L.blurPitch;
   const __amdgpu_buffer_rsrc_t rb =
       make_rsrc(blur + (long long)img * blurPitch + L.blurOff, (uint32_t)(L.h * bp));
-  const int cofs = cy * bp + cx;
+  const int colA = cx - 18, psh = colA & 3;  // wave-uniform alignment of the patch
+  {
+    const uint32_t base = (uint32_t)((cy - 18) * bp + (colA & ~3));
+    uint32_t pv[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int i = min(lane + 64 * q, 37 * 11 - 1);
+      const int r = i / 11, k = i - r * 11;
+      pv[q] = buf_ld32(rb, base + (uint32_t)(r * bp + 4 * k));
+    }
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int i = lane + 64 * q;
+      if (i < 37 * 11) {
+        const int r = i / 11, k = i - r * 11;
+        patch[w][r][k] = pv[q];
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint8_t* pb = reinterpret_cast<const uint8_t*>(&patch[w][0][0]) + 18 * (ORB_PATCH_DW * 4) + 18 + psh;
   int v0[4], v1[4];
 #pragma unroll
   for (int kq = 0; kq < 4; ++kq) {
     const int test = lane + 64 * kq;
     const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
     const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
-    const int o0 = cofs + cv_round(px0 * b + py0 * a) * bp + cv_round(px0 * a - py0 * b);
-    const int o1 = cofs + cv_round(px1 * b + py1 * a) * bp + cv_round(px1 * a - py1 * b);
-    v0[kq] = __builtin_amdgcn_raw_buffer_load_b8(rb, o0, 0, 0);
-    v1[kq] = __builtin_amdgcn_raw_buffer_load_b8(rb, o1, 0, 0);
+    v0[kq] = pb[cv_round(px0 * b + py0 * a) * (ORB_PATCH_DW * 4) + cv_round(px0 * a - py0 * b)];
+    v1[kq] = pb[cv_round(px1 * b + py1 * a) * (ORB_PATCH_DW * 4) + cv_round(px1 * a - py1 * b)];
   }
   unsigned long long words[4];
 #pragma unroll
