@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""Secondary measurements for BASELINE.json's other configs (C1, C2, C3, C5).
+
+bench.py is the driver contract and measures the headline C4 workload; this
+script reports the remaining configs, one JSON line each, for BASELINE.md's
+results table:
+
+  C1  CPU oracle only: 1241x376, 1000 features, 100-frame synthetic sequence,
+      extraction; 1 thread and all host cores (frames/s)
+  C2  640x480, 1000 features, GPU extraction only (frames/s) + bit-exact check
+  C3  1241x376 stereo pairs, 2000 features per image, both extractions +
+      ComputeStereoMatches on the GPU (pairs/s) + bit-exact check
+  C5  1920x1080, 4000 features, SearchByProjection against a 50,000-point
+      local map (th 1, nnratio 0.8), 16 problems per launch (problems/s for
+      extract+match, and the matcher alone with its HBM roofline)
+
+Usage: python tools/bench_configs.py [--configs C1,C2,C3,C5] [--steps K]
+The oracle (CPU restatement) is used only for the CPU rows and parity checks.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "oracle"), str(ROOT / "tests")]
+
+import bench  # noqa: E402
+
+SEED = 0x4B495454
+
+
+def timed(fn, steps, warmup, torch):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def cpu_rate(fn, items, seconds, threads=1):
+    """items/s of fn(i) over a bounded sample, on `threads` host threads (the
+    oracle's ctypes calls release the GIL)."""
+    done = [0]
+    lock = threading.Lock()
+    stop = time.perf_counter() + seconds
+
+    def worker(t):
+        i = t
+        while time.perf_counter() < stop:
+            fn(i % items)
+            with lock:
+                done[0] += 1
+            i += threads
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    return done[0] / (time.perf_counter() - t0)
+
+
+def c1(args, orb, oracle):
+    W, H = 1241, 376
+    imgs = [oracle.synth_image(SEED, f, W, H) for f in range(100)]
+    one = cpu_rate(lambda i: oracle.extract(imgs[i], 1000), 100, args.cpu_seconds, 1)
+    nthr = int(os.environ.get("OMP_NUM_THREADS", 0)) or os.cpu_count() or 1  # the box grants 16
+    allc = cpu_rate(lambda i: oracle.extract(imgs[i], 1000), 100, args.cpu_seconds, nthr)
+    return {"config": "C1", "workload": "1241x376 synthetic 100-frame sequence, 1000 feat, CPU "
+            "oracle ORBextractor only", "unit": "frames/s", "cpu_1_thread": one,
+            "cpu_all_cores": allc, "cores": nthr, "ms_per_frame_1_thread": 1e3 / one}
+
+
+def c2(args, orb, oracle, torch):
+    W, H, B = 640, 480, args.batch
+    imgs = np.stack([orb.synth_image(1 + (f % 3), 0 if f < 3 else f, W, H) for f in range(B)])
+    ext = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    cap = ext.capacity(W, H)
+    d = torch.from_numpy(imgs).cuda()
+    k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    de = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
+                          n.data_ptr(), s)
+
+    sec = timed(step, args.steps, 2, torch)
+    exact = True
+    for i in range(3):  # seeds 1..3, frame 0
+        kr, dr, _ = oracle.extract(imgs[i], 1000)
+        ni = int(n[i].item())
+        kg = k[i, :ni].cpu().numpy().view(orb.KEYPOINT_DTYPE).reshape(-1)
+        exact &= ni == len(kr) and kg.tobytes() == kr.tobytes() and \
+            de[i, :ni].cpu().numpy().tobytes() == dr.tobytes()
+    cpu = cpu_rate(lambda i: oracle.extract(imgs[i], 1000), 3, args.cpu_seconds, 1)
+    return {"config": "C2", "workload": f"640x480 synthetic, 1000 feat, GPU extraction, batch {B}",
+            "unit": "frames/s", "value": B / sec, "ms_per_step": sec * 1e3,
+            "bit_exact_seeds_1_3": bool(exact), "cpu_1_thread": cpu}
+
+
+def c3(args, orb, oracle, torch):
+    import scenarios
+
+    W, H, P, NF = 1241, 376, args.batch // 2, 2000
+    L = orb.ORBextractor(NF, 1.2, 8, 20, 7)
+    R = orb.ORBextractor(NF, 1.2, 8, 20, 7)
+    cap = L.capacity(W, H)
+    il = np.stack([orb.synth_image(SEED + p, 0, W, H, 0) for p in range(P)])
+    ir = np.stack([orb.synth_image(SEED + p, 0, W, H, 1) for p in range(P)])
+    dl, dr = torch.from_numpy(il).cuda(), torch.from_numpy(ir).cuda()
+    out = {}
+    for name in ("l", "r"):
+        out[name] = (torch.zeros((P, cap, 7), dtype=torch.int32, device="cuda"),
+                     torch.zeros((P, cap, 32), dtype=torch.uint8, device="cuda"),
+                     torch.zeros(P, dtype=torch.int32, device="cuda"))
+    ur = torch.zeros((P, cap), dtype=torch.float32, device="cuda")
+    dp = torch.zeros((P, cap), dtype=torch.float32, device="cuda")
+    sad = torch.zeros((P, cap), dtype=torch.int32, device="cuda")
+    m = orb.ORBmatcher()
+    s = torch.cuda.current_stream().cuda_stream
+    (kl, dsl, nl), (kr, dsr, nr) = out["l"], out["r"]
+
+    def step():
+        L.extract_batch(dl.data_ptr(), P, W, H, W, W * H, kl.data_ptr(), dsl.data_ptr(), cap,
+                        nl.data_ptr(), s)
+        R.extract_batch(dr.data_ptr(), P, W, H, W, W * H, kr.data_ptr(), dsr.data_ptr(), cap,
+                        nr.data_ptr(), s)
+        m.stereo_match_batch(P, L, R, kl.data_ptr(), dsl.data_ptr(), nl.data_ptr(), kr.data_ptr(),
+                             dsr.data_ptr(), nr.data_ptr(), cap, scenarios.BF, scenarios.FX,
+                             ur.data_ptr(), dp.data_ptr(), sad.data_ptr(), s)
+
+    sec = timed(step, args.steps, 2, torch)
+    p = oracle.params(NF)
+    klh, dlh, _ = oracle.extract(il[0], NF)
+    krh, drh, _ = oracle.extract(ir[0], NF)
+    ur_ref, dp_ref = oracle.stereo_match(klh, dlh, p["scale"], krh, drh, oracle.pyramid(il[0]),
+                                         oracle.pyramid(ir[0]), p["inv_scale"], scenarios.BF,
+                                         scenarios.FX, W, H)
+    n0 = int(nl[0].item())
+    exact = n0 == len(klh) and ur[0, :n0].cpu().numpy().tobytes() == ur_ref.tobytes() and \
+        dp[0, :n0].cpu().numpy().tobytes() == dp_ref.tobytes()
+
+    def cpu_pair(i):
+        a, da, _ = oracle.extract(il[i], NF)
+        b, db, _ = oracle.extract(ir[i], NF)
+        oracle.stereo_match(a, da, p["scale"], b, db, oracle.pyramid(il[i]), oracle.pyramid(ir[i]),
+                            p["inv_scale"], scenarios.BF, scenarios.FX, W, H)
+
+    cpu = cpu_rate(cpu_pair, min(P, 4), args.cpu_seconds, 1)
+    return {"config": "C3", "workload": f"1241x376 stereo pairs, 2000 feat/img, extraction x2 + "
+            f"ComputeStereoMatches, {P} pairs per step", "unit": "pairs/s", "value": P / sec,
+            "ms_per_step": sec * 1e3, "bit_exact_pair_0": bool(exact), "cpu_1_thread": cpu}
+
+
+def c5(args, orb, oracle, torch):
+    W, H, NF, M, B = 1920, 1080, 4000, 50000, 16
+    ext = orb.ORBextractor(NF, 1.2, 8, 20, 7)
+    scale = np.float32(ext.GetScaleFactors())
+    cap = ext.capacity(W, H)
+    imgs = np.stack([orb.synth_image(5, f, W, H) for f in range(B)])
+    d = torch.from_numpy(imgs).cuda()
+    k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    de = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
+                      n.data_ptr(), s)
+    torch.cuda.synchronize()
+    kh = k.cpu().numpy().view(orb.KEYPOINT_DTYPE).reshape(B, cap)
+    dh, nh = de.cpu().numpy(), n.cpu().numpy()
+    mps = np.zeros((B, M), orb.MP_TRACK_DTYPE)
+    mpd = np.zeros((B, M, 32), np.uint8)
+    lk = np.zeros((B, cap), np.uint8)
+    for i in range(B):
+        a, b_, c_ = orb.synth_local_map(5 + i, kh[i, :nh[i]], dh[i, :nh[i]], M, W, H)
+        mps[i], mpd[i], lk[i, :nh[i]] = a, b_, c_
+    d_mps = torch.from_numpy(mps.view(np.uint8).reshape(B, -1)).cuda()
+    d_mpd = torch.from_numpy(mpd).cuda()
+    d_lk = torch.from_numpy(lk).cuda()
+    d_nm = torch.full((B,), M, dtype=torch.int32, device="cuda")
+    d_km = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
+    d_nmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
+    mt = orb.ORBmatcher(0.8)
+
+    def match():
+        mt.search_by_projection_batch(B, k.data_ptr(), de.data_ptr(), n.data_ptr(), d_lk.data_ptr(),
+                                      cap, d_mps.data_ptr(), d_mpd.data_ptr(), d_nm.data_ptr(), M,
+                                      W, H, scale, 1.0, d_km.data_ptr(), d_nmatch.data_ptr(), s)
+
+    def step():
+        ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
+                          n.data_ptr(), s)
+        match()
+
+    sec = timed(step, args.steps, 2, torch)
+    msec = timed(match, args.steps, 2, torch)
+    n_kp = float(n.float().mean().item())
+    b_lm = 60 * M + 48 * n_kp + 24576  # SURVEY §8(d) B_lm
+    n0 = int(nh[0])
+    nr, kmr = oracle.match_projection_local(kh[0, :n0], dh[0, :n0], scale, W, H, mps[0], mpd[0],
+                                            1.0, 0.8, lk[0, :n0])
+    exact = int(d_nmatch[0].item()) == nr and np.array_equal(d_km[0, :n0].cpu().numpy(), kmr)
+    return {"config": "C5", "workload": "1920x1080, 4000 feat, SearchByProjection vs 50,000 "
+            f"map points, {B} problems per launch", "unit": "problems/s", "value": B / sec,
+            "ms_per_step": sec * 1e3, "match_only_problems_per_s": B / msec,
+            "match_only_alg_GBps": b_lm * B / msec / 1e9,
+            "match_only_frac_of_8TBps": b_lm * B / msec / 8e12,
+            "mean_keypoints": n_kp, "bit_exact_problem_0": bool(exact)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C1,C2,C3,C5")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0)
+    args = ap.parse_args()
+    import torch
+    import oracle
+
+    orb = bench.load_package()
+    for c in args.configs.split(","):
+        if c == "C1":
+            r = c1(args, orb, oracle)
+        elif c == "C2":
+            r = c2(args, orb, oracle, torch)
+        elif c == "C3":
+            r = c3(args, orb, oracle, torch)
+        elif c == "C5":
+            r = c5(args, orb, oracle, torch)
+        else:
+            raise SystemExit(f"unknown config {c}")
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
