@@ -316,23 +316,30 @@ __global__ __launch_bounds__(256) void k_fast_band(
   uint8_t* cellOf = colf + bandBytes / 7 + 8;                 // cell of each interior column
   {
     // Realigning copy: LDS dword k of row r = bytes [x0 + 4k, x0 + 4k + 4) of
-    // the row (level 0 rows can start at any byte: caller stride).  All of a
-    // thread's loads are issued before the first LDS store (one HBM round trip).
+    // the row (level 0 rows can start at any byte: caller stride), through a
+    // buffer resource (32-bit offsets) with the row split by a 32-bit
+    // multiply-high instead of a division.  All of a thread's loads are issued
+    // before the first LDS store (one HBM round trip).
     const int n = R * nD;
-    const float invN = 1.0f / (float)nD;
+    const uint32_t magic = (uint32_t)((0xFFFFFFFFull + (uint64_t)nD) / (uint64_t)nD);  // ceil(2^32/nD)
+    const int lh = plan.lv[l].h, lw = plan.lv[l].w;
+    const ImgRsrc im = img_rsrc(lvl, (uint32_t)((lh - 1) * pitch + lw));
+    const uint32_t org = (uint32_t)(bd.y0 * pitch + bd.x0) + im.sh;
     for (int i0 = 0; i0 < n; i0 += FAST_LOADS * 256) {
-      RawDw v[FAST_LOADS];
+      uint32_t lo[FAST_LOADS], hi[FAST_LOADS], sft[FAST_LOADS];
 #pragma unroll
       for (int q = 0; q < FAST_LOADS; ++q) {
-        const int i = min(i0 + q * 256 + tid, n - 1);  // branch-free loads
-        const int r = (int)(((float)i + 0.5f) * invN), k = i - r * nD;
-        const uint8_t* row = lvl + (long long)(bd.y0 + r) * pitch + bd.x0;
-        v[q] = raw_u32_any(row + 4 * k, row + C - 1);
+        const uint32_t i = (uint32_t)min(i0 + q * 256 + tid, n - 1);  // branch-free loads
+        const uint32_t r = __umulhi(i, magic), k = i - r * (uint32_t)nD;
+        const uint32_t o = org + r * (uint32_t)pitch + 4 * k;
+        sft[q] = o & 3u;
+        lo[q] = buf_ld32(im.r, o & ~3u);
+        hi[q] = buf_ld32(im.r, (o & ~3u) + 4);
       }
 #pragma unroll
       for (int q = 0; q < FAST_LOADS; ++q) {
         const int i = i0 + q * 256 + tid;
-        if (i < n) roi32[i] = v[q].get();
+        if (i < n) roi32[i] = __builtin_amdgcn_alignbyte(hi[q], lo[q], sft[q]);
       }
     }
   }
