@@ -61,7 +61,7 @@ struct OrbBandDesc {
   int16_t level, y0, y1, x0, x1, nCells;
   int32_t cellBeg;
 };
-#define ORB_BAND_BYTES 10240  // LDS budget for one band's pixels (and again for scores)
+#define ORB_BAND_BYTES 8192  // LDS budget for one band's pixels (and again for scores)
 
 // One ORB_BLUR_TW x ORB_BLUR_TH output tile of the 7x7 Gaussian pass over level `level`.
 struct OrbTileDesc {

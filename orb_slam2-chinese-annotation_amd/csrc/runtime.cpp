@@ -304,6 +304,8 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   std::vector<OrbTileDesc> tiles;
   std::vector<OrbBandDesc> bands;
   int maxBandBytes = 0;
+  static const int bandBudget =
+      getenv("ORB_BAND_BYTES") ? std::max(2048, atoi(getenv("ORB_BAND_BYTES"))) : ORB_BAND_BYTES;
   long long arena = 0, blurArena = 0;
   int keyCap = 1, maxRows = 7, maxCols = 7, maxCellsPerLevel = 1, nodeCapMax = 1, slots = 0;
   for (int l = 0; l < L; ++l) {
@@ -364,7 +366,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     }
     d.cellEnd = (int)cells.size();
     // FAST bands: runs of consecutive cells of one cell row whose union ROI
-    // fits ORB_BAND_BYTES of LDS (k_fast_band)
+    // fits the band LDS budget (k_fast_band; ORB_BAND_BYTES, env ORB_BAND_BYTES)
     for (int c = d.cellBeg; c < d.cellEnd;) {
       OrbBandDesc b;
       b.level = (int16_t)l;
@@ -376,7 +378,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
       int e = c + 1;
       while (e < d.cellEnd && cells[e].y0 == b.y0 && e - c < 64) {  // k_fast_band: <= 64 cells
         const int x1 = std::max<int>(b.x1, cells[e].x1);
-        if ((b.y1 - b.y0) * ((x1 - b.x0 + 3) & ~3) > ORB_BAND_BYTES) break;
+        if ((b.y1 - b.y0) * ((x1 - b.x0 + 3) & ~3) > bandBudget) break;
         b.x1 = (int16_t)x1;
         ++e;
       }
