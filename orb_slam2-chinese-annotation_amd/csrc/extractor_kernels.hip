@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbBandDesc* __restrict__ bands, const OrbCellDesc* __restrict__ cells,
-    uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount, int dbg) {
+    uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qCount, cCount;
   __shared__ uint32_t fbMask[2];  // cells (of this band) that fall back to minThFAST
@@ -359,7 +359,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
       for (int x = 0; x < ww; ++x) cellOf[cx0 + x] = (uint8_t)ci;
     }
   }
-  if (dbg == 1) return;
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
   const unsigned long long ltMask = (1ull << lane) - 1ull;
 
@@ -427,7 +426,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
         base += nj[j];
       }
       __syncthreads();
-      const int nq = dbg == 3 ? 0 : qCount;
+      const int nq = qCount;
       for (int j0 = 0; j0 < nq; j0 += 256) {
         const int j = j0 + tid;
         bool corner = false;
@@ -517,7 +516,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
 
   // ---- phase A: every cell at iniThFAST
   fast_pass(ti, std::false_type{});
-  if (dbg == 3 || dbg == 4) return;
   nms_pass(ti, bitsIni, false);
   __syncthreads();
   for (int ci = wave; ci < bd.nCells; ci += nw) {
@@ -529,7 +527,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
   }
   if (tid == 0) cCount = 0;
   __syncthreads();
-  if ((fbMask[0] | fbMask[1]) == 0 || dbg == 2) return;
+  if ((fbMask[0] | fbMask[1]) == 0) return;
   // ---- phase B: cells without an iniThFAST keypoint, at minThFAST, over the
   // group columns that touch one (wave 0 lists them in order with ballots)
   if (wave == 0) {
@@ -1270,9 +1268,8 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
                      2 * bitBytes + 2 * ((size_t)plan->maxBandBytes / 7 + 8) +
                      2 * ((size_t)plan->maxBandBytes / 28 + 8);
   dim3 grid(nbands, nimg), block(256);
-  static const int dbg = getenv("ORB_FAST_DBG") ? atoi(getenv("ORB_FAST_DBG")) : 0;
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, bands, cells, cellKeys, cellCount, dbg);
+                     arenaPitch, *plan, bands, cells, cellKeys, cellCount);
   return hipGetLastError();
 }
 
