@@ -30,6 +30,10 @@
  *                                  (Tracking::SearchLocalPoints src/Tracking.cc:1360-1377,
  *                                  MapPoint::PredictScale src/MapPoint.cc:435-450)
  *   orb_stereo_match_batch         device-batched ComputeStereoMatches (pairs from two extractors)
+ *   orb_search_for_initialization(_batch)  ORBmatcher::SearchForInitialization
+ *                                  src/ORBmatcher.cc:429-577
+ *   orb_distinctive_descriptors(_batch)    MapPoint::ComputeDistinctiveDescriptors
+ *                                  src/MapPoint.cc:250-326
  *
  * Error behaviour: the reference has no status codes (an empty image returns
  * silently with outputs untouched, src/ORBextractor.cc:1095-1096; a non-8UC1
@@ -325,6 +329,48 @@ orb_status_t orb_match_bow(orb_matcher_t* m, int n_kf, const uint8_t* kf_desc,
                            const uint32_t* f_node_ids, const int32_t* f_offs,
                            const uint32_t* f_feats, float nnratio, int check_orientation,
                            int32_t* f_match, int32_t* nmatches);
+
+/* ORBmatcher(nnratio, checkOri).SearchForInitialization(F1, F2, vbPrevMatched,
+ * vnMatches12, windowSize), src/ORBmatcher.cc:429-577 (called from
+ * Tracking::MonocularInitialization, src/Tracking.cc:698-701).  Level-0
+ * keypoints of f1 are matched to level-0 keypoints of f2 within windowSize of
+ * prev_matched[i] (x, y pairs); f2's grid bounds are min_x..max_y.
+ * matches12[i] = F2 index or -1; prev_matched is updated in place for matched
+ * keypoints (:571-574); *nmatches = the reference's return value.  Host buffers;
+ * both frames must have fewer than 2^19 keypoints and 4 * 4 * max(N1, N2) bytes
+ * must fit the 160 KiB LDS of one CU (N <= 10240), else ORB_ECAPACITY. */
+orb_status_t orb_search_for_initialization(orb_matcher_t* m, const orb_frame_t* f1,
+                                           const orb_frame_t* f2, float* prev_matched,
+                                           int window_size, float nnratio,
+                                           int check_orientation, int32_t* matches12,
+                                           int32_t* nmatches);
+
+/* Device-batched form: problem p uses d_keys1/d_desc1/d_prev_matched/d_matches12
+ * at offset p*kp_stride (keypoints; x2 floats, x32 bytes as applicable), counts
+ * d_n1[p], d_n2[p] <= kp_stride, shared frame bounds. */
+orb_status_t orb_search_for_initialization_batch(
+    orb_matcher_t* m, int n_problems, const orb_keypoint_t* d_keys1, const uint8_t* d_desc1,
+    const int32_t* d_n1, const orb_keypoint_t* d_keys2, const uint8_t* d_desc2,
+    const int32_t* d_n2, int kp_stride, float min_x, float max_x, float min_y, float max_y,
+    int window_size, float nnratio, int check_orientation, float* d_prev_matched,
+    int32_t* d_matches12, int32_t* d_nmatches, void* stream);
+
+/* MapPoint::ComputeDistinctiveDescriptors, src/MapPoint.cc:250-326, for n_mp
+ * points at once.  Point p's candidate descriptors are obs_desc rows
+ * obs_offs[p] .. obs_offs[p+1]-1: its observations in mObservations (map) order,
+ * bad KeyFrames left out (:279-283).  best_idx[p] = BestIdx within that list,
+ * -1 for an empty list (the reference returns without touching mDescriptor).
+ * If descriptors != NULL, row p is overwritten with the chosen descriptor
+ * (left untouched for empty lists).  Host buffers. */
+orb_status_t orb_distinctive_descriptors(orb_matcher_t* m, int n_mp, const int32_t* obs_offs,
+                                         const uint8_t* obs_desc, int32_t* best_idx,
+                                         uint8_t* descriptors);
+
+/* Device-batched form (device pointers, asynchronous on `stream`). */
+orb_status_t orb_distinctive_descriptors_batch(orb_matcher_t* m, int n_mp,
+                                               const int32_t* d_obs_offs,
+                                               const uint8_t* d_obs_desc, int32_t* d_best_idx,
+                                               uint8_t* d_descriptors, void* stream);
 
 /* ---------------------------------------------------------- synthetic input */
 

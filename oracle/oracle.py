@@ -365,3 +365,38 @@ def frustum(mps, pose, cam, width, height, cos_limit=0.5, log_scale=None, n_leve
     n = fn(len(mps), _p(mps), _p(pose), ctypes.byref(c), min_x, float(width), min_y, float(height),
            cos_limit, float(log_scale), n_levels, _p(tracks))
     return n, tracks
+
+
+def search_for_initialization(keys1, desc1, keys2, desc2, width, height, prev_matched,
+                              window_size=100, nnratio=0.9, check_ori=True, scale=None):
+    """ORBmatcher(nnratio, check_ori).SearchForInitialization(F1, F2, vbPrevMatched,
+    vnMatches12, windowSize) on the CPU (src/ORBmatcher.cc:429-577).
+
+    Returns (nmatches, matches12, prev_matched_updated)."""
+    scale = np.ones(8, np.float32) if scale is None else scale
+    f1, k1 = frame_struct(keys1, desc1, scale, width, height)
+    f2, k2 = frame_struct(keys2, desc2, scale, width, height)
+    prev = np.array(prev_matched, np.float32).reshape(len(keys1), 2).copy()
+    m12 = np.full(len(keys1), -1, np.int32)
+    fn = lib().oracle_search_for_initialization
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                   ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    n = fn(ctypes.byref(f1), ctypes.byref(f2), _p(prev), int(window_size), float(nnratio),
+           int(check_ori), _p(m12))
+    return n, m12, prev
+
+
+def distinctive_descriptors(offs, desc):
+    """MapPoint::ComputeDistinctiveDescriptors over CSR observation lists
+    (src/MapPoint.cc:250-326): BestIdx per point, -1 for an empty list."""
+    offs = np.ascontiguousarray(offs, np.int32)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    n = len(offs) - 1
+    best = np.full(max(n, 0), -1, np.int32)
+    fn = lib().oracle_distinctive_descriptors
+    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = None
+    if n > 0:
+        fn(n, _p(offs), _p(desc), _p(best))
+    return best

@@ -30,6 +30,7 @@
 // Build: oracle/Makefile (g++ -O2 -ffp-contract=off; no FMA contraction so the
 // float expressions round exactly as written).
 
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -1107,6 +1108,94 @@ static void stereo_matches(const orb_stereo_input_t* in, float* uRight, float* d
   }
 }
 
+// f1: ORBmatcher::SearchForInitialization, src/ORBmatcher.cc:429-577.
+// prev is vbPrevMatched as (x, y) pairs, updated in place; m12 = vnMatches12.
+static int search_for_initialization(const orb_frame_t* F1, const orb_frame_t* F2, float* prev,
+                                     int windowSize, float nnratio, int checkOri, int32_t* m12) {
+  static Grid g;
+  assign_grid(g, F2->keys, F2->n, F2->min_x, F2->max_x, F2->min_y, F2->max_y);
+  const int N1 = F1->n, N2 = F2->n;
+  int nmatches = 0;
+  for (int i = 0; i < N1; ++i) m12[i] = -1;
+  std::vector<int> rotHist[30];
+  std::vector<int> matchedDist(N2, INT_MAX), m21(N2, -1);
+  std::vector<size_t> cand;
+  for (int i1 = 0; i1 < N1; ++i1) {
+    const int level1 = F1->keys[i1].octave;
+    if (level1 > 0) continue;                                            // :449-451
+    features_in_area(g, F2->keys, prev[2 * i1], prev[2 * i1 + 1], (float)windowSize, level1,
+                     level1, cand);                                       // :453
+    if (cand.empty()) continue;
+    const uint8_t* d1 = F1->descriptors + (size_t)i1 * 32;
+    int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+    for (size_t i2 : cand) {                                              // :463-486
+      const int dist = descriptor_distance(d1, F2->descriptors + i2 * 32);
+      if (matchedDist[i2] <= dist) continue;
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestIdx2 = (int)i2;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= 50 && (float)bestDist < (float)bestDist2 * nnratio) {  // TH_LOW, :488-492
+      if (m21[bestIdx2] >= 0) {  // steal: the earlier frame-1 point loses its match
+        m12[m21[bestIdx2]] = -1;
+        --nmatches;
+      }
+      m12[i1] = bestIdx2;
+      m21[bestIdx2] = i1;
+      matchedDist[bestIdx2] = bestDist;
+      ++nmatches;
+      if (checkOri) rotHist[rot_bin(F1->keys[i1].angle - F2->keys[bestIdx2].angle)].push_back(i1);
+    }
+  }
+  if (checkOri) {                                                         // :540-568
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, 30, ind1, ind2, ind3);
+    for (int i = 0; i < 30; ++i) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (int idx1 : rotHist[i])
+        if (m12[idx1] >= 0) {
+          m12[idx1] = -1;
+          --nmatches;
+        }
+    }
+  }
+  for (int i1 = 0; i1 < N1; ++i1)                                         // :571-574
+    if (m12[i1] >= 0) {
+      prev[2 * i1] = F2->keys[m12[i1]].x;
+      prev[2 * i1 + 1] = F2->keys[m12[i1]].y;
+    }
+  return nmatches;
+}
+
+// f2: MapPoint::ComputeDistinctiveDescriptors, src/MapPoint.cc:250-326, for one
+// point whose usable observation descriptors (observations in map order, bad
+// KeyFrames dropped) are desc[0..n).  Returns BestIdx, or -1 when n == 0 (the
+// reference returns without touching mDescriptor).
+static int distinctive_descriptor(const uint8_t* desc, int n) {
+  if (n <= 0) return -1;
+  std::vector<int> D((size_t)n * n, 0);
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j)
+      D[(size_t)i * n + j] = D[(size_t)j * n + i] =
+          descriptor_distance(desc + (size_t)i * 32, desc + (size_t)j * 32);
+  int bestMedian = INT_MAX, bestIdx = 0;
+  std::vector<int> row(n);
+  for (int i = 0; i < n; ++i) {
+    row.assign(D.begin() + (size_t)i * n, D.begin() + (size_t)(i + 1) * n);
+    std::sort(row.begin(), row.end());
+    const int median = row[(size_t)(0.5 * (n - 1))];
+    if (median < bestMedian) {
+      bestMedian = median;
+      bestIdx = i;
+    }
+  }
+  return bestIdx;
+}
+
 }  // namespace oracle
 
 // ===================================================================== C API
@@ -1270,6 +1359,20 @@ int oracle_match_bow(int n_kf, const uint8_t* kf_desc, const float* kf_angle,
   return search_by_bow(n_kf, kf_desc, kf_angle, kf_mp, kf_mp_bad, kf_nodes, kf_node_ids,
                        kf_offs, kf_feats, n_f, f_desc, f_angle, f_nodes, f_node_ids, f_offs,
                        f_feats, nnratio, check_orientation, f_match);
+}
+
+int oracle_search_for_initialization(const orb_frame_t* F1, const orb_frame_t* F2, float* prev,
+                                     int window_size, float nnratio, int check_orientation,
+                                     int32_t* matches12) {
+  return search_for_initialization(F1, F2, prev, window_size, nnratio, check_orientation,
+                                   matches12);
+}
+
+// best[p] = BestIdx of point p over desc[offs[p]..offs[p+1]) (-1 when empty)
+void oracle_distinctive_descriptors(int n_mp, const int32_t* offs, const uint8_t* desc,
+                                    int32_t* best) {
+  for (int p = 0; p < n_mp; ++p)
+    best[p] = distinctive_descriptor(desc + (size_t)offs[p] * 32, offs[p + 1] - offs[p]);
 }
 
 int oracle_stereo_match(const orb_stereo_input_t* in, float* u_right, float* depth) {

@@ -131,6 +131,12 @@ def lib() -> ctypes.CDLL:
         "orb_frustum": (i32, [vp, i32, vp, vp, vp, f32, f32, f32, f32, f32, f32, i32, vp, vp]),
         "orb_frustum_batch": (i32, [vp, i32, vp, vp, i32, vp, vp, f32, f32, f32, f32, f32, f32,
                                     i32, vp, vp, vp]),
+        "orb_search_for_initialization": (i32, [vp, vp, vp, vp, i32, f32, i32, vp, vp]),
+        "orb_search_for_initialization_batch": (
+            i32, [vp, i32, vp, vp, vp, vp, vp, vp, i32, f32, f32, f32, f32, i32, f32, i32, vp, vp,
+                  vp, vp]),
+        "orb_distinctive_descriptors": (i32, [vp, i32, vp, vp, vp, vp]),
+        "orb_distinctive_descriptors_batch": (i32, [vp, i32, vp, vp, vp, vp, vp]),
         "orb_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
         "orb_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     }
@@ -546,3 +552,53 @@ class ORBmatcher:
             len(ffv[0]), _ptr(ffv[0]), _ptr(ffv[1]), _ptr(ffv[2]), self.mfNNratio,
             int(self.mbCheckOrientation), _ptr(fm), ctypes.byref(nm)), "SearchByBoW")
         return nm.value, fm
+
+    # ------------------------------------------------- SearchForInitialization
+    def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched, windowSize: int = 10):
+        """SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+        (src/ORBmatcher.cc:429-577): returns (nmatches, vnMatches12, vbPrevMatched
+        updated).  vbPrevMatched: (N1, 2) float32 points."""
+        prev = np.array(vbPrevMatched, np.float32).reshape(F1.N, 2).copy()
+        m12 = np.full(F1.N, -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f1, f2 = F1._c(), F2._c()
+        _check(lib().orb_search_for_initialization(
+            self._h, ctypes.byref(f1), ctypes.byref(f2), _ptr(prev) if F1.N else None,
+            int(windowSize), self.mfNNratio, int(self.mbCheckOrientation),
+            _ptr(m12) if F1.N else None, ctypes.byref(nm)), "SearchForInitialization")
+        return nm.value, m12, prev
+
+    def search_for_initialization_batch(self, n_problems, d_keys1, d_desc1, d_n1, d_keys2,
+                                        d_desc2, d_n2, kp_stride, min_x, max_x, min_y, max_y,
+                                        windowSize, d_prev, d_matches12, d_nmatches,
+                                        stream: int = 0):
+        _check(lib().orb_search_for_initialization_batch(
+            self._h, n_problems, d_keys1, d_desc1, d_n1, d_keys2, d_desc2, d_n2, kp_stride,
+            min_x, max_x, min_y, max_y, int(windowSize), self.mfNNratio,
+            int(self.mbCheckOrientation), d_prev, d_matches12, d_nmatches, stream or None),
+            "search_for_initialization_batch")
+
+    # ------------------------------------------ MapPoint::ComputeDistinctiveDescriptors
+    def ComputeDistinctiveDescriptors(self, obs_offs, obs_desc, descriptors=None):
+        """MapPoint::ComputeDistinctiveDescriptors for many points (src/MapPoint.cc:250-326).
+        obs_offs (n_mp + 1) CSR offsets into obs_desc rows (observations in map
+        order, bad KeyFrames dropped).  Returns (best_idx, descriptors): best_idx
+        -1 for empty lists, whose descriptor rows keep their input value."""
+        offs = np.ascontiguousarray(obs_offs, np.int32)
+        od = np.ascontiguousarray(obs_desc, np.uint8).reshape(-1, 32)
+        n = len(offs) - 1
+        best = np.full(max(n, 0), -1, np.int32)
+        out = (np.zeros((max(n, 0), 32), np.uint8) if descriptors is None
+               else np.array(descriptors, np.uint8).reshape(n, 32))
+        if n <= 0:
+            return best, out
+        _check(lib().orb_distinctive_descriptors(
+            self._h, n, _ptr(offs), _ptr(od) if len(od) else None, _ptr(best), _ptr(out)),
+            "ComputeDistinctiveDescriptors")
+        return best, out
+
+    def distinctive_descriptors_batch(self, n_mp, d_offs, d_desc, d_best, d_out=None,
+                                      stream: int = 0):
+        _check(lib().orb_distinctive_descriptors_batch(self._h, n_mp, d_offs, d_desc, d_best,
+                                                       d_out, stream or None),
+               "distinctive_descriptors_batch")

@@ -88,6 +88,18 @@ hipError_t orb_k_bow(const uint8_t* kfDesc, const float* kfAngle, const int32_t*
                      const uint32_t* fNodeIds, const int32_t* fOffs, const uint32_t* fFeats,
                      int nF, float nnratio, int checkOri, int32_t* fMatch, int32_t* accF,
                      int32_t* nmatches, hipStream_t s);
+size_t orb_k_init_params_size(void);
+size_t orb_k_init_list_len(void);
+size_t orb_k_init_topk(void);
+size_t orb_k_init_lds(int kpStride);
+hipError_t orb_k_search_init(const orb_keypoint_t* keys1, const uint8_t* desc1, const int32_t* n1,
+                             const orb_keypoint_t* keys2, const uint8_t* desc2, const int32_t* n2,
+                             int kpStride, float* prev, const int32_t* cellStart,
+                             const int32_t* cellIdx, const void* params, uint32_t* topk,
+                             uint32_t* list, int32_t* ncand, int32_t* m12, int32_t* nmatches,
+                             int nproblems, hipStream_t s);
+hipError_t orb_k_distinctive(const int32_t* offs, const uint8_t* desc, int nmp, int32_t* best,
+                             uint8_t* out, hipStream_t s);
 }
 
 namespace {
@@ -888,6 +900,12 @@ struct FrameProjParamsHost {  // mirrors FrameProjParams
   float scale[ORB_MAX_LEVELS];
 };
 
+struct InitParamsHost {  // mirrors InitParams in mapping_kernels.hip
+  float minX, minY, invW, invH;
+  float r, nnratio;
+  int checkOri;
+};
+
 struct orb_matcher {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -901,6 +919,8 @@ struct orb_matcher {
       dBowF, dBowG, dBowH, dBowI, dBowJ, dBowK;
   // frustum scratch
   DevBuf dMapPts, dPose, dTracks, dNInView;
+  // SearchForInitialization / ComputeDistinctiveDescriptors scratch
+  DevBuf dK1, dD1, dK2, dD2, dN1, dN2, dPrev, dList, dM12, dOffs, dObsDesc, dBest, dBestDesc;
   std::vector<uint8_t> hostScratch;
 };
 
@@ -927,7 +947,8 @@ orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
   if (orb_k_proj_params_size() != sizeof(ProjParamsHost) ||
       orb_k_stereo_params_size() != sizeof(StereoParamsHost) ||
       orb_k_frame_params_size() != sizeof(FrameProjParamsHost) ||
-      orb_k_frustum_params_size() != sizeof(FrustumParamsHost))
+      orb_k_frustum_params_size() != sizeof(FrustumParamsHost) ||
+      orb_k_init_params_size() != sizeof(InitParamsHost))
     return ORB_EINVAL;
   orb_matcher* m = new orb_matcher();
   m->device = device;
@@ -954,7 +975,10 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut,
                     &m->dRKeys, &m->dRDesc, &m->dNR, &m->dPyr, &m->dPairLv, &m->dDepth,
                     &m->dSad, &m->dBowA, &m->dBowB, &m->dBowC, &m->dBowD, &m->dBowE,
-                    &m->dBowF, &m->dBowG, &m->dBowH, &m->dBowI, &m->dBowJ, &m->dBowK};
+                    &m->dBowF, &m->dBowG, &m->dBowH, &m->dBowI, &m->dBowJ, &m->dBowK,
+                    &m->dMapPts, &m->dPose, &m->dTracks, &m->dNInView, &m->dK1, &m->dD1,
+                    &m->dK2, &m->dD2, &m->dN1, &m->dN2, &m->dPrev, &m->dList, &m->dM12,
+                    &m->dOffs, &m->dObsDesc, &m->dBest, &m->dBestDesc};
   for (DevBuf* b : bufs) b->release();
   m->prof.destroy();
   hipStreamDestroy(m->stream);
@@ -1419,6 +1443,149 @@ orb_status_t orb_match_bow(orb_matcher_t* m, int n_kf, const uint8_t* kf_desc,
   HIP_TRY(hipMemcpyAsync(f_match, m->dKpMatch.p, (size_t)n_f * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+// ------------------------------------------------- SearchForInitialization
+static orb_status_t search_init_device(orb_matcher_t* m, int P, const orb_keypoint_t* d_keys1,
+                                       const uint8_t* d_desc1, const int32_t* d_n1,
+                                       const orb_keypoint_t* d_keys2, const uint8_t* d_desc2,
+                                       const int32_t* d_n2, int kp_stride, float min_x,
+                                       float max_x, float min_y, float max_y, int window_size,
+                                       float nnratio, int check_orientation, float* d_prev,
+                                       int32_t* d_m12, int32_t* d_nmatches, hipStream_t s) {
+  InitParamsHost ip;
+  memset(&ip, 0, sizeof(ip));
+  ip.minX = min_x;
+  ip.minY = min_y;
+  ip.invW = (float)ORB_GRID_COLS / (max_x - min_x);  // src/Frame.cc:240-241
+  ip.invH = (float)ORB_GRID_ROWS / (max_y - min_y);
+  ip.r = (float)window_size;
+  ip.nnratio = nnratio;
+  ip.checkOri = check_orientation ? 1 : 0;
+  const size_t slots = (size_t)P * kp_stride;
+  orb_status_t st;
+  if ((st = m->dCellStart.ensure((size_t)P * (ORB_GRID_COLS * ORB_GRID_ROWS + 1) * 4))) return st;
+  if ((st = m->dCellIdx.ensure(slots * 4))) return st;
+  if ((st = m->dTopk.ensure(slots * orb_k_init_topk() * 4))) return st;
+  if ((st = m->dList.ensure(slots * orb_k_init_list_len() * 4))) return st;
+  if ((st = m->dNcand.ensure(slots * 4))) return st;
+  HIP_TRY(orb_k_grid_build(d_keys2, d_n2, kp_stride, ip.minX, ip.minY, ip.invW, ip.invH,
+                           m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), P, s));
+  HIP_TRY(orb_k_search_init(d_keys1, d_desc1, d_n1, d_keys2, d_desc2, d_n2, kp_stride, d_prev,
+                            m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &ip,
+                            m->dTopk.as<uint32_t>(), m->dList.as<uint32_t>(),
+                            m->dNcand.as<int32_t>(), d_m12, d_nmatches, P, s));
+  return ORB_OK;
+}
+
+static bool init_stride_ok(int kp_stride) {
+  return kp_stride > 0 && kp_stride < (1 << 19) && orb_k_init_lds(kp_stride) <= 160 * 1024;
+}
+
+orb_status_t orb_search_for_initialization(orb_matcher_t* m, const orb_frame_t* f1,
+                                           const orb_frame_t* f2, float* prev_matched,
+                                           int window_size, float nnratio,
+                                           int check_orientation, int32_t* matches12,
+                                           int32_t* nmatches) {
+  if (!m || !f1 || !f2 || !nmatches || f1->n < 0 || f2->n < 0 ||
+      (f1->n > 0 && (!f1->keys || !f1->descriptors || !prev_matched || !matches12)) ||
+      (f2->n > 0 && (!f2->keys || !f2->descriptors)) || !(f2->max_x > f2->min_x) ||
+      !(f2->max_y > f2->min_y))
+    return ORB_EINVAL;
+  *nmatches = 0;
+  const int N1 = f1->n, N2 = f2->n;
+  for (int i = 0; i < N1; ++i) matches12[i] = -1;
+  if (N1 == 0 || N2 == 0) return ORB_OK;
+  const int stride = std::max(N1, N2);
+  if (!init_stride_ok(stride)) return ORB_ECAPACITY;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  orb_status_t st;
+  if ((st = upload(m->dK1, f1->keys, (size_t)N1 * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(m->dD1, f1->descriptors, (size_t)N1 * 32, s))) return st;
+  if ((st = upload(m->dK2, f2->keys, (size_t)N2 * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(m->dD2, f2->descriptors, (size_t)N2 * 32, s))) return st;
+  if ((st = upload(m->dPrev, prev_matched, (size_t)N1 * 8, s))) return st;
+  const int32_t ns[2] = {N1, N2};
+  if ((st = upload(m->dN1, ns, 8, s))) return st;
+  if ((st = m->dM12.ensure((size_t)stride * 4))) return st;
+  if ((st = m->dNMatch.ensure(16))) return st;
+  if ((st = search_init_device(m, 1, m->dK1.as<orb_keypoint_t>(), m->dD1.as<uint8_t>(),
+                               m->dN1.as<int32_t>(), m->dK2.as<orb_keypoint_t>(),
+                               m->dD2.as<uint8_t>(), m->dN1.as<int32_t>() + 1, stride, f2->min_x,
+                               f2->max_x, f2->min_y, f2->max_y, window_size, nnratio,
+                               check_orientation, m->dPrev.as<float>(), m->dM12.as<int32_t>(),
+                               m->dNMatch.as<int32_t>(), s)))
+    return st;
+  HIP_TRY(hipMemcpyAsync(matches12, m->dM12.p, (size_t)N1 * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(prev_matched, m->dPrev.p, (size_t)N1 * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_search_for_initialization_batch(
+    orb_matcher_t* m, int n_problems, const orb_keypoint_t* d_keys1, const uint8_t* d_desc1,
+    const int32_t* d_n1, const orb_keypoint_t* d_keys2, const uint8_t* d_desc2,
+    const int32_t* d_n2, int kp_stride, float min_x, float max_x, float min_y, float max_y,
+    int window_size, float nnratio, int check_orientation, float* d_prev_matched,
+    int32_t* d_matches12, int32_t* d_nmatches, void* stream) {
+  if (!m || n_problems < 0 || !(max_x > min_x) || !(max_y > min_y)) return ORB_EINVAL;
+  if (n_problems == 0) return ORB_OK;
+  if (!d_keys1 || !d_desc1 || !d_n1 || !d_keys2 || !d_desc2 || !d_n2 || !d_prev_matched ||
+      !d_matches12 || !d_nmatches || n_problems > 65535)
+    return ORB_EINVAL;
+  if (!init_stride_ok(kp_stride)) return kp_stride <= 0 ? ORB_EINVAL : ORB_ECAPACITY;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  return search_init_device(m, n_problems, d_keys1, d_desc1, d_n1, d_keys2, d_desc2, d_n2,
+                            kp_stride, min_x, max_x, min_y, max_y, window_size, nnratio,
+                            check_orientation, d_prev_matched, d_matches12, d_nmatches, s);
+}
+
+// ------------------------------------------ ComputeDistinctiveDescriptors
+orb_status_t orb_distinctive_descriptors(orb_matcher_t* m, int n_mp, const int32_t* obs_offs,
+                                         const uint8_t* obs_desc, int32_t* best_idx,
+                                         uint8_t* descriptors) {
+  if (!m || n_mp < 0 || (n_mp > 0 && (!obs_offs || !best_idx))) return ORB_EINVAL;
+  if (n_mp == 0) return ORB_OK;
+  if (obs_offs[0] != 0) return ORB_EINVAL;
+  for (int i = 0; i < n_mp; ++i)
+    if (obs_offs[i + 1] < obs_offs[i]) return ORB_EINVAL;
+  const size_t nobs = (size_t)obs_offs[n_mp];
+  if (nobs > 0 && !obs_desc) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  orb_status_t st;
+  if ((st = upload(m->dOffs, obs_offs, (size_t)(n_mp + 1) * 4, s))) return st;
+  if ((st = upload(m->dObsDesc, obs_desc, nobs * 32, s))) return st;
+  if ((st = m->dBest.ensure((size_t)n_mp * 4))) return st;
+  if (descriptors && (st = upload(m->dBestDesc, descriptors, (size_t)n_mp * 32, s))) return st;
+  HIP_TRY(orb_k_distinctive(m->dOffs.as<int32_t>(), m->dObsDesc.as<uint8_t>(), n_mp,
+                            m->dBest.as<int32_t>(),
+                            descriptors ? m->dBestDesc.as<uint8_t>() : nullptr, s));
+  HIP_TRY(hipMemcpyAsync(best_idx, m->dBest.p, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s));
+  if (descriptors)
+    HIP_TRY(hipMemcpyAsync(descriptors, m->dBestDesc.p, (size_t)n_mp * 32, hipMemcpyDeviceToHost,
+                           s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_distinctive_descriptors_batch(orb_matcher_t* m, int n_mp,
+                                               const int32_t* d_obs_offs,
+                                               const uint8_t* d_obs_desc, int32_t* d_best_idx,
+                                               uint8_t* d_descriptors, void* stream) {
+  if (!m || n_mp < 0) return ORB_EINVAL;
+  if (n_mp == 0) return ORB_OK;
+  if (!d_obs_offs || !d_obs_desc || !d_best_idx) return ORB_EINVAL;
+  hipSetDevice(m->device);
+  HIP_TRY(orb_k_distinctive(d_obs_offs, d_obs_desc, n_mp, d_best_idx, d_descriptors,
+                            stream ? (hipStream_t)stream : m->stream));
   return ORB_OK;
 }
 

@@ -361,3 +361,94 @@ def frustum(mps, rcw, tcw, ow, cam, width, height, cos_limit, log_scale, n_level
         level = np.where(q < 0, 0, np.where(q >= n_levels, n_levels - 1,
                                             np.nan_to_num(q).astype(np.int64)))
     return ok, u, v, u - bf * invz, view_cos, level
+
+
+def _rot_bin(a1, a2):
+    # ORBmatcher's histogram bin with factor 1/HISTO_LENGTH (src/ORBmatcher.cc:516-524)
+    rot = f32(f32(a1) - f32(a2))
+    if rot < 0.0:
+        rot = f32(rot + f32(360.0))
+    v = f32(rot * f32(f32(1.0) / f32(30)))
+    b = int(math.floor(float(v) + 0.5))
+    return 0 if b == 30 else b
+
+
+def _three_maxima(counts):
+    m1 = m2 = m3 = 0
+    i1 = i2 = i3 = -1
+    for i, s in enumerate(counts):
+        if s > m1:
+            m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, i
+        elif s > m2:
+            m3, m2, i3, i2 = m2, s, i2, i
+        elif s > m3:
+            m3, i3 = s, i
+    if m2 < f32(0.1) * f32(m1):
+        i2 = i3 = -1
+    elif m3 < f32(0.1) * f32(m1):
+        i3 = -1
+    return i1, i2, i3
+
+
+def search_for_initialization(keys1, desc1, keys2, desc2, width, height, prev, window,
+                              nnratio, check_ori):
+    """Independent restatement of ORBmatcher::SearchForInitialization
+    (src/ORBmatcher.cc:429-577) in plain Python."""
+    cells, invW, invH = grid_cells(keys2, width, height)
+    prev = np.array(prev, np.float32).reshape(len(keys1), 2).copy()
+    m12 = np.full(len(keys1), -1, np.int32)
+    mdist = [1 << 31] * len(keys2)
+    m21 = [-1] * len(keys2)
+    hist = [[] for _ in range(30)]
+    n = 0
+    for i1 in range(len(keys1)):
+        if keys1[i1]["octave"] > 0:
+            continue
+        idx = features_in_area(keys2, cells, invW, invH, prev[i1, 0], prev[i1, 1], window, 0, 0)
+        if not idx:
+            continue
+        b1, b2, bi = 1 << 31, 1 << 31, -1
+        for i2 in idx:
+            d = hamming(desc1[i1], desc2[i2])
+            if mdist[i2] <= d:
+                continue
+            if d < b1:
+                b2, b1, bi = b1, d, i2
+            elif d < b2:
+                b2 = d
+        if b1 <= 50 and f32(b1) < f32(f32(b2) * f32(nnratio)):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                n -= 1
+            m12[i1], m21[bi], mdist[bi] = bi, i1, b1
+            n += 1
+            if check_ori:
+                hist[_rot_bin(keys1[i1]["angle"], keys2[bi]["angle"])].append(i1)
+    if check_ori:
+        keep = _three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b in keep:
+                continue
+            for i1 in hist[b]:
+                if m12[i1] >= 0:
+                    m12[i1] = -1
+                    n -= 1
+    for i1 in range(len(keys1)):
+        if m12[i1] >= 0:
+            prev[i1] = (keys2[m12[i1]]["x"], keys2[m12[i1]]["y"])
+    return n, m12, prev
+
+
+def distinctive_descriptor(desc):
+    """MapPoint::ComputeDistinctiveDescriptors' BestIdx (src/MapPoint.cc:285-318)."""
+    n = len(desc)
+    if n == 0:
+        return -1
+    bits = np.unpackbits(desc, axis=1).astype(np.int32)
+    D = (bits[:, None, :] != bits[None, :, :]).sum(-1)
+    best, bi = 1 << 31, 0
+    for i in range(n):
+        med = int(np.sort(D[i])[int(0.5 * (n - 1))])
+        if med < best:
+            best, bi = med, i
+    return bi

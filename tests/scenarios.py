@@ -151,3 +151,36 @@ def local_map_3d(oracle, keys, desc, n_mp, width, height, rng_seed=0, scale_fact
     rec["tcw"] = t
     rec["ow"] = ow
     return rec, P, np.ascontiguousarray(mpd, np.uint8)
+
+
+def init_pair(oracle, seed, frame2=1, w=640, h=480, nf=2000):
+    """Tracking::MonocularInitialization's first SearchForInitialization call:
+    the initial extractor runs with 2*nFeatures (src/Tracking.cc:126),
+    vbPrevMatched starts as the initial frame's keypoint positions
+    (src/Tracking.cc:661-664; call at :698-701), windowSize 100, ORBmatcher(0.9, true)."""
+    a = oracle.synth_image(seed, 0, w, h)
+    b = oracle.synth_image(seed, frame2, w, h)
+    k1, d1, _ = oracle.extract(a, nf)
+    k2, d2, _ = oracle.extract(b, nf)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    return dict(k1=k1, d1=d1, k2=k2, d2=d2, prev=prev, w=w, h=h)
+
+
+def observation_sets(rng, n_mp, max_obs=40, flip=0.08):
+    """CSR observation descriptors for MapPoints: noisy copies of one base
+    descriptor per point (a point seen from several KeyFrames), a few empty
+    lists, a few long ones; duplicated rows create median ties."""
+    counts = rng.integers(1, max_obs + 1, n_mp)
+    counts[rng.random(n_mp) < 0.05] = 0
+    counts[rng.random(n_mp) < 0.02] = rng.integers(65, 300)
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    desc = np.zeros((int(offs[-1]), 32), np.uint8)
+    for p in range(n_mp):
+        base = rng.integers(0, 256, 32, dtype=np.uint8)
+        bits = np.unpackbits(np.tile(base, (counts[p], 1)), axis=1)
+        noise = rng.random(bits.shape) < rng.uniform(0.0, flip * 2)
+        rows = np.packbits(bits ^ noise, axis=1)
+        if counts[p] > 3 and rng.random() < 0.3:
+            rows[1] = rows[0]
+        desc[offs[p]:offs[p + 1]] = rows
+    return offs, desc
