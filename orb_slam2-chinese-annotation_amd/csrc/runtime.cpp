@@ -95,9 +95,11 @@ size_t orb_k_init_lds(int kpStride);
 hipError_t orb_k_search_init(const orb_keypoint_t* keys1, const uint8_t* desc1, const int32_t* n1,
                              const orb_keypoint_t* keys2, const uint8_t* desc2, const int32_t* n2,
                              int kpStride, float* prev, const int32_t* cellStart,
-                             const int32_t* cellIdx, const void* params, uint32_t* topk,
+                             const int32_t* cellIdx, const void* params, int32_t* qList,
+                             int32_t* qOrder, int32_t* nQ, void* stage, int32_t* nStage, uint32_t* topk,
                              uint32_t* list, int32_t* ncand, int32_t* m12, int32_t* nmatches,
                              int nproblems, hipStream_t s);
+size_t orb_k_init_key_size(void);
 hipError_t orb_k_distinctive(const int32_t* offs, const uint8_t* desc, int nmp, int32_t* best,
                              uint8_t* out, hipStream_t s);
 }
@@ -920,7 +922,8 @@ struct orb_matcher {
   // frustum scratch
   DevBuf dMapPts, dPose, dTracks, dNInView;
   // SearchForInitialization / ComputeDistinctiveDescriptors scratch
-  DevBuf dK1, dD1, dK2, dD2, dN1, dN2, dPrev, dList, dM12, dOffs, dObsDesc, dBest, dBestDesc;
+  DevBuf dK1, dD1, dK2, dD2, dN1, dN2, dPrev, dList, dM12, dOffs, dObsDesc, dBest, dBestDesc,
+      dInitQ, dInitStage, dInitCounts;
   std::vector<uint8_t> hostScratch;
 };
 
@@ -978,7 +981,8 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dBowF, &m->dBowG, &m->dBowH, &m->dBowI, &m->dBowJ, &m->dBowK,
                     &m->dMapPts, &m->dPose, &m->dTracks, &m->dNInView, &m->dK1, &m->dD1,
                     &m->dK2, &m->dD2, &m->dN1, &m->dN2, &m->dPrev, &m->dList, &m->dM12,
-                    &m->dOffs, &m->dObsDesc, &m->dBest, &m->dBestDesc};
+                    &m->dOffs, &m->dObsDesc, &m->dBest, &m->dBestDesc, &m->dInitQ,
+                    &m->dInitStage, &m->dInitCounts};
   for (DevBuf* b : bufs) b->release();
   m->prof.destroy();
   hipStreamDestroy(m->stream);
@@ -1470,10 +1474,16 @@ static orb_status_t search_init_device(orb_matcher_t* m, int P, const orb_keypoi
   if ((st = m->dTopk.ensure(slots * orb_k_init_topk() * 4))) return st;
   if ((st = m->dList.ensure(slots * orb_k_init_list_len() * 4))) return st;
   if ((st = m->dNcand.ensure(slots * 4))) return st;
+  if ((st = m->dInitQ.ensure(slots * 8))) return st;
+  if ((st = m->dInitStage.ensure(slots * orb_k_init_key_size()))) return st;
+  if ((st = m->dInitCounts.ensure((size_t)P * 8))) return st;
   HIP_TRY(orb_k_grid_build(d_keys2, d_n2, kp_stride, ip.minX, ip.minY, ip.invW, ip.invH,
                            m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), P, s));
   HIP_TRY(orb_k_search_init(d_keys1, d_desc1, d_n1, d_keys2, d_desc2, d_n2, kp_stride, d_prev,
                             m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &ip,
+                            m->dInitQ.as<int32_t>(), m->dInitQ.as<int32_t>() + slots,
+                            m->dInitCounts.as<int32_t>(),
+                            m->dInitStage.p, m->dInitCounts.as<int32_t>() + P,
                             m->dTopk.as<uint32_t>(), m->dList.as<uint32_t>(),
                             m->dNcand.as<int32_t>(), d_m12, d_nmatches, P, s));
   return ORB_OK;

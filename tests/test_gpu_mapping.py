@@ -65,6 +65,29 @@ def test_search_for_initialization_collisions(gpu, oracle):
         assert n == rn and np.array_equal(m12, rm) and p.tobytes() == rp.tobytes()
 
 
+def test_search_for_initialization_unstaged(gpu, oracle):
+    # more level-0 F2 keypoints than the LDS stage holds: global grid scan path
+    rng = np.random.default_rng(12)
+    n = 2600
+    k1 = np.zeros(n, oracle.KEYPOINT_DTYPE)
+    k2 = np.zeros(n, oracle.KEYPOINT_DTYPE)
+    for k in (k1, k2):
+        k["x"] = rng.uniform(0, 640, n)
+        k["y"] = rng.uniform(0, 480, n)
+        k["angle"] = rng.uniform(0, 360, n)
+    base = rng.integers(0, 256, (40, 32), dtype=np.uint8)
+    d1 = base[rng.integers(0, 40, n)].copy()
+    d2 = base[rng.integers(0, 40, n)].copy()
+    for d in (d1, d2):
+        bits = np.unpackbits(d, axis=1)
+        bits ^= (rng.random(bits.shape) < 0.05).astype(np.uint8)
+        d[:] = np.packbits(bits, axis=1)
+    s = dict(k1=k1, d1=d1, k2=k2, d2=d2, prev=np.stack([k1["x"], k1["y"]], 1), w=640, h=480)
+    (rn, rm, rp), (got_n, m12, p) = _init_both(gpu, oracle, s, 30, 0.9, True)
+    assert rn > 10
+    assert got_n == rn and np.array_equal(m12, rm) and p.tobytes() == rp.tobytes()
+
+
 def test_search_for_initialization_empty(gpu, oracle):
     m = gpu.ORBmatcher(0.9, True)
     s = scenarios.init_pair(oracle, 1, 1, w=640, h=480, nf=500)

@@ -13,8 +13,13 @@ results table:
   C5  1920x1080, 4000 features, SearchByProjection against a 50,000-point
       local map (th 1, nnratio 0.8), 16 problems per launch (problems/s for
       extract+match, and the matcher alone with its HBM roofline)
+  F1  SURVEY §8(f): SearchForInitialization, 640x480 frames from the 2000-feature
+      initial extractor, window 100, ORBmatcher(0.9, true), 64 pairs per launch
+      (pairs/s) + CPU oracle rate + exact check
+  F3  SURVEY §8(f): ComputeDistinctiveDescriptors over 100,000 map points with
+      1..20 observations (points/s) + CPU oracle rate + exact check
 
-Usage: python tools/bench_configs.py [--configs C1,C2,C3,C5] [--steps K]
+Usage: python tools/bench_configs.py [--configs C1,C2,C3,C5,F1,F3] [--steps K]
 The oracle (CPU restatement) is used only for the CPU rows and parity checks.
 """
 import argparse
@@ -220,6 +225,97 @@ def c5(args, orb, oracle, torch):
             "mean_keypoints": n_kp, "bit_exact_problem_0": bool(exact)}
 
 
+def f1(args, orb, oracle, torch):
+    import scenarios
+    W, H, P, U = 640, 480, 64, 16
+    pairs = [scenarios.init_pair(oracle, 100 + i, 1 + i % 3, w=W, h=H, nf=2000) for i in range(U)]
+    stride = max(max(len(s["k1"]), len(s["k2"])) for s in pairs)
+    K1 = np.zeros((P, stride), orb.KEYPOINT_DTYPE)
+    K2 = np.zeros((P, stride), orb.KEYPOINT_DTYPE)
+    D1 = np.zeros((P, stride, 32), np.uint8)
+    D2 = np.zeros((P, stride, 32), np.uint8)
+    PR = np.zeros((P, stride, 2), np.float32)
+    n1 = np.zeros(P, np.int32)
+    n2 = np.zeros(P, np.int32)
+    for i in range(P):
+        s = pairs[i % U]
+        n1[i], n2[i] = len(s["k1"]), len(s["k2"])
+        K1[i, :n1[i]], D1[i, :n1[i]], PR[i, :n1[i]] = s["k1"], s["d1"], s["prev"]
+        K2[i, :n2[i]], D2[i, :n2[i]] = s["k2"], s["d2"]
+    t = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8)).cuda()
+         for k, v in dict(K1=K1, K2=K2, D1=D1, D2=D2, n1=n1, n2=n2).items()}
+    pr0 = torch.from_numpy(PR).cuda()
+    pr = pr0.clone()
+    m12 = torch.zeros((P, stride), dtype=torch.int32, device="cuda")
+    nm = torch.zeros(P, dtype=torch.int32, device="cuda")
+    mt = orb.ORBmatcher(0.9, True)
+    # a real stream shared with torch: the prev-position reset must be ordered
+    # before the kernels (handle 0 would select the matcher's own stream)
+    ts = torch.cuda.Stream()
+    s_ = ts.cuda_stream
+
+    def step():
+        with torch.cuda.stream(ts):
+            pr.copy_(pr0)  # vbPrevMatched is in/out: restore the initial positions
+        mt.search_for_initialization_batch(P, t["K1"].data_ptr(), t["D1"].data_ptr(),
+                                           t["n1"].data_ptr(), t["K2"].data_ptr(),
+                                           t["D2"].data_ptr(), t["n2"].data_ptr(), stride, 0.0,
+                                           float(W), 0.0, float(H), 100, pr.data_ptr(),
+                                           m12.data_ptr(), nm.data_ptr(), s_)
+
+    sec = timed(step, args.steps, 2, torch)
+    exact = True
+    for i in range(U):
+        s = pairs[i]
+        rn, rm, rp = oracle.search_for_initialization(s["k1"], s["d1"], s["k2"], s["d2"], W, H,
+                                                      s["prev"], 100, 0.9, True)
+        exact &= int(nm[i].item()) == rn and np.array_equal(m12[i, :n1[i]].cpu().numpy(), rm)
+    cpu = cpu_rate(lambda i: oracle.search_for_initialization(
+        pairs[i]["k1"], pairs[i]["d1"], pairs[i]["k2"], pairs[i]["d2"], W, H, pairs[i]["prev"],
+        100, 0.9, True), U, args.cpu_seconds, 1)
+    return {"config": "F1", "workload": f"SearchForInitialization 640x480, 2000-feature initial "
+            f"extractor, window 100, {P} pairs per launch", "unit": "pairs/s", "value": P / sec,
+            "ms_per_step": sec * 1e3, "cpu_oracle_1_thread": cpu,
+            "mean_level0_keypoints": float(np.mean([(s["k1"]["octave"] == 0).sum() for s in pairs])),
+            "bit_exact": bool(exact)}
+
+
+def f3(args, orb, oracle, torch):
+    import scenarios
+    M = 100000
+    rng = np.random.default_rng(9)
+    counts = rng.integers(1, 21, M)
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    base = rng.integers(0, 256, (M, 32), dtype=np.uint8)
+    rows = np.repeat(base, counts, axis=0)
+    bits = np.unpackbits(rows, axis=1)
+    bits ^= (rng.random(bits.shape) < 0.1).astype(np.uint8)
+    desc = np.packbits(bits, axis=1)
+    d_offs = torch.from_numpy(offs).cuda()
+    d_desc = torch.from_numpy(desc).cuda()
+    d_best = torch.zeros(M, dtype=torch.int32, device="cuda")
+    d_out = torch.zeros((M, 32), dtype=torch.uint8, device="cuda")
+    mt = orb.ORBmatcher()
+    s_ = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        mt.distinctive_descriptors_batch(M, d_offs.data_ptr(), d_desc.data_ptr(),
+                                         d_best.data_ptr(), d_out.data_ptr(), s_)
+
+    sec = timed(step, args.steps, 2, torch)
+    ref = oracle.distinctive_descriptors(offs, desc)
+    exact = np.array_equal(d_best.cpu().numpy(), ref)
+    chunk = 1000
+    cpu = cpu_rate(lambda i: oracle.distinctive_descriptors(
+        offs[i * chunk:(i + 1) * chunk + 1] - offs[i * chunk],
+        desc[offs[i * chunk]:offs[(i + 1) * chunk]]), M // chunk, args.cpu_seconds, 1) * chunk
+    alg_bytes = offs[-1] * 32 + (M + 1) * 4 + M * 36
+    return {"config": "F3", "workload": "ComputeDistinctiveDescriptors, 100,000 map points, "
+            "1..20 observations each", "unit": "points/s", "value": M / sec,
+            "ms_per_step": sec * 1e3, "cpu_oracle_1_thread": cpu,
+            "alg_GBps": alg_bytes / sec / 1e9, "bit_exact": bool(exact)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="C1,C2,C3,C5")
@@ -240,6 +336,10 @@ def main():
             r = c3(args, orb, oracle, torch)
         elif c == "C5":
             r = c5(args, orb, oracle, torch)
+        elif c == "F1":
+            r = f1(args, orb, oracle, torch)
+        elif c == "F3":
+            r = f3(args, orb, oracle, torch)
         else:
             raise SystemExit(f"unknown config {c}")
         print(json.dumps(r), flush=True)
