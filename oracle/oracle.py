@@ -400,3 +400,174 @@ def distinctive_descriptors(offs, desc):
     if n > 0:
         fn(n, _p(offs), _p(desc), _p(best))
     return best
+
+
+def _fr(keys, desc, scale, width, height, u_right=None):
+    """orb_frame_t for a (Key)Frame; keeps the numpy buffers alive with it."""
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    ur = None if u_right is None else np.ascontiguousarray(u_right, np.float32)
+    f, keep = frame_struct(keys, desc, scale, width, height, ur)
+    return f, keep
+
+
+def _f32(a, n=None):
+    a = np.ascontiguousarray(a, np.float32)
+    return a if n is None else a.reshape(n)
+
+
+def search_by_projection_reloc(keys, desc, scale, width, height, pose, cam, mps, mp_desc,
+                               kf_angle, th, orb_dist, check_ori=True, kp_locked=None,
+                               log_scale=None):
+    """SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:1622-1759):
+    (nmatches, kp_match) with kp_match[j] = point index, -1 untouched, -2 reset."""
+    f, keep = _fr(keys, desc, scale, width, height)
+    pose = np.ascontiguousarray(pose, POSE_DTYPE).reshape(1)
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    mpd = np.ascontiguousarray(mp_desc, np.uint8)
+    ka = _f32(kf_angle)
+    lk = None if kp_locked is None else np.ascontiguousarray(kp_locked, np.uint8)
+    km = np.full(len(keys), -1, np.int32)
+    ls = np.float32(pinned_log(np.float32(1.2))) if log_scale is None else log_scale
+    c = _Camera(*cam)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fn = lib().oracle_search_by_projection_reloc
+    fn.argtypes = [vp, vp, vp, vp, f32, i32, vp, vp, vp, f32, i32, i32, vp]
+    fn.restype = i32
+    n = fn(ctypes.byref(f), _p(lk) if lk is not None else None, _p(pose), ctypes.byref(c), ls,
+           len(mps), _p(mps), _p(mpd), _p(ka), th, int(orb_dist), int(check_ori), _p(km))
+    return n, km
+
+
+def search_by_projection_sim3(keys, desc, scale, width, height, scw, cam, mps, mp_desc, th,
+                              kp_matched, log_scale=None):
+    """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (src/ORBmatcher.cc:311-425):
+    (nmatches, kp_matched updated)."""
+    f, keep = _fr(keys, desc, scale, width, height)
+    S = _f32(scw, 12)
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    mpd = np.ascontiguousarray(mp_desc, np.uint8)
+    km = np.array(kp_matched, np.int32).copy()
+    ls = np.float32(pinned_log(np.float32(1.2))) if log_scale is None else log_scale
+    c = _Camera(*cam)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fn = lib().oracle_search_by_projection_sim3
+    fn.argtypes = [vp, vp, vp, f32, i32, vp, vp, f32, vp]
+    fn.restype = i32
+    n = fn(ctypes.byref(f), _p(S), ctypes.byref(c), ls, len(mps), _p(mps), _p(mpd), th, _p(km))
+    return n, km
+
+
+def fuse(keys, desc, scale, inv_sigma2, width, height, u_right, pose, cam, mps, mp_desc, th,
+         log_scale=None):
+    """Fuse(pKF, vpMapPoints, th) target selection (src/ORBmatcher.cc:903-1077):
+    (n_with_target, best keypoint per point or -1)."""
+    f, keep = _fr(keys, desc, scale, width, height, u_right)
+    inv = _f32(inv_sigma2)
+    pose = np.ascontiguousarray(pose, POSE_DTYPE).reshape(1)
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    mpd = np.ascontiguousarray(mp_desc, np.uint8)
+    best = np.full(len(mps), -1, np.int32)
+    ls = np.float32(pinned_log(np.float32(1.2))) if log_scale is None else log_scale
+    c = _Camera(*cam)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fn = lib().oracle_fuse
+    fn.argtypes = [vp, vp, vp, vp, f32, i32, vp, vp, f32, vp]
+    fn.restype = i32
+    n = fn(ctypes.byref(f), _p(inv), _p(pose), ctypes.byref(c), ls, len(mps), _p(mps), _p(mpd),
+           th, _p(best))
+    return n, best
+
+
+def fuse_sim3(keys, desc, scale, width, height, scw, cam, mps, mp_desc, th, log_scale=None):
+    """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) target selection
+    (src/ORBmatcher.cc:1079-1210): (n_with_target, best keypoint per point or -1)."""
+    f, keep = _fr(keys, desc, scale, width, height)
+    S = _f32(scw, 12)
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    mpd = np.ascontiguousarray(mp_desc, np.uint8)
+    best = np.full(len(mps), -1, np.int32)
+    ls = np.float32(pinned_log(np.float32(1.2))) if log_scale is None else log_scale
+    c = _Camera(*cam)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fn = lib().oracle_fuse_sim3
+    fn.argtypes = [vp, vp, vp, f32, i32, vp, vp, f32, vp]
+    fn.restype = i32
+    n = fn(ctypes.byref(f), _p(S), ctypes.byref(c), ls, len(mps), _p(mps), _p(mpd), th,
+           _p(best))
+    return n, best
+
+
+def search_by_sim3(kf1, kf2, cam, s12, R12, t12, th, log_scale=None):
+    """SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+    (src/ORBmatcher.cc:1212-1458).  kfX = dict(keys, desc, scale, width, height,
+    Rw (3x3), tw (3), mps (MAP_POINT_DTYPE per keypoint), valid, already, mp_desc).
+    Returns (nFound, match12)."""
+    ls = np.float32(pinned_log(np.float32(1.2))) if log_scale is None else log_scale
+    f1, k1 = _fr(kf1["keys"], kf1["desc"], kf1["scale"], kf1["width"], kf1["height"])
+    f2, k2 = _fr(kf2["keys"], kf2["desc"], kf2["scale"], kf2["width"], kf2["height"])
+    arrs = []
+    for kf in (kf1, kf2):
+        arrs.append([_f32(kf["Rw"], 9), _f32(kf["tw"], 3),
+                     np.ascontiguousarray(kf["mps"], MAP_POINT_DTYPE),
+                     np.ascontiguousarray(kf["valid"], np.uint8),
+                     np.ascontiguousarray(kf["already"], np.uint8),
+                     np.ascontiguousarray(kf["mp_desc"], np.uint8)])
+    R12, t12 = _f32(R12, 9), _f32(t12, 3)
+    m12 = np.full(len(kf1["keys"]), -1, np.int32)
+    c = _Camera(*cam)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fn = lib().oracle_search_by_sim3
+    fn.argtypes = [vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp,
+                   vp, f32, vp]
+    fn.restype = i32
+    a1, a2 = arrs
+    n = fn(ctypes.byref(f1), ctypes.byref(f2), ls, ls, ctypes.byref(c), _p(a1[0]), _p(a1[1]),
+           _p(a2[0]), _p(a2[1]), _p(a1[2]), _p(a1[3]), _p(a1[4]), _p(a1[5]), _p(a2[2]),
+           _p(a2[3]), _p(a2[4]), _p(a2[5]), s12, _p(R12), _p(t12), th, _p(m12))
+    return n, m12
+
+
+def search_by_bow_kf(d1, a1, mp1, bad1, fv1, d2, a2, mp2, bad2, fv2, nnratio, check_ori):
+    """SearchByBoW(pKF1, pKF2, vpMatches12) (src/ORBmatcher.cc:581-716):
+    (nmatches, match12 = MapPoint id of KF2 or -1)."""
+    d1, d2 = np.ascontiguousarray(d1, np.uint8), np.ascontiguousarray(d2, np.uint8)
+    a1, a2 = _f32(a1), _f32(a2)
+    mp1, mp2 = np.ascontiguousarray(mp1, np.int32), np.ascontiguousarray(mp2, np.int32)
+    b1 = None if bad1 is None else np.ascontiguousarray(bad1, np.uint8)
+    b2 = None if bad2 is None else np.ascontiguousarray(bad2, np.uint8)
+    m12 = np.full(len(d1), -1, np.int32)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fn = lib().oracle_search_by_bow_kf
+    fn.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp,
+                   f32, i32, vp]
+    fn.restype = i32
+    n = fn(_p(d1), _p(a1), _p(mp1), _p(b1) if b1 is not None else None, len(d1), len(fv1[0]),
+           _p(fv1[0]), _p(fv1[1]), _p(fv1[2]), _p(d2), _p(a2), _p(mp2),
+           _p(b2) if b2 is not None else None, len(d2), len(fv2[0]), _p(fv2[0]), _p(fv2[1]),
+           _p(fv2[2]), nnratio, int(check_ori), _p(m12))
+    return n, m12
+
+
+def search_for_triangulation(kf1, kf2, level_sigma2, F12, cam, Cw, R2w, t2w, fv1, fv2,
+                             only_stereo=False, check_ori=True):
+    """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+    (src/ORBmatcher.cc:718-901): (nmatches, match12 = KF2 index or -1).
+    kfX = dict(keys, desc, scale, width, height, u_right, has_mp)."""
+    f1, k1 = _fr(kf1["keys"], kf1["desc"], kf1["scale"], kf1["width"], kf1["height"],
+                 kf1["u_right"])
+    f2, k2 = _fr(kf2["keys"], kf2["desc"], kf2["scale"], kf2["width"], kf2["height"],
+                 kf2["u_right"])
+    h1 = np.ascontiguousarray(kf1["has_mp"], np.uint8)
+    h2 = np.ascontiguousarray(kf2["has_mp"], np.uint8)
+    ls2, F, C, R, t = _f32(level_sigma2), _f32(F12, 9), _f32(Cw, 3), _f32(R2w, 9), _f32(t2w, 3)
+    m12 = np.full(len(kf1["keys"]), -1, np.int32)
+    c = _Camera(*cam)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    fn = lib().oracle_search_for_triangulation
+    fn.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32,
+                   i32, vp]
+    fn.restype = i32
+    n = fn(ctypes.byref(f1), _p(h1), ctypes.byref(f2), _p(h2), _p(ls2), _p(F), ctypes.byref(c),
+           _p(C), _p(R), _p(t), len(fv1[0]), _p(fv1[0]), _p(fv1[1]), _p(fv1[2]), len(fv2[0]),
+           _p(fv2[0]), _p(fv2[1]), _p(fv2[2]), int(only_stereo), int(check_ori), _p(m12))
+    return n, m12

@@ -1196,6 +1196,499 @@ static int distinctive_descriptor(const uint8_t* desc, int n) {
   return bestIdx;
 }
 
+// ------------------------------------------------------------------------
+// §8(f) ORBmatcher variants.  Shared pinned arithmetic (parity unpinned: no
+// reference fixture covers these; same cv::Mat pinning as frustum_one):
+//   Mat*Mat (3x3 * 3x1) + Mat: float dot products left to right, then + t
+//   scalar * Mat, Mat / scalar: (float)((double)x * alpha) with alpha double
+//   Mat::dot, cv::norm: double accumulation; norm -> sqrt(double) -> float
+//   -R^T t: float dot left to right, negated
+struct Rt {
+  float R[9], t[3], Ow[3];
+};
+
+static inline void xform(const float* R, const float* t, const float* P, float* out) {
+  for (int r = 0; r < 3; ++r)
+    out[r] = ((R[3 * r] * P[0] + R[3 * r + 1] * P[1]) + R[3 * r + 2] * P[2]) + t[r];
+}
+
+static inline void neg_rt_t(const float* R, const float* t, float* Ow) {
+  for (int i = 0; i < 3; ++i) Ow[i] = -((R[i] * t[0] + R[3 + i] * t[1]) + R[6 + i] * t[2]);
+}
+
+// Scw (3x4, row-major [sR | st]) -> Rcw = sRcw/scw, tcw = st/scw, Ow = -Rcw^T tcw
+// (src/ORBmatcher.cc:320-327, 1086-1092)
+static Rt sim3_pose(const float* S) {
+  Rt p;
+  double ss = 0.0;
+  for (int k = 0; k < 3; ++k) ss += (double)S[k] * S[k];
+  const float scw = (float)sqrt(ss);
+  const double inv = 1.0 / (double)scw;
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) p.R[3 * r + c] = (float)((double)S[4 * r + c] * inv);
+    p.t[r] = (float)((double)S[4 * r + 3] * inv);
+  }
+  neg_rt_t(p.R, p.t, p.Ow);
+  return p;
+}
+
+static inline float norm3(const float* a) {
+  double ss = 0.0;
+  for (int k = 0; k < 3; ++k) ss += (double)a[k] * a[k];
+  return (float)sqrt(ss);
+}
+
+static inline double dot3(const float* a, const float* b) {
+  double d = 0.0;
+  for (int k = 0; k < 3; ++k) d += (double)a[k] * b[k];
+  return d;
+}
+
+// MapPoint::PredictScale (src/MapPoint.cc:417-450), logf pinned
+static inline int predict_scale(float maxDistance, float dist, float logScale, int nLevels) {
+  const float ratio = maxDistance / dist;
+  const float q = ceilf((float)pinned_log((double)ratio) / logScale);
+  if (q < 0.f) return 0;
+  if (q >= (float)nLevels) return nLevels - 1;
+  return (int)q;
+}
+
+static inline bool kf_in_image(const orb_frame_t* K, float x, float y) {  // KeyFrame::IsInImage
+  return x >= K->min_x && x < K->max_x && y >= K->min_y && y < K->max_y;
+}
+
+// f4: SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist),
+// src/ORBmatcher.cc:1622-1759 (relocalisation).  Point i = the KeyFrame's map
+// point of keypoint i (seen = in sAlreadyFound); kp_match[j] = point index
+// assigned to frame keypoint j by this call, -2 reset by the rotation filter.
+static int search_by_projection_reloc(const orb_frame_t* F, const uint8_t* kp_locked,
+                                      const orb_pose_t* T, const orb_camera_t* cam,
+                                      float logScale, int n, const orb_map_point_t* mps,
+                                      const uint8_t* mpDesc, const float* kfAngle, float th,
+                                      int orbDist, int checkOri, int32_t* kp_match) {
+  static Grid g;
+  assign_grid(g, F->keys, F->n, F->min_x, F->max_x, F->min_y, F->max_y);
+  std::vector<uint8_t> locked(F->n, 0);
+  for (int j = 0; j < F->n; ++j) {
+    locked[j] = kp_locked ? kp_locked[j] : 0;
+    kp_match[j] = -1;
+  }
+  std::vector<int> rotHist[30];
+  std::vector<size_t> idxs;
+  int nmatches = 0;
+  for (int i = 0; i < n; ++i) {
+    const orb_map_point_t& mp = mps[i];
+    if (mp.bad || mp.seen) continue;
+    float Pc[3];
+    xform(T->rcw, T->tcw, mp.pos, Pc);
+    const float invzc = (float)(1.0 / (double)Pc[2]);            // no z test here (:1660)
+    const float u = cam->fx * Pc[0] * invzc + cam->cx;
+    const float v = cam->fy * Pc[1] * invzc + cam->cy;
+    if (u < F->min_x || u > F->max_x) continue;
+    if (v < F->min_y || v > F->max_y) continue;
+    const float PO[3] = {mp.pos[0] - T->ow[0], mp.pos[1] - T->ow[1], mp.pos[2] - T->ow[2]};
+    const float dist3D = norm3(PO);
+    if (dist3D < 0.8f * mp.min_distance || dist3D > 1.2f * mp.max_distance) continue;
+    const int lvl = predict_scale(mp.max_distance, dist3D, logScale, F->n_levels);
+    const float radius = th * F->scale_factors[lvl];
+    features_in_area(g, F->keys, u, v, radius, lvl - 1, lvl + 1, idxs);
+    if (idxs.empty()) continue;
+    const uint8_t* dMP = mpDesc + (size_t)i * 32;
+    int bestDist = 256, bestIdx = -1;
+    for (size_t j : idxs) {
+      if (locked[j]) continue;
+      const int d = descriptor_distance(dMP, F->descriptors + j * 32);
+      if (d < bestDist) { bestDist = d; bestIdx = (int)j; }
+    }
+    if (bestDist <= orbDist) {
+      locked[bestIdx] = 1;
+      kp_match[bestIdx] = i;
+      ++nmatches;
+      if (checkOri) rotHist[rot_bin(kfAngle[i] - F->keys[bestIdx].angle)].push_back(bestIdx);
+    }
+  }
+  if (checkOri) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, 30, ind1, ind2, ind3);
+    for (int b = 0; b < 30; ++b) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (int j : rotHist[b]) { kp_match[j] = -2; --nmatches; }
+    }
+  }
+  return nmatches;
+}
+
+// f5: SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th),
+// src/ORBmatcher.cc:311-425 (loop closing).  kp_matched[j] = index of the
+// point in vpMatched[j] or -1 (in/out); seen = in spAlreadyFound.
+static int search_by_projection_sim3(const orb_frame_t* K, const float* Scw,
+                                     const orb_camera_t* cam, float logScale, int n,
+                                     const orb_map_point_t* mps, const uint8_t* mpDesc, float th,
+                                     int32_t* kp_matched) {
+  static Grid g;
+  assign_grid(g, K->keys, K->n, K->min_x, K->max_x, K->min_y, K->max_y);
+  const Rt T = sim3_pose(Scw);
+  std::vector<size_t> idxs;
+  int nmatches = 0;
+  for (int i = 0; i < n; ++i) {
+    const orb_map_point_t& mp = mps[i];
+    if (mp.bad || mp.seen) continue;
+    float Pc[3];
+    xform(T.R, T.t, mp.pos, Pc);
+    if (Pc[2] < 0.0) continue;
+    const float invz = 1 / Pc[2];
+    const float x = Pc[0] * invz, y = Pc[1] * invz;
+    const float u = cam->fx * x + cam->cx, v = cam->fy * y + cam->cy;
+    if (!kf_in_image(K, u, v)) continue;
+    const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
+    const float PO[3] = {mp.pos[0] - T.Ow[0], mp.pos[1] - T.Ow[1], mp.pos[2] - T.Ow[2]};
+    const float dist = norm3(PO);
+    if (dist < minD || dist > maxD) continue;
+    if (dot3(PO, mp.normal) < 0.5 * dist) continue;
+    const int lvl = predict_scale(mp.max_distance, dist, logScale, K->n_levels);
+    const float radius = th * K->scale_factors[lvl];
+    features_in_area(g, K->keys, u, v, radius, -1, -1, idxs);
+    if (idxs.empty()) continue;
+    const uint8_t* dMP = mpDesc + (size_t)i * 32;
+    int bestDist = 256, bestIdx = -1;
+    for (size_t j : idxs) {
+      if (kp_matched[j] >= 0) continue;
+      const int kl = K->keys[j].octave;
+      if (kl < lvl - 1 || kl > lvl) continue;
+      const int d = descriptor_distance(dMP, K->descriptors + j * 32);
+      if (d < bestDist) { bestDist = d; bestIdx = (int)j; }
+    }
+    if (bestDist <= 50) {
+      kp_matched[bestIdx] = i;
+      ++nmatches;
+    }
+  }
+  return nmatches;
+}
+
+// f6: Fuse(KeyFrame*, vpMapPoints, th), src/ORBmatcher.cc:903-1077: the keypoint
+// each point fuses into (best[i], -1 = none), from the state at entry; the
+// Replace / AddObservation side effects stay with the caller (seen =
+// IsInKeyFrame(pKF)).  Returns the number of points with a fuse target.
+static int fuse_candidates(const orb_frame_t* K, const float* invSigma2, const orb_pose_t* T,
+                           const orb_camera_t* cam, float logScale, int n,
+                           const orb_map_point_t* mps, const uint8_t* mpDesc, float th,
+                           int32_t* best) {
+  static Grid g;
+  assign_grid(g, K->keys, K->n, K->min_x, K->max_x, K->min_y, K->max_y);
+  std::vector<size_t> idxs;
+  int nf = 0;
+  for (int i = 0; i < n; ++i) {
+    best[i] = -1;
+    const orb_map_point_t& mp = mps[i];
+    if (mp.bad || mp.seen) continue;
+    float Pc[3];
+    xform(T->rcw, T->tcw, mp.pos, Pc);
+    if (Pc[2] < 0.0f) continue;
+    const float invz = 1 / Pc[2];
+    const float x = Pc[0] * invz, y = Pc[1] * invz;
+    const float u = cam->fx * x + cam->cx, v = cam->fy * y + cam->cy;
+    if (!kf_in_image(K, u, v)) continue;
+    const float ur = u - cam->bf * invz;
+    const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
+    const float PO[3] = {mp.pos[0] - T->ow[0], mp.pos[1] - T->ow[1], mp.pos[2] - T->ow[2]};
+    const float dist3D = norm3(PO);
+    if (dist3D < minD || dist3D > maxD) continue;
+    if (dot3(PO, mp.normal) < 0.5 * dist3D) continue;
+    const int lvl = predict_scale(mp.max_distance, dist3D, logScale, K->n_levels);
+    const float radius = th * K->scale_factors[lvl];
+    features_in_area(g, K->keys, u, v, radius, -1, -1, idxs);
+    if (idxs.empty()) continue;
+    const uint8_t* dMP = mpDesc + (size_t)i * 32;
+    int bestDist = 256, bestIdx = -1;
+    for (size_t j : idxs) {
+      const KP& kp = K->keys[j];
+      const int kl = kp.octave;
+      if (kl < lvl - 1 || kl > lvl) continue;
+      if (K->u_right && K->u_right[j] >= 0) {
+        const float ex = u - kp.x, ey = v - kp.y, er = ur - K->u_right[j];
+        const float e2 = ex * ex + ey * ey + er * er;
+        if (e2 * invSigma2[kl] > 7.8) continue;
+      } else {
+        const float ex = u - kp.x, ey = v - kp.y;
+        const float e2 = ex * ex + ey * ey;
+        if (e2 * invSigma2[kl] > 5.99) continue;
+      }
+      const int d = descriptor_distance(dMP, K->descriptors + j * 32);
+      if (d < bestDist) { bestDist = d; bestIdx = (int)j; }
+    }
+    if (bestDist <= 50) {
+      best[i] = bestIdx;
+      ++nf;
+    }
+  }
+  return nf;
+}
+
+// f7: Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint), src/ORBmatcher.cc:1079-1210:
+// fuse target per point from the state at entry (seen = in spAlreadyFound).
+static int fuse_sim3_candidates(const orb_frame_t* K, const float* Scw, const orb_camera_t* cam,
+                                float logScale, int n, const orb_map_point_t* mps,
+                                const uint8_t* mpDesc, float th, int32_t* best) {
+  static Grid g;
+  assign_grid(g, K->keys, K->n, K->min_x, K->max_x, K->min_y, K->max_y);
+  const Rt T = sim3_pose(Scw);
+  std::vector<size_t> idxs;
+  int nf = 0;
+  for (int i = 0; i < n; ++i) {
+    best[i] = -1;
+    const orb_map_point_t& mp = mps[i];
+    if (mp.bad || mp.seen) continue;
+    float Pc[3];
+    xform(T.R, T.t, mp.pos, Pc);
+    if (Pc[2] < 0.0f) continue;
+    const float invz = (float)(1.0 / (double)Pc[2]);
+    const float x = Pc[0] * invz, y = Pc[1] * invz;
+    const float u = cam->fx * x + cam->cx, v = cam->fy * y + cam->cy;
+    if (!kf_in_image(K, u, v)) continue;
+    const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
+    const float PO[3] = {mp.pos[0] - T.Ow[0], mp.pos[1] - T.Ow[1], mp.pos[2] - T.Ow[2]};
+    const float dist3D = norm3(PO);
+    if (dist3D < minD || dist3D > maxD) continue;
+    if (dot3(PO, mp.normal) < 0.5 * dist3D) continue;
+    const int lvl = predict_scale(mp.max_distance, dist3D, logScale, K->n_levels);
+    const float radius = th * K->scale_factors[lvl];
+    features_in_area(g, K->keys, u, v, radius, -1, -1, idxs);
+    if (idxs.empty()) continue;
+    const uint8_t* dMP = mpDesc + (size_t)i * 32;
+    int bestDist = INT_MAX, bestIdx = -1;
+    for (size_t j : idxs) {
+      const int kl = K->keys[j].octave;
+      if (kl < lvl - 1 || kl > lvl) continue;
+      const int d = descriptor_distance(dMP, K->descriptors + j * 32);
+      if (d < bestDist) { bestDist = d; bestIdx = (int)j; }
+    }
+    if (bestDist <= 50) {
+      best[i] = bestIdx;
+      ++nf;
+    }
+  }
+  return nf;
+}
+
+// One direction of SearchBySim3 (src/ORBmatcher.cc:1256-1330 / 1332-1404):
+// points of keyframe A (pose RAw, tAw) through the similarity (sR, t) into
+// keyframe B; out[i] = best B keypoint (<= TH_HIGH) or -1.
+static void sim3_direction(const orb_frame_t* B, float logScaleB, const orb_camera_t* cam,
+                           const float* RAw, const float* tAw, const float* sR, const float* t,
+                           int nA, const orb_map_point_t* mpsA, const uint8_t* validA,
+                           const uint8_t* alreadyA, const uint8_t* descA, float th,
+                           int32_t* out) {
+  static Grid g;
+  assign_grid(g, B->keys, B->n, B->min_x, B->max_x, B->min_y, B->max_y);
+  std::vector<size_t> idxs;
+  for (int i = 0; i < nA; ++i) {
+    out[i] = -1;
+    if (!validA[i] || alreadyA[i]) continue;
+    const orb_map_point_t& mp = mpsA[i];
+    if (mp.bad) continue;
+    float Pa[3], Pb[3];
+    xform(RAw, tAw, mp.pos, Pa);
+    xform(sR, t, Pa, Pb);
+    if (Pb[2] < 0.0) continue;
+    const float invz = (float)(1.0 / (double)Pb[2]);
+    const float x = Pb[0] * invz, y = Pb[1] * invz;
+    const float u = cam->fx * x + cam->cx, v = cam->fy * y + cam->cy;
+    if (!kf_in_image(B, u, v)) continue;
+    const float maxD = 1.2f * mp.max_distance, minD = 0.8f * mp.min_distance;
+    const float dist3D = norm3(Pb);
+    if (dist3D < minD || dist3D > maxD) continue;
+    const int lvl = predict_scale(mp.max_distance, dist3D, logScaleB, B->n_levels);
+    const float radius = th * B->scale_factors[lvl];
+    features_in_area(g, B->keys, u, v, radius, -1, -1, idxs);
+    if (idxs.empty()) continue;
+    const uint8_t* dMP = descA + (size_t)i * 32;
+    int bestDist = INT_MAX, bestIdx = -1;
+    for (size_t j : idxs) {
+      const int kl = B->keys[j].octave;
+      if (kl < lvl - 1 || kl > lvl) continue;
+      const int d = descriptor_distance(dMP, B->descriptors + j * 32);
+      if (d < bestDist) { bestDist = d; bestIdx = (int)j; }
+    }
+    if (bestDist <= 100) out[i] = bestIdx;
+  }
+}
+
+// f8: SearchBySim3, src/ORBmatcher.cc:1212-1458.  match12[i1] = idx2 of a
+// mutual match (vpMatches12[i1] = vpMapPoints2[idx2]) or -1.
+static int search_by_sim3(const orb_frame_t* K1, const orb_frame_t* K2, float logScale1,
+                          float logScale2, const orb_camera_t* cam, const float* R1w,
+                          const float* t1w, const float* R2w, const float* t2w,
+                          const orb_map_point_t* mps1, const uint8_t* valid1,
+                          const uint8_t* already1, const uint8_t* mpDesc1,
+                          const orb_map_point_t* mps2, const uint8_t* valid2,
+                          const uint8_t* already2, const uint8_t* mpDesc2, float s12,
+                          const float* R12, const float* t12, float th, int32_t* match12) {
+  float sR12[9], sR21[9], t21[3];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      sR12[3 * r + c] = (float)((double)s12 * (double)R12[3 * r + c]);
+      sR21[3 * r + c] = (float)((1.0 / (double)s12) * (double)R12[3 * c + r]);
+    }
+  for (int r = 0; r < 3; ++r)
+    t21[r] = -((sR21[3 * r] * t12[0] + sR21[3 * r + 1] * t12[1]) + sR21[3 * r + 2] * t12[2]);
+  std::vector<int32_t> m1(K1->n), m2(K2->n);
+  sim3_direction(K2, logScale2, cam, R1w, t1w, sR21, t21, K1->n, mps1, valid1, already1,
+                 mpDesc1, th, m1.data());
+  sim3_direction(K1, logScale1, cam, R2w, t2w, sR12, t12, K2->n, mps2, valid2, already2,
+                 mpDesc2, th, m2.data());
+  int nFound = 0;
+  for (int i1 = 0; i1 < K1->n; ++i1) {
+    match12[i1] = -1;
+    const int idx2 = m1[i1];
+    if (idx2 >= 0 && m2[idx2] == i1) {
+      match12[i1] = idx2;
+      ++nFound;
+    }
+  }
+  return nFound;
+}
+
+// f9: SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12), src/ORBmatcher.cc:581-716.
+// match12[idx1] = MapPoint id of the matched KF2 keypoint or -1.
+static int search_by_bow_kf(const uint8_t* d1, const float* a1, const int32_t* mp1,
+                            const uint8_t* bad1, int n1, int nodes1, const uint32_t* ids1,
+                            const int32_t* offs1, const uint32_t* feats1, const uint8_t* d2,
+                            const float* a2, const int32_t* mp2, const uint8_t* bad2, int n2,
+                            int nodes2, const uint32_t* ids2, const int32_t* offs2,
+                            const uint32_t* feats2, float nnratio, int checkOri,
+                            int32_t* match12) {
+  for (int i = 0; i < n1; ++i) match12[i] = -1;
+  std::vector<uint8_t> matched2(n2, 0);
+  std::vector<int> rotHist[30];
+  int nmatches = 0;
+  int a = 0, b = 0;
+  while (a < nodes1 && b < nodes2) {
+    if (ids1[a] == ids2[b]) {
+      for (int p = offs1[a]; p < offs1[a + 1]; ++p) {
+        const int idx1 = (int)feats1[p];
+        if (mp1[idx1] < 0 || (bad1 && bad1[idx1])) continue;
+        int best1 = 256, bestIdx2 = -1, best2 = 256;
+        for (int q = offs2[b]; q < offs2[b + 1]; ++q) {
+          const int idx2 = (int)feats2[q];
+          if (matched2[idx2] || mp2[idx2] < 0) continue;
+          if (bad2 && bad2[idx2]) continue;
+          const int dist = descriptor_distance(d1 + (size_t)idx1 * 32, d2 + (size_t)idx2 * 32);
+          if (dist < best1) { best2 = best1; best1 = dist; bestIdx2 = idx2; }
+          else if (dist < best2) best2 = dist;
+        }
+        if (best1 < 50 && (float)best1 < nnratio * (float)best2) {  // TH_LOW strict (:650)
+          match12[idx1] = mp2[bestIdx2];
+          matched2[bestIdx2] = 1;
+          if (checkOri) rotHist[rot_bin(a1[idx1] - a2[bestIdx2])].push_back(idx1);
+          ++nmatches;
+        }
+      }
+      ++a;
+      ++b;
+    } else if (ids1[a] < ids2[b]) {
+      a = (int)(std::lower_bound(ids1 + a, ids1 + nodes1, ids2[b]) - ids1);
+    } else {
+      b = (int)(std::lower_bound(ids2 + b, ids2 + nodes2, ids1[a]) - ids2);
+    }
+  }
+  if (checkOri) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, 30, ind1, ind2, ind3);
+    for (int bb = 0; bb < 30; ++bb) {
+      if (bb == ind1 || bb == ind2 || bb == ind3) continue;
+      for (int idx : rotHist[bb]) { match12[idx] = -1; --nmatches; }
+    }
+  }
+  return nmatches;
+}
+
+// CheckDistEpipolarLine, src/ORBmatcher.cc:144-161 (3.84 is a double literal)
+static inline bool epipolar_ok(const KP& k1, const KP& k2, const float* F, float sigma2) {
+  const float a = k1.x * F[0] + k1.y * F[3] + F[6];
+  const float b = k1.x * F[1] + k1.y * F[4] + F[7];
+  const float c = k1.x * F[2] + k1.y * F[5] + F[8];
+  const float num = a * k2.x + b * k2.y + c;
+  const float den = a * a + b * b;
+  if (den == 0) return false;
+  const float dsqr = num * num / den;
+  return dsqr < 3.84 * sigma2;
+}
+
+// f10: SearchForTriangulation, src/ORBmatcher.cc:718-901.  Note the fork (as
+// upstream) never sets vbMatched2, so idx1 queries are independent; among the
+// passing candidates the LAST one with the smallest distance wins (<=).
+// Epipole (ex, ey) from C2 = R2w*Cw + t2w (:728-733).
+static int search_for_triangulation(const orb_frame_t* K1, const uint8_t* has_mp1,
+                                    const orb_frame_t* K2, const uint8_t* has_mp2,
+                                    const float* levelSigma2, const float* F12,
+                                    const orb_camera_t* cam, const float* Cw, const float* R2w,
+                                    const float* t2w, int nodes1, const uint32_t* ids1,
+                                    const int32_t* offs1, const uint32_t* feats1, int nodes2,
+                                    const uint32_t* ids2, const int32_t* offs2,
+                                    const uint32_t* feats2, int onlyStereo, int checkOri,
+                                    int32_t* match12) {
+  float C2[3];
+  xform(R2w, t2w, Cw, C2);
+  const float invz = 1.0f / C2[2];
+  const float ex = cam->fx * C2[0] * invz + cam->cx;
+  const float ey = cam->fy * C2[1] * invz + cam->cy;
+  for (int i = 0; i < K1->n; ++i) match12[i] = -1;
+  std::vector<int> rotHist[30];
+  int nmatches = 0;
+  int a = 0, b = 0;
+  while (a < nodes1 && b < nodes2) {
+    if (ids1[a] == ids2[b]) {
+      for (int p = offs1[a]; p < offs1[a + 1]; ++p) {
+        const int idx1 = (int)feats1[p];
+        if (has_mp1[idx1]) continue;
+        const bool st1 = K1->u_right && K1->u_right[idx1] >= 0;
+        if (onlyStereo && !st1) continue;
+        const KP& kp1 = K1->keys[idx1];
+        const uint8_t* d1 = K1->descriptors + (size_t)idx1 * 32;
+        int bestDist = 50, bestIdx2 = -1;
+        for (int q = offs2[b]; q < offs2[b + 1]; ++q) {
+          const int idx2 = (int)feats2[q];
+          if (has_mp2[idx2]) continue;  // vbMatched2 is never set (:785)
+          const bool st2 = K2->u_right && K2->u_right[idx2] >= 0;
+          if (onlyStereo && !st2) continue;
+          const int dist = descriptor_distance(d1, K2->descriptors + (size_t)idx2 * 32);
+          if (dist > 50 || dist > bestDist) continue;
+          const KP& kp2 = K2->keys[idx2];
+          if (!st1 && !st2) {
+            const float dx = ex - kp2.x, dy = ey - kp2.y;
+            if (dx * dx + dy * dy < 100 * K2->scale_factors[kp2.octave]) continue;
+          }
+          if (epipolar_ok(kp1, kp2, F12, levelSigma2[kp2.octave])) {
+            bestIdx2 = idx2;
+            bestDist = dist;
+          }
+        }
+        if (bestIdx2 >= 0) {
+          match12[idx1] = bestIdx2;
+          ++nmatches;
+          if (checkOri) rotHist[rot_bin(kp1.angle - K2->keys[bestIdx2].angle)].push_back(idx1);
+        }
+      }
+      ++a;
+      ++b;
+    } else if (ids1[a] < ids2[b]) {
+      a = (int)(std::lower_bound(ids1 + a, ids1 + nodes1, ids2[b]) - ids1);
+    } else {
+      b = (int)(std::lower_bound(ids2 + b, ids2 + nodes2, ids1[a]) - ids2);
+    }
+  }
+  if (checkOri) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, 30, ind1, ind2, ind3);
+    for (int bb = 0; bb < 30; ++bb) {
+      if (bb == ind1 || bb == ind2 || bb == ind3) continue;
+      for (int idx : rotHist[bb]) { match12[idx] = -1; --nmatches; }
+    }
+  }
+  return nmatches;
+}
+
 }  // namespace oracle
 
 // ===================================================================== C API
@@ -1373,6 +1866,72 @@ void oracle_distinctive_descriptors(int n_mp, const int32_t* offs, const uint8_t
                                     int32_t* best) {
   for (int p = 0; p < n_mp; ++p)
     best[p] = distinctive_descriptor(desc + (size_t)offs[p] * 32, offs[p + 1] - offs[p]);
+}
+
+int oracle_search_by_projection_reloc(const orb_frame_t* F, const uint8_t* kp_locked,
+                                      const orb_pose_t* T, const orb_camera_t* cam,
+                                      float log_scale, int n, const orb_map_point_t* mps,
+                                      const uint8_t* mp_desc, const float* kf_angle, float th,
+                                      int orb_dist, int check_ori, int32_t* kp_match) {
+  return search_by_projection_reloc(F, kp_locked, T, cam, log_scale, n, mps, mp_desc, kf_angle,
+                                    th, orb_dist, check_ori, kp_match);
+}
+
+int oracle_search_by_projection_sim3(const orb_frame_t* K, const float* scw,
+                                     const orb_camera_t* cam, float log_scale, int n,
+                                     const orb_map_point_t* mps, const uint8_t* mp_desc, float th,
+                                     int32_t* kp_matched) {
+  return search_by_projection_sim3(K, scw, cam, log_scale, n, mps, mp_desc, th, kp_matched);
+}
+
+int oracle_fuse(const orb_frame_t* K, const float* inv_sigma2, const orb_pose_t* T,
+                const orb_camera_t* cam, float log_scale, int n, const orb_map_point_t* mps,
+                const uint8_t* mp_desc, float th, int32_t* best) {
+  return fuse_candidates(K, inv_sigma2, T, cam, log_scale, n, mps, mp_desc, th, best);
+}
+
+int oracle_fuse_sim3(const orb_frame_t* K, const float* scw, const orb_camera_t* cam,
+                     float log_scale, int n, const orb_map_point_t* mps, const uint8_t* mp_desc,
+                     float th, int32_t* best) {
+  return fuse_sim3_candidates(K, scw, cam, log_scale, n, mps, mp_desc, th, best);
+}
+
+int oracle_search_by_sim3(const orb_frame_t* K1, const orb_frame_t* K2, float log_scale1,
+                          float log_scale2, const orb_camera_t* cam, const float* R1w,
+                          const float* t1w, const float* R2w, const float* t2w,
+                          const orb_map_point_t* mps1, const uint8_t* valid1,
+                          const uint8_t* already1, const uint8_t* mp_desc1,
+                          const orb_map_point_t* mps2, const uint8_t* valid2,
+                          const uint8_t* already2, const uint8_t* mp_desc2, float s12,
+                          const float* R12, const float* t12, float th, int32_t* match12) {
+  return search_by_sim3(K1, K2, log_scale1, log_scale2, cam, R1w, t1w, R2w, t2w, mps1, valid1,
+                        already1, mp_desc1, mps2, valid2, already2, mp_desc2, s12, R12, t12, th,
+                        match12);
+}
+
+int oracle_search_by_bow_kf(const uint8_t* d1, const float* a1, const int32_t* mp1,
+                            const uint8_t* bad1, int n1, int nodes1, const uint32_t* ids1,
+                            const int32_t* offs1, const uint32_t* feats1, const uint8_t* d2,
+                            const float* a2, const int32_t* mp2, const uint8_t* bad2, int n2,
+                            int nodes2, const uint32_t* ids2, const int32_t* offs2,
+                            const uint32_t* feats2, float nnratio, int check_ori,
+                            int32_t* match12) {
+  return search_by_bow_kf(d1, a1, mp1, bad1, n1, nodes1, ids1, offs1, feats1, d2, a2, mp2, bad2,
+                          n2, nodes2, ids2, offs2, feats2, nnratio, check_ori, match12);
+}
+
+int oracle_search_for_triangulation(const orb_frame_t* K1, const uint8_t* has_mp1,
+                                    const orb_frame_t* K2, const uint8_t* has_mp2,
+                                    const float* level_sigma2, const float* F12,
+                                    const orb_camera_t* cam, const float* Cw, const float* R2w,
+                                    const float* t2w, int nodes1, const uint32_t* ids1,
+                                    const int32_t* offs1, const uint32_t* feats1, int nodes2,
+                                    const uint32_t* ids2, const int32_t* offs2,
+                                    const uint32_t* feats2, int only_stereo, int check_ori,
+                                    int32_t* match12) {
+  return search_for_triangulation(K1, has_mp1, K2, has_mp2, level_sigma2, F12, cam, Cw, R2w, t2w,
+                                  nodes1, ids1, offs1, feats1, nodes2, ids2, offs2, feats2,
+                                  only_stereo, check_ori, match12);
 }
 
 int oracle_stereo_match(const orb_stereo_input_t* in, float* u_right, float* depth) {

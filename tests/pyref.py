@@ -452,3 +452,309 @@ def distinctive_descriptor(desc):
         if med < best:
             best, bi = med, i
     return bi
+
+
+# ------------------------------------------- §8(f) ORBmatcher variants (scalar)
+def _xf(R, t, P):
+    R = np.asarray(R, np.float32).reshape(3, 3)
+    return [f32(f32(f32(R[r, 0] * f32(P[0])) + f32(R[r, 1] * f32(P[1]))) + f32(R[r, 2] * f32(P[2])))
+            + f32(t[r]) for r in range(3)]
+
+
+def _norm(a):
+    return f32(math.sqrt(sum(float(x) * float(x) for x in a)))
+
+
+def _dotd(a, b):
+    return sum(float(x) * float(y) for x, y in zip(a, b))
+
+
+def _level(maxd, dist, log_scale, n_levels):
+    ratio = f32(f32(maxd) / f32(dist))
+    q = np.ceil(f32(f32(math.log(float(ratio))) / f32(log_scale)))
+    return 0 if q < 0 else (n_levels - 1 if q >= n_levels else int(q))
+
+
+def _sim3_pose(S):
+    S = np.asarray(S, np.float32).reshape(3, 4)
+    scw = f32(math.sqrt(sum(float(S[0, k]) ** 2 for k in range(3))))
+    inv = 1.0 / float(scw)
+    R = np.array([[f32(float(S[r, c]) * inv) for c in range(3)] for r in range(3)], np.float32)
+    t = np.array([f32(float(S[r, 3]) * inv) for r in range(3)], np.float32)
+    ow = np.array([-(f32(f32(R[0, i] * t[0]) + f32(R[1, i] * t[1])) + f32(R[2, i] * t[2]))
+                   for i in range(3)], np.float32)
+    return R, t, ow
+
+
+def _in_kf(x, y, w, h):
+    return 0 <= x < w and 0 <= y < h
+
+
+def _best(keys, desc, cells, invW, invH, dq, u, v, r, lo, hi, skip=None, gate=None,
+          check_levels=False, init=256):
+    """GetFeaturesInArea + first-minimum scan; the level filter is either the
+    function's (check_levels) or the loop's (kpLevel < lo || > hi)."""
+    idx = features_in_area(keys, cells, invW, invH, u, v, r, lo if check_levels else -1,
+                           hi if check_levels else -1)
+    bd, bi = init, -1
+    for j in idx:
+        if skip is not None and skip(j):
+            continue
+        o = int(keys[j]["octave"])
+        if not check_levels and (o < lo or o > hi):
+            continue
+        if gate is not None and not gate(j):
+            continue
+        d = hamming(dq, desc[j])
+        if d < bd:
+            bd, bi = d, j
+    return bd, bi
+
+
+def search_by_projection_sim3(keys, desc, scale, width, height, S, cam, mps, mp_desc, th,
+                              kp_matched, log_scale, n_levels=8):
+    fx, fy, cx, cy = (f32(c) for c in cam[:4])
+    cells, invW, invH = grid_cells(keys, width, height)
+    R, t, ow = _sim3_pose(S)
+    km = np.array(kp_matched, np.int32).copy()
+    n = 0
+    for i, mp in enumerate(mps):
+        if mp["bad"] or mp["seen"]:
+            continue
+        Pc = _xf(R, t, mp["pos"])
+        if Pc[2] < 0:
+            continue
+        invz = f32(f32(1) / Pc[2])
+        u = f32(f32(fx * f32(Pc[0] * invz)) + cx)
+        v = f32(f32(fy * f32(Pc[1] * invz)) + cy)
+        if not _in_kf(u, v, width, height):
+            continue
+        PO = [f32(f32(mp["pos"][k]) - ow[k]) for k in range(3)]
+        dist = _norm(PO)
+        if dist < f32(f32(0.8) * mp["min_distance"]) or dist > f32(f32(1.2) * mp["max_distance"]):
+            continue
+        if _dotd(PO, mp["normal"]) < 0.5 * float(dist):
+            continue
+        lvl = _level(mp["max_distance"], dist, log_scale, n_levels)
+        bd, bi = _best(keys, desc, cells, invW, invH, mp_desc[i], u, v,
+                       f32(f32(th) * f32(scale[lvl])), lvl - 1, lvl, skip=lambda j: km[j] >= 0)
+        if bd <= 50:
+            km[bi] = i
+            n += 1
+    return n, km
+
+
+def fuse(keys, desc, scale, inv_sigma2, width, height, u_right, R, t, ow, cam, mps, mp_desc, th,
+         log_scale, n_levels=8):
+    fx, fy, cx, cy, bf = (f32(c) for c in cam[:5])
+    cells, invW, invH = grid_cells(keys, width, height)
+    best = np.full(len(mps), -1, np.int32)
+    n = 0
+    for i, mp in enumerate(mps):
+        if mp["bad"] or mp["seen"]:
+            continue
+        Pc = _xf(R, t, mp["pos"])
+        if Pc[2] < 0:
+            continue
+        invz = f32(f32(1) / Pc[2])
+        u = f32(f32(fx * f32(Pc[0] * invz)) + cx)
+        v = f32(f32(fy * f32(Pc[1] * invz)) + cy)
+        if not _in_kf(u, v, width, height):
+            continue
+        ur = f32(u - f32(bf * invz))
+        PO = [f32(f32(mp["pos"][k]) - f32(ow[k])) for k in range(3)]
+        dist = _norm(PO)
+        if dist < f32(f32(0.8) * mp["min_distance"]) or dist > f32(f32(1.2) * mp["max_distance"]):
+            continue
+        if _dotd(PO, mp["normal"]) < 0.5 * float(dist):
+            continue
+        lvl = _level(mp["max_distance"], dist, log_scale, n_levels)
+
+        def gate(j):
+            k = keys[j]
+            ex, ey = f32(u - f32(k["x"])), f32(v - f32(k["y"]))
+            e2 = f32(f32(ex * ex) + f32(ey * ey))
+            if u_right[j] >= 0:
+                er = f32(ur - f32(u_right[j]))
+                return float(f32(f32(e2 + f32(er * er)) * f32(inv_sigma2[k["octave"]]))) <= 7.8
+            return float(f32(e2 * f32(inv_sigma2[k["octave"]]))) <= 5.99
+
+        bd, bi = _best(keys, desc, cells, invW, invH, mp_desc[i], u, v,
+                       f32(f32(th) * f32(scale[lvl])), lvl - 1, lvl, gate=gate)
+        if bd <= 50:
+            best[i] = bi
+            n += 1
+    return n, best
+
+
+def search_by_sim3(kf1, kf2, cam, s12, R12, t12, th, log_scale, n_levels=8):
+    fx, fy, cx, cy = (f32(c) for c in cam[:4])
+    R12 = np.asarray(R12, np.float32).reshape(3, 3)
+    sR12 = np.array([[f32(float(s12) * float(R12[r, c])) for c in range(3)] for r in range(3)])
+    sR21 = np.array([[f32((1.0 / float(s12)) * float(R12[c, r])) for c in range(3)]
+                     for r in range(3)])
+    t21 = np.array([-(f32(f32(sR21[r, 0] * f32(t12[0])) + f32(sR21[r, 1] * f32(t12[1])))
+                      + f32(sR21[r, 2] * f32(t12[2]))) for r in range(3)], np.float32)
+
+    def direction(A, B, sR, tt):
+        cells, invW, invH = grid_cells(B["keys"], B["width"], B["height"])
+        out = np.full(len(A["keys"]), -1, np.int32)
+        for i, mp in enumerate(A["mps"]):
+            if not A["valid"][i] or A["already"][i] or mp["bad"]:
+                continue
+            Pb = _xf(sR, tt, _xf(A["Rw"], A["tw"], mp["pos"]))
+            if Pb[2] < 0:
+                continue
+            invz = f32(1.0 / float(Pb[2]))
+            u = f32(f32(fx * f32(Pb[0] * invz)) + cx)
+            v = f32(f32(fy * f32(Pb[1] * invz)) + cy)
+            if not _in_kf(u, v, B["width"], B["height"]):
+                continue
+            dist = _norm(Pb)
+            if dist < f32(f32(0.8) * mp["min_distance"]) or dist > f32(f32(1.2) * mp["max_distance"]):
+                continue
+            lvl = _level(mp["max_distance"], dist, log_scale, n_levels)
+            bd, bi = _best(B["keys"], B["desc"], cells, invW, invH, A["mp_desc"][i], u, v,
+                           f32(f32(th) * f32(B["scale"][lvl])), lvl - 1, lvl, init=1 << 31)
+            if bd <= 100:
+                out[i] = bi
+        return out
+
+    m1 = direction(kf1, kf2, sR21, t21)
+    m2 = direction(kf2, kf1, sR12, np.asarray(t12, np.float32))
+    m12 = np.array([j if j >= 0 and m2[j] == i else -1 for i, j in enumerate(m1)], np.int32)
+    return int((m12 >= 0).sum()), m12
+
+
+def search_by_bow_kf(d1, a1, mp1, bad1, fv1, d2, a2, mp2, bad2, fv2, nnratio, check_ori):
+    m12 = np.full(len(d1), -1, np.int32)
+    matched2 = np.zeros(len(d2), bool)
+    hist = [[] for _ in range(30)]
+    nodes2 = {int(fv2[0][k]): fv2[2][fv2[1][k]:fv2[1][k + 1]] for k in range(len(fv2[0]))}
+    for k in range(len(fv1[0])):
+        f2 = nodes2.get(int(fv1[0][k]))
+        if f2 is None:
+            continue
+        for i1 in fv1[2][fv1[1][k]:fv1[1][k + 1]]:
+            if mp1[i1] < 0 or bad1[i1]:
+                continue
+            b1, b2, bi = 256, 256, -1
+            for i2 in f2:
+                if matched2[i2] or mp2[i2] < 0 or bad2[i2]:
+                    continue
+                d = hamming(d1[i1], d2[i2])
+                if d < b1:
+                    b2, b1, bi = b1, d, i2
+                elif d < b2:
+                    b2 = d
+            if b1 < 50 and f32(b1) < f32(f32(nnratio) * f32(b2)):
+                m12[i1] = mp2[bi]
+                matched2[bi] = True
+                if check_ori:
+                    hist[_rot_bin(a1[i1], a2[bi])].append(i1)
+    if check_ori:
+        keep = _three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b not in keep:
+                for i1 in hist[b]:
+                    m12[i1] = -1
+    return int((m12 >= 0).sum()), m12
+
+
+def search_by_projection_reloc(keys, desc, scale, width, height, R, t, ow, cam, mps, mp_desc,
+                               kf_angle, th, orb_dist, check_ori, kp_locked, log_scale,
+                               n_levels=8):
+    fx, fy, cx, cy = (f32(c) for c in cam[:4])
+    cells, invW, invH = grid_cells(keys, width, height)
+    lock = np.asarray(kp_locked, bool).copy()
+    km = np.full(len(keys), -1, np.int32)
+    hist = [[] for _ in range(30)]
+    for i, mp in enumerate(mps):
+        if mp["bad"] or mp["seen"]:
+            continue
+        Pc = _xf(R, t, mp["pos"])
+        invz = f32(1.0 / float(Pc[2]))
+        u = f32(f32(f32(fx * Pc[0]) * invz) + cx)
+        v = f32(f32(f32(fy * Pc[1]) * invz) + cy)
+        if u < 0 or u > width or v < 0 or v > height:
+            continue
+        PO = [f32(f32(mp["pos"][k]) - f32(ow[k])) for k in range(3)]
+        dist = _norm(PO)
+        if dist < f32(f32(0.8) * mp["min_distance"]) or dist > f32(f32(1.2) * mp["max_distance"]):
+            continue
+        lvl = _level(mp["max_distance"], dist, log_scale, n_levels)
+        bd, bi = _best(keys, desc, cells, invW, invH, mp_desc[i], u, v,
+                       f32(f32(th) * f32(scale[lvl])), lvl - 1, lvl + 1, skip=lambda j: lock[j],
+                       check_levels=True)
+        if bd <= orb_dist:
+            lock[bi] = True
+            km[bi] = i
+            if check_ori:
+                hist[_rot_bin(kf_angle[i], keys[bi]["angle"])].append(bi)
+    if check_ori:
+        keep = _three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b not in keep:
+                for j in hist[b]:
+                    km[j] = -2
+    return int((km >= 0).sum()), km
+
+
+def search_for_triangulation(kf1, kf2, level_sigma2, F12, cam, Cw, R2w, t2w, fv1, fv2,
+                             only_stereo, check_ori):
+    fx, fy, cx, cy = (f32(c) for c in cam[:4])
+    F = np.asarray(F12, np.float32).reshape(3, 3)
+    C2 = _xf(R2w, t2w, Cw)
+    invz = f32(f32(1) / C2[2])
+    ex = f32(f32(f32(fx * C2[0]) * invz) + cx)
+    ey = f32(f32(f32(fy * C2[1]) * invz) + cy)
+    k1s, k2s = kf1["keys"], kf2["keys"]
+    m12 = np.full(len(k1s), -1, np.int32)
+    hist = [[] for _ in range(30)]
+    nodes2 = {int(fv2[0][k]): fv2[2][fv2[1][k]:fv2[1][k + 1]] for k in range(len(fv2[0]))}
+    for k in range(len(fv1[0])):
+        f2 = nodes2.get(int(fv1[0][k]))
+        if f2 is None:
+            continue
+        for i1 in fv1[2][fv1[1][k]:fv1[1][k + 1]]:
+            if kf1["has_mp"][i1]:
+                continue
+            st1 = kf1["u_right"][i1] >= 0
+            if only_stereo and not st1:
+                continue
+            kp1 = k1s[i1]
+            a = f32(f32(f32(kp1["x"] * F[0, 0]) + f32(kp1["y"] * F[1, 0])) + F[2, 0])
+            b = f32(f32(f32(kp1["x"] * F[0, 1]) + f32(kp1["y"] * F[1, 1])) + F[2, 1])
+            c = f32(f32(f32(kp1["x"] * F[0, 2]) + f32(kp1["y"] * F[1, 2])) + F[2, 2])
+            bd, bi = 50, -1
+            for i2 in f2:
+                if kf2["has_mp"][i2]:
+                    continue
+                st2 = kf2["u_right"][i2] >= 0
+                if only_stereo and not st2:
+                    continue
+                d = hamming(kf1["desc"][i1], kf2["desc"][i2])
+                if d > 50 or d > bd:
+                    continue
+                kp2 = k2s[i2]
+                if not st1 and not st2:
+                    dx, dy = f32(ex - kp2["x"]), f32(ey - kp2["y"])
+                    if f32(f32(dx * dx) + f32(dy * dy)) < f32(100 * kf2["scale"][kp2["octave"]]):
+                        continue
+                num = f32(f32(f32(a * kp2["x"]) + f32(b * kp2["y"])) + c)
+                den = f32(f32(a * a) + f32(b * b))
+                if den == 0:
+                    continue
+                if float(f32(f32(num * num) / den)) < 3.84 * float(level_sigma2[kp2["octave"]]):
+                    bd, bi = d, i2
+            if bi >= 0:
+                m12[i1] = bi
+                if check_ori:
+                    hist[_rot_bin(kp1["angle"], k2s[bi]["angle"])].append(i1)
+    if check_ori:
+        keep = _three_maxima([len(h) for h in hist])
+        for bb in range(30):
+            if bb not in keep:
+                for i1 in hist[bb]:
+                    m12[i1] = -1
+    return int((m12 >= 0).sum()), m12

@@ -184,3 +184,99 @@ def observation_sets(rng, n_mp, max_obs=40, flip=0.08):
             rows[1] = rows[0]
         desc[offs[p]:offs[p + 1]] = rows
     return offs, desc
+
+
+# --------------------------------------------------------------- keyframes in 3D
+def _ry(theta):
+    c, s = np.cos(theta), np.sin(theta)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def _camera_center(R, t):
+    ow = np.zeros(3, np.float32)
+    for i in range(3):  # -R^T t, float dot left to right
+        ow[i] = -((R[0, i] * t[0] + R[1, i] * t[1]) + R[2, i] * t[2])
+    return ow
+
+
+def keyframe(oracle, seed, frame, R, t, rng, w=1241, h=376, nf=1000, frac_mp=0.8,
+             frac_stereo=0.5):
+    """A KeyFrame of the synthetic sequence with a MapPoint behind most keypoints:
+    back-projection at random depth (world frame through the pose R, t), normal
+    towards the camera with noise, scale-invariance range from the keypoint
+    octave, descriptor = keypoint descriptor with ~5 % bit flips; stereo
+    keypoints get mvuRight = u - bf/z."""
+    img = oracle.synth_image(seed, frame, w, h)
+    keys, desc, _ = oracle.extract(img, nf)
+    n = len(keys)
+    p = oracle.params(nf)
+    R = np.asarray(R, np.float32)
+    t = np.asarray(t, np.float32)
+    ow = _camera_center(R, t)
+    z = rng.uniform(4.0, 40.0, n)
+    pc = np.stack([(keys["x"] - CX) / FX * z, (keys["y"] - CY) / FY * z, z], 1)
+    pw = (pc - t.astype(np.float64)) @ R.astype(np.float64)
+    mps = np.zeros(n, oracle.MAP_POINT_DTYPE)
+    mps["pos"] = pw.astype(np.float32)
+    d = ow.astype(np.float64) - pw
+    dist = np.linalg.norm(d, axis=1)
+    nrm = -d / dist[:, None] + rng.normal(0, 0.2, (n, 3))
+    mps["normal"] = (nrm / np.linalg.norm(nrm, axis=1)[:, None]).astype(np.float32)
+    maxd = dist * 1.2 ** keys["octave"] * rng.uniform(0.9, 1.1, n)
+    mps["max_distance"] = maxd.astype(np.float32)
+    mps["min_distance"] = (maxd / 1.2 ** 7).astype(np.float32)
+    mps["bad"] = rng.random(n) < 0.03
+    valid = (rng.random(n) < frac_mp).astype(np.uint8)
+    bits = np.unpackbits(desc, axis=1) ^ (rng.random((n, 256)) < 0.05)
+    mp_desc = np.packbits(bits.astype(np.uint8), axis=1)
+    ur = np.where(rng.random(n) < frac_stereo, keys["x"] - BF / z, -1.0).astype(np.float32)
+    return dict(keys=keys, desc=desc, scale=p["scale"], inv_sigma2=p["inv_sigma2"],
+                sigma2=p["sigma2"], width=w, height=h, Rw=R, tw=t, ow=ow, mps=mps, valid=valid,
+                mp_desc=mp_desc, u_right=ur, already=np.zeros(n, np.uint8))
+
+
+def keyframe_pair(oracle, seed, rng_seed=0, w=1241, h=376, nf=1000, baseline=None):
+    """KeyFrames on frames 0 and 1 of a synthetic sequence.  Frame 1 is frame 0
+    shifted by the sequence's ego shift; KF1's pose is KF0's rotated about y by
+    atan(shift / fx), so KF0's points project near their KF1 keypoints.  With
+    `baseline` (x, y, z) KF1's centre also moves (epipolar geometry)."""
+    rng = np.random.default_rng(rng_seed)
+    R0, t0, _ = pose(rng)
+    th = np.arctan(_ego_shift(seed) / FX)
+    Ry = _ry(th)
+    R1 = (Ry @ R0.astype(np.float64)).astype(np.float32)
+    t1 = (Ry @ t0.astype(np.float64))
+    if baseline is not None:
+        t1 = t1 - R1.astype(np.float64) @ np.asarray(baseline, np.float64)
+    t1 = t1.astype(np.float32)
+    kf0 = keyframe(oracle, seed, 0, R0, t0, rng, w, h, nf)
+    kf1 = keyframe(oracle, seed, 1, R1, t1, rng, w, h, nf)
+    return kf0, kf1
+
+
+def pose_record(oracle, R, t):
+    rec = np.zeros(1, oracle.POSE_DTYPE)
+    rec["rcw"] = np.asarray(R, np.float32).reshape(1, 9)
+    rec["tcw"] = np.asarray(t, np.float32)
+    rec["ow"] = _camera_center(np.asarray(R, np.float32), np.asarray(t, np.float32))
+    return rec
+
+
+def scw(R, t, s):
+    """Scw (3x4 row-major [sR | st]) of a similarity with rotation R, translation t."""
+    S = np.zeros((3, 4), np.float32)
+    S[:, :3] = (s * np.asarray(R, np.float64)).astype(np.float32)
+    S[:, 3] = (s * np.asarray(t, np.float64)).astype(np.float32)
+    return S
+
+
+def fundamental(kf1, kf2):
+    """LocalMapping::ComputeF12 in float64 (an input to SearchForTriangulation)."""
+    R1, t1 = kf1["Rw"].astype(np.float64), kf1["tw"].astype(np.float64)
+    R2, t2 = kf2["Rw"].astype(np.float64), kf2["tw"].astype(np.float64)
+    R12 = R1 @ R2.T
+    t12 = -R1 @ R2.T @ t2 + t1
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1]])
+    Ki = np.linalg.inv(K)
+    return (Ki.T @ tx @ R12 @ Ki).astype(np.float32)
