@@ -34,6 +34,13 @@
  *                                  src/ORBmatcher.cc:429-577
  *   orb_distinctive_descriptors(_batch)    MapPoint::ComputeDistinctiveDescriptors
  *                                  src/MapPoint.cc:250-326
+ *   orb_search_by_projection_reloc SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist)
+ *                                  src/ORBmatcher.cc:1622-1759
+ *   orb_search_by_projection_sim3  SearchByProjection(KeyFrame*, Scw, ...) src/ORBmatcher.cc:311-425
+ *   orb_fuse / orb_fuse_sim3       Fuse(KeyFrame*, ...) x2   src/ORBmatcher.cc:903-1210
+ *   orb_search_by_sim3             SearchBySim3              src/ORBmatcher.cc:1212-1458
+ *   orb_match_bow_kf               SearchByBoW(KeyFrame*, KeyFrame*, ...) src/ORBmatcher.cc:581-716
+ *   orb_search_for_triangulation   SearchForTriangulation    src/ORBmatcher.cc:718-901
  *
  * Error behaviour: the reference has no status codes (an empty image returns
  * silently with outputs untouched, src/ORBextractor.cc:1095-1096; a non-8UC1
@@ -371,6 +378,98 @@ orb_status_t orb_distinctive_descriptors_batch(orb_matcher_t* m, int n_mp,
                                                const int32_t* d_obs_offs,
                                                const uint8_t* d_obs_desc, int32_t* d_best_idx,
                                                uint8_t* d_descriptors, void* stream);
+
+/* ---- projection-window ORBmatcher variants.  Map points use
+ * orb_map_point_t; its `seen` flag marks the variant's "already found" set
+ * (documented per call).  Host buffers; log_scale_factor = mfLogScaleFactor;
+ * KeyFrame bounds come from the orb_frame_t (KeyFrame::IsInImage is
+ * half-open, Frame bounds closed, as in the reference). */
+
+/* SearchByProjection(Frame& F, KeyFrame* pKF, sAlreadyFound, th, ORBdist),
+ * src/ORBmatcher.cc:1622-1759 (Tracking::Relocalization).  Point i = the
+ * MapPoint of KF keypoint i (NULL -> bad = 1; seen = in sAlreadyFound),
+ * kf_angle[i] = pKF->mvKeysUn[i].angle, pose = F.mTcw (+ mOw).
+ * kp_locked[j] = F.mvpMapPoints[j] != NULL on entry.  kp_match[j] (out) = point
+ * assigned to frame keypoint j by this call, -1 none, -2 reset by the rotation
+ * filter.  *nmatches = the reference's return value. */
+orb_status_t orb_search_by_projection_reloc(orb_matcher_t* m, const orb_frame_t* frame,
+                                            const uint8_t* kp_locked, const orb_pose_t* pose,
+                                            const orb_camera_t* cam, float log_scale_factor,
+                                            int n_mp, const orb_map_point_t* mps,
+                                            const uint8_t* mp_desc, const float* kf_angle,
+                                            float th, int orb_dist, int check_orientation,
+                                            int32_t* kp_match, int32_t* nmatches);
+
+/* SearchByProjection(KeyFrame* pKF, Scw, vpPoints, vpMatched, th),
+ * src/ORBmatcher.cc:311-425 (LoopClosing::ComputeSim3).  scw = the top 3 rows of
+ * Scw, row-major.  seen = in spAlreadyFound (vpMatched's points).
+ * kp_matched[j] (in/out) = index into vpPoints of vpMatched[j], -1 = NULL. */
+orb_status_t orb_search_by_projection_sim3(orb_matcher_t* m, const orb_frame_t* kf,
+                                           const float* scw, const orb_camera_t* cam,
+                                           float log_scale_factor, int n_mp,
+                                           const orb_map_point_t* mps, const uint8_t* mp_desc,
+                                           float th, int32_t* kp_matched, int32_t* nmatches);
+
+/* Fuse(KeyFrame* pKF, vpMapPoints, th), src/ORBmatcher.cc:903-1077: the match
+ * half.  fuse_idx[i] (out) = keypoint of pKF point i fuses into (bestIdx) or
+ * -1; seen = pMP->IsInKeyFrame(pKF); pose = pKF's Tcw with Ow = camera centre;
+ * kf->u_right = mvuRight.  The caller applies Replace / AddObservation in
+ * point order (:1048-1070), re-checking isBad() / IsInKeyFrame() first: the
+ * targets only depend on entry state for points the reference still visits. */
+orb_status_t orb_fuse(orb_matcher_t* m, const orb_frame_t* kf, const float* inv_level_sigma2,
+                      const orb_pose_t* pose, const orb_camera_t* cam, float log_scale_factor,
+                      int n_mp, const orb_map_point_t* mps, const uint8_t* mp_desc, float th,
+                      int32_t* fuse_idx, int32_t* n_fuse);
+
+/* Fuse(KeyFrame* pKF, Scw, vpPoints, th, vpReplacePoint),
+ * src/ORBmatcher.cc:1079-1210: fuse_idx[i] = bestIdx or -1 (seen = in
+ * pKF->GetMapPoints() at entry); vpReplacePoint / AddMapPoint stay with the
+ * caller. */
+orb_status_t orb_fuse_sim3(orb_matcher_t* m, const orb_frame_t* kf, const float* scw,
+                           const orb_camera_t* cam, float log_scale_factor, int n_mp,
+                           const orb_map_point_t* mps, const uint8_t* mp_desc, float th,
+                           int32_t* fuse_idx, int32_t* n_fuse);
+
+/* SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th),
+ * src/ORBmatcher.cc:1212-1458.  mpsX[i] / mp_descX[i] = the MapPoint of
+ * keypoint i of KF X (validX[i] = non-NULL), alreadyX = vbAlreadyMatchedX
+ * (:1240-1252).  rXw / tXw = KF rotations (row-major) and translations.
+ * match12[i1] (out) = idx2 with vpMatches12[i1] = vpMapPoints2[idx2], or -1. */
+orb_status_t orb_search_by_sim3(orb_matcher_t* m, const orb_frame_t* kf1, const orb_frame_t* kf2,
+                                float log_scale_factor, const orb_camera_t* cam,
+                                const float* r1w, const float* t1w, const float* r2w,
+                                const float* t2w, const orb_map_point_t* mps1,
+                                const uint8_t* valid1, const uint8_t* already1,
+                                const uint8_t* mp_desc1, const orb_map_point_t* mps2,
+                                const uint8_t* valid2, const uint8_t* already2,
+                                const uint8_t* mp_desc2, float s12, const float* r12,
+                                const float* t12, float th, int32_t* match12, int32_t* nfound);
+
+/* SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vpMatches12),
+ * src/ORBmatcher.cc:581-716 (FeatureVectors as in orb_match_bow).
+ * match12[i] (out) = MapPoint id of the KF2 keypoint matched to KF1 keypoint i,
+ * or -1. */
+orb_status_t orb_match_bow_kf(orb_matcher_t* m, int n1, const uint8_t* desc1,
+                              const float* angle1, const int32_t* mp1, const uint8_t* mp1_bad,
+                              int nodes1, const uint32_t* node_ids1, const int32_t* offs1,
+                              const uint32_t* feats1, int n2, const uint8_t* desc2,
+                              const float* angle2, const int32_t* mp2, const uint8_t* mp2_bad,
+                              int nodes2, const uint32_t* node_ids2, const int32_t* offs2,
+                              const uint32_t* feats2, float nnratio, int check_orientation,
+                              int32_t* match12, int32_t* nmatches);
+
+/* SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo),
+ * src/ORBmatcher.cc:718-901.  has_mpX[i] = GetMapPoint(i) != NULL;
+ * level_sigma2 = pKF2->mvLevelSigma2; f12 row-major; cw = pKF1 camera centre,
+ * r2w/t2w = pKF2 pose.  match12[i] (out) = KF2 index or -1; vMatchedPairs =
+ * the (i, match12[i]) with match12[i] >= 0 in ascending i. */
+orb_status_t orb_search_for_triangulation(
+    orb_matcher_t* m, const orb_frame_t* kf1, const uint8_t* has_mp1, const orb_frame_t* kf2,
+    const uint8_t* has_mp2, const float* level_sigma2, const float* f12,
+    const orb_camera_t* cam, const float* cw, const float* r2w, const float* t2w, int nodes1,
+    const uint32_t* node_ids1, const int32_t* offs1, const uint32_t* feats1, int nodes2,
+    const uint32_t* node_ids2, const int32_t* offs2, const uint32_t* feats2, int only_stereo,
+    int check_orientation, int32_t* match12, int32_t* nmatches);
 
 /* ---------------------------------------------------------- synthetic input */
 

@@ -137,6 +137,17 @@ def lib() -> ctypes.CDLL:
                   vp, vp]),
         "orb_distinctive_descriptors": (i32, [vp, i32, vp, vp, vp, vp]),
         "orb_distinctive_descriptors_batch": (i32, [vp, i32, vp, vp, vp, vp, vp]),
+        "orb_search_by_projection_reloc": (i32, [vp, vp, vp, vp, vp, f32, i32, vp, vp, vp, f32,
+                                                 i32, i32, vp, vp]),
+        "orb_search_by_projection_sim3": (i32, [vp, vp, vp, vp, f32, i32, vp, vp, f32, vp, vp]),
+        "orb_fuse": (i32, [vp, vp, vp, vp, vp, f32, i32, vp, vp, f32, vp, vp]),
+        "orb_fuse_sim3": (i32, [vp, vp, vp, vp, f32, i32, vp, vp, f32, vp, vp]),
+        "orb_search_by_sim3": (i32, [vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                     vp, vp, f32, vp, vp, f32, vp, vp]),
+        "orb_match_bow_kf": (i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, vp,
+                                   i32, vp, vp, vp, f32, i32, vp, vp]),
+        "orb_search_for_triangulation": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32,
+                                               vp, vp, vp, i32, vp, vp, vp, i32, i32, vp, vp]),
         "orb_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
         "orb_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     }
@@ -552,6 +563,141 @@ class ORBmatcher:
             len(ffv[0]), _ptr(ffv[0]), _ptr(ffv[1]), _ptr(ffv[2]), self.mfNNratio,
             int(self.mbCheckOrientation), _ptr(fm), ctypes.byref(nm)), "SearchByBoW")
         return nm.value, fm
+
+    # ------------------------------------------- projection-window variants (§8(f))
+    @staticmethod
+    def _mps(mps):
+        return np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+
+    def SearchByProjectionKF(self, F: Frame, pose, cam, logScaleFactor: float, mps, mp_desc,
+                             kf_angle, th: float, ORBdist: int, kp_locked=None):
+        """SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:1622-1759):
+        (nmatches, kp_match) -- point index per frame keypoint, -1 none, -2 reset."""
+        mps = self._mps(mps)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        ka = np.ascontiguousarray(kf_angle, np.float32)
+        pose = np.ascontiguousarray(pose, POSE_DTYPE).reshape(1)
+        lk = None if kp_locked is None else np.ascontiguousarray(kp_locked, np.uint8)
+        km = np.full(F.N, -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f, c = F._c(), _Camera(*cam)
+        _check(lib().orb_search_by_projection_reloc(
+            self._h, ctypes.byref(f), _ptr(lk) if lk is not None else None, _ptr(pose),
+            ctypes.byref(c), logScaleFactor, len(mps), _ptr(mps) if len(mps) else None,
+            _ptr(md) if len(mps) else None, _ptr(ka) if len(mps) else None, th, int(ORBdist),
+            int(self.mbCheckOrientation), _ptr(km) if F.N else None, ctypes.byref(nm)),
+            "SearchByProjection(F, KF)")
+        return nm.value, km
+
+    def SearchByProjectionSim3(self, KF: Frame, Scw, cam, logScaleFactor: float, mps, mp_desc,
+                               th: float, kp_matched):
+        """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (src/ORBmatcher.cc:311-425):
+        (nmatches, kp_matched updated)."""
+        mps = self._mps(mps)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        S = np.ascontiguousarray(Scw, np.float32).reshape(12)
+        km = np.array(kp_matched, np.int32).copy()
+        nm = ctypes.c_int32(0)
+        f, c = KF._c(), _Camera(*cam)
+        _check(lib().orb_search_by_projection_sim3(
+            self._h, ctypes.byref(f), _ptr(S), ctypes.byref(c), logScaleFactor, len(mps),
+            _ptr(mps) if len(mps) else None, _ptr(md) if len(mps) else None, th,
+            _ptr(km) if KF.N else None, ctypes.byref(nm)), "SearchByProjection(KF, Scw)")
+        return nm.value, km
+
+    def Fuse(self, KF: Frame, invLevelSigma2, pose, cam, logScaleFactor: float, mps, mp_desc,
+             th: float = 3.0):
+        """Fuse(pKF, vpMapPoints, th) targets (src/ORBmatcher.cc:903-1077): (n, fuse_idx)."""
+        mps = self._mps(mps)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        inv = np.ascontiguousarray(invLevelSigma2, np.float32)
+        pose = np.ascontiguousarray(pose, POSE_DTYPE).reshape(1)
+        out = np.full(len(mps), -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f, c = KF._c(), _Camera(*cam)
+        _check(lib().orb_fuse(self._h, ctypes.byref(f), _ptr(inv), _ptr(pose), ctypes.byref(c),
+                              logScaleFactor, len(mps), _ptr(mps) if len(mps) else None,
+                              _ptr(md) if len(mps) else None, th,
+                              _ptr(out) if len(mps) else None, ctypes.byref(nm)), "Fuse")
+        return nm.value, out
+
+    def FuseSim3(self, KF: Frame, Scw, cam, logScaleFactor: float, mps, mp_desc, th: float):
+        """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) targets (src/ORBmatcher.cc:1079-1210)."""
+        mps = self._mps(mps)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        S = np.ascontiguousarray(Scw, np.float32).reshape(12)
+        out = np.full(len(mps), -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f, c = KF._c(), _Camera(*cam)
+        _check(lib().orb_fuse_sim3(self._h, ctypes.byref(f), _ptr(S), ctypes.byref(c),
+                                   logScaleFactor, len(mps), _ptr(mps) if len(mps) else None,
+                                   _ptr(md) if len(mps) else None, th,
+                                   _ptr(out) if len(mps) else None, ctypes.byref(nm)),
+               "Fuse(Scw)")
+        return nm.value, out
+
+    def SearchBySim3(self, KF1: Frame, KF2: Frame, logScaleFactor: float, cam, R1w, t1w, R2w,
+                     t2w, mps1, valid1, already1, mp_desc1, mps2, valid2, already2, mp_desc2,
+                     s12: float, R12, t12, th: float):
+        """SearchBySim3 (src/ORBmatcher.cc:1212-1458): (nFound, match12 = idx2 or -1)."""
+        f32a = lambda a, n: np.ascontiguousarray(a, np.float32).reshape(n)
+        u8 = lambda a: np.ascontiguousarray(a, np.uint8)
+        keep = [f32a(R1w, 9), f32a(t1w, 3), f32a(R2w, 9), f32a(t2w, 3), self._mps(mps1),
+                u8(valid1), u8(already1), u8(mp_desc1), self._mps(mps2), u8(valid2),
+                u8(already2), u8(mp_desc2), f32a(R12, 9), f32a(t12, 3)]
+        m12 = np.full(KF1.N, -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f1, f2, c = KF1._c(), KF2._c(), _Camera(*cam)
+        p = [_ptr(a) if a.size else None for a in keep]
+        _check(lib().orb_search_by_sim3(self._h, ctypes.byref(f1), ctypes.byref(f2),
+                                        logScaleFactor, ctypes.byref(c), *p[:12], s12, p[12],
+                                        p[13], th, _ptr(m12) if KF1.N else None,
+                                        ctypes.byref(nm)), "SearchBySim3")
+        return nm.value, m12
+
+    def SearchByBoWKF(self, desc1, angle1, mp1, bad1, fv1, desc2, angle2, mp2, bad2, fv2):
+        """SearchByBoW(pKF1, pKF2, vpMatches12) (src/ORBmatcher.cc:581-716):
+        (nmatches, match12 = MapPoint id of KF2 or -1)."""
+        d1 = np.ascontiguousarray(desc1, np.uint8)
+        d2 = np.ascontiguousarray(desc2, np.uint8)
+        a1, a2 = (np.ascontiguousarray(a, np.float32) for a in (angle1, angle2))
+        m1, m2 = (np.ascontiguousarray(a, np.int32) for a in (mp1, mp2))
+        b1 = None if bad1 is None else np.ascontiguousarray(bad1, np.uint8)
+        b2 = None if bad2 is None else np.ascontiguousarray(bad2, np.uint8)
+        v1 = [np.ascontiguousarray(fv1[0], np.uint32), np.ascontiguousarray(fv1[1], np.int32),
+              np.ascontiguousarray(fv1[2], np.uint32)]
+        v2 = [np.ascontiguousarray(fv2[0], np.uint32), np.ascontiguousarray(fv2[1], np.int32),
+              np.ascontiguousarray(fv2[2], np.uint32)]
+        out = np.full(len(d1), -1, np.int32)
+        nm = ctypes.c_int32(0)
+        _check(lib().orb_match_bow_kf(
+            self._h, len(d1), _ptr(d1), _ptr(a1), _ptr(m1), _ptr(b1) if b1 is not None else None,
+            len(v1[0]), _ptr(v1[0]), _ptr(v1[1]), _ptr(v1[2]), len(d2), _ptr(d2), _ptr(a2),
+            _ptr(m2), _ptr(b2) if b2 is not None else None, len(v2[0]), _ptr(v2[0]), _ptr(v2[1]),
+            _ptr(v2[2]), self.mfNNratio, int(self.mbCheckOrientation), _ptr(out),
+            ctypes.byref(nm)), "SearchByBoW(KF, KF)")
+        return nm.value, out
+
+    def SearchForTriangulation(self, KF1: Frame, has_mp1, KF2: Frame, has_mp2, levelSigma2, F12,
+                               cam, Cw, R2w, t2w, fv1, fv2, bOnlyStereo: bool = False):
+        """SearchForTriangulation (src/ORBmatcher.cc:718-901): (nmatches, match12)."""
+        h1, h2 = (np.ascontiguousarray(a, np.uint8) for a in (has_mp1, has_mp2))
+        keep = [np.ascontiguousarray(a, np.float32).reshape(-1)
+                for a in (levelSigma2, F12, Cw, R2w, t2w)]
+        v1 = [np.ascontiguousarray(fv1[0], np.uint32), np.ascontiguousarray(fv1[1], np.int32),
+              np.ascontiguousarray(fv1[2], np.uint32)]
+        v2 = [np.ascontiguousarray(fv2[0], np.uint32), np.ascontiguousarray(fv2[1], np.int32),
+              np.ascontiguousarray(fv2[2], np.uint32)]
+        out = np.full(KF1.N, -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f1, f2, c = KF1._c(), KF2._c(), _Camera(*cam)
+        _check(lib().orb_search_for_triangulation(
+            self._h, ctypes.byref(f1), _ptr(h1), ctypes.byref(f2), _ptr(h2), _ptr(keep[0]),
+            _ptr(keep[1]), ctypes.byref(c), _ptr(keep[2]), _ptr(keep[3]), _ptr(keep[4]),
+            len(v1[0]), _ptr(v1[0]), _ptr(v1[1]), _ptr(v1[2]), len(v2[0]), _ptr(v2[0]),
+            _ptr(v2[1]), _ptr(v2[2]), int(bOnlyStereo), int(self.mbCheckOrientation), _ptr(out),
+            ctypes.byref(nm)), "SearchForTriangulation")
+        return nm.value, out
 
     # ------------------------------------------------- SearchForInitialization
     def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched, windowSize: int = 10):

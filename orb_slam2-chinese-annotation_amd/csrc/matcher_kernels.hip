@@ -845,7 +845,8 @@ __global__ __launch_bounds__(256) void k_bow_match(
     const uint32_t* __restrict__ kfFeats, const uint8_t* __restrict__ fDesc,
     const float* __restrict__ fAngle, int fNodes, const uint32_t* __restrict__ fNodeIds,
     const int32_t* __restrict__ fOffs, const uint32_t* __restrict__ fFeats, float nnratio,
-    int nF, int32_t* __restrict__ fMatch, int32_t* __restrict__ accF) {
+    int nF, const int32_t* __restrict__ fMp, const uint8_t* __restrict__ fBad, int thLow,
+    int32_t* __restrict__ accF) {
   // per-wave LDS bitmap of the frame features this wave's node has claimed
   extern __shared__ __attribute__((aligned(16))) uint32_t claimBits[];
   const int lane = threadIdx.x & 63;
@@ -877,6 +878,7 @@ __global__ __launch_bounds__(256) void k_bow_match(
     for (int q = fb + lane; q < fe; q += 64) {
       const int realIdxF = (int)fFeats[q];
       if ((claimed[realIdxF >> 5] >> (realIdxF & 31)) & 1u) continue;
+      if (fMp && (fMp[realIdxF] < 0 || (fBad && fBad[realIdxF]))) continue;  // KF-KF (:628-632)
       const int dist = hamming256(dKF, load_desc(fDesc + (size_t)realIdxF * 32));
       if (dist < d1) { d2 = d1; q2 = q1; d1 = dist; q1 = q; }
       else if (dist < d2) { d2 = dist; q2 = q; }
@@ -895,11 +897,11 @@ __global__ __launch_bounds__(256) void k_bow_match(
       d2 = c1First ? c1d : c2d;
       q2 = c1First ? c1q : c2q;
     }
-    if (d1 <= 50 && (float)d1 < nnratio * (float)d2) {  // TH_LOW, ratio (:239-242)
+    // TH_LOW: <= 50 against a Frame (:239), < 50 between KeyFrames (:650)
+    if (d1 <= thLow && (float)d1 < nnratio * (float)d2) {
       const int realIdxF = (int)fFeats[q1];
       if (lane == 0) {
         claimed[realIdxF >> 5] |= 1u << (realIdxF & 31);
-        fMatch[realIdxF] = kfMp[realIdxKF];
         accF[p] = realIdxF;
       }
     }
@@ -909,9 +911,13 @@ __global__ __launch_bounds__(256) void k_bow_match(
   }
 }
 
+// Output: against a Frame (fMp == NULL) fMatch[f] = the KeyFrame keypoint's
+// MapPoint id; between KeyFrames fMatch[kf keypoint] = the matched KF2
+// keypoint's MapPoint id (vpMatches12).  Rotation-filtered matches stay -1.
 __global__ __launch_bounds__(256) void k_bow_finish(
     int nKfFeats, const uint32_t* __restrict__ kfFeats, const float* __restrict__ kfAngle,
     const float* __restrict__ fAngle, int checkOri, const int32_t* __restrict__ accF,
+    const int32_t* __restrict__ kfMp, const int32_t* __restrict__ fMp,
     int32_t* __restrict__ fMatch, int32_t* __restrict__ nmatches) {
   __shared__ int hist[32];
   __shared__ int tmp[17];
@@ -929,16 +935,19 @@ __global__ __launch_bounds__(256) void k_bow_finish(
   int ind1 = -1, ind2 = -1, ind3 = -1;
   if (checkOri) three_maxima(hist, ind1, ind2, ind3);
   int removed = 0;
-  if (checkOri) {
-    for (int p = t; p < nKfFeats; p += 256) {
-      const int f = accF[p];
-      if (f < 0) continue;
+  for (int p = t; p < nKfFeats; p += 256) {
+    const int f = accF[p];
+    if (f < 0) continue;
+    if (checkOri) {
       const int b = rot_bin(kfAngle[kfFeats[p]] - fAngle[f]);
       if (b != ind1 && b != ind2 && b != ind3) {
-        fMatch[f] = -1;
         ++removed;
+        continue;
       }
     }
+    const int k = (int)kfFeats[p];
+    if (fMp) fMatch[k] = fMp[f];
+    else fMatch[f] = kfMp[k];
   }
   int totA, totR;
   block_excl_scan(acc, tmp, &totA);
@@ -951,7 +960,8 @@ extern "C" hipError_t orb_k_bow(const uint8_t* kfDesc, const float* kfAngle, con
                                 const int32_t* kfOffs, const uint32_t* kfFeats, int nKfFeats,
                                 const uint8_t* fDesc, const float* fAngle, int fNodes,
                                 const uint32_t* fNodeIds, const int32_t* fOffs,
-                                const uint32_t* fFeats, int nF, float nnratio, int checkOri,
+                                const uint32_t* fFeats, int nF, const int32_t* fMp,
+                                const uint8_t* fBad, int thLow, float nnratio, int checkOri,
                                 int32_t* fMatch, int32_t* accF, int32_t* nmatches,
                                 hipStream_t s) {
   if (kfNodes > 0) {
@@ -959,12 +969,12 @@ extern "C" hipError_t orb_k_bow(const uint8_t* kfDesc, const float* kfAngle, con
     if (lds > 65536) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bow_match, dim3((kfNodes + 3) / 4), dim3(256), lds, s, kfDesc, kfAngle,
                        kfMp, kfBad, kfNodes, kfNodeIds, kfOffs, kfFeats, fDesc, fAngle, fNodes,
-                       fNodeIds, fOffs, fFeats, nnratio, nF, fMatch, accF);
+                       fNodeIds, fOffs, fFeats, nnratio, nF, fMp, fBad, thLow, accF);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_bow_finish, dim3(1), dim3(256), 0, s, nKfFeats, kfFeats, kfAngle, fAngle,
-                     checkOri, accF, fMatch, nmatches);
+                     checkOri, accF, kfMp, fMp, fMatch, nmatches);
   return hipGetLastError();
 }
 

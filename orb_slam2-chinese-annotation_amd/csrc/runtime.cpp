@@ -86,8 +86,34 @@ hipError_t orb_k_bow(const uint8_t* kfDesc, const float* kfAngle, const int32_t*
                      const int32_t* kfOffs, const uint32_t* kfFeats, int nKfFeats,
                      const uint8_t* fDesc, const float* fAngle, int fNodes,
                      const uint32_t* fNodeIds, const int32_t* fOffs, const uint32_t* fFeats,
-                     int nF, float nnratio, int checkOri, int32_t* fMatch, int32_t* accF,
+                     int nF, const int32_t* fMp, const uint8_t* fBad, int thLow,
+                     float nnratio, int checkOri, int32_t* fMatch, int32_t* accF,
                      int32_t* nmatches, hipStream_t s);
+size_t orb_k_pp_params_size(void);
+size_t orb_k_pp_rec_size(void);
+size_t orb_k_tri_params_size(void);
+size_t orb_k_pp_resolve_lds(int nkeys, int n);
+hipError_t orb_k_pp_match(int mode, const orb_map_point_t* mps, const uint8_t* mpValid,
+                          const uint8_t* mpSkip, const uint8_t* mpDesc, int n,
+                          const orb_keypoint_t* keys, const uint8_t* desc, const float* uright,
+                          const int32_t* cellStart, const int32_t* cellIdx, const void* params,
+                          void* recs, int32_t* best, uint32_t* topk, int32_t* ncand,
+                          hipStream_t s);
+hipError_t orb_k_pp_resolve(const orb_keypoint_t* keys, const uint8_t* desc, int nkeys,
+                            const uint8_t* kpLocked, const uint8_t* mpDesc, const float* mpAngle,
+                            int n, const int32_t* cellStart, const int32_t* cellIdx,
+                            const void* params, const void* recs, const uint32_t* topk,
+                            const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
+                            hipStream_t s);
+hipError_t orb_k_sim3_mutual(const int32_t* m1, int n1, const int32_t* m2, int32_t* match12,
+                             int32_t* nfound, hipStream_t s);
+hipError_t orb_k_triangulation(const orb_keypoint_t* k1, const uint8_t* d1, const float* ur1,
+                               const uint8_t* hasMp1, int nodes1, const uint32_t* ids1,
+                               const int32_t* offs1, const uint32_t* feats1, int nFeats1,
+                               const orb_keypoint_t* k2, const uint8_t* d2, const float* ur2,
+                               const uint8_t* hasMp2, int nodes2, const uint32_t* ids2,
+                               const int32_t* offs2, const uint32_t* feats2, const void* params,
+                               int32_t* match12, int32_t* acc, int32_t* nmatches, hipStream_t s);
 size_t orb_k_init_params_size(void);
 size_t orb_k_init_list_len(void);
 size_t orb_k_init_topk(void);
@@ -902,6 +928,23 @@ struct FrameProjParamsHost {  // mirrors FrameProjParams
   float scale[ORB_MAX_LEVELS];
 };
 
+struct PPParamsHost {  // mirrors PPParams in projection_kernels.hip
+  float R[9], t[3], Ow[3];
+  float R2[9], t2[3];
+  float fx, fy, cx, cy, bf;
+  float minX, maxX, minY, maxY, invW, invH;
+  float th, logScale;
+  int nLevels, thr, checkOri;
+  float scale[ORB_MAX_LEVELS], invSigma2[ORB_MAX_LEVELS];
+};
+
+struct TriParamsHost {  // mirrors TriParams
+  float F[9];
+  float ex, ey;
+  int onlyStereo, checkOri;
+  float scale[ORB_MAX_LEVELS], sigma2[ORB_MAX_LEVELS];
+};
+
 struct InitParamsHost {  // mirrors InitParams in mapping_kernels.hip
   float minX, minY, invW, invH;
   float r, nnratio;
@@ -924,6 +967,7 @@ struct orb_matcher {
   // SearchForInitialization / ComputeDistinctiveDescriptors scratch
   DevBuf dK1, dD1, dK2, dD2, dN1, dN2, dPrev, dList, dM12, dOffs, dObsDesc, dBest, dBestDesc,
       dInitQ, dInitStage, dInitCounts;
+  DevBuf sx[24];  // projection / triangulation / KF-KF BoW scratch
   std::vector<uint8_t> hostScratch;
 };
 
@@ -951,7 +995,9 @@ orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
       orb_k_stereo_params_size() != sizeof(StereoParamsHost) ||
       orb_k_frame_params_size() != sizeof(FrameProjParamsHost) ||
       orb_k_frustum_params_size() != sizeof(FrustumParamsHost) ||
-      orb_k_init_params_size() != sizeof(InitParamsHost))
+      orb_k_init_params_size() != sizeof(InitParamsHost) ||
+      orb_k_pp_params_size() != sizeof(PPParamsHost) ||
+      orb_k_tri_params_size() != sizeof(TriParamsHost))
     return ORB_EINVAL;
   orb_matcher* m = new orb_matcher();
   m->device = device;
@@ -984,6 +1030,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dOffs, &m->dObsDesc, &m->dBest, &m->dBestDesc, &m->dInitQ,
                     &m->dInitStage, &m->dInitCounts};
   for (DevBuf* b : bufs) b->release();
+  for (DevBuf& b : m->sx) b.release();
   m->prof.destroy();
   hipStreamDestroy(m->stream);
   delete m;
@@ -1442,7 +1489,7 @@ orb_status_t orb_match_bow(orb_matcher_t* m, int n_kf, const uint8_t* kf_desc,
                     m->dBowE.as<uint32_t>(), m->dBowF.as<int32_t>(), m->dBowG.as<uint32_t>(),
                     nKfFeats, m->dDesc.as<uint8_t>(), m->dBowH.as<float>(), f_nodes,
                     m->dBowI.as<uint32_t>(), m->dBowJ.as<int32_t>(), m->dBowK.as<uint32_t>(), n_f,
-                    nnratio, check_orientation, m->dKpMatch.as<int32_t>(),
+                    nullptr, nullptr, 50, nnratio, check_orientation, m->dKpMatch.as<int32_t>(),
                     m->dTopk.as<int32_t>(), m->dNMatch.as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(f_match, m->dKpMatch.p, (size_t)n_f * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
@@ -1596,6 +1643,404 @@ orb_status_t orb_distinctive_descriptors_batch(orb_matcher_t* m, int n_mp,
   hipSetDevice(m->device);
   HIP_TRY(orb_k_distinctive(d_obs_offs, d_obs_desc, n_mp, d_best_idx, d_descriptors,
                             stream ? (hipStream_t)stream : m->stream));
+  return ORB_OK;
+}
+
+// ------------------------------------------- projection-window ORBmatcher variants
+// Host-side pose algebra of the reference, in the pinned arithmetic of
+// oracle/orb_oracle.cpp (cv::Mat products as float dots left to right,
+// scalar scaling through double, norms/dots accumulated in double).
+static void rt_xform(const float* R, const float* t, const float* P, float* o) {
+  for (int r = 0; r < 3; ++r)
+    o[r] = ((R[3 * r] * P[0] + R[3 * r + 1] * P[1]) + R[3 * r + 2] * P[2]) + t[r];
+}
+
+static void rt_center(const float* R, const float* t, float* Ow) {  // -R^T t
+  for (int i = 0; i < 3; ++i) Ow[i] = -((R[i] * t[0] + R[3 + i] * t[1]) + R[6 + i] * t[2]);
+}
+
+static void sim3_normalise(const float* S, float* R, float* t, float* Ow) {
+  double ss = 0.0;
+  for (int k = 0; k < 3; ++k) ss += (double)S[k] * S[k];
+  const float scw = (float)sqrt(ss);  // sqrt(sRcw.row(0).dot(sRcw.row(0))) (:320)
+  const double inv = 1.0 / (double)scw;
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) R[3 * r + c] = (float)((double)S[4 * r + c] * inv);
+    t[r] = (float)((double)S[4 * r + 3] * inv);
+  }
+  rt_center(R, t, Ow);
+}
+
+static orb_status_t pp_base(PPParamsHost& P, const orb_frame_t* K, const orb_camera_t* cam,
+                            float logScale, float th, int thr) {
+  memset(&P, 0, sizeof(P));
+  if (!K || !cam || K->n_levels <= 0 || K->n_levels > ORB_MAX_LEVELS || !K->scale_factors ||
+      !(K->max_x > K->min_x) || !(K->max_y > K->min_y))
+    return ORB_EINVAL;
+  P.fx = cam->fx; P.fy = cam->fy; P.cx = cam->cx; P.cy = cam->cy; P.bf = cam->bf;
+  P.minX = K->min_x; P.maxX = K->max_x; P.minY = K->min_y; P.maxY = K->max_y;
+  P.invW = (float)ORB_GRID_COLS / (K->max_x - K->min_x);
+  P.invH = (float)ORB_GRID_ROWS / (K->max_y - K->min_y);
+  P.th = th;
+  P.logScale = logScale;
+  P.nLevels = K->n_levels;
+  P.thr = thr;
+  for (int l = 0; l < K->n_levels; ++l) P.scale[l] = K->scale_factors[l];
+  return ORB_OK;
+}
+
+// upload the searched (key)frame and build its grid; slots 0..3
+static orb_status_t pp_frame(orb_matcher_t* m, const orb_frame_t* K, const PPParamsHost& P,
+                             int slot, hipStream_t s) {
+  orb_status_t st;
+  const int n = K->n;
+  if (n > 0 && (!K->keys || !K->descriptors)) return ORB_EINVAL;
+  if ((st = upload(m->sx[slot], K->keys, (size_t)n * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(m->sx[slot + 1], K->descriptors, (size_t)n * 32, s))) return st;
+  if ((st = upload(m->sx[slot + 2], &n, 4, s))) return st;
+  if ((st = m->sx[slot + 3].ensure(((size_t)(ORB_GRID_COLS * ORB_GRID_ROWS + 1) + n + 1) * 4)))
+    return st;
+  int32_t* cs = m->sx[slot + 3].as<int32_t>();
+  HIP_TRY(orb_k_grid_build(m->sx[slot].as<orb_keypoint_t>(), m->sx[slot + 2].as<int32_t>(),
+                           std::max(n, 1), P.minX, P.minY, P.invW, P.invH, cs,
+                           cs + ORB_GRID_COLS * ORB_GRID_ROWS + 1, 1, s));
+  return ORB_OK;
+}
+
+static int32_t* pp_cells(orb_matcher_t* m, int slot) { return m->sx[slot + 3].as<int32_t>(); }
+static int32_t* pp_cellidx(orb_matcher_t* m, int slot) {
+  return m->sx[slot + 3].as<int32_t>() + ORB_GRID_COLS * ORB_GRID_ROWS + 1;
+}
+
+// Per-point matching of n_mp map points into the frame at `slot`; claiming
+// modes replay the first-come order into kp_match (host in/out, nkeys).
+static orb_status_t pp_run(orb_matcher_t* m, int mode, const PPParamsHost& P, int slot,
+                           const orb_frame_t* K, const uint8_t* kpLocked, int n_mp,
+                           const orb_map_point_t* mps, const uint8_t* valid,
+                           const uint8_t* skip, const uint8_t* mpDesc, const float* mpAngle,
+                           int32_t* best_host, int32_t* kp_match_host, int32_t* count_host,
+                           hipStream_t s, int32_t* best_dev = nullptr) {
+  orb_status_t st;
+  const bool claims = mode <= 1;
+  if (n_mp > 0 && (!mps || !mpDesc)) return ORB_EINVAL;
+  if ((st = upload(m->sx[8], mps, (size_t)n_mp * sizeof(orb_map_point_t), s))) return st;
+  if ((st = upload(m->sx[9], mpDesc, (size_t)n_mp * 32, s))) return st;
+  if (valid && (st = upload(m->sx[10], valid, (size_t)n_mp, s))) return st;
+  if (skip && (st = upload(m->sx[11], skip, (size_t)n_mp, s))) return st;
+  if (mpAngle && (st = upload(m->sx[12], mpAngle, (size_t)n_mp * 4, s))) return st;
+  if (K->u_right && (st = upload(m->sx[13], K->u_right, (size_t)K->n * 4, s))) return st;
+  if ((st = m->sx[14].ensure((size_t)std::max(n_mp, 1) * orb_k_pp_rec_size()))) return st;
+  if ((st = m->sx[15].ensure((size_t)std::max(n_mp, 1) * 16))) return st;   // topk
+  if ((st = m->sx[16].ensure((size_t)std::max(n_mp, 1) * 4))) return st;    // ncand
+  int32_t* best = best_dev;
+  if (!best) {
+    if ((st = m->sx[17].ensure((size_t)std::max(n_mp, 1) * 4))) return st;
+    best = m->sx[17].as<int32_t>();
+  }
+  HIP_TRY(orb_k_pp_match(mode, m->sx[8].as<orb_map_point_t>(),
+                         valid ? m->sx[10].as<uint8_t>() : nullptr,
+                         skip ? m->sx[11].as<uint8_t>() : nullptr, m->sx[9].as<uint8_t>(), n_mp,
+                         m->sx[slot].as<orb_keypoint_t>(), m->sx[slot + 1].as<uint8_t>(),
+                         K->u_right ? m->sx[13].as<float>() : nullptr, pp_cells(m, slot),
+                         pp_cellidx(m, slot), &P, m->sx[14].p, best, m->sx[15].as<uint32_t>(),
+                         m->sx[16].as<int32_t>(), s));
+  if (claims) {
+    const size_t lds = orb_k_pp_resolve_lds(K->n, n_mp);
+    if (lds > 160 * 1024) return ORB_ECAPACITY;
+    if (kpLocked && (st = upload(m->sx[18], kpLocked, (size_t)K->n, s))) return st;
+    if ((st = upload(m->sx[19], kp_match_host, (size_t)K->n * 4, s))) return st;
+    if ((st = m->sx[20].ensure(16))) return st;
+    HIP_TRY(orb_k_pp_resolve(m->sx[slot].as<orb_keypoint_t>(), m->sx[slot + 1].as<uint8_t>(),
+                             K->n, kpLocked ? m->sx[18].as<uint8_t>() : nullptr,
+                             m->sx[9].as<uint8_t>(), mpAngle ? m->sx[12].as<float>() : nullptr,
+                             n_mp, pp_cells(m, slot), pp_cellidx(m, slot), &P, m->sx[14].p,
+                             m->sx[15].as<uint32_t>(), m->sx[16].as<int32_t>(),
+                             m->sx[19].as<int32_t>(), m->sx[20].as<int32_t>(), s));
+    HIP_TRY(hipMemcpyAsync(kp_match_host, m->sx[19].p, (size_t)K->n * 4, hipMemcpyDeviceToHost,
+                           s));
+    HIP_TRY(hipMemcpyAsync(count_host, m->sx[20].p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else if (best_host) {
+    HIP_TRY(hipMemcpyAsync(best_host, best, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int c = 0;
+    for (int i = 0; i < n_mp; ++i) c += best_host[i] >= 0;
+    *count_host = c;
+  }
+  return ORB_OK;
+}
+
+orb_status_t orb_search_by_projection_reloc(orb_matcher_t* m, const orb_frame_t* frame,
+                                            const uint8_t* kp_locked, const orb_pose_t* pose,
+                                            const orb_camera_t* cam, float log_scale_factor,
+                                            int n_mp, const orb_map_point_t* mps,
+                                            const uint8_t* mp_desc, const float* kf_angle,
+                                            float th, int orb_dist, int check_orientation,
+                                            int32_t* kp_match, int32_t* nmatches) {
+  if (!m || !frame || !pose || !nmatches || n_mp < 0 || frame->n < 0 ||
+      (frame->n > 0 && !kp_match) || (n_mp > 0 && check_orientation && !kf_angle))
+    return ORB_EINVAL;
+  PPParamsHost P;
+  orb_status_t st = pp_base(P, frame, cam, log_scale_factor, th, orb_dist);
+  if (st) return st;
+  memcpy(P.R, pose->rcw, sizeof(P.R));
+  memcpy(P.t, pose->tcw, sizeof(P.t));
+  memcpy(P.Ow, pose->ow, sizeof(P.Ow));
+  P.checkOri = check_orientation ? 1 : 0;
+  *nmatches = 0;
+  for (int j = 0; j < frame->n; ++j) kp_match[j] = -1;
+  if (frame->n == 0 || n_mp == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  if ((st = pp_frame(m, frame, P, 0, s))) return st;
+  return pp_run(m, 0, P, 0, frame, kp_locked, n_mp, mps, nullptr, nullptr, mp_desc,
+                check_orientation ? kf_angle : nullptr, nullptr, kp_match, nmatches, s);
+}
+
+orb_status_t orb_search_by_projection_sim3(orb_matcher_t* m, const orb_frame_t* kf,
+                                           const float* scw, const orb_camera_t* cam,
+                                           float log_scale_factor, int n_mp,
+                                           const orb_map_point_t* mps, const uint8_t* mp_desc,
+                                           float th, int32_t* kp_matched, int32_t* nmatches) {
+  if (!m || !kf || !scw || !nmatches || n_mp < 0 || kf->n < 0 || (kf->n > 0 && !kp_matched))
+    return ORB_EINVAL;
+  PPParamsHost P;
+  orb_status_t st = pp_base(P, kf, cam, log_scale_factor, th, 50);
+  if (st) return st;
+  sim3_normalise(scw, P.R, P.t, P.Ow);
+  *nmatches = 0;
+  if (kf->n == 0 || n_mp == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  if ((st = pp_frame(m, kf, P, 0, s))) return st;
+  return pp_run(m, 1, P, 0, kf, nullptr, n_mp, mps, nullptr, nullptr, mp_desc, nullptr, nullptr,
+                kp_matched, nmatches, s);
+}
+
+orb_status_t orb_fuse(orb_matcher_t* m, const orb_frame_t* kf, const float* inv_level_sigma2,
+                      const orb_pose_t* pose, const orb_camera_t* cam, float log_scale_factor,
+                      int n_mp, const orb_map_point_t* mps, const uint8_t* mp_desc, float th,
+                      int32_t* fuse_idx, int32_t* n_fuse) {
+  if (!m || !kf || !pose || !inv_level_sigma2 || !n_fuse || n_mp < 0 || kf->n < 0 ||
+      (n_mp > 0 && !fuse_idx))
+    return ORB_EINVAL;
+  PPParamsHost P;
+  orb_status_t st = pp_base(P, kf, cam, log_scale_factor, th, 50);
+  if (st) return st;
+  memcpy(P.R, pose->rcw, sizeof(P.R));
+  memcpy(P.t, pose->tcw, sizeof(P.t));
+  memcpy(P.Ow, pose->ow, sizeof(P.Ow));
+  for (int l = 0; l < kf->n_levels; ++l) P.invSigma2[l] = inv_level_sigma2[l];
+  *n_fuse = 0;
+  for (int i = 0; i < n_mp; ++i) fuse_idx[i] = -1;
+  if (kf->n == 0 || n_mp == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  if ((st = pp_frame(m, kf, P, 0, s))) return st;
+  return pp_run(m, 2, P, 0, kf, nullptr, n_mp, mps, nullptr, nullptr, mp_desc, nullptr,
+                fuse_idx, nullptr, n_fuse, s);
+}
+
+orb_status_t orb_fuse_sim3(orb_matcher_t* m, const orb_frame_t* kf, const float* scw,
+                           const orb_camera_t* cam, float log_scale_factor, int n_mp,
+                           const orb_map_point_t* mps, const uint8_t* mp_desc, float th,
+                           int32_t* fuse_idx, int32_t* n_fuse) {
+  if (!m || !kf || !scw || !n_fuse || n_mp < 0 || kf->n < 0 || (n_mp > 0 && !fuse_idx))
+    return ORB_EINVAL;
+  PPParamsHost P;
+  orb_status_t st = pp_base(P, kf, cam, log_scale_factor, th, 50);
+  if (st) return st;
+  sim3_normalise(scw, P.R, P.t, P.Ow);
+  *n_fuse = 0;
+  for (int i = 0; i < n_mp; ++i) fuse_idx[i] = -1;
+  if (kf->n == 0 || n_mp == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  if ((st = pp_frame(m, kf, P, 0, s))) return st;
+  return pp_run(m, 3, P, 0, kf, nullptr, n_mp, mps, nullptr, nullptr, mp_desc, nullptr,
+                fuse_idx, nullptr, n_fuse, s);
+}
+
+orb_status_t orb_search_by_sim3(orb_matcher_t* m, const orb_frame_t* kf1, const orb_frame_t* kf2,
+                                float log_scale_factor, const orb_camera_t* cam,
+                                const float* r1w, const float* t1w, const float* r2w,
+                                const float* t2w, const orb_map_point_t* mps1,
+                                const uint8_t* valid1, const uint8_t* already1,
+                                const uint8_t* mp_desc1, const orb_map_point_t* mps2,
+                                const uint8_t* valid2, const uint8_t* already2,
+                                const uint8_t* mp_desc2, float s12, const float* r12,
+                                const float* t12, float th, int32_t* match12,
+                                int32_t* nfound) {
+  if (!m || !kf1 || !kf2 || !r1w || !t1w || !r2w || !t2w || !r12 || !t12 || !nfound ||
+      kf1->n < 0 || kf2->n < 0 || (kf1->n > 0 && (!mps1 || !valid1 || !mp_desc1 || !match12)) ||
+      (kf2->n > 0 && (!mps2 || !valid2 || !mp_desc2)))
+    return ORB_EINVAL;
+  PPParamsHost P1, P2;  // P1: KF1 points into KF2, P2: KF2 points into KF1
+  orb_status_t st;
+  if ((st = pp_base(P1, kf2, cam, log_scale_factor, th, 100))) return st;
+  if ((st = pp_base(P2, kf1, cam, log_scale_factor, th, 100))) return st;
+  float sR12[9], sR21[9], t21[3];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      sR12[3 * r + c] = (float)((double)s12 * (double)r12[3 * r + c]);
+      sR21[3 * r + c] = (float)((1.0 / (double)s12) * (double)r12[3 * c + r]);
+    }
+  for (int r = 0; r < 3; ++r)  // t21 = -sR21 * t12 (:1235)
+    t21[r] = -((sR21[3 * r] * t12[0] + sR21[3 * r + 1] * t12[1]) + sR21[3 * r + 2] * t12[2]);
+  memcpy(P1.R, r1w, 36); memcpy(P1.t, t1w, 12); memcpy(P1.R2, sR21, 36); memcpy(P1.t2, t21, 12);
+  memcpy(P2.R, r2w, 36); memcpy(P2.t, t2w, 12); memcpy(P2.R2, sR12, 36); memcpy(P2.t2, t12, 12);
+  *nfound = 0;
+  for (int i = 0; i < kf1->n; ++i) match12[i] = -1;
+  if (kf1->n == 0 || kf2->n == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  if ((st = pp_frame(m, kf2, P1, 0, s))) return st;
+  if ((st = pp_frame(m, kf1, P2, 4, s))) return st;
+  if ((st = m->sx[21].ensure((size_t)kf1->n * 4))) return st;
+  if ((st = m->sx[22].ensure((size_t)kf2->n * 4))) return st;
+  if ((st = m->sx[23].ensure((size_t)kf1->n * 4 + 16))) return st;
+  // direction 1 runs to completion before its point buffers are reused
+  if ((st = pp_run(m, 4, P1, 0, kf2, nullptr, kf1->n, mps1, valid1, already1, mp_desc1, nullptr,
+                   nullptr, nullptr, nullptr, s, m->sx[21].as<int32_t>())))
+    return st;
+  HIP_TRY(hipStreamSynchronize(s));
+  if ((st = pp_run(m, 4, P2, 4, kf1, nullptr, kf2->n, mps2, valid2, already2, mp_desc2, nullptr,
+                   nullptr, nullptr, nullptr, s, m->sx[22].as<int32_t>())))
+    return st;
+  int32_t* out = m->sx[23].as<int32_t>();
+  HIP_TRY(orb_k_sim3_mutual(m->sx[21].as<int32_t>(), kf1->n, m->sx[22].as<int32_t>(), out,
+                            out + kf1->n, s));
+  HIP_TRY(hipMemcpyAsync(match12, out, (size_t)kf1->n * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nfound, out + kf1->n, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_match_bow_kf(orb_matcher_t* m, int n1, const uint8_t* desc1,
+                              const float* angle1, const int32_t* mp1, const uint8_t* mp1_bad,
+                              int nodes1, const uint32_t* node_ids1, const int32_t* offs1,
+                              const uint32_t* feats1, int n2, const uint8_t* desc2,
+                              const float* angle2, const int32_t* mp2, const uint8_t* mp2_bad,
+                              int nodes2, const uint32_t* node_ids2, const int32_t* offs2,
+                              const uint32_t* feats2, float nnratio, int check_orientation,
+                              int32_t* match12, int32_t* nmatches) {
+  if (!m || n1 < 0 || n2 < 0 || nodes1 < 0 || nodes2 < 0 || !nmatches ||
+      (n1 > 0 && (!desc1 || !angle1 || !mp1 || !match12)) ||
+      (n2 > 0 && (!desc2 || !angle2 || !mp2)) || (nodes1 > 0 && (!node_ids1 || !offs1)) ||
+      (nodes2 > 0 && (!node_ids2 || !offs2)))
+    return ORB_EINVAL;
+  *nmatches = 0;
+  for (int i = 0; i < n1; ++i) match12[i] = -1;
+  if (n1 == 0 || n2 == 0 || nodes1 == 0 || nodes2 == 0) return ORB_OK;
+  if ((size_t)4 * ((n2 + 31) / 32) * 4 > 65536) return ORB_ECAPACITY;
+  const int nF1 = offs1[nodes1], nF2 = offs2[nodes2];
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  orb_status_t st;
+  DevBuf* b = m->sx;
+  if ((st = upload(b[0], desc1, (size_t)n1 * 32, s))) return st;
+  if ((st = upload(b[1], angle1, (size_t)n1 * 4, s))) return st;
+  if ((st = upload(b[2], mp1, (size_t)n1 * 4, s))) return st;
+  if (mp1_bad && (st = upload(b[3], mp1_bad, (size_t)n1, s))) return st;
+  if ((st = upload(b[4], node_ids1, (size_t)nodes1 * 4, s))) return st;
+  if ((st = upload(b[5], offs1, (size_t)(nodes1 + 1) * 4, s))) return st;
+  if ((st = upload(b[6], feats1, (size_t)nF1 * 4, s))) return st;
+  if ((st = upload(b[7], desc2, (size_t)n2 * 32, s))) return st;
+  if ((st = upload(b[8], angle2, (size_t)n2 * 4, s))) return st;
+  if ((st = upload(b[9], mp2, (size_t)n2 * 4, s))) return st;
+  if (mp2_bad && (st = upload(b[10], mp2_bad, (size_t)n2, s))) return st;
+  if ((st = upload(b[11], node_ids2, (size_t)nodes2 * 4, s))) return st;
+  if ((st = upload(b[12], offs2, (size_t)(nodes2 + 1) * 4, s))) return st;
+  if ((st = upload(b[13], feats2, (size_t)nF2 * 4, s))) return st;
+  if ((st = b[14].ensure((size_t)n1 * 4))) return st;
+  if ((st = b[15].ensure((size_t)std::max(nF1, 1) * 4))) return st;
+  if ((st = b[16].ensure(16))) return st;
+  HIP_TRY(hipMemsetAsync(b[14].p, 0xFF, (size_t)n1 * 4, s));
+  HIP_TRY(orb_k_bow(b[0].as<uint8_t>(), b[1].as<float>(), b[2].as<int32_t>(),
+                    mp1_bad ? b[3].as<uint8_t>() : nullptr, nodes1, b[4].as<uint32_t>(),
+                    b[5].as<int32_t>(), b[6].as<uint32_t>(), nF1, b[7].as<uint8_t>(),
+                    b[8].as<float>(), nodes2, b[11].as<uint32_t>(), b[12].as<int32_t>(),
+                    b[13].as<uint32_t>(), n2, b[9].as<int32_t>(),
+                    mp2_bad ? b[10].as<uint8_t>() : nullptr, 49, nnratio, check_orientation,
+                    b[14].as<int32_t>(), b[15].as<int32_t>(), b[16].as<int32_t>(), s));
+  HIP_TRY(hipMemcpyAsync(match12, b[14].p, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nmatches, b[16].p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_search_for_triangulation(
+    orb_matcher_t* m, const orb_frame_t* kf1, const uint8_t* has_mp1, const orb_frame_t* kf2,
+    const uint8_t* has_mp2, const float* level_sigma2, const float* f12,
+    const orb_camera_t* cam, const float* cw, const float* r2w, const float* t2w, int nodes1,
+    const uint32_t* node_ids1, const int32_t* offs1, const uint32_t* feats1, int nodes2,
+    const uint32_t* node_ids2, const int32_t* offs2, const uint32_t* feats2, int only_stereo,
+    int check_orientation, int32_t* match12, int32_t* nmatches) {
+  if (!m || !kf1 || !kf2 || !level_sigma2 || !f12 || !cam || !cw || !r2w || !t2w || !nmatches ||
+      kf1->n < 0 || kf2->n < 0 || nodes1 < 0 || nodes2 < 0 || !kf2->scale_factors ||
+      kf2->n_levels <= 0 || kf2->n_levels > ORB_MAX_LEVELS ||
+      (kf1->n > 0 && (!kf1->keys || !kf1->descriptors || !has_mp1 || !match12)) ||
+      (kf2->n > 0 && (!kf2->keys || !kf2->descriptors || !has_mp2)) ||
+      (nodes1 > 0 && (!node_ids1 || !offs1)) || (nodes2 > 0 && (!node_ids2 || !offs2)))
+    return ORB_EINVAL;
+  TriParamsHost T;
+  memset(&T, 0, sizeof(T));
+  memcpy(T.F, f12, sizeof(T.F));
+  float C2[3];
+  rt_xform(r2w, t2w, cw, C2);  // epipole of KF1 in KF2 (:728-733)
+  const float invz = 1.0f / C2[2];
+  T.ex = cam->fx * C2[0] * invz + cam->cx;
+  T.ey = cam->fy * C2[1] * invz + cam->cy;
+  T.onlyStereo = only_stereo ? 1 : 0;
+  T.checkOri = check_orientation ? 1 : 0;
+  for (int l = 0; l < kf2->n_levels; ++l) {
+    T.scale[l] = kf2->scale_factors[l];
+    T.sigma2[l] = level_sigma2[l];
+  }
+  *nmatches = 0;
+  for (int i = 0; i < kf1->n; ++i) match12[i] = -1;
+  if (kf1->n == 0 || kf2->n == 0 || nodes1 == 0 || nodes2 == 0) return ORB_OK;
+  const int nF1 = offs1[nodes1], nF2 = offs2[nodes2];
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  orb_status_t st;
+  DevBuf* b = m->sx;
+  const int n1 = kf1->n, n2 = kf2->n;
+  if ((st = upload(b[0], kf1->keys, (size_t)n1 * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(b[1], kf1->descriptors, (size_t)n1 * 32, s))) return st;
+  if (kf1->u_right && (st = upload(b[2], kf1->u_right, (size_t)n1 * 4, s))) return st;
+  if ((st = upload(b[3], has_mp1, (size_t)n1, s))) return st;
+  if ((st = upload(b[4], node_ids1, (size_t)nodes1 * 4, s))) return st;
+  if ((st = upload(b[5], offs1, (size_t)(nodes1 + 1) * 4, s))) return st;
+  if ((st = upload(b[6], feats1, (size_t)nF1 * 4, s))) return st;
+  if ((st = upload(b[7], kf2->keys, (size_t)n2 * sizeof(orb_keypoint_t), s))) return st;
+  if ((st = upload(b[8], kf2->descriptors, (size_t)n2 * 32, s))) return st;
+  if (kf2->u_right && (st = upload(b[9], kf2->u_right, (size_t)n2 * 4, s))) return st;
+  if ((st = upload(b[10], has_mp2, (size_t)n2, s))) return st;
+  if ((st = upload(b[11], node_ids2, (size_t)nodes2 * 4, s))) return st;
+  if ((st = upload(b[12], offs2, (size_t)(nodes2 + 1) * 4, s))) return st;
+  if ((st = upload(b[13], feats2, (size_t)nF2 * 4, s))) return st;
+  if ((st = b[14].ensure((size_t)n1 * 4))) return st;
+  if ((st = b[15].ensure((size_t)std::max(nF1, 1) * 4))) return st;
+  if ((st = b[16].ensure(16))) return st;
+  HIP_TRY(hipMemsetAsync(b[14].p, 0xFF, (size_t)n1 * 4, s));
+  HIP_TRY(orb_k_triangulation(
+      b[0].as<orb_keypoint_t>(), b[1].as<uint8_t>(), kf1->u_right ? b[2].as<float>() : nullptr,
+      b[3].as<uint8_t>(), nodes1, b[4].as<uint32_t>(), b[5].as<int32_t>(), b[6].as<uint32_t>(),
+      nF1, b[7].as<orb_keypoint_t>(), b[8].as<uint8_t>(),
+      kf2->u_right ? b[9].as<float>() : nullptr, b[10].as<uint8_t>(), nodes2,
+      b[11].as<uint32_t>(), b[12].as<int32_t>(), b[13].as<uint32_t>(), &T, b[14].as<int32_t>(),
+      b[15].as<int32_t>(), b[16].as<int32_t>(), s));
+  HIP_TRY(hipMemcpyAsync(match12, b[14].p, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nmatches, b[16].p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
   return ORB_OK;
 }
 
