@@ -41,6 +41,15 @@
  *   orb_search_by_sim3             SearchBySim3              src/ORBmatcher.cc:1212-1458
  *   orb_match_bow_kf               SearchByBoW(KeyFrame*, KeyFrame*, ...) src/ORBmatcher.cc:581-716
  *   orb_search_for_triangulation   SearchForTriangulation    src/ORBmatcher.cc:718-901
+ *   orb_vocabulary_create / _load_text / _destroy
+ *                                  DBoW2 TemplatedVocabulary ctor + loadFromTextFile
+ *                                  Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1362-1448
+ *                                  (ORBVocabulary, include/ORBVocabulary.h; loaded by
+ *                                  System::System src/System.cc)
+ *   orb_vocabulary_transform(_batch)  Frame::ComputeBoW src/Frame.cc:439-449,
+ *                                  KeyFrame::ComputeBoW src/KeyFrame.cc:60-71 ->
+ *                                  TemplatedVocabulary::transform(features, BowVector&,
+ *                                  FeatureVector&, levelsup) TemplatedVocabulary.h:1128-1283
  *
  * Error behaviour: the reference has no status codes (an empty image returns
  * silently with outputs untouched, src/ORBextractor.cc:1095-1096; a non-8UC1
@@ -470,6 +479,63 @@ orb_status_t orb_search_for_triangulation(
     const uint32_t* node_ids1, const int32_t* offs1, const uint32_t* feats1, int nodes2,
     const uint32_t* node_ids2, const int32_t* offs2, const uint32_t* feats2, int only_stereo,
     int check_orientation, int32_t* match12, int32_t* nmatches);
+
+/* ------------------------------------------------------ DBoW2 vocabulary */
+
+typedef struct orb_vocabulary orb_vocabulary_t;
+
+/* ScoringType / WeightingType values (Thirdparty/DBoW2/DBoW2/BowVector.h:36-53). */
+#define ORB_VOC_L1_NORM 0
+#define ORB_VOC_L2_NORM 1
+#define ORB_VOC_CHI_SQUARE 2
+#define ORB_VOC_KL 3
+#define ORB_VOC_BHATTACHARYYA 4
+#define ORB_VOC_DOT_PRODUCT 5
+#define ORB_VOC_TF_IDF 0
+#define ORB_VOC_TF 1
+#define ORB_VOC_IDF 2
+#define ORB_VOC_BINARY 3
+
+/* A vocabulary tree from the node table loadFromTextFile builds
+ * (TemplatedVocabulary.h:1400-1444): node 0 is the root; node i >= 1 has
+ * parent[i] < i (its children are ordered by id), leaf_flag[i] (word ids go to
+ * flagged nodes in id order), descriptor 32 bytes at descriptors + 32 i and
+ * weight[i].  Entry 0 of each array is ignored.  k, L, scoring, weighting as in
+ * the text header (validated as at :1383).  The tree is copied to the device. */
+orb_status_t orb_vocabulary_create(int device, int k, int L, int scoring, int weighting,
+                                   int n_nodes, const int32_t* parent, const uint8_t* leaf_flag,
+                                   const uint8_t* descriptors, const double* weights,
+                                   orb_vocabulary_t** out);
+/* loadFromTextFile(path) (ORBvoc.txt format). */
+orb_status_t orb_vocabulary_load_text(int device, const char* path, orb_vocabulary_t** out);
+void orb_vocabulary_destroy(orb_vocabulary_t* v);
+/* info6 = {k, L, scoring, weighting, nodes (incl. root), words}. */
+orb_status_t orb_vocabulary_info(const orb_vocabulary_t* v, int32_t* info6);
+void* orb_vocabulary_stream(orb_vocabulary_t* v);
+
+/* transform(desc rows, mBowVec, mFeatVec, levelsup) for one frame of n <= 8192
+ * descriptors.  BowVector (std::map<WordId, double>) as bow_words ascending +
+ * bow_values; FeatureVector (std::map<NodeId, vector<unsigned>>) as CSR in
+ * the orb_match_bow layout: fv_nodes ascending, fv_offs[n_fv_nodes + 1],
+ * fv_feats.  Every output holds up to n entries (fv_offs n + 1).  Optional
+ * per-feature feat_word (0xFFFFFFFF = stopped, weight <= 0) and feat_node. */
+orb_status_t orb_vocabulary_transform(orb_vocabulary_t* v, int n, const uint8_t* desc,
+                                      int levelsup, uint32_t* bow_words, double* bow_values,
+                                      int32_t* n_words, uint32_t* fv_nodes, int32_t* fv_offs,
+                                      uint32_t* fv_feats, int32_t* n_fv_nodes,
+                                      uint32_t* feat_word, uint32_t* feat_node);
+/* Device-batched form: frame f has d_counts[f] descriptors at
+ * d_desc + 32 * f * stride (stride <= 8192).  Per-frame outputs at offset
+ * f * stride (fv_offs: f * (stride + 1)); d_feat_* are per-feature scratch
+ * (also outputs) of n_frames * stride entries.  Asynchronous on `stream`. */
+orb_status_t orb_vocabulary_transform_batch(orb_vocabulary_t* v, int n_frames,
+                                            const int32_t* d_counts, const uint8_t* d_desc,
+                                            int stride, int levelsup, uint32_t* d_feat_word,
+                                            double* d_feat_weight, uint32_t* d_feat_node,
+                                            uint32_t* d_bow_words, double* d_bow_values,
+                                            int32_t* d_n_words, uint32_t* d_fv_nodes,
+                                            int32_t* d_fv_offs, uint32_t* d_fv_feats,
+                                            int32_t* d_n_fv_nodes, void* stream);
 
 /* ---------------------------------------------------------- synthetic input */
 

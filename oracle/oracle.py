@@ -571,3 +571,59 @@ def search_for_triangulation(kf1, kf2, level_sigma2, F12, cam, Cw, R2w, t2w, fv1
            _p(C), _p(R), _p(t), len(fv1[0]), _p(fv1[0]), _p(fv1[1]), _p(fv1[2]), len(fv2[0]),
            _p(fv2[0]), _p(fv2[1]), _p(fv2[2]), int(only_stereo), int(check_ori), _p(m12))
     return n, m12
+
+
+def vocab_transform(voc, desc, levelsup=4, scoring=0, weighting=0):
+    """TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
+    (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1128-1283) on the node table
+    `voc` (dict parent/leaf/desc/weight, k, L).  Returns (bow_words, bow_values,
+    fv_nodes, fv_offs, fv_feats, feat_word, feat_node)."""
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(desc)
+    parent = np.ascontiguousarray(voc["parent"], np.int32)
+    leaf = np.ascontiguousarray(voc["leaf"], np.uint8)
+    nd = np.ascontiguousarray(voc["desc"], np.uint8)
+    nw = np.ascontiguousarray(voc["weight"], np.float64)
+    cap = max(n, 1)
+    bw = np.zeros(cap, np.uint32)
+    bv = np.zeros(cap, np.float64)
+    fvn = np.zeros(cap, np.uint32)
+    fvo = np.zeros(cap + 1, np.int32)
+    fvf = np.zeros(cap, np.uint32)
+    fw = np.zeros(cap, np.uint32)
+    fnode = np.zeros(cap, np.uint32)
+    n_words = ctypes.c_int(0)
+    n_fv = ctypes.c_int(0)
+    fn = lib().oracle_vocab_transform
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    fn.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
+                   vp, vp, vp]
+    fn.restype = i32
+    r = fn(int(voc["k"]), int(voc["L"]), scoring, weighting, len(parent), _p(parent), _p(leaf),
+           _p(nd), _p(nw), n, _p(desc), levelsup, _p(bw), _p(bv), ctypes.byref(n_words), _p(fvn),
+           _p(fvo), _p(fvf), ctypes.byref(n_fv), _p(fw), _p(fnode))
+    if r != 0:
+        raise ValueError("malformed vocabulary node table")
+    a, b = n_words.value, n_fv.value
+    return (bw[:a], bv[:a], fvn[:b], fvo[:b + 1], fvf[:fvo[b]], fw[:n], fnode[:n])
+
+
+def vocab_parse_text(path):
+    """loadFromTextFile (TemplatedVocabulary.h:1362-1448): the header and node
+    table, as a dict like tests/scenarios.vocabulary returns (plus scoring,
+    weighting)."""
+    fn = lib().oracle_vocab_parse_text
+    vp = ctypes.c_void_p
+    fn.argtypes = [ctypes.c_char_p, vp, ctypes.c_int, vp, vp, vp, vp]
+    fn.restype = ctypes.c_int
+    hdr = np.zeros(4, np.int32)
+    n = fn(str(path).encode(), _p(hdr), 0, None, None, None, None)
+    if n < 0:
+        raise ValueError(f"cannot parse vocabulary {path}")
+    parent = np.zeros(n, np.int32)
+    leaf = np.zeros(n, np.uint8)
+    desc = np.zeros((n, 32), np.uint8)
+    weight = np.zeros(n, np.float64)
+    fn(str(path).encode(), _p(hdr), n, _p(parent), _p(leaf), _p(desc), _p(weight))
+    return dict(k=int(hdr[0]), L=int(hdr[1]), scoring=int(hdr[2]), weighting=int(hdr[3]),
+                parent=parent, leaf=leaf, desc=desc, weight=weight)

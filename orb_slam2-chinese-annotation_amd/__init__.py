@@ -148,6 +148,14 @@ def lib() -> ctypes.CDLL:
                                    i32, vp, vp, vp, f32, i32, vp, vp]),
         "orb_search_for_triangulation": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32,
                                                vp, vp, vp, i32, vp, vp, vp, i32, i32, vp, vp]),
+        "orb_vocabulary_create": (i32, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
+        "orb_vocabulary_load_text": (i32, [i32, ctypes.c_char_p, vp]),
+        "orb_vocabulary_destroy": (None, [vp]),
+        "orb_vocabulary_info": (i32, [vp, vp]),
+        "orb_vocabulary_stream": (vp, [vp]),
+        "orb_vocabulary_transform": (i32, [vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "orb_vocabulary_transform_batch": (i32, [vp, i32, vp, vp, i32, i32, vp, vp, vp, vp, vp,
+                                                 vp, vp, vp, vp, vp, vp]),
         "orb_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
         "orb_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     }
@@ -748,3 +756,98 @@ class ORBmatcher:
         _check(lib().orb_distinctive_descriptors_batch(self._h, n_mp, d_offs, d_desc, d_best,
                                                        d_out, stream or None),
                "distinctive_descriptors_batch")
+
+
+# ------------------------------------------------------------------ vocabulary
+class ORBVocabulary:
+    """DBoW2 TemplatedVocabulary<FORB::TDescriptor, FORB> (include/ORBVocabulary.h),
+    device-resident.  Built from a loadFromTextFile node table
+    (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1362-1448) or a text file.
+    Scoring / weighting codes as BowVector.h:36-53 (L1_NORM 0 ... DOT_PRODUCT 5;
+    TF_IDF 0, TF 1, IDF 2, BINARY 3)."""
+
+    def __init__(self, k: int, L: int, parent, leaf, descriptors, weights, scoring: int = 0,
+                 weighting: int = 0, device: int = 0, _handle=None):
+        if _handle is not None:
+            self._h = _handle
+        else:
+            parent = np.ascontiguousarray(parent, np.int32)
+            leaf = np.ascontiguousarray(leaf, np.uint8)
+            desc = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
+            w = np.ascontiguousarray(weights, np.float64)
+            n = len(parent)
+            if not (len(leaf) == n and len(desc) == n and len(w) == n):
+                raise ValueError("vocabulary node table arrays differ in length")
+            h = ctypes.c_void_p()
+            _check(lib().orb_vocabulary_create(device, k, L, scoring, weighting, n, _ptr(parent),
+                                               _ptr(leaf), _ptr(desc), _ptr(w), ctypes.byref(h)),
+                   "orb_vocabulary_create")
+            self._h = h
+        info = np.zeros(6, np.int32)
+        _check(lib().orb_vocabulary_info(self._h, _ptr(info)), "orb_vocabulary_info")
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = map(int, info)
+
+    @classmethod
+    def loadFromTextFile(cls, path, device: int = 0) -> "ORBVocabulary":
+        h = ctypes.c_void_p()
+        _check(lib().orb_vocabulary_load_text(device, str(path).encode(), ctypes.byref(h)),
+               "orb_vocabulary_load_text")
+        return cls(0, 0, None, None, None, None, _handle=h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orb_vocabulary_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return self.n_words
+
+    def empty(self) -> bool:
+        return self.n_words == 0
+
+    @property
+    def stream(self) -> int:
+        return lib().orb_vocabulary_stream(self._h) or 0
+
+    def transform(self, descriptors, levelsup: int = 4, per_feature: bool = False):
+        """transform(features, BowVector&, FeatureVector&, levelsup) as called by
+        Frame::ComputeBoW (src/Frame.cc:439-449).  Returns (bow_words, bow_values,
+        feat_vec) with feat_vec = (node ids, CSR offsets, feature indices) in the
+        layout ORBmatcher.SearchByBoW takes; with per_feature also (word per
+        feature, 0xFFFFFFFF if stopped; FeatureVector node per feature)."""
+        d = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
+        n = len(d)
+        cap = max(n, 1)
+        bw = np.zeros(cap, np.uint32)
+        bv = np.zeros(cap, np.float64)
+        fvn = np.zeros(cap, np.uint32)
+        fvo = np.zeros(cap + 1, np.int32)
+        fvf = np.zeros(cap, np.uint32)
+        fw = np.zeros(cap, np.uint32) if per_feature else None
+        fn = np.zeros(cap, np.uint32) if per_feature else None
+        nw = ctypes.c_int(0)
+        nf = ctypes.c_int(0)
+        _check(lib().orb_vocabulary_transform(
+            self._h, n, _ptr(d) if n else None, levelsup, _ptr(bw), _ptr(bv), ctypes.byref(nw),
+            _ptr(fvn), _ptr(fvo), _ptr(fvf), ctypes.byref(nf),
+            _ptr(fw) if per_feature else None, _ptr(fn) if per_feature else None), "transform")
+        a, b = nw.value, nf.value
+        fv = (fvn[:b], fvo[:b + 1], fvf[:fvo[b]])
+        if per_feature:
+            return bw[:a], bv[:a], fv, fw[:n], fn[:n]
+        return bw[:a], bv[:a], fv
+
+    def transform_batch(self, n_frames, d_counts, d_desc, stride, levelsup, d_feat_word,
+                        d_feat_weight, d_feat_node, d_bow_words, d_bow_values, d_n_words,
+                        d_fv_nodes, d_fv_offs, d_fv_feats, d_n_fv_nodes, stream: int = 0):
+        """Device-resident batch form (raw device pointers, e.g. torch .data_ptr())."""
+        _check(lib().orb_vocabulary_transform_batch(
+            self._h, n_frames, d_counts, d_desc, stride, levelsup, d_feat_word, d_feat_weight,
+            d_feat_node, d_bow_words, d_bow_values, d_n_words, d_fv_nodes, d_fv_offs, d_fv_feats,
+            d_n_fv_nodes, stream or None), "transform_batch")

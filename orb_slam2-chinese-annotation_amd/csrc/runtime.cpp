@@ -128,6 +128,17 @@ hipError_t orb_k_search_init(const orb_keypoint_t* keys1, const uint8_t* desc1, 
 size_t orb_k_init_key_size(void);
 hipError_t orb_k_distinctive(const int32_t* offs, const uint8_t* desc, int nmp, int32_t* best,
                              uint8_t* out, hipStream_t s);
+hipError_t orb_k_voc_descend(const void* info, const void* ndesc, const uint32_t* nword,
+                             const double* nweight, const uint32_t* norig, int nidLevel,
+                             const uint8_t* desc, const int32_t* counts, int nSingle, int stride,
+                             int nFrames, uint32_t* fword, double* fweight, uint32_t* fnode,
+                             hipStream_t s);
+int orb_k_voc_max_features(void);
+hipError_t orb_k_voc_vectors(const uint32_t* fword, const double* fweight, const uint32_t* fnode,
+                             const int32_t* counts, int nSingle, int stride, int tf, int must,
+                             int l2, int nFrames, uint32_t* bowWords, double* bowValues,
+                             int32_t* nWords, uint32_t* fvNodes, int32_t* fvOffs,
+                             uint32_t* fvFeats, int32_t* nFv, hipStream_t s);
 }
 
 namespace {
@@ -2042,6 +2053,294 @@ orb_status_t orb_search_for_triangulation(
   HIP_TRY(hipMemcpyAsync(nmatches, b[16].p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return ORB_OK;
+}
+
+// ------------------------------------------------------- DBoW2 vocabulary
+// TemplatedVocabulary<FORB::TDescriptor, FORB> as loaded by loadFromTextFile
+// (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1362-1448) and its transform
+// (:1128-1283), the producer of Frame/KeyFrame::mBowVec and mFeatVec
+// (src/Frame.cc:439-449, src/KeyFrame.cc:60-71).  The tree lives on the
+// device, renumbered breadth-first (vocab_kernels.hip).
+struct orb_vocabulary {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  int k = 0, L = 0, scoring = 0, weighting = 0, nNodes = 0, nWords = 0;
+  DevBuf dInfo, dDesc, dWord, dWeight, dOrig;
+  DevBuf dIn, dCounts, dFWord, dFWeight, dFNode, dBowW, dBowV, dNW, dFvN, dFvO, dFvF, dNFv;
+};
+
+static orb_status_t vocab_build(orb_vocabulary* V, int n_nodes, const int32_t* parent,
+                                const uint8_t* leaf, const uint8_t* desc, const double* weight) {
+  // children in creation order (m_nodes[pid].children.push_back(nid), :1416)
+  std::vector<int32_t> ccount(n_nodes, 0), cstart(n_nodes + 1, 0), clist(std::max(n_nodes - 1, 1));
+  for (int i = 1; i < n_nodes; ++i) {
+    if (parent[i] < 0 || parent[i] >= i) return ORB_EINVAL;
+    ++ccount[parent[i]];
+  }
+  for (int i = 0; i < n_nodes; ++i) cstart[i + 1] = cstart[i] + ccount[i];
+  {
+    std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
+    for (int i = 1; i < n_nodes; ++i) clist[fill[parent[i]]++] = i;
+  }
+  // word ids: leaf-flagged nodes in file order (:1432-1439); others keep 0 (Node())
+  std::vector<uint32_t> wordOf(n_nodes, 0);
+  int nw = 0;
+  for (int i = 1; i < n_nodes; ++i)
+    if (leaf[i]) wordOf[i] = (uint32_t)nw++;
+  // breadth-first renumbering: children of the node at position p occupy
+  // consecutive positions, in child order
+  struct Info { int32_t first, count; };
+  std::vector<Info> info(n_nodes);
+  std::vector<int32_t> orig(n_nodes);
+  std::vector<uint8_t> ddesc((size_t)n_nodes * 32);
+  std::vector<uint32_t> dword(n_nodes);
+  std::vector<double> dweight(n_nodes);
+  orig[0] = 0;
+  int next = 1;
+  for (int p = 0; p < n_nodes; ++p) {
+    const int id = orig[p];
+    info[p].first = next;
+    info[p].count = ccount[id];
+    for (int c = cstart[id]; c < cstart[id + 1]; ++c) orig[next++] = clist[c];
+    memcpy(&ddesc[(size_t)p * 32], desc + (size_t)id * 32, 32);
+    dword[p] = wordOf[id];
+    dweight[p] = id == 0 ? 0.0 : weight[id];
+  }
+  if (next != n_nodes) return ORB_EINVAL;
+  V->nNodes = n_nodes;
+  V->nWords = nw;
+  hipStream_t s = V->stream;
+  orb_status_t st;
+  if ((st = upload(V->dInfo, info.data(), info.size() * sizeof(Info), s))) return st;
+  if ((st = upload(V->dDesc, ddesc.data(), ddesc.size(), s))) return st;
+  if ((st = upload(V->dWord, dword.data(), dword.size() * 4, s))) return st;
+  if ((st = upload(V->dWeight, dweight.data(), dweight.size() * 8, s))) return st;
+  if ((st = upload(V->dOrig, orig.data(), orig.size() * 4, s))) return st;
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+static orb_status_t vocab_new(int device, int k, int L, int scoring, int weighting,
+                              orb_vocabulary** out) {
+  orb_status_t st = check_device(device);
+  if (st) return st;
+  orb_vocabulary* V = new orb_vocabulary();
+  V->device = device;
+  V->k = k; V->L = L; V->scoring = scoring; V->weighting = weighting;
+  hipSetDevice(device);
+  if (hipStreamCreateWithFlags(&V->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete V;
+    return ORB_EDEVICE;
+  }
+  *out = V;
+  return ORB_OK;
+}
+
+orb_status_t orb_vocabulary_create(int device, int k, int L, int scoring, int weighting,
+                                   int n_nodes, const int32_t* parent, const uint8_t* leaf_flag,
+                                   const uint8_t* descriptors, const double* weights,
+                                   orb_vocabulary_t** out) {
+  if (!out) return ORB_EINVAL;
+  *out = nullptr;
+  // loadFromTextFile's header check (:1383)
+  if (k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 ||
+      weighting > 3 || n_nodes < 1 ||
+      (n_nodes > 1 && (!parent || !leaf_flag || !descriptors || !weights)))
+    return ORB_EINVAL;
+  orb_vocabulary* V = nullptr;
+  orb_status_t st = vocab_new(device, k, L, scoring, weighting, &V);
+  if (st) return st;
+  std::vector<int32_t> p0(1, 0);
+  std::vector<uint8_t> l0(1, 0), d0(32, 0);
+  std::vector<double> w0(1, 0.0);
+  st = n_nodes > 1 ? vocab_build(V, n_nodes, parent, leaf_flag, descriptors, weights)
+                   : vocab_build(V, 1, p0.data(), l0.data(), d0.data(), w0.data());
+  if (st) {
+    orb_vocabulary_destroy(V);
+    return st;
+  }
+  *out = V;
+  return ORB_OK;
+}
+
+// Text format of loadFromTextFile: "k L scoring weighting", then one line per
+// node "parent isLeaf d0 .. d31 weight" (descriptor bytes as integers,
+// FORB::fromString FORB.cpp:120-135).  Lines without a parent field are
+// skipped (the reference's eof loop turns a trailing empty line into a root
+// child with an uninitialised descriptor).
+orb_status_t orb_vocabulary_load_text(int device, const char* path, orb_vocabulary_t** out) {
+  if (!out || !path) return ORB_EINVAL;
+  *out = nullptr;
+  FILE* fp = fopen(path, "rb");
+  if (!fp) return ORB_EINVAL;
+  std::vector<char> text;
+  {
+    char buf[1 << 16];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof(buf), fp)) > 0) text.insert(text.end(), buf, buf + r);
+    fclose(fp);
+  }
+  text.push_back('\0');
+  char* c = text.data();
+  char* eol = strchr(c, '\n');
+  int hdr[4];
+  for (int i = 0; i < 4; ++i) {
+    char* e;
+    const long v = strtol(c, &e, 10);
+    if (e == c || (eol && e > eol)) return ORB_EINVAL;
+    hdr[i] = (int)v;
+    c = e;
+  }
+  c = eol ? eol + 1 : c + strlen(c);
+  std::vector<int32_t> parent(1, 0);
+  std::vector<uint8_t> leaf(1, 0), desc(32, 0);
+  std::vector<double> weight(1, 0.0);
+  while (*c) {
+    char* le = strchr(c, '\n');
+    if (le) *le = '\0';
+    char* e;
+    const long pid = strtol(c, &e, 10);
+    if (e != c) {
+      c = e;
+      const long isLeaf = strtol(c, &e, 10);
+      c = e;
+      uint8_t d[32] = {0};
+      for (int i = 0; i < 32; ++i) {
+        const long v = strtol(c, &e, 10);
+        if (e == c) break;
+        d[i] = (uint8_t)v;
+        c = e;
+      }
+      const double w = strtod(c, &e);
+      parent.push_back((int32_t)pid);
+      leaf.push_back(isLeaf > 0);
+      desc.insert(desc.end(), d, d + 32);
+      weight.push_back(e == c ? 0.0 : w);
+    }
+    if (!le) break;
+    c = le + 1;
+  }
+  return orb_vocabulary_create(device, hdr[0], hdr[1], hdr[2], hdr[3], (int)parent.size(),
+                               parent.data(), leaf.data(), desc.data(), weight.data(), out);
+}
+
+void orb_vocabulary_destroy(orb_vocabulary_t* V) {
+  if (!V) return;
+  hipSetDevice(V->device);
+  hipStreamSynchronize(V->stream);
+  DevBuf* bufs[] = {&V->dInfo, &V->dDesc, &V->dWord, &V->dWeight, &V->dOrig, &V->dIn,
+                    &V->dCounts, &V->dFWord, &V->dFWeight, &V->dFNode, &V->dBowW, &V->dBowV,
+                    &V->dNW, &V->dFvN, &V->dFvO, &V->dFvF, &V->dNFv};
+  for (DevBuf* b : bufs) b->release();
+  hipStreamDestroy(V->stream);
+  delete V;
+}
+
+orb_status_t orb_vocabulary_info(const orb_vocabulary_t* V, int32_t* info6) {
+  if (!V || !info6) return ORB_EINVAL;
+  info6[0] = V->k; info6[1] = V->L; info6[2] = V->scoring; info6[3] = V->weighting;
+  info6[4] = V->nNodes; info6[5] = V->nWords;
+  return ORB_OK;
+}
+
+void* orb_vocabulary_stream(orb_vocabulary_t* V) { return V ? (void*)V->stream : nullptr; }
+
+static orb_status_t vocab_launch(orb_vocabulary* V, int n_frames, const int32_t* d_counts,
+                                 int n_single, const uint8_t* d_desc, int stride, int levelsup,
+                                 uint32_t* fword, double* fweight, uint32_t* fnode,
+                                 uint32_t* bw, double* bv, int32_t* nw, uint32_t* fvn,
+                                 int32_t* fvo, uint32_t* fvf, int32_t* nfv, hipStream_t s) {
+  int l2 = V->scoring == 1;
+  const int must = V->scoring != 5;  // ScoringObject.h:74-89
+  const int tf = V->weighting == 0 || V->weighting == 1;
+  if (V->nWords == 0) {  // empty(): v, fv cleared (:1136-1140)
+    HIP_TRY(hipMemsetAsync(nw, 0, (size_t)n_frames * 4, s));
+    HIP_TRY(hipMemsetAsync(nfv, 0, (size_t)n_frames * 4, s));
+    for (int f = 0; f < n_frames; ++f)
+      HIP_TRY(hipMemsetAsync(fvo + (size_t)f * (stride + 1), 0, 4, s));
+    return ORB_OK;
+  }
+  HIP_TRY(orb_k_voc_descend(V->dInfo.p, V->dDesc.p, V->dWord.as<uint32_t>(),
+                            V->dWeight.as<double>(), V->dOrig.as<uint32_t>(), V->L - levelsup,
+                            d_desc, d_counts, n_single, stride, n_frames, fword, fweight, fnode,
+                            s));
+  HIP_TRY(orb_k_voc_vectors(fword, fweight, fnode, d_counts, n_single, stride, tf, must, l2,
+                            n_frames, bw, bv, nw, fvn, fvo, fvf, nfv, s));
+  return ORB_OK;
+}
+
+orb_status_t orb_vocabulary_transform(orb_vocabulary_t* V, int n, const uint8_t* desc,
+                                      int levelsup, uint32_t* bow_words, double* bow_values,
+                                      int32_t* n_words, uint32_t* fv_nodes, int32_t* fv_offs,
+                                      uint32_t* fv_feats, int32_t* n_fv_nodes,
+                                      uint32_t* feat_word, uint32_t* feat_node) {
+  if (!V || n < 0 || n > orb_k_voc_max_features() || (n > 0 && !desc) || !bow_words ||
+      !bow_values || !n_words || !fv_nodes || !fv_offs || !fv_feats || !n_fv_nodes)
+    return ORB_EINVAL;
+  if (n == 0 || V->nWords == 0) {
+    *n_words = 0;
+    *n_fv_nodes = 0;
+    fv_offs[0] = 0;
+    return ORB_OK;
+  }
+  std::lock_guard<std::mutex> g(V->mu);
+  hipSetDevice(V->device);
+  hipStream_t s = V->stream;
+  orb_status_t st;
+  const size_t N = (size_t)n;
+  if ((st = upload(V->dIn, desc, N * 32, s))) return st;
+  if ((st = V->dFWord.ensure(N * 4)) || (st = V->dFWeight.ensure(N * 8)) ||
+      (st = V->dFNode.ensure(N * 4)) || (st = V->dBowW.ensure(N * 4)) ||
+      (st = V->dBowV.ensure(N * 8)) || (st = V->dNW.ensure(16)) || (st = V->dFvN.ensure(N * 4)) ||
+      (st = V->dFvO.ensure((N + 1) * 4)) || (st = V->dFvF.ensure(N * 4)) ||
+      (st = V->dNFv.ensure(16)))
+    return st;
+  if ((st = vocab_launch(V, 1, nullptr, n, V->dIn.as<uint8_t>(), n, levelsup,
+                         V->dFWord.as<uint32_t>(), V->dFWeight.as<double>(),
+                         V->dFNode.as<uint32_t>(), V->dBowW.as<uint32_t>(),
+                         V->dBowV.as<double>(), V->dNW.as<int32_t>(), V->dFvN.as<uint32_t>(),
+                         V->dFvO.as<int32_t>(), V->dFvF.as<uint32_t>(), V->dNFv.as<int32_t>(), s)))
+    return st;
+  int32_t counts[2];
+  HIP_TRY(hipMemcpyAsync(&counts[0], V->dNW.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&counts[1], V->dNFv.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *n_words = counts[0];
+  *n_fv_nodes = counts[1];
+  HIP_TRY(hipMemcpyAsync(bow_words, V->dBowW.p, (size_t)counts[0] * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(bow_values, V->dBowV.p, (size_t)counts[0] * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(fv_nodes, V->dFvN.p, (size_t)counts[1] * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(fv_offs, V->dFvO.p, (size_t)(counts[1] + 1) * 4, hipMemcpyDeviceToHost,
+                         s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const int nfeat = fv_offs[counts[1]];
+  if (nfeat > 0)
+    HIP_TRY(hipMemcpyAsync(fv_feats, V->dFvF.p, (size_t)nfeat * 4, hipMemcpyDeviceToHost, s));
+  if (feat_word) HIP_TRY(hipMemcpyAsync(feat_word, V->dFWord.p, N * 4, hipMemcpyDeviceToHost, s));
+  if (feat_node) HIP_TRY(hipMemcpyAsync(feat_node, V->dFNode.p, N * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_vocabulary_transform_batch(orb_vocabulary_t* V, int n_frames,
+                                            const int32_t* d_counts, const uint8_t* d_desc,
+                                            int stride, int levelsup, uint32_t* d_feat_word,
+                                            double* d_feat_weight, uint32_t* d_feat_node,
+                                            uint32_t* d_bow_words, double* d_bow_values,
+                                            int32_t* d_n_words, uint32_t* d_fv_nodes,
+                                            int32_t* d_fv_offs, uint32_t* d_fv_feats,
+                                            int32_t* d_n_fv_nodes, void* stream) {
+  if (!V || n_frames < 0 || stride <= 0 || stride > orb_k_voc_max_features()) return ORB_EINVAL;
+  if (n_frames == 0) return ORB_OK;
+  if (!d_counts || !d_desc || !d_feat_word || !d_feat_weight || !d_feat_node || !d_bow_words ||
+      !d_bow_values || !d_n_words || !d_fv_nodes || !d_fv_offs || !d_fv_feats || !d_n_fv_nodes)
+    return ORB_EINVAL;
+  hipSetDevice(V->device);
+  return vocab_launch(V, n_frames, d_counts, 0, d_desc, stride, levelsup, d_feat_word,
+                      d_feat_weight, d_feat_node, d_bow_words, d_bow_values, d_n_words,
+                      d_fv_nodes, d_fv_offs, d_fv_feats, d_n_fv_nodes,
+                      stream ? (hipStream_t)stream : V->stream);
 }
 
 // ------------------------------------------------------------ synthetic input

@@ -758,3 +758,77 @@ def search_for_triangulation(kf1, kf2, level_sigma2, F12, cam, Cw, R2w, t2w, fv1
                 for i1 in hist[bb]:
                     m12[i1] = -1
     return int((m12 >= 0).sum()), m12
+
+
+_POP8 = np.array([bin(i).count("1") for i in range(256)], np.int64)
+
+
+def vocab_transform(voc, desc, levelsup, scoring, weighting):
+    """DBoW2 TemplatedVocabulary::transform (TemplatedVocabulary.h:1128-1283),
+    written from the text a second time: children lists rebuilt from the
+    parent table in file order, descent by a first-index argmin (strict '<'),
+    BowVector / FeatureVector as dicts sorted at the end."""
+    parent = np.asarray(voc["parent"])
+    n_nodes = len(parent)
+    children = [[] for _ in range(n_nodes)]
+    for i in range(1, n_nodes):
+        children[int(parent[i])].append(i)
+    words = {}
+    for i in range(1, n_nodes):
+        if voc["leaf"][i]:
+            words[i] = len(words)
+    nd = np.asarray(voc["desc"], np.uint8)
+    L = int(voc["L"])
+    nid_level = L - levelsup
+    bow, fv = {}, {}
+    fword, fnode = [], []
+    tf = weighting in (0, 1)
+    if not words:
+        return [], [], [], [0], [], [], []
+    for i, f in enumerate(np.asarray(desc, np.uint8).reshape(-1, 32)):
+        node, level, nid = 0, 0, 0
+        nid_set = nid_level <= 0
+        while True:
+            level += 1
+            ch = children[node]
+            d = _POP8[np.bitwise_xor(nd[ch], f)].sum(axis=1)
+            node = ch[int(np.argmin(d))]  # first minimum
+            if level == nid_level:
+                nid, nid_set = node, True
+            if not children[node]:
+                break
+        if not nid_set:
+            nid = node
+        w = float(voc["weight"][node])
+        wid = words.get(node, 0)
+        fword.append(wid if w > 0 else 0xFFFFFFFF)
+        fnode.append(nid)
+        if w > 0:
+            if tf:
+                bow[wid] = bow[wid] + w if wid in bow else w
+            elif wid not in bow:
+                bow[wid] = w
+            fv.setdefault(nid, []).append(i)
+    keys = sorted(bow)
+    vals = [bow[k] for k in keys]
+    must = scoring != 5
+    if tf and vals and not must:
+        vals = [v / float(len(vals)) for v in vals]
+    if must:
+        norm = 0.0
+        if scoring == 1:
+            for v in vals:
+                norm += v * v
+            norm = math.sqrt(norm)
+        else:
+            for v in vals:
+                norm += abs(v)
+        if norm > 0.0:
+            vals = [v / norm for v in vals]
+    nodes = sorted(fv)
+    offs = [0]
+    feats = []
+    for k in nodes:
+        feats.extend(fv[k])
+        offs.append(len(feats))
+    return keys, vals, nodes, offs, feats, fword, fnode

@@ -280,3 +280,117 @@ def fundamental(kf1, kf2):
     K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1]])
     Ki = np.linalg.inv(K)
     return (Ki.T @ tx @ R12 @ Ki).astype(np.float32)
+
+
+def vocabulary(rng_seed=0, k=10, L=4, irregular=False, stop_frac=0.0, ties=False,
+               order="hkmeans"):
+    """Synthetic DBoW2 vocabulary tree as the node table loadFromTextFile builds
+    (TemplatedVocabulary.h:1400-1444).  The ORB vocabulary (ORBvoc.txt) is not in
+    the reference tree, so the tree is generated: each child descriptor is its
+    parent's with bits flipped (fewer further down), leaves at depth L carry an
+    idf-like weight > 0.  `order` "hkmeans" numbers nodes the way HKmeansStep
+    creates them (a node's children consecutive, then each child's subtree in
+    turn, :475-610) -- the order a saved vocabulary lists them in; "bfs" is
+    level order.  `irregular`: nodes with fewer than k children and leaves
+    above depth L (clusters with fewer than k descriptors stop early).
+    `stop_frac`: words with weight 0 (stopWords, :1349-1360).  `ties`: sibling
+    pairs with identical descriptors (first child must win, strict '<').
+    Returns dict(k, L, parent, leaf, desc, weight) with entry 0 the root."""
+    rng = np.random.default_rng(rng_seed)
+    # level-order construction: per node its children's count
+    levels = [np.zeros(1, np.int64)]  # node indices (bfs) per depth
+    parent_bfs = [-1]
+    depth = [0]
+    nchild_bfs = []
+    desc_bfs = [rng.integers(0, 256, 32, dtype=np.uint8)]
+    n = 1
+    for d in range(1, L + 1):
+        prev = levels[-1]
+        if irregular:
+            nc = np.where(rng.random(len(prev)) < 0.15, rng.integers(2, k + 1, len(prev)), k)
+            if d > 1:
+                nc = np.where(rng.random(len(prev)) < 0.06, 0, nc)  # early leaf
+        else:
+            nc = np.full(len(prev), k)
+        nchild_bfs.append(nc)
+        tot = int(nc.sum())
+        par = np.repeat(prev, nc)
+        levels.append(np.arange(n, n + tot))
+        parent_bfs.extend(par.tolist())
+        depth.extend([d] * tot)
+        n += tot
+    parent_bfs = np.array(parent_bfs, np.int64)
+    depth = np.array(depth, np.int64)
+    # descriptors: flip probability per depth
+    pflip = {1: 0.5, 2: 0.3, 3: 0.2, 4: 0.12, 5: 0.08, 6: 0.05}
+    desc = np.zeros((n, 32), np.uint8)
+    desc[0] = desc_bfs[0]
+    for d in range(1, L + 1):
+        idx = levels[d]
+        if len(idx) == 0:
+            continue
+        bits = np.unpackbits(desc[parent_bfs[idx]], axis=1)
+        flips = (rng.random(bits.shape) < pflip.get(d, 0.04)).astype(np.uint8)
+        desc[idx] = np.packbits(bits ^ flips, axis=1)
+    nchildren = np.bincount(parent_bfs[1:], minlength=n)
+    leaf = (nchildren == 0).astype(np.uint8)
+    leaf[0] = 0
+    if ties:
+        # copy the first child's descriptor onto a later sibling for ~10% of parents
+        first = {}
+        for i in range(1, n):
+            first.setdefault(int(parent_bfs[i]), i)
+        for p, c0 in first.items():
+            if nchildren[p] >= 3 and rng.random() < 0.1:
+                desc[c0 + 1 + rng.integers(0, nchildren[p] - 1)] = desc[c0]
+    weight = np.where(leaf == 1, rng.uniform(0.5, 8.0, n), 0.0)
+    if stop_frac > 0:
+        weight[(leaf == 1) & (rng.random(n) < stop_frac)] = 0.0
+    weight[0] = 0.0
+    if order == "bfs":
+        perm = np.arange(n)
+    else:
+        # HKmeansStep creation order: children consecutive, then recurse per child
+        kids = [[] for _ in range(n)]
+        for i in range(1, n):
+            kids[int(parent_bfs[i])].append(i)
+        perm = np.empty(n, np.int64)  # perm[new id] = bfs index
+        perm[0] = 0
+        nxt = 1
+        stack = [0]
+        while stack:
+            p = stack.pop()
+            ch = kids[p]
+            perm[nxt:nxt + len(ch)] = ch
+            nxt += len(ch)
+            stack.extend(reversed(ch))  # first child's subtree first
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    parent = np.zeros(n, np.int32)
+    parent[1:] = inv[parent_bfs[perm[1:]]]
+    return dict(k=k, L=L, parent=parent, leaf=leaf[perm].copy(), desc=desc[perm].copy(),
+                weight=weight[perm].copy())
+
+
+def vocab_features(voc, n, rng_seed=0, flip=0.06, random_frac=0.1):
+    """Features near vocabulary leaves: a random leaf's descriptor with bits
+    flipped, plus a fraction of uniformly random descriptors."""
+    rng = np.random.default_rng(rng_seed)
+    leaves = np.flatnonzero(voc["leaf"])
+    src = voc["desc"][rng.choice(leaves, n)]
+    bits = np.unpackbits(src, axis=1)
+    bits ^= (rng.random(bits.shape) < flip).astype(np.uint8)
+    out = np.packbits(bits, axis=1)
+    rnd = rng.random(n) < random_frac
+    out[rnd] = rng.integers(0, 256, (int(rnd.sum()), 32), dtype=np.uint8)
+    return out
+
+
+def write_vocabulary_text(voc, path, scoring=0, weighting=0):
+    """ORBvoc.txt layout read by loadFromTextFile (:1362-1448): header
+    "k L scoring weighting", then per node "parent isLeaf d0 .. d31 weight"."""
+    with open(path, "w") as f:
+        f.write(f"{voc['k']} {voc['L']}  {scoring} {weighting}\n")
+        for i in range(1, len(voc["parent"])):
+            d = " ".join(str(int(x)) for x in voc["desc"][i])
+            f.write(f"{int(voc['parent'][i])} {int(voc['leaf'][i])} {d} {float(voc['weight'][i])!r}\n")
