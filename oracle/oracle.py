@@ -627,3 +627,19 @@ def vocab_parse_text(path):
     fn(str(path).encode(), _p(hdr), n, _p(parent), _p(leaf), _p(desc), _p(weight))
     return dict(k=int(hdr[0]), L=int(hdr[1]), scoring=int(hdr[2]), weighting=int(hdr[3]),
                 parent=parent, leaf=leaf, desc=desc, weight=weight)
+
+
+def vocab_time(voc, desc, n_frames, n_per_frame, levelsup=4, scoring=0, weighting=0):
+    """Seconds the oracle spends in transform() over n_frames frames (tree built
+    once, outside the timed region).  CPU baseline only."""
+    desc = np.ascontiguousarray(desc, np.uint8)
+    parent = np.ascontiguousarray(voc["parent"], np.int32)
+    leaf = np.ascontiguousarray(voc["leaf"], np.uint8)
+    nd = np.ascontiguousarray(voc["desc"], np.uint8)
+    nw = np.ascontiguousarray(voc["weight"], np.float64)
+    fn = lib().oracle_vocab_time
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    fn.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, vp, i32]
+    fn.restype = ctypes.c_double
+    return fn(int(voc["k"]), int(voc["L"]), scoring, weighting, len(parent), _p(parent),
+              _p(leaf), _p(nd), _p(nw), n_frames, n_per_frame, _p(desc), levelsup)

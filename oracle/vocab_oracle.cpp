@@ -34,6 +34,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <chrono>
 #include <fstream>
 #include <map>
 #include <sstream>
@@ -315,6 +316,27 @@ int oracle_vocab_parse_text(const char* path, int32_t* header, int cap, int32_t*
     memcpy(weight, w.data(), (size_t)n * 8);
   }
   return n;
+}
+
+// CPU baseline for the transform (bench leg): builds the tree once, then
+// runs transform() over n_frames frames of n_per_frame descriptors each on
+// this thread; returns the seconds spent in transform() only (the reference
+// loads the vocabulary once at start-up, System::System src/System.cc).
+double oracle_vocab_time(int k, int L, int scoring, int weighting, int n_nodes,
+                         const int32_t* parent, const uint8_t* leaf, const uint8_t* node_desc,
+                         const double* node_weight, int n_frames, int n_per_frame,
+                         const uint8_t* desc, int levelsup) {
+  Vocabulary V;
+  if (!build(V, k, L, scoring, weighting, n_nodes, parent, leaf, node_desc, node_weight))
+    return -1.0;
+  BowVector v;
+  FeatureVector fv;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int f = 0; f < n_frames; ++f)
+    transform(V, n_per_frame, desc + (size_t)f * n_per_frame * 32, levelsup, v, fv, nullptr,
+              nullptr);
+  const auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double>(t1 - t0).count();
 }
 
 }  // extern "C"

@@ -13,6 +13,7 @@
 
 #include <cassert>
 #include <cstdint>
+#include <map>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -121,6 +122,102 @@ class ORBextractor {
     return v;
   }
   orb_extractor_t* h_ = nullptr;
+};
+
+// --------------------------------------------------------------- DBoW2 types
+// DBoW2::BowVector (std::map<WordId, WordValue>, Thirdparty/DBoW2/DBoW2/BowVector.h)
+// and DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>,
+// FeatureVector.h): the same containers, so Frame::mBowVec / mFeatVec keep their
+// types.  CsrFeatureVector is the flat form the C ABI takes.
+using WordId = uint32_t;
+using NodeId = uint32_t;
+using BowVector = std::map<WordId, double>;
+using FeatureVector = std::map<NodeId, std::vector<unsigned int>>;
+
+struct CsrFeatureVector {
+  std::vector<uint32_t> nodes;
+  std::vector<int32_t> offs{0};
+  std::vector<uint32_t> feats;
+  int size() const { return (int)nodes.size(); }
+};
+
+inline CsrFeatureVector flatten(const FeatureVector& fv) {
+  CsrFeatureVector c;
+  c.nodes.reserve(fv.size());
+  c.offs.reserve(fv.size() + 1);
+  for (const auto& it : fv) {
+    c.nodes.push_back(it.first);
+    c.feats.insert(c.feats.end(), it.second.begin(), it.second.end());
+    c.offs.push_back((int32_t)c.feats.size());
+  }
+  return c;
+}
+
+// ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
+// (include/ORBVocabulary.h), device-resident.  loadFromTextFile as
+// TemplatedVocabulary.h:1362-1448 (returns false on a malformed header);
+// transform as Frame::ComputeBoW calls it (src/Frame.cc:439-449:
+// transform(vCurrentDesc, mBowVec, mFeatVec, 4)).
+class ORBVocabulary {
+ public:
+  explicit ORBVocabulary(int device = 0) : device_(device) {}
+  ~ORBVocabulary() { orb_vocabulary_destroy(h_); }
+  ORBVocabulary(const ORBVocabulary&) = delete;
+  ORBVocabulary& operator=(const ORBVocabulary&) = delete;
+
+  bool loadFromTextFile(const std::string& filename) {
+    orb_vocabulary_t* h = nullptr;
+    if (orb_vocabulary_load_text(device_, filename.c_str(), &h) != ORB_OK) return false;
+    orb_vocabulary_destroy(h_);
+    h_ = h;
+    return true;
+  }
+  // Node table form (node 0 = root; parent[i] < i; entry 0 ignored).
+  void create(int k, int L, int scoring, int weighting, const std::vector<int32_t>& parent,
+              const std::vector<uint8_t>& leaf, const std::vector<uint8_t>& descriptors,
+              const std::vector<double>& weights) {
+    orb_vocabulary_t* h = nullptr;
+    check(orb_vocabulary_create(device_, k, L, scoring, weighting, (int)parent.size(),
+                                parent.data(), leaf.data(), descriptors.data(), weights.data(),
+                                &h),
+          "ORBVocabulary::create");
+    orb_vocabulary_destroy(h_);
+    h_ = h;
+  }
+  unsigned int size() const { return (unsigned)info()[5]; }
+  bool empty() const { return size() == 0; }
+  unsigned int getBranchingFactor() const { return (unsigned)info()[0]; }
+  unsigned int getDepthLevels() const { return (unsigned)info()[1]; }
+
+  // transform(const vector<cv::Mat>& features, BowVector&, FeatureVector&, levelsup),
+  // TemplatedVocabulary.h:1128-1210; desc rows are the features in order.
+  void transform(const Descriptors& desc, BowVector& v, FeatureVector& fv, int levelsup) const {
+    v.clear();
+    fv.clear();
+    if (!h_ || desc.rows == 0) return;
+    const int n = desc.rows;
+    std::vector<uint32_t> bw(n), fvn(n), fvf(n);
+    std::vector<double> bv(n);
+    std::vector<int32_t> fvo(n + 1);
+    int32_t nw = 0, nf = 0;
+    check(orb_vocabulary_transform(h_, n, desc.data.data(), levelsup, bw.data(), bv.data(), &nw,
+                                   fvn.data(), fvo.data(), fvf.data(), &nf, nullptr, nullptr),
+          "ORBVocabulary::transform");
+    for (int i = 0; i < nw; ++i) v.emplace_hint(v.end(), bw[i], bv[i]);
+    for (int j = 0; j < nf; ++j)
+      fv.emplace_hint(fv.end(), fvn[j],
+                      std::vector<unsigned int>(fvf.begin() + fvo[j], fvf.begin() + fvo[j + 1]));
+  }
+  orb_vocabulary_t* handle() { return h_; }
+
+ private:
+  std::vector<int32_t> info() const {
+    std::vector<int32_t> i(6, 0);
+    if (h_) orb_vocabulary_info(h_, i.data());
+    return i;
+  }
+  int device_;
+  orb_vocabulary_t* h_ = nullptr;
 };
 
 // ------------------------------------------------------------------ matcher
@@ -245,11 +342,165 @@ class ORBmatcher {
     check(orb_stereo_match(h_, &in, mvuRight.data(), mvDepth.data()), "ComputeStereoMatches");
   }
 
+  // SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches),
+  // src/ORBmatcher.cc:164-306.  kfMapPoints[i] = MapPoint id of KF keypoint i or
+  // -1; kfBad[i] = isBad().  vpMapPointMatches (out) = MapPoint id per F keypoint.
+  int SearchByBoW(const FrameView& KF, const std::vector<int32_t>& kfMapPoints,
+                  const std::vector<uint8_t>& kfBad, const FeatureVector& kfFeatVec,
+                  const FrameView& F, const FeatureVector& fFeatVec,
+                  std::vector<int32_t>& vpMapPointMatches) {
+    const CsrFeatureVector a = flatten(kfFeatVec), b = flatten(fFeatVec);
+    const std::vector<float> ka = angles(KF), fa = angles(F);
+    vpMapPointMatches.assign(F.N(), -1);
+    int32_t n = 0;
+    check(orb_match_bow(h_, KF.N(), KF.mDescriptors.data.data(), ka.data(), kfMapPoints.data(),
+                        kfBad.empty() ? nullptr : kfBad.data(), a.size(), a.nodes.data(),
+                        a.offs.data(), a.feats.data(), F.N(), F.mDescriptors.data.data(),
+                        fa.data(), b.size(), b.nodes.data(), b.offs.data(), b.feats.data(),
+                        mfNNratio, mbCheckOrientation ? 1 : 0, vpMapPointMatches.data(), &n),
+          "SearchByBoW(KF, F)");
+    return n;
+  }
+
+  // SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12),
+  // src/ORBmatcher.cc:581-716.  vpMatches12 (out) = KF2 MapPoint id per KF1 keypoint.
+  int SearchByBoW(const FrameView& KF1, const std::vector<int32_t>& mp1,
+                  const std::vector<uint8_t>& bad1, const FeatureVector& fv1,
+                  const FrameView& KF2, const std::vector<int32_t>& mp2,
+                  const std::vector<uint8_t>& bad2, const FeatureVector& fv2,
+                  std::vector<int32_t>& vpMatches12) {
+    const CsrFeatureVector a = flatten(fv1), b = flatten(fv2);
+    const std::vector<float> a1 = angles(KF1), a2 = angles(KF2);
+    vpMatches12.assign(KF1.N(), -1);
+    int32_t n = 0;
+    check(orb_match_bow_kf(h_, KF1.N(), KF1.mDescriptors.data.data(), a1.data(), mp1.data(),
+                           bad1.empty() ? nullptr : bad1.data(), a.size(), a.nodes.data(),
+                           a.offs.data(), a.feats.data(), KF2.N(), KF2.mDescriptors.data.data(),
+                           a2.data(), mp2.data(), bad2.empty() ? nullptr : bad2.data(), b.size(),
+                           b.nodes.data(), b.offs.data(), b.feats.data(), mfNNratio,
+                           mbCheckOrientation ? 1 : 0, vpMatches12.data(), &n),
+          "SearchByBoW(KF, KF)");
+    return n;
+  }
+
+  // SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize),
+  // src/ORBmatcher.cc:429-577.  vbPrevMatched as (x, y) pairs, updated in place.
+  int SearchForInitialization(const FrameView& F1, const FrameView& F2,
+                              std::vector<float>& vbPrevMatched, std::vector<int>& vnMatches12,
+                              int windowSize = 10) {
+    const orb_frame_t f1 = F1.c(), f2 = F2.c();
+    std::vector<int32_t> m(F1.N(), -1);
+    int32_t n = 0;
+    check(orb_search_for_initialization(h_, &f1, &f2, vbPrevMatched.data(), windowSize,
+                                        mfNNratio, mbCheckOrientation ? 1 : 0, m.data(), &n),
+          "SearchForInitialization");
+    vnMatches12.assign(m.begin(), m.end());
+    return n;
+  }
+
+  // Tracking::SearchLocalPoints' isInFrustum pass (src/Tracking.cc:1360-1377,
+  // src/Frame.cc:303-366); returns nToMatch, tracks feed SearchByProjection.
+  int isInFrustum(const std::vector<orb_map_point_t>& mps, const orb_pose_t& pose,
+                  const orb_camera_t& cam, const FrameView& F, float viewingCosLimit,
+                  float logScaleFactor, std::vector<orb_mp_track_t>& tracks) {
+    tracks.assign(mps.size(), orb_mp_track_t{});
+    int32_t n = 0;
+    check(orb_frustum(h_, (int)mps.size(), mps.data(), &pose, &cam, F.mnMinX, F.mnMaxX, F.mnMinY,
+                      F.mnMaxY, viewingCosLimit, logScaleFactor, (int)F.mvScaleFactors.size(),
+                      tracks.data(), &n),
+          "isInFrustum");
+    return n;
+  }
+
+  // MapPoint::ComputeDistinctiveDescriptors for many points (src/MapPoint.cc:250-326):
+  // observation descriptors in CSR (obsOffs.size() = points + 1).  Returns BestIdx
+  // per point (-1 for an empty list, whose descriptor row is left untouched).
+  std::vector<int32_t> ComputeDistinctiveDescriptors(const std::vector<int32_t>& obsOffs,
+                                                     const std::vector<uint8_t>& obsDesc,
+                                                     std::vector<uint8_t>& descriptors) {
+    const int n = (int)obsOffs.size() - 1;
+    std::vector<int32_t> best(n > 0 ? n : 0, -1);
+    if (n <= 0) return best;
+    descriptors.resize((size_t)n * ORB_DESC_BYTES);
+    check(orb_distinctive_descriptors(h_, n, obsOffs.data(),
+                                      obsDesc.empty() ? nullptr : obsDesc.data(), best.data(),
+                                      descriptors.data()),
+          "ComputeDistinctiveDescriptors");
+    return best;
+  }
+
+  // Fuse(KeyFrame* pKF, vpMapPoints, th), src/ORBmatcher.cc:903-1077 (match half):
+  // fuseIdx[i] = keypoint point i fuses into, or -1.
+  int Fuse(const FrameView& KF, const std::vector<float>& invLevelSigma2, const orb_pose_t& pose,
+           const orb_camera_t& cam, float logScaleFactor,
+           const std::vector<orb_map_point_t>& mps, const std::vector<uint8_t>& mpDesc, float th,
+           std::vector<int32_t>& fuseIdx) {
+    const orb_frame_t f = KF.c();
+    fuseIdx.assign(mps.size(), -1);
+    int32_t n = 0;
+    check(orb_fuse(h_, &f, invLevelSigma2.data(), &pose, &cam, logScaleFactor, (int)mps.size(),
+                   mps.data(), mpDesc.data(), th, fuseIdx.data(), &n),
+          "Fuse");
+    return n;
+  }
+
+  // Fuse(KeyFrame* pKF, Scw, vpPoints, th, vpReplacePoint), src/ORBmatcher.cc:1079-1210.
+  int Fuse(const FrameView& KF, const float scw[12], const orb_camera_t& cam,
+           float logScaleFactor, const std::vector<orb_map_point_t>& mps,
+           const std::vector<uint8_t>& mpDesc, float th, std::vector<int32_t>& fuseIdx) {
+    const orb_frame_t f = KF.c();
+    fuseIdx.assign(mps.size(), -1);
+    int32_t n = 0;
+    check(orb_fuse_sim3(h_, &f, scw, &cam, logScaleFactor, (int)mps.size(), mps.data(),
+                        mpDesc.data(), th, fuseIdx.data(), &n),
+          "Fuse(KF, Scw)");
+    return n;
+  }
+
+  // SearchByProjection(Frame& F, KeyFrame* pKF, sAlreadyFound, th, ORBdist),
+  // src/ORBmatcher.cc:1622-1759: kpMatch[j] = point assigned, -1 none, -2 reset.
+  int SearchByProjection(const FrameView& F, const std::vector<uint8_t>& locked,
+                         const orb_pose_t& pose, const orb_camera_t& cam, float logScaleFactor,
+                         const std::vector<orb_map_point_t>& mps,
+                         const std::vector<uint8_t>& mpDesc, const std::vector<float>& kfAngle,
+                         float th, int ORBdist, std::vector<int32_t>& kpMatch) {
+    const orb_frame_t f = F.c();
+    kpMatch.assign(F.N(), -1);
+    int32_t n = 0;
+    check(orb_search_by_projection_reloc(h_, &f, locked.empty() ? nullptr : locked.data(), &pose,
+                                         &cam, logScaleFactor, (int)mps.size(), mps.data(),
+                                         mpDesc.data(), kfAngle.data(), th, ORBdist,
+                                         mbCheckOrientation ? 1 : 0, kpMatch.data(), &n),
+          "SearchByProjection(F, KF)");
+    return n;
+  }
+
+  // SearchByProjection(KeyFrame* pKF, Scw, vpPoints, vpMatched, th),
+  // src/ORBmatcher.cc:311-425: vpMatched[j] = index into vpPoints or -1 (in/out).
+  int SearchByProjection(const FrameView& KF, const float scw[12], const orb_camera_t& cam,
+                         float logScaleFactor, const std::vector<orb_map_point_t>& mps,
+                         const std::vector<uint8_t>& mpDesc, std::vector<int32_t>& vpMatched,
+                         int th) {
+    const orb_frame_t f = KF.c();
+    if ((int)vpMatched.size() != KF.N()) vpMatched.assign(KF.N(), -1);
+    int32_t n = 0;
+    check(orb_search_by_projection_sim3(h_, &f, scw, &cam, logScaleFactor, (int)mps.size(),
+                                        mps.data(), mpDesc.data(), (float)th, vpMatched.data(),
+                                        &n),
+          "SearchByProjection(KF, Scw)");
+    return n;
+  }
+
   float mfNNratio;
   bool mbCheckOrientation;
   orb_matcher_t* handle() { return h_; }
 
  private:
+  static std::vector<float> angles(const FrameView& F) {
+    std::vector<float> a(F.N());
+    for (int i = 0; i < F.N(); ++i) a[i] = F.mvKeysUn[i].angle;
+    return a;
+  }
   orb_matcher_t* h_ = nullptr;
 };
 

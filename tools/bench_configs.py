@@ -16,6 +16,10 @@ results table:
   F1  SURVEY §8(f): SearchForInitialization, 640x480 frames from the 2000-feature
       initial extractor, window 100, ORBmatcher(0.9, true), 64 pairs per launch
       (pairs/s) + CPU oracle rate + exact check
+  F2  SURVEY §8(f): Frame::ComputeBoW (DBoW2 transform, levelsup 4) on an
+      ORBvoc-shaped synthetic vocabulary (k 10, L 6, 10^6 words, TF-IDF, L1),
+      1000 extracted descriptors per frame, 512 frames per launch (frames/s)
+      + CPU oracle rate + exact check
   F3  SURVEY §8(f): ComputeDistinctiveDescriptors over 100,000 map points with
       1..20 observations (points/s) + CPU oracle rate + exact check
 
@@ -316,6 +320,62 @@ def f3(args, orb, oracle, torch):
             "alg_GBps": alg_bytes / sec / 1e9, "bit_exact": bool(exact)}
 
 
+def f2(args, orb, oracle, torch):
+    import scenarios
+    W, H, NF = 1241, 376, 1000
+    voc = scenarios.vocabulary(rng_seed=11, k=10, L=6)
+    V = orb.ORBVocabulary(voc["k"], voc["L"], voc["parent"], voc["leaf"], voc["desc"],
+                          voc["weight"])
+    B = args.batch
+    ext = orb.ORBextractor(NF, 1.2, 8, 20, 7)
+    frames = []
+    for f in range(32):
+        _, d = ext(orb.synth_image(SEED, f, W, H))
+        frames.append(d[:NF])
+    stride = NF + 8
+    counts = np.array([len(frames[f % 32]) for f in range(B)], np.int32)
+    desc = np.zeros((B, stride, 32), np.uint8)
+    for f in range(B):
+        desc[f, :counts[f]] = frames[f % 32]
+    dev = torch.device("cuda:0")
+    d_counts = torch.from_numpy(counts).to(dev)
+    d_desc = torch.from_numpy(desc).to(dev)
+    n = B * stride
+    i32 = lambda m: torch.zeros(m, dtype=torch.int32, device=dev)
+    f64 = lambda m: torch.zeros(m, dtype=torch.float64, device=dev)
+    fw, fwt, fn, bw, bv, nw = i32(n), f64(n), i32(n), i32(n), f64(n), i32(B)
+    fvn, fvo, fvf, nfv = i32(n), i32(B * (stride + 1)), i32(n), i32(B)
+    s_ = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        V.transform_batch(B, d_counts.data_ptr(), d_desc.data_ptr(), stride, 4, fw.data_ptr(),
+                          fwt.data_ptr(), fn.data_ptr(), bw.data_ptr(), bv.data_ptr(),
+                          nw.data_ptr(), fvn.data_ptr(), fvo.data_ptr(), fvf.data_ptr(),
+                          nfv.data_ptr(), s_)
+
+    sec = timed(step, args.steps, 2, torch)
+    exact = True
+    h = lambda t: t.cpu().numpy()
+    bw_, bv_, nw_, fvn_, fvf_ = h(bw).view(np.uint32), h(bv), h(nw), h(fvn).view(np.uint32), h(fvf)
+    for f in range(4):
+        r = oracle.vocab_transform(voc, frames[f], 4)
+        o = f * stride
+        exact &= (np.array_equal(bw_[o:o + nw_[f]], r[0]) and
+                  np.array_equal(bv_[o:o + nw_[f]].view(np.uint64), r[1].view(np.uint64)) and
+                  np.array_equal(fvn_[o:o + len(r[2])], r[2]) and
+                  np.array_equal(fvf_[o:o + len(r[4])].view(np.uint32), r[4]))
+    cpu_frames = 8
+    cpu_sec = oracle.vocab_time(voc, np.concatenate(frames[:cpu_frames]), cpu_frames, NF, 4)
+    feats = int(counts.sum())
+    tree_bytes = len(voc["parent"]) * (32 + 8 + 4 + 8 + 4)
+    alg_bytes = tree_bytes + feats * (32 + 4 + 8 + 4 + 4 + 8 + 4 + 4 + 4)
+    return {"config": "F2", "workload": "Frame::ComputeBoW, ORBvoc-shaped synthetic vocabulary "
+            "(k 10, L 6, 10^6 words), 1000 descriptors/frame, levelsup 4", "unit": "frames/s",
+            "value": B / sec, "ms_per_step": sec * 1e3, "frames_per_launch": B,
+            "features_per_s": feats / sec, "cpu_oracle_1_thread": cpu_frames / cpu_sec,
+            "alg_GBps": alg_bytes / sec / 1e9, "bit_exact": bool(exact)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="C1,C2,C3,C5")
@@ -338,6 +398,8 @@ def main():
             r = c5(args, orb, oracle, torch)
         elif c == "F1":
             r = f1(args, orb, oracle, torch)
+        elif c == "F2":
+            r = f2(args, orb, oracle, torch)
         elif c == "F3":
             r = f3(args, orb, oracle, torch)
         else:
