@@ -41,6 +41,9 @@
  *   orb_search_by_sim3             SearchBySim3              src/ORBmatcher.cc:1212-1458
  *   orb_match_bow_kf               SearchByBoW(KeyFrame*, KeyFrame*, ...) src/ORBmatcher.cc:581-716
  *   orb_search_for_triangulation   SearchForTriangulation    src/ORBmatcher.cc:718-901
+ *   orb_undistort_points / orb_undistort_keypoints(_batch) / orb_compute_image_bounds
+ *                                  cv::undistortPoints in Frame::UndistortKeyPoints
+ *                                  src/Frame.cc:452-482 and ComputeImageBounds :484-514
  *   orb_vocabulary_create / _load_text / _destroy
  *                                  DBoW2 TemplatedVocabulary ctor + loadFromTextFile
  *                                  Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1362-1448
@@ -479,6 +482,32 @@ orb_status_t orb_search_for_triangulation(
     const uint32_t* node_ids1, const int32_t* offs1, const uint32_t* feats1, int nodes2,
     const uint32_t* node_ids2, const int32_t* offs2, const uint32_t* feats2, int only_stereo,
     int check_orientation, int32_t* match12, int32_t* nmatches);
+
+/* -------------------------------------------------------- undistortion */
+
+/* cv::undistortPoints(src, dst, mK, mDistCoef, cv::Mat(), mK), the call in
+ * Frame::UndistortKeyPoints and Frame::ComputeImageBounds (src/Frame.cc:452-514),
+ * with OpenCV's cvUndistortPoints arithmetic (double, 5 fixed iterations,
+ * RR = mK): K = mK as 9 floats row-major, dist = mDistCoef (n_dist 4, 5, 8 or
+ * 12: k1 k2 p1 p2 [k3 [k4 k5 k6 [s1 s2 s3 s4]]]; the tilted 14-term model is
+ * not supported).  Points as (x, y) float pairs.  Host buffers. */
+orb_status_t orb_undistort_points(orb_matcher_t* m, int n, const float* xy, const float* K,
+                                  const float* dist, int n_dist, float* out_xy);
+/* Frame::UndistortKeyPoints: mvKeysUn from mvKeys (dist[0] == 0 -> copy,
+ * :454-458); every field but pt is copied.  keys_un may equal keys. */
+orb_status_t orb_undistort_keypoints(orb_matcher_t* m, int n, const orb_keypoint_t* keys,
+                                     const float* K, const float* dist, int n_dist,
+                                     orb_keypoint_t* keys_un);
+/* Frame::ComputeImageBounds: bounds = {mnMinX, mnMaxX, mnMinY, mnMaxY}. */
+orb_status_t orb_compute_image_bounds(orb_matcher_t* m, int cols, int rows, const float* K,
+                                      const float* dist, int n_dist, float* bounds);
+/* Device-batched UndistortKeyPoints: frame f has d_n[f] keypoints at
+ * d_keys + f * stride (e.g. the output of orb_extractor_extract_batch);
+ * writes d_keys_un at the same offsets.  Asynchronous on `stream`. */
+orb_status_t orb_undistort_keypoints_batch(orb_matcher_t* m, int n_frames, const int32_t* d_n,
+                                           const orb_keypoint_t* d_keys, int stride,
+                                           const float* K, const float* dist, int n_dist,
+                                           orb_keypoint_t* d_keys_un, void* stream);
 
 /* ------------------------------------------------------ DBoW2 vocabulary */
 

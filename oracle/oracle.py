@@ -643,3 +643,52 @@ def vocab_time(voc, desc, n_frames, n_per_frame, levelsup=4, scoring=0, weightin
     fn.restype = ctypes.c_double
     return fn(int(voc["k"]), int(voc["L"]), scoring, weighting, len(parent), _p(parent),
               _p(leaf), _p(nd), _p(nw), n_frames, n_per_frame, _p(desc), levelsup)
+
+
+def _cam_args(K, dist):
+    K = np.ascontiguousarray(K, np.float32).reshape(9)
+    dist = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    return K, dist
+
+
+def undistort_points(xy, K, dist):
+    """cv::undistortPoints(src, dst, K, D, noArray(), K) on (n, 2) float points
+    (OpenCV cvUndistortPoints arithmetic; see camera_oracle.cpp)."""
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    K, dist = _cam_args(K, dist)
+    out = np.zeros_like(xy)
+    fn = lib().oracle_undistort_points
+    vp = ctypes.c_void_p
+    fn.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int, vp]
+    fn.restype = ctypes.c_int
+    if fn(len(xy), _p(xy), _p(K), _p(dist), len(dist), _p(out)) != 0:
+        raise ValueError("unsupported distortion model")
+    return out
+
+
+def undistort_keypoints(keys, K, dist):
+    """Frame::UndistortKeyPoints (src/Frame.cc:452-482) -> mvKeysUn."""
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    K, dist = _cam_args(K, dist)
+    out = np.zeros_like(keys)
+    fn = lib().oracle_undistort_keypoints
+    vp = ctypes.c_void_p
+    fn.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int, vp]
+    fn.restype = ctypes.c_int
+    if fn(len(keys), _p(keys) if len(keys) else None, _p(K), _p(dist), len(dist),
+          _p(out) if len(keys) else None) != 0:
+        raise ValueError("unsupported distortion model")
+    return out
+
+
+def compute_image_bounds(cols, rows, K, dist):
+    """Frame::ComputeImageBounds (src/Frame.cc:484-514) -> (minX, maxX, minY, maxY)."""
+    K, dist = _cam_args(K, dist)
+    b = np.zeros(4, np.float32)
+    fn = lib().oracle_compute_image_bounds
+    vp = ctypes.c_void_p
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, vp]
+    fn.restype = ctypes.c_int
+    if fn(cols, rows, _p(K), _p(dist), len(dist), _p(b)) != 0:
+        raise ValueError("unsupported distortion model")
+    return b

@@ -156,6 +156,10 @@ def lib() -> ctypes.CDLL:
         "orb_vocabulary_transform": (i32, [vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "orb_vocabulary_transform_batch": (i32, [vp, i32, vp, vp, i32, i32, vp, vp, vp, vp, vp,
                                                  vp, vp, vp, vp, vp, vp]),
+        "orb_undistort_points": (i32, [vp, i32, vp, vp, vp, i32, vp]),
+        "orb_undistort_keypoints": (i32, [vp, i32, vp, vp, vp, i32, vp]),
+        "orb_compute_image_bounds": (i32, [vp, i32, i32, vp, vp, i32, vp]),
+        "orb_undistort_keypoints_batch": (i32, [vp, i32, vp, vp, i32, vp, vp, i32, vp, vp]),
         "orb_synth_image": (None, [ctypes.c_uint64, i32, i32, i32, i32, vp, sz]),
         "orb_synth_local_map": (None, [ctypes.c_uint64, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     }
@@ -731,6 +735,49 @@ class ORBmatcher:
             min_x, max_x, min_y, max_y, int(windowSize), self.mfNNratio,
             int(self.mbCheckOrientation), d_prev, d_matches12, d_nmatches, stream or None),
             "search_for_initialization_batch")
+
+    # ----------------------------------------------------- undistortion (Frame)
+    @staticmethod
+    def _cam(K, dist):
+        K = np.ascontiguousarray(K, np.float32).reshape(9)
+        dist = np.ascontiguousarray(dist, np.float32).reshape(-1)
+        return K, dist
+
+    def undistort_points(self, xy, K, dist):
+        """cv::undistortPoints(src, dst, K, D, noArray(), K) on (n, 2) float points."""
+        xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+        K, dist = self._cam(K, dist)
+        out = np.zeros_like(xy)
+        _check(lib().orb_undistort_points(self._h, len(xy), _ptr(xy) if len(xy) else None,
+                                          _ptr(K), _ptr(dist), len(dist),
+                                          _ptr(out) if len(xy) else None), "undistortPoints")
+        return out
+
+    def UndistortKeyPoints(self, mvKeys, K, dist):
+        """Frame::UndistortKeyPoints (src/Frame.cc:452-482): returns mvKeysUn."""
+        keys = np.ascontiguousarray(mvKeys, KEYPOINT_DTYPE)
+        K, dist = self._cam(K, dist)
+        out = np.zeros_like(keys)
+        _check(lib().orb_undistort_keypoints(self._h, len(keys), _ptr(keys) if len(keys) else None,
+                                             _ptr(K), _ptr(dist), len(dist),
+                                             _ptr(out) if len(keys) else None),
+               "UndistortKeyPoints")
+        return out
+
+    def ComputeImageBounds(self, cols, rows, K, dist):
+        """Frame::ComputeImageBounds (src/Frame.cc:484-514): (mnMinX, mnMaxX, mnMinY, mnMaxY)."""
+        K, dist = self._cam(K, dist)
+        b = np.zeros(4, np.float32)
+        _check(lib().orb_compute_image_bounds(self._h, cols, rows, _ptr(K), _ptr(dist), len(dist),
+                                              _ptr(b)), "ComputeImageBounds")
+        return tuple(float(v) for v in b)
+
+    def undistort_keypoints_batch(self, n_frames, d_n, d_keys, stride, K, dist, d_keys_un,
+                                  stream: int = 0):
+        K, dist = self._cam(K, dist)
+        _check(lib().orb_undistort_keypoints_batch(self._h, n_frames, d_n, d_keys, stride, _ptr(K),
+                                                   _ptr(dist), len(dist), d_keys_un,
+                                                   stream or None), "undistort_keypoints_batch")
 
     # ------------------------------------------ MapPoint::ComputeDistinctiveDescriptors
     def ComputeDistinctiveDescriptors(self, obs_offs, obs_desc, descriptors=None):

@@ -134,6 +134,12 @@ hipError_t orb_k_voc_descend(const void* info, const void* ndesc, const uint32_t
                              int nFrames, uint32_t* fword, double* fweight, uint32_t* fnode,
                              hipStream_t s);
 int orb_k_voc_max_features(void);
+hipError_t orb_k_undistort_points(const void* params, int n, const float* in, float* out,
+                                  hipStream_t s);
+hipError_t orb_k_undistort_keys(const void* params, int nFrames, const int32_t* counts,
+                                int nSingle, int stride, const void* in, void* out, int copyOnly,
+                                hipStream_t s);
+size_t orb_k_undistort_params_size(void);
 hipError_t orb_k_voc_vectors(const uint32_t* fword, const double* fweight, const uint32_t* fnode,
                              const int32_t* counts, int nSingle, int stride, int tf, int must,
                              int l2, int nFrames, uint32_t* bowWords, double* bowValues,
@@ -2341,6 +2347,111 @@ orb_status_t orb_vocabulary_transform_batch(orb_vocabulary_t* V, int n_frames,
                       d_feat_weight, d_feat_node, d_bow_words, d_bow_values, d_n_words,
                       d_fv_nodes, d_fv_offs, d_fv_feats, d_n_fv_nodes,
                       stream ? (hipStream_t)stream : V->stream);
+}
+
+// ------------------------------------------------------------ undistortion
+// cv::undistortPoints(src, dst, mK, mDistCoef, cv::Mat(), mK) as called by
+// Frame::UndistortKeyPoints / ComputeImageBounds (src/Frame.cc:452-514); the
+// double parameter block of camera_kernels.hip (cvConvert of the CV_32F
+// matrices, ifx = 1./fx, RR = mK * I).
+struct UndistortParamsHost {
+  double fx, fy, cx, cy, ifx, ify;
+  double rr[9];
+  double k[12];
+};
+
+static orb_status_t undistort_params(const float* K, const float* dist, int n_dist,
+                                     UndistortParamsHost& P) {
+  static_assert(sizeof(UndistortParamsHost) == 27 * 8, "parameter block layout");
+  if (orb_k_undistort_params_size() != sizeof(UndistortParamsHost)) return ORB_EINVAL;
+  if (!K || !dist || !(n_dist == 4 || n_dist == 5 || n_dist == 8 || n_dist == 12))
+    return ORB_EINVAL;
+  memset(&P, 0, sizeof(P));
+  P.fx = K[0]; P.fy = K[4]; P.cx = K[2]; P.cy = K[5];
+  P.ifx = 1. / P.fx;
+  P.ify = 1. / P.fy;
+  for (int i = 0; i < 9; ++i) P.rr[i] = (double)K[i];
+  for (int i = 0; i < n_dist; ++i) P.k[i] = (double)dist[i];
+  return ORB_OK;
+}
+
+orb_status_t orb_undistort_points(orb_matcher_t* m, int n, const float* xy, const float* K,
+                                  const float* dist, int n_dist, float* out_xy) {
+  if (!m || n < 0 || (n > 0 && (!xy || !out_xy))) return ORB_EINVAL;
+  UndistortParamsHost P;
+  orb_status_t st = undistort_params(K, dist, n_dist, P);
+  if (st) return st;
+  if (n == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  if ((st = upload(m->dA, xy, (size_t)n * 8, s)) || (st = m->dB.ensure((size_t)n * 8))) return st;
+  HIP_TRY(orb_k_undistort_points(&P, n, m->dA.as<float>(), m->dB.as<float>(), s));
+  HIP_TRY(hipMemcpyAsync(out_xy, m->dB.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_undistort_keypoints(orb_matcher_t* m, int n, const orb_keypoint_t* keys,
+                                     const float* K, const float* dist, int n_dist,
+                                     orb_keypoint_t* keys_un) {
+  if (!m || n < 0 || (n > 0 && (!keys || !keys_un))) return ORB_EINVAL;
+  UndistortParamsHost P;
+  orb_status_t st = undistort_params(K, dist, n_dist, P);
+  if (st) return st;
+  if (n == 0) return ORB_OK;
+  if (dist[0] == 0.0f) {  // mvKeysUn = mvKeys (:454-458)
+    if (keys_un != keys) memmove(keys_un, keys, (size_t)n * sizeof(orb_keypoint_t));
+    return ORB_OK;
+  }
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  const size_t bytes = (size_t)n * sizeof(orb_keypoint_t);
+  if ((st = upload(m->dA, keys, bytes, s)) || (st = m->dB.ensure(bytes))) return st;
+  HIP_TRY(orb_k_undistort_keys(&P, 1, nullptr, n, n, m->dA.p, m->dB.p, 0, s));
+  HIP_TRY(hipMemcpyAsync(keys_un, m->dB.p, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+orb_status_t orb_compute_image_bounds(orb_matcher_t* m, int cols, int rows, const float* K,
+                                      const float* dist, int n_dist, float* bounds) {
+  if (!m || !bounds || cols < 0 || rows < 0) return ORB_EINVAL;
+  UndistortParamsHost P;
+  orb_status_t st = undistort_params(K, dist, n_dist, P);
+  if (st) return st;
+  if (dist[0] == 0.0f) {  // :506-512
+    bounds[0] = 0.0f;
+    bounds[1] = (float)cols;
+    bounds[2] = 0.0f;
+    bounds[3] = (float)rows;
+    return ORB_OK;
+  }
+  const float c[8] = {0.0f, 0.0f, (float)cols, 0.0f, 0.0f, (float)rows, (float)cols, (float)rows};
+  float u[8];
+  if ((st = orb_undistort_points(m, 4, c, K, dist, n_dist, u))) return st;
+  bounds[0] = std::min(u[0], u[4]);  // mnMinX = min(mat(0,0), mat(2,0)) (:496-499)
+  bounds[1] = std::max(u[2], u[6]);
+  bounds[2] = std::min(u[1], u[3]);
+  bounds[3] = std::max(u[5], u[7]);
+  return ORB_OK;
+}
+
+orb_status_t orb_undistort_keypoints_batch(orb_matcher_t* m, int n_frames, const int32_t* d_n,
+                                           const orb_keypoint_t* d_keys, int stride,
+                                           const float* K, const float* dist, int n_dist,
+                                           orb_keypoint_t* d_keys_un, void* stream) {
+  if (!m || n_frames < 0 || stride <= 0) return ORB_EINVAL;
+  UndistortParamsHost P;
+  orb_status_t st = undistort_params(K, dist, n_dist, P);
+  if (st) return st;
+  if (n_frames == 0) return ORB_OK;
+  if (!d_n || !d_keys || !d_keys_un) return ORB_EINVAL;
+  hipSetDevice(m->device);
+  HIP_TRY(orb_k_undistort_keys(&P, n_frames, d_n, 0, stride, d_keys, d_keys_un,
+                               dist[0] == 0.0f ? 1 : 0, stream ? (hipStream_t)stream : m->stream));
+  return ORB_OK;
 }
 
 // ------------------------------------------------------------ synthetic input

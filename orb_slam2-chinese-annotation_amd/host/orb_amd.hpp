@@ -491,6 +491,28 @@ class ORBmatcher {
     return n;
   }
 
+  // Frame::UndistortKeyPoints (src/Frame.cc:452-482): mvKeysUn from mvKeys with
+  // cv::undistortPoints(mat, mat, mK, mDistCoef, cv::Mat(), mK).  K = mK row-major.
+  void UndistortKeyPoints(const std::vector<KeyPoint>& mvKeys, const float K[9],
+                          const std::vector<float>& mDistCoef, std::vector<KeyPoint>& mvKeysUn) {
+    mvKeysUn.resize(mvKeys.size());
+    check(orb_undistort_keypoints(h_, (int)mvKeys.size(), mvKeys.data(), K, mDistCoef.data(),
+                                  (int)mDistCoef.size(), mvKeysUn.data()),
+          "UndistortKeyPoints");
+  }
+
+  // Frame::ComputeImageBounds (src/Frame.cc:484-514) -> F.mnMinX .. mnMaxY.
+  void ComputeImageBounds(int cols, int rows, const float K[9],
+                          const std::vector<float>& mDistCoef, FrameView& F) {
+    float b[4];
+    check(orb_compute_image_bounds(h_, cols, rows, K, mDistCoef.data(), (int)mDistCoef.size(), b),
+          "ComputeImageBounds");
+    F.mnMinX = b[0];
+    F.mnMaxX = b[1];
+    F.mnMinY = b[2];
+    F.mnMaxY = b[3];
+  }
+
   float mfNNratio;
   bool mbCheckOrientation;
   orb_matcher_t* handle() { return h_; }

@@ -832,3 +832,33 @@ def vocab_transform(voc, desc, levelsup, scoring, weighting):
         feats.extend(fv[k])
         offs.append(len(feats))
     return keys, vals, nodes, offs, feats, fword, fnode
+
+
+def undistort_points(xy, K, dist):
+    """cvUndistortPoints (OpenCV, as Frame::UndistortKeyPoints calls it with
+    P = mK, src/Frame.cc:468), restated a second time with Python floats
+    (IEEE doubles, no fused multiply-add): widen, 5 fixed-point iterations,
+    map through RR = K, narrow to float32."""
+    K = [float(np.float32(v)) for v in np.asarray(K, np.float32).reshape(9)]
+    k = [float(np.float32(v)) for v in np.asarray(dist, np.float32).reshape(-1)]
+    k = k + [0.0] * (12 - len(k))
+    fx, fy, cx, cy = K[0], K[4], K[2], K[5]
+    ifx, ify = 1.0 / fx, 1.0 / fy
+    out = np.zeros((len(xy), 2), np.float32)
+    for i, (u, v) in enumerate(np.asarray(xy, np.float32).reshape(-1, 2)):
+        x = (float(u) - cx) * ifx
+        y = (float(v) - cy) * ify
+        x0, y0 = x, y
+        for _ in range(5):
+            r2 = x * x + y * y
+            icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / \
+                (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2)
+            dx = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2
+            dy = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2
+            x = (x0 - dx) * icdist
+            y = (y0 - dy) * icdist
+        xx = K[0] * x + K[1] * y + K[2]
+        yy = K[3] * x + K[4] * y + K[5]
+        ww = 1.0 / (K[6] * x + K[7] * y + K[8])
+        out[i] = (np.float32(xx * ww), np.float32(yy * ww))
+    return out

@@ -394,3 +394,35 @@ def write_vocabulary_text(voc, path, scoring=0, weighting=0):
         for i in range(1, len(voc["parent"])):
             d = " ".join(str(int(x)) for x in voc["desc"][i])
             f.write(f"{int(voc['parent'][i])} {int(voc['leaf'][i])} {d} {float(voc['weight'][i])!r}\n")
+
+
+# Camera models for Frame::UndistortKeyPoints / ComputeImageBounds: mK as 3x3
+# float rows and mDistCoef as Tracking builds it (src/Tracking.cc:66-78: 4
+# coefficients, a 5th only when k3 != 0).  TUM1/TUM2 from Examples/Monocular.
+def cameras():
+    def K(fx, fy, cx, cy):
+        return np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1]], np.float32)
+    return {
+        "tum1": (K(517.306408, 516.469215, 318.643040, 255.313989),
+                 np.array([0.262383, -0.953104, -0.005358, 0.002628, 1.163314], np.float32)),
+        "tum2": (K(520.908620, 521.007327, 325.141442, 249.701764),
+                 np.array([0.231222, -0.784899, -0.003257, -0.000105, 0.917205], np.float32)),
+        "kitti": (K(718.856, 718.856, 607.1928, 185.2157), np.zeros(4, np.float32)),
+        "k4": (K(458.654, 457.296, 367.215, 248.375),
+               np.array([-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05], np.float32)),
+        "rational8": (K(500.0, 505.0, 320.5, 240.25),
+                      np.array([0.1, -0.05, 0.001, -0.002, 0.01, 0.02, -0.01, 0.005], np.float32)),
+        "prism12": (K(600.0, 600.0, 310.0, 250.0),
+                    np.array([-0.2, 0.05, 0.0005, 0.0003, 0.0, 0.0, 0.0, 0.0, 0.001, -0.0005,
+                              0.0008, 0.0002], np.float32)),
+    }
+
+
+def undistort_points_grid(w=640, h=480, rng_seed=0, n_random=500):
+    """Image corners, a grid and random sub-pixel points (some outside)."""
+    rng = np.random.default_rng(rng_seed)
+    gx, gy = np.meshgrid(np.linspace(0, w, 17), np.linspace(0, h, 13))
+    pts = [np.array([[0, 0], [w, 0], [0, h], [w, h]], np.float32),
+           np.stack([gx.ravel(), gy.ravel()], 1).astype(np.float32),
+           rng.uniform([-20, -20], [w + 20, h + 20], (n_random, 2)).astype(np.float32)]
+    return np.concatenate(pts)
