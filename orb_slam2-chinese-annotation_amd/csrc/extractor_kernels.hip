@@ -129,29 +129,35 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
 }
 
 // ============================================================ k_fast_band
-// FAST arc strength at the pixel `c` points to (LDS tile, row pitch `p`):
-// m = max(best dark 9-arc, best bright 9-arc), where an arc's strength is the
-// min over its 9 pixels of |I(p) - I(q)| on the matching side.  FAST(t) detects
-// the pixel iff m > t, and for a detected corner OpenCV's cornerScore<16> is
-// m - 1 whatever t is.
+// FAST arc strength at the pixel `c` points to (LDS band of biased f16 pixels,
+// row pitch `p` elements): m = max(best dark 9-arc, best bright 9-arc), where
+// an arc's strength is the min over its 9 pixels of |I(p) - I(q)| on the
+// matching side.  FAST(t) detects the pixel iff m > t, and for a detected
+// corner OpenCV's cornerScore<16> is m - 1 whatever t is (SURVEY.md
+// Appendix A.1).
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
+// Band pixels are staged as f16 1024 + I (bit pattern 0x6400 | I): every
+// difference of two pixels, and every pixel +- (t + 1) with t <= 255, is an
+// integer in a range f16 represents exactly, so the packed f16 min/max/add
+// below are exact integer arithmetic with no conversion after staging.
+#define FAST_BIAS 0x64006400u
+
+__device__ __forceinline__ int fast_score(const _Float16* c, int p) {
   const int off[16] = {3 * p,      3 * p + 1,  2 * p + 2,  p + 3,       3,  -p + 3,
                        -2 * p + 2, -3 * p + 1, -3 * p,     -3 * p - 1, -2 * p - 2, -p - 3,
                        -3,         p - 3,      2 * p - 2,  3 * p - 1};
-  // lane .x carries d = v - ring (dark side), .y carries -d (bright side), as
-  // f16: every value is an integer in [-255, 255], exact in half precision, so
+  // lane .x carries d = v - ring (dark side), .y carries -d (bright side):
   // the packed three-input v_pk_minimum3_f16 / v_pk_maximum3_f16 of gfx950 do
   // the arc network in 40 instructions.
-  const _Float16 v = (_Float16)(int)c[0];
+  const _Float16 v = c[0];
   const h16x2 vv = {v, -v}, sg = {(_Float16)-1.0f, (_Float16)1.0f};
   h16x2 q[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const _Float16 ck = (_Float16)(int)c[off[k]];
+    const _Float16 ck = c[off[k]];
     const h16x2 cc = {ck, ck};
     q[k] = __builtin_elementwise_fma(cc, sg, vv);  // (v - ck, ck - v), exact
   }
@@ -175,7 +181,7 @@ __device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
   const h16x2 ma = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m5[0], m5[1]), m5[2]);
   const h16x2 mb = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m5[3], m5[4]), m5[5]);
   const h16x2 best = __builtin_elementwise_maximum(ma, mb);
-  return max((int)best.x, (int)best.y);
+  return (int)(float)__builtin_fmaxf16(best.x, best.y);
 }
 
 // One workgroup per (band, image).  A band is a run of cells of one cell row
@@ -183,8 +189,12 @@ __device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
 // src/ORBextractor.cc:819-843) tile the band interior without overlap, so
 // every pixel's FAST arc strength is computed at most once for the whole band.
 //
-// Phase A (every cell, FAST at iniThFAST): packed compass pretest on 4 pixels
-// per lane, arc strengths of the survivors, NMS of pixels with m > iniTh.
+// LDS band: R rows x P f16 elements; element e of a row is band column
+// e - FAST_LPAD, so interior column 3 (the first detectable one) sits at
+// element 8 and 8-pixel groups of the interior start 16-byte aligned.
+// Phase A (every cell, FAST at iniThFAST): compass pretest on 8 pixels per
+// lane (packed f16, four pixel pairs), candidates appended to a queue that is
+// scored in dense flushes (arc strengths), NMS of pixels with m > iniTh.
 // Phase B (only cells with no phase-A keypoint, src/ORBextractor.cc:846-850):
 // the same at minThFAST over those cells' windows, reusing phase-A strengths.
 // NMS is per cell: a window's edge acts as cv::FAST's zero border (column
@@ -193,9 +203,14 @@ __device__ __forceinline__ int fast_score(const uint8_t* c, int p) {
 // in row-major window order (cv::FAST's order), packed x | y<<12 | score<<24
 // in level coordinates, and their count.
 #define FAST_GROUPS 256    // 8-pixel groups pretested per round (one per thread)
-#define FAST_QUEUE (8 * FAST_GROUPS)
-#define FAST_CORNERS 2048  // corner list capacity; beyond it NMS runs densely
-#define FAST_LOADS 10      // dwords per thread in flight while staging a band (10 KB)
+#define FAST_QCAP 2560     // candidate queue (u16 element offsets)
+#define FAST_QFLUSH (FAST_QCAP - 8 * FAST_GROUPS)  // score once the queue holds more
+#define FAST_CORNERS 1024  // corner list capacity; beyond it NMS runs densely
+#define FAST_LOADS 8       // source dwords per thread in flight while staging
+#define FAST_LPAD 5        // element of band column 0
+// Strength byte of a group pixel outside the interior: 1 is never a corner
+// (m >= 2) and never suppresses one in NMS, so it only has to stop scoring.
+#define FAST_OUTSIDE 0x01
 
 __device__ __forceinline__ unsigned long long bit_run(const uint32_t* bits, int start, int n) {
   // bits [start, start + n) of a little-endian bit array, n <= 64
@@ -206,70 +221,25 @@ __device__ __forceinline__ unsigned long long bit_run(const uint32_t* bits, int 
   return n >= 64 ? v : (v & ((1ull << n) - 1ull));
 }
 
-// Compass pretest of one parity (two pixels as u16 halves): a pixel can be a
-// FAST(t) corner only if two circularly adjacent compass pixels (circle
-// positions 0,4,8,12) are both darker than v - t or both brighter than v + t.
-// Sign bits (15, 31) of the result are set for passing pixels.
-__device__ __forceinline__ uint32_t pretest_half(uint32_t v, uint32_t q0, uint32_t q4, uint32_t q8,
-                                                 uint32_t q12, s16x2 t1, s16x2 nt1) {
-  const s16x2 V = __builtin_bit_cast(s16x2, v);
-  const s16x2 d0 = V - __builtin_bit_cast(s16x2, q0), d4 = V - __builtin_bit_cast(s16x2, q4);
-  const s16x2 d8 = V - __builtin_bit_cast(s16x2, q8), d12 = V - __builtin_bit_cast(s16x2, q12);
-  // (v - q) - (t+1) >= 0  <=>  dark;  -(t+1) - (v - q) >= 0  <=>  bright
-  const uint32_t nd0 = __builtin_bit_cast(uint32_t, d0 - t1), nd4 = __builtin_bit_cast(uint32_t, d4 - t1);
-  const uint32_t nd8 = __builtin_bit_cast(uint32_t, d8 - t1), nd12 = __builtin_bit_cast(uint32_t, d12 - t1);
-  const uint32_t nb0 = __builtin_bit_cast(uint32_t, nt1 - d0), nb4 = __builtin_bit_cast(uint32_t, nt1 - d4);
-  const uint32_t nb8 = __builtin_bit_cast(uint32_t, nt1 - d8), nb12 = __builtin_bit_cast(uint32_t, nt1 - d12);
-  // some adjacent pair (0,4)(4,8)(8,12)(12,0) both dark  <=>  (d0|d8) & (d4|d12)
-  const uint32_t failD = (nd0 & nd8) | (nd4 & nd12);
-  const uint32_t failB = (nb0 & nb8) | (nb4 & nb12);
-  return ~(failD & failB) & 0x80008000u;
-}
-
-// Pretest of the 4 pixels at region columns 4k..4k+3 of region row r (r in
-// [3, R-3)); bit j of the result = pixel 4k+j passes.
-__device__ __forceinline__ uint32_t pretest4(const uint32_t* roi32, int nD, int r, int k, s16x2 t1,
-                                             s16x2 nt1) {
-  const uint32_t* row = roi32 + r * nD + k;
-  const uint32_t A = row[-1], B = row[0], Cn = row[1];  // row[-1]: only bytes of valid pixels are used
-  const uint32_t Q0 = row[3 * nD], Q8 = row[-3 * nD];
-  const uint32_t Q4 = __builtin_amdgcn_alignbyte(Cn, B, 3);   // columns 4k+3 .. 4k+6
-  const uint32_t Q12 = __builtin_amdgcn_alignbyte(B, A, 1);   // columns 4k-3 .. 4k
-  // even bytes (0, 2) and odd bytes (1, 3) as u16 lanes, one v_perm each
-  constexpr uint32_t SE = 0x0C020C00u, SO = 0x0C030C01u;
-#define ORB_PK(x, sel) __builtin_amdgcn_perm(0u, (x), (sel))
-  const uint32_t e = pretest_half(ORB_PK(B, SE), ORB_PK(Q0, SE), ORB_PK(Q4, SE), ORB_PK(Q8, SE),
-                                  ORB_PK(Q12, SE), t1, nt1);
-  const uint32_t o = pretest_half(ORB_PK(B, SO), ORB_PK(Q0, SO), ORB_PK(Q4, SO), ORB_PK(Q8, SO),
-                                  ORB_PK(Q12, SO), t1, nt1);
-#undef ORB_PK
-  return ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
-}
-
-// Pretest of the 8 pixels at region columns 8k..8k+7 of region row r: bit j
-// of the result = pixel 8k+j passes.  (Dwords past the row end are read but
-// only feed masked-off pixels.)
-__device__ __forceinline__ uint32_t pretest8(const uint32_t* roi32, int nD, int r, int k, s16x2 t1,
-                                             s16x2 nt1) {
-  const uint32_t* row = roi32 + r * nD + 2 * k;
-  const uint32_t A = row[-1], B0 = row[0], B1 = row[1], Cn = row[2];
-  const uint32_t Q0a = row[3 * nD], Q0b = row[3 * nD + 1];
-  const uint32_t Q8a = row[-3 * nD], Q8b = row[-3 * nD + 1];
-  const uint32_t Q4a = __builtin_amdgcn_alignbyte(B1, B0, 3), Q4b = __builtin_amdgcn_alignbyte(Cn, B1, 3);
-  const uint32_t Q12a = __builtin_amdgcn_alignbyte(B0, A, 1), Q12b = __builtin_amdgcn_alignbyte(B1, B0, 1);
-  constexpr uint32_t SE = 0x0C020C00u, SO = 0x0C030C01u;
-#define ORB_PK(x, sel) __builtin_amdgcn_perm(0u, (x), (sel))
-  const uint32_t ea = pretest_half(ORB_PK(B0, SE), ORB_PK(Q0a, SE), ORB_PK(Q4a, SE),
-                                   ORB_PK(Q8a, SE), ORB_PK(Q12a, SE), t1, nt1);
-  const uint32_t oa = pretest_half(ORB_PK(B0, SO), ORB_PK(Q0a, SO), ORB_PK(Q4a, SO),
-                                   ORB_PK(Q8a, SO), ORB_PK(Q12a, SO), t1, nt1);
-  const uint32_t eb = pretest_half(ORB_PK(B1, SE), ORB_PK(Q0b, SE), ORB_PK(Q4b, SE),
-                                   ORB_PK(Q8b, SE), ORB_PK(Q12b, SE), t1, nt1);
-  const uint32_t ob = pretest_half(ORB_PK(B1, SO), ORB_PK(Q0b, SO), ORB_PK(Q4b, SO),
-                                   ORB_PK(Q8b, SO), ORB_PK(Q12b, SO), t1, nt1);
-#undef ORB_PK
-  return ((ea >> 15) & 1u) | ((oa >> 14) & 2u) | ((ea >> 29) & 4u) | ((oa >> 28) & 8u) |
-         ((eb >> 11) & 16u) | ((ob >> 10) & 32u) | ((eb >> 25) & 64u) | ((ob >> 24) & 128u);
+// Compass pretest of a pixel pair (f16 halves): a pixel can be a FAST(t)
+// corner only if two circularly adjacent compass pixels (circle positions
+// 0,4,8,12) are both darker than v - t or both brighter than v + t.  Each
+// adjacent pair takes one pixel of {0, 8} and one of {4, 12}, so
+//   dark   <=>  max(min(q0, q8), min(q4, q12)) <= v - (t + 1)
+//   bright <=>  min(max(q0, q8), max(q4, q12)) >= v + (t + 1).
+// The sign bit (15 / 31) of the result is set for a pixel that fails both.
+__device__ __forceinline__ uint32_t pretest_pair(uint32_t v, uint32_t q0, uint32_t q4, uint32_t q8,
+                                                 uint32_t q12, h16x2 T) {
+  const h16x2 V = __builtin_bit_cast(h16x2, v);
+  const h16x2 Q0 = __builtin_bit_cast(h16x2, q0), Q4 = __builtin_bit_cast(h16x2, q4);
+  const h16x2 Q8 = __builtin_bit_cast(h16x2, q8), Q12 = __builtin_bit_cast(h16x2, q12);
+  const h16x2 A = __builtin_elementwise_maximum(__builtin_elementwise_minimum(Q0, Q8),
+                                                __builtin_elementwise_minimum(Q4, Q12));
+  const h16x2 B = __builtin_elementwise_minimum(__builtin_elementwise_maximum(Q0, Q8),
+                                                __builtin_elementwise_maximum(Q4, Q12));
+  const h16x2 x = (V - T) - A;  // >= +0: dark
+  const h16x2 y = B - (V + T);  // >= +0: bright
+  return __builtin_bit_cast(uint32_t, x) & __builtin_bit_cast(uint32_t, y);
 }
 
 __global__ __launch_bounds__(256) void k_fast_band(
@@ -299,38 +269,41 @@ __global__ __launch_bounds__(256) void k_fast_band(
     lvl = arena + (long long)img * arenaPitch + plan.lv[l].arenaOff;
     pitch = plan.lv[l].pitch;
   }
-  const int P = (C + 3) & ~3;  // LDS row pitch (bytes)
-  const int nD = P >> 2;       // dwords per LDS row
+  const int P = (C + 20) & ~7;  // LDS row pitch (elements): groups read up to element C + 12
+  const int PD = P >> 1;        // dwords per LDS row (f16 pairs)
   const int iw = C - 6, ih = R - 6, ni = iw * ih;
+  const int nK = (iw + 7) >> 3;  // 8-pixel groups per interior row
   const int nBitWords = (ni >> 5) + 3;
-  const int bandBytes = plan.maxBandBytes;
-  const int bitStride = (bandBytes >> 5) + 3;
-  uint8_t* roi = smem;                                        // R x P band pixels
-  uint32_t* roi32 = (uint32_t*)roi;
-  uint8_t* sc = smem + bandBytes;                             // R x P arc strengths
-  uint16_t* queue = (uint16_t*)(smem + 2 * bandBytes);        // FAST_QUEUE candidates
-  uint16_t* corners = queue + FAST_QUEUE;                     // FAST_CORNERS corners
-  uint32_t* bitsIni = (uint32_t*)(corners + FAST_CORNERS);    // interior survivors, iniTh
-  uint32_t* bitsMin = bitsIni + bitStride;                    // interior survivors, minTh
-  uint8_t* colf = (uint8_t*)(bitsMin + bitStride);            // window edge flags per column
-  uint8_t* cellOf = colf + bandBytes / 7 + 8;                 // cell of each interior column
+  const int bandElems = plan.maxBandBytes;
+  const int bitStride = (bandElems >> 5) + 3;
+  uint32_t* roi32 = (uint32_t*)smem;                            // R x P f16 band pixels
+  const _Float16* roih = (const _Float16*)smem;
+  uint8_t* sc = smem + 2 * bandElems;                           // R x P arc strengths
+  uint16_t* queue = (uint16_t*)(sc + bandElems);                // FAST_QCAP candidates
+  uint16_t* corners = queue + FAST_QCAP;                        // FAST_CORNERS corners
+  uint32_t* bitsIni = (uint32_t*)(corners + FAST_CORNERS);      // interior survivors, iniTh
+  uint32_t* bitsMin = bitsIni + bitStride;                      // interior survivors, minTh
+  uint8_t* colf = (uint8_t*)(bitsMin + bitStride);              // window edge flags per column
+  uint8_t* cellOf = colf + bandElems / 7 + 8;                   // cell of each interior column
   {
-    // Realigning copy: LDS dword k of row r = bytes [x0 + 4k, x0 + 4k + 4) of
+    // Realigning copy: source dword k of row r = bytes [x0 - LPAD + 4k, +4) of
     // the row (level 0 rows can start at any byte: caller stride), through a
     // buffer resource (32-bit offsets) with the row split by a 32-bit
-    // multiply-high instead of a division.  All of a thread's loads are issued
-    // before the first LDS store (one HBM round trip).
-    const int n = R * nD;
-    const uint32_t magic = (uint32_t)((0xFFFFFFFFull + (uint64_t)nD) / (uint64_t)nD);  // ceil(2^32/nD)
+    // multiply-high instead of a division; each source dword becomes two f16
+    // pairs (v_perm + bias).  All of a thread's loads are issued before the
+    // first LDS store (one HBM round trip per batch).
+    const int nS = P >> 2;  // source dwords per row
+    const int n = R * nS;
+    const uint32_t magic = (uint32_t)((0xFFFFFFFFull + (uint64_t)nS) / (uint64_t)nS);  // ceil(2^32/nS)
     const int lh = plan.lv[l].h, lw = plan.lv[l].w;
     const ImgRsrc im = img_rsrc(lvl, (uint32_t)((lh - 1) * pitch + lw));
-    const uint32_t org = (uint32_t)(bd.y0 * pitch + bd.x0) + im.sh;
+    const uint32_t org = (uint32_t)(bd.y0 * pitch + bd.x0 - FAST_LPAD) + im.sh;
     for (int i0 = 0; i0 < n; i0 += FAST_LOADS * 256) {
       uint32_t lo[FAST_LOADS], hi[FAST_LOADS], sft[FAST_LOADS];
 #pragma unroll
       for (int q = 0; q < FAST_LOADS; ++q) {
         const uint32_t i = (uint32_t)min(i0 + q * 256 + tid, n - 1);  // branch-free loads
-        const uint32_t r = __umulhi(i, magic), k = i - r * (uint32_t)nD;
+        const uint32_t r = __umulhi(i, magic), k = i - r * (uint32_t)nS;
         const uint32_t o = org + r * (uint32_t)pitch + 4 * k;
         sft[q] = o & 3u;
         lo[q] = buf_ld32(im.r, o & ~3u);
@@ -339,7 +312,13 @@ __global__ __launch_bounds__(256) void k_fast_band(
 #pragma unroll
       for (int q = 0; q < FAST_LOADS; ++q) {
         const int i = i0 + q * 256 + tid;
-        if (i < n) roi32[i] = __builtin_amdgcn_alignbyte(hi[q], lo[q], sft[q]);
+        if (i < n) {
+          const uint32_t w = __builtin_amdgcn_alignbyte(hi[q], lo[q], sft[q]);
+          uint2 h;
+          h.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | FAST_BIAS;
+          h.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | FAST_BIAS;
+          reinterpret_cast<uint2*>(roi32)[i] = h;
+        }
       }
     }
   }
@@ -360,95 +339,125 @@ __global__ __launch_bounds__(256) void k_fast_band(
     }
   }
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
-  const unsigned long long ltMask = (1ull << lane) - 1ull;
+  // Pixels j >= nvLast of a row's last group lie past the interior.  Phase A
+  // does not mask them in the pretest: their strength byte starts at
+  // FAST_OUTSIDE instead of 0, so a queued one is never scored or listed
+  // (NMS and compaction never read those columns).
+  const int nvLast = iw - 8 * (nK - 1);
+  const unsigned long long outsideLast =
+      nvLast >= 8 ? 0ull : (0x0101010101010101ull << (8 * nvLast));
 
   // Group columns pretested by a pass: all of them in phase A, only those
   // touching a fallback cell in phase B (fbK, built before phase B).
   __shared__ int nFbK;
-  uint16_t* fbK = (uint16_t*)(cellOf + bandBytes / 7 + 8);
+  uint16_t* fbK = (uint16_t*)(cellOf + bandElems / 7 + 8);
 
-  // One FAST pass at threshold t: pretest, arc strengths, corner list (m > t).
-  // In phase B (FB) only pixels of fallback cells, and strengths already known
-  // from phase A are kept.
+  // Score the queued candidates (dense: 256 per pass) and list the corners
+  // (m > t).  In phase B strengths already known from phase A are kept.
+  auto flush = [&](int t, int nq) {
+    for (int j0 = 0; j0 < nq; j0 += 256) {
+      const int j = j0 + tid;
+      bool corner = false;
+      int off = 0;
+      if (j < nq) {
+        off = queue[j];
+        int m = sc[off];  // 0: not scored yet; phase B keeps phase-A strengths
+        if (m == 0) {
+          m = min(max(fast_score(roih + off, P), 0), 255);
+          sc[off] = (uint8_t)m;
+        }
+        corner = m > t && m >= 2;
+      }
+      const unsigned long long bal = __ballot(corner);
+      int cb = 0;
+      if (lane == 0 && bal) cb = atomicAdd(&cCount, __popcll(bal));
+      cb = __builtin_amdgcn_readfirstlane(cb) +
+           (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      if (corner && cb < FAST_CORNERS) corners[cb] = (uint16_t)off;
+    }
+    __syncthreads();
+    if (tid == 0) qCount = 0;
+    __syncthreads();
+  };
+
+  // One FAST pass at threshold t: pretest, queue, arc strengths, corner list.
   auto fast_pass = [&](int t, auto fbTag) {
     constexpr bool FB = decltype(fbTag)::value;
-    s16x2 t1, nt1;
-    t1.x = t1.y = (short)(t + 1);
-    nt1.x = nt1.y = (short)(-(t + 1));
-    // 8-pixel groups (two LDS dwords): phase A covers every group column of
-    // the band, phase B only those listed in fbK
-    const int nK = FB ? nFbK : (nD + 1) >> 1;
-    const int nG = ih * nK;
-    const float invK = 1.0f / (float)nK;
+    h16x2 T;
+    T.x = T.y = (_Float16)(float)(t + 1);
+    const int nKp = FB ? nFbK : nK;
+    const int nG = ih * nKp;
+    const float invK = 1.0f / (float)nKp;
     for (int g0 = 0; g0 < nG; g0 += FAST_GROUPS) {
       const int gi = g0 + tid;
-      uint32_t m8 = 0;
+      uint32_t rp[4] = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
       int off = 0;
       if (gi < nG) {
-        const int rr = (int)(((float)gi + 0.5f) * invK), kk = gi - rr * nK;
+        const int rr = (int)(((float)gi + 0.5f) * invK), kk = gi - rr * nKp;
         const int k = FB ? (int)fbK[kk] : kk;
         const int r = rr + 3;
-        off = r * P + 8 * k;
-        // valid columns 3 <= 8k+j < C-3 (and, in phase B, in a fallback cell)
-        const int lo = max(3 - 8 * k, 0), hi = min(C - 3 - 8 * k, 8);
-        uint32_t cm = hi > lo ? ((1u << hi) - (1u << lo)) : 0u;
+        off = r * P + 8 + 8 * k;  // element of interior column 8k
+        const uint32_t* row = roi32 + r * PD + 4 + 4 * k;
+        const uint2 a = *reinterpret_cast<const uint2*>(row - 2);
+        const uint4 b = *reinterpret_cast<const uint4*>(row);
+        const uint2 c = *reinterpret_cast<const uint2*>(row + 4);
+        const uint4 u = *reinterpret_cast<const uint4*>(row + 3 * PD);  // circle 0 (y + 3)
+        const uint4 d = *reinterpret_cast<const uint4*>(row - 3 * PD);  // circle 8 (y - 3)
+        const uint32_t D[8] = {a.x, a.y, b.x, b.y, b.z, b.w, c.x, c.y};  // dwords -2 .. 5
+        const uint32_t U[4] = {u.x, u.y, u.z, u.w}, Dn[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t q4 = __builtin_amdgcn_alignbyte(D[i + 4], D[i + 3], 2);   // x + 3
+          const uint32_t q12 = __builtin_amdgcn_alignbyte(D[i + 1], D[i], 2);      // x - 3
+          rp[i] = pretest_pair(D[i + 2], U[i], q4, Dn[i], q12, T);
+        }
         if (FB) {
+          // only pixels of fallback cells (and of the interior)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            if ((cm >> j) & 1u) {
-              const int c = cellOf[8 * k + j - 3];
-              if (!((fbMask[c >> 5] >> (c & 31)) & 1u)) cm &= ~(1u << j);
+            const int x = 8 * k + j;
+            bool in = x < iw;
+            if (in) {
+              const int cc = cellOf[x];
+              in = (fbMask[cc >> 5] >> (cc & 31)) & 1u;
             }
+            if (!in) rp[j >> 1] |= (j & 1) ? 0x80000000u : 0x8000u;
           }
-        }
-        if (cm) m8 = pretest8(roi32, nD, r, k, t1, nt1) & cm;
-        if (!FB) {  // non-corners store 0 (two dwords; the second may be the row's pad)
-          uint32_t* z = (uint32_t*)sc + r * nD + 2 * k;
-          z[0] = 0;
-          if (2 * k + 1 < nD) z[1] = 0;
+        } else {
+          // strengths start at 0 (8 bytes, 8-aligned), FAST_OUTSIDE past the interior
+          const unsigned long long z = k == nK - 1 ? outsideLast : 0ull;
+          *reinterpret_cast<unsigned long long*>(sc + off) = z;
         }
       }
       // wave-aggregated append: one LDS atomic per wave, lane offsets by mbcnt
       unsigned long long bj[8];
-      int nj[8], tot = 0;
+      bool pass[8];
+      int tot = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        bj[j] = __ballot((m8 >> j) & 1u);
-        nj[j] = __popcll(bj[j]);
-        tot += nj[j];
+        const uint32_t w = rp[j >> 1];
+        pass[j] = (j & 1) ? ((int)w >= 0) : ((short)(w & 0xFFFFu) >= 0);
+        bj[j] = __ballot(pass[j]);
+        tot += __popcll(bj[j]);
       }
-      int base = 0;
-      if (lane == 0 && tot) base = atomicAdd(&qCount, tot);
-      base = __shfl(base, 0, 64);
+      if (tot) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&qCount, tot);
+        base = __builtin_amdgcn_readfirstlane(base);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if ((m8 >> j) & 1u) queue[base + __popcll(bj[j] & ltMask)] = (uint16_t)(off + j);
-        base += nj[j];
-      }
-      __syncthreads();
-      const int nq = qCount;
-      for (int j0 = 0; j0 < nq; j0 += 256) {
-        const int j = j0 + tid;
-        bool corner = false;
-        int off = 0;
-        if (j < nq) {
-          off = queue[j];
-          int m = FB ? sc[off] : 0;
-          if (m == 0) {
-            m = min(max(fast_score(roi + off, P), 0), 255);
-            sc[off] = (uint8_t)m;
-          }
-          corner = m > t && m >= 2;
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(bj[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], (uint32_t)base));
+          if (pass[j]) queue[pos] = (uint16_t)(off + j);
+          base += __popcll(bj[j]);
         }
-        const unsigned long long bal = __ballot(corner);
-        int cb = 0;
-        if (lane == 0 && bal) cb = atomicAdd(&cCount, __popcll(bal));
-        cb = __shfl(cb, 0, 64) + __popcll(bal & ltMask);
-        if (corner && cb < FAST_CORNERS) corners[cb] = (uint16_t)off;
       }
       __syncthreads();
-      if (tid == 0) qCount = 0;
-      __syncthreads();
+      // every wave reads the count before any wave appends again: the flush
+      // synchronises; a round without one takes a second barrier
+      const int nq = qCount;
+      if (nq > FAST_QFLUSH || g0 + FAST_GROUPS >= nG) flush(t, nq);
+      else __syncthreads();
     }
   };
 
@@ -464,7 +473,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
       if (dense) {
         y = (int)(((float)j + 0.5f) / (float)iw);
         x = j - y * iw;
-        off = (y + 3) * P + (x + 3);
+        off = (y + 3) * P + (x + 8);
         if (fallbackOnly) {
           const int c = cellOf[x];
           if (!((fbMask[c >> 5] >> (c & 31)) & 1u)) continue;
@@ -473,7 +482,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
         off = corners[j];
         const int ry = (int)(((float)off + 0.5f) / (float)P);
         y = ry - 3;
-        x = off - ry * P - 3;
+        x = off - ry * P - 8;
       }
       const uint8_t* c = sc + off;
       const int m = c[0];
@@ -508,7 +517,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
     while (row) {
       const int x = __builtin_ctzll(row);
       row &= row - 1;
-      const int m = sc[(lane + 3) * P + cx0 + x + 3];
+      const int m = sc[(lane + 3) * P + cx0 + x + 8];
       out[o++] = pack_key(bd.x0 + 3 + cx0 + x, bd.y0 + 3 + lane, m - 1);
     }
     return total;
@@ -532,22 +541,21 @@ __global__ __launch_bounds__(256) void k_fast_band(
   // group columns that touch one (wave 0 lists them in order with ballots)
   if (wave == 0) {
     int cnt = 0;
-    const int nK8 = (nD + 1) >> 1;
-    for (int k0 = 0; k0 < nK8; k0 += 64) {
+    for (int k0 = 0; k0 < nK; k0 += 64) {
       const int k = k0 + lane;
       bool hit = false;
-      if (k < nK8) {
+      if (k < nK) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int col = 8 * k + j;
-          if (col >= 3 && col < C - 3) {
-            const int c = cellOf[col - 3];
+          const int x = 8 * k + j;
+          if (x < iw) {
+            const int c = cellOf[x];
             hit = hit || ((fbMask[c >> 5] >> (c & 31)) & 1u);
           }
         }
       }
       const unsigned long long b = __ballot(hit);
-      if (hit) fbK[cnt + __popcll(b & ltMask)] = (uint16_t)k;
+      if (hit) fbK[cnt + __popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)k;
       cnt += __popcll(b);
     }
     if (lane == 0) nFbK = cnt;
@@ -1259,14 +1267,20 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   return hipGetLastError();
 }
 
+// Dynamic LDS of k_fast_band for bands of up to `bandElems` elements (rows x
+// element pitch): f16 pixels, strengths, queue, corner list, two interior
+// bitmaps, per-column flags / cells, phase-B group list.
+size_t orb_k_fast_band_lds(int bandElems) {
+  const size_t bitBytes = 4 * (size_t)((bandElems >> 5) + 3);
+  return (size_t)bandElems * 3 + FAST_QCAP * 2 + FAST_CORNERS * 2 + 2 * bitBytes +
+         2 * ((size_t)bandElems / 7 + 8) + 2 * ((size_t)bandElems / 28 + 8);
+}
+
 hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
                            uint32_t* cellKeys, int32_t* cellCount, int nimg, hipStream_t s) {
-  const size_t bitBytes = 4 * (size_t)((plan->maxBandBytes >> 5) + 3);
-  const size_t lds = (size_t)plan->maxBandBytes * 2 + FAST_QUEUE * 2 + FAST_CORNERS * 2 +
-                     2 * bitBytes + 2 * ((size_t)plan->maxBandBytes / 7 + 8) +
-                     2 * ((size_t)plan->maxBandBytes / 28 + 8);
+  const size_t lds = orb_k_fast_band_lds(plan->maxBandBytes);
   dim3 grid(nbands, nimg), block(256);
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, *plan, bands, cells, cellKeys, cellCount);

@@ -43,7 +43,7 @@ struct OrbPlanDesc {
   int srcW, srcH;
   int nBlurTiles;    // blur tiles over all levels of one image
   int nBands;        // FAST bands over all levels
-  int maxBandBytes;  // largest band's LDS footprint: rows x (cols rounded up to 4)
+  int maxBandBytes;  // largest FAST band in elements: rows x LDS pitch ((cols + 20) & ~7)
   OrbLevelDesc lv[ORB_MAX_LEVELS];
 };
 
@@ -61,7 +61,7 @@ struct OrbBandDesc {
   int16_t level, y0, y1, x0, x1, nCells;
   int32_t cellBeg;
 };
-#define ORB_BAND_BYTES 8192  // LDS budget for one band's pixels (and again for scores)
+#define ORB_BAND_BYTES 6656  // elements (rows x LDS pitch) of one FAST band: f16 pixels + strengths; 5 workgroups per CU (swept 4-10 K)
 
 // One ORB_BLUR_TW x ORB_BLUR_TH output tile of the 7x7 Gaussian pass over level `level`.
 struct OrbTileDesc {

@@ -27,6 +27,7 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
                             int dh, const int* xofs, const void* alpha, const int* yofs,
                             const void* beta, int xmax, int nimg, hipStream_t s);
+size_t orb_k_fast_band_lds(int bandElems);
 hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
@@ -435,7 +436,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
       int e = c + 1;
       while (e < d.cellEnd && cells[e].y0 == b.y0 && e - c < 64) {  // k_fast_band: <= 64 cells
         const int x1 = std::max<int>(b.x1, cells[e].x1);
-        if ((b.y1 - b.y0) * ((x1 - b.x0 + 3) & ~3) > bandBudget) break;
+        if ((b.y1 - b.y0) * ((x1 - b.x0 + 20) & ~7) > bandBudget) break;
         b.x1 = (int16_t)x1;
         ++e;
       }
@@ -445,7 +446,8 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
       if (b.y1 - b.y0 - 6 > 64) return ORB_EINVAL;
       for (int k = c; k < e; ++k)
         if (cells[k].x1 - cells[k].x0 - 6 > 64) return ORB_EINVAL;
-      maxBandBytes = std::max(maxBandBytes, (b.y1 - b.y0) * ((b.x1 - b.x0 + 3) & ~3));
+      // k_fast_band's LDS row pitch in elements ((C + 20) & ~7, see the kernel)
+      maxBandBytes = std::max(maxBandBytes, (b.y1 - b.y0) * ((b.x1 - b.x0 + 20) & ~7));
       bands.push_back(b);
       c = e;
     }
@@ -495,7 +497,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   }
   // k_fast_band: one band = at least one cell; its pixels and scores + the
   // candidate queue must fit the 64 KiB a workgroup may allocate
-  if (2 * (size_t)maxBandBytes + 4096 > 64 * 1024) return ORB_EINVAL;
+  if (orb_k_fast_band_lds(maxBandBytes) > 64 * 1024) return ORB_EINVAL;
   P.ncells = (int)cells.size();
   P.nBlurTiles = (int)tiles.size();
   P.nBands = (int)bands.size();
