@@ -1112,6 +1112,25 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     lvl = arena + (long long)img * arenaPitch + L.arenaOff;
     pitch = L.pitch;
   }
+  // The blurred 37 x 37 patch the descriptor samples (rotated pattern within
+  // +-18 px, max radius 18.38) does not depend on the angle: its loads are
+  // issued first, so they are in flight together with the IC_Angle loads
+  // (one memory round trip per keypoint).
+  __shared__ __attribute__((aligned(16))) uint32_t patch[4][37][ORB_PATCH_DW];
+  const int bp = L.blurPitch;
+  const __amdgpu_buffer_rsrc_t rb =
+      make_rsrc(blur + (long long)img * blurPitch + L.blurOff, (uint32_t)(L.h * bp));
+  const int colA = cx - 18, psh = colA & 3;  // wave-uniform alignment of the patch
+  uint32_t pv[7];
+  {
+    const uint32_t pbase = (uint32_t)((cy - 18) * bp + (colA & ~3));
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int i = min(lane + 64 * q, 37 * 11 - 1);
+      const int r = i / 11, k = i - r * 11;
+      pv[q] = buf_ld32(rb, pbase + (uint32_t)(r * bp + 4 * k));
+    }
+  }
   // ---- IC_Angle (src/ORBextractor.cc:77-113), exact integer moments.
   // Lane = (row v = (lane & 31) - 15, half = lane >> 5): 16 bytes at columns
   // 16*half-16 .. 16*half-1 of row cy+v, masked to |u| <= umax[|v|].  Row sum
@@ -1151,32 +1170,16 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     a = c;
     b = s;
   }
-  // 512 samples of the blurred level around (cx, cy).  The rotated pattern
-  // stays within +-18 px (max pattern radius 18.38), so the wave first stages
-  // the 37 x 37 patch into LDS with row-contiguous loads (11 aligned dwords
-  // per row, shared by the whole wave), then gathers bytes from LDS: scattered
-  // byte loads from global memory cost one L1 tag lookup per distinct line.
-  __shared__ __attribute__((aligned(16))) uint32_t patch[4][37][ORB_PATCH_DW];
-  const int bp = L.blurPitch;
-  const __amdgpu_buffer_rsrc_t rb =
-      make_rsrc(blur + (long long)img * blurPitch + L.blurOff, (uint32_t)(L.h * bp));
-  const int colA = cx - 18, psh = colA & 3;  // wave-uniform alignment of the patch
-  {
-    const uint32_t base = (uint32_t)((cy - 18) * bp + (colA & ~3));
-    uint32_t pv[7];
+  // 512 samples of the blurred level around (cx, cy): the patch (loaded
+  // above, 11 aligned dwords per row, row-contiguous) goes to LDS and the
+  // samples are byte gathers from LDS: scattered byte loads from global memory
+  // cost one L1 tag lookup per distinct line.
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int i = min(lane + 64 * q, 37 * 11 - 1);
+  for (int q = 0; q < 7; ++q) {
+    const int i = lane + 64 * q;
+    if (i < 37 * 11) {
       const int r = i / 11, k = i - r * 11;
-      pv[q] = buf_ld32(rb, base + (uint32_t)(r * bp + 4 * k));
-    }
-#pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int i = lane + 64 * q;
-      if (i < 37 * 11) {
-        const int r = i / 11, k = i - r * 11;
-        patch[w][r][k] = pv[q];
-      }
+      patch[w][r][k] = pv[q];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1187,10 +1190,13 @@ __global__ __launch_bounds__(256) void k_orient_desc(
 #pragma unroll
   for (int kq = 0; kq < 4; ++kq) {
     const int test = lane + 64 * kq;
+    // one 4-byte load per test (x0, y0, x1, y1 as int8): the whole table is
+    // 1 KB per wave through L1 (a float4 table would be 4 KB)
     const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
     const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
-    v0[kq] = pb[cv_round(px0 * b + py0 * a) * (ORB_PATCH_DW * 4) + cv_round(px0 * a - py0 * b)];
-    v1[kq] = pb[cv_round(px1 * b + py1 * a) * (ORB_PATCH_DW * 4) + cv_round(px1 * a - py1 * b)];
+    // |rounded offsets| <= 19: 24-bit multiplies (full rate)
+    v0[kq] = pb[__mul24(cv_round(px0 * b + py0 * a), ORB_PATCH_DW * 4) + cv_round(px0 * a - py0 * b)];
+    v1[kq] = pb[__mul24(cv_round(px1 * b + py1 * a), ORB_PATCH_DW * 4) + cv_round(px1 * a - py1 * b)];
   }
   unsigned long long words[4];
 #pragma unroll
@@ -1219,12 +1225,12 @@ __global__ __launch_bounds__(256) void k_orient_desc(
 extern "C" {
 
 hipError_t orb_k_upload_constants(hipStream_t s) {
-  int8_t pat[2 * ORB_PATTERN_POINTS];
+  static int8_t pat[2 * ORB_PATTERN_POINTS];
   for (int i = 0; i < 2 * ORB_PATTERN_POINTS; ++i) pat[i] = (int8_t)kOrbPatternXY[i];
   hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_pattern), pat, sizeof(pat), 0,
                                         hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return e;
-  return hipSuccess;
+  return hipStreamSynchronize(s);  // the static staging array is reused
 }
 
 hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s) {
