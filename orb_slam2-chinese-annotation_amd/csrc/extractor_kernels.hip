@@ -242,38 +242,24 @@ __device__ __forceinline__ uint32_t pretest_pair(uint32_t v, uint32_t q0, uint32
   return __builtin_bit_cast(uint32_t, x) & __builtin_bit_cast(uint32_t, y);
 }
 
+#ifdef ORB_FAST_STAMPS  // phase timing probe (tools/probe/fast_stamps.py), off by default
+__device__ unsigned long long g_fast_stamps[4096][8];
+#define FSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.y == 0 && b < 4096) g_fast_stamps[b][k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define FSTAMP(k) do { } while (0)
+#endif
 __global__ __launch_bounds__(256) void k_fast_band(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
-    const OrbBandDesc* __restrict__ bands, const OrbCellDesc* __restrict__ cells,
+    const OrbBandDesc* __restrict__ bands, const OrbCellDesc* __restrict__ cells, int nBands,
     uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qCount, cCount;
   __shared__ uint32_t fbMask[2];  // cells (of this band) that fall back to minThFAST
+  __shared__ int16_t cellX0[64], cellWW[64];  // cell windows: first interior column, width
+  __shared__ int nFbK;
   const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = blockDim.x >> 6;
-  const OrbBandDesc bd = bands[blockIdx.x];
-  const int l = bd.level;
-  const int R = bd.y1 - bd.y0, C = bd.x1 - bd.x0;
-  const long long slot0 = (long long)img * plan.ncells + bd.cellBeg;
-  if (R < 7 || C < 7) {
-    for (int c = tid; c < bd.nCells; c += 256) cellCount[slot0 + c] = 0;
-    return;
-  }
-  const uint8_t* lvl;
-  int pitch;
-  if (l == 0) {
-    lvl = img0 + (long long)img * img0Pitch;
-    pitch = img0Stride;
-  } else {
-    lvl = arena + (long long)img * arenaPitch + plan.lv[l].arenaOff;
-    pitch = plan.lv[l].pitch;
-  }
-  const int P = (C + 20) & ~7;  // LDS row pitch (elements): groups read up to element C + 12
-  const int PD = P >> 1;        // dwords per LDS row (f16 pairs)
-  const int iw = C - 6, ih = R - 6, ni = iw * ih;
-  const int nK = (iw + 7) >> 3;  // 8-pixel groups per interior row
-  const int nBitWords = (ni >> 5) + 3;
   const int bandElems = plan.maxBandBytes;
   const int bitStride = (bandElems >> 5) + 3;
   uint32_t* roi32 = (uint32_t*)smem;                            // R x P f16 band pixels
@@ -285,42 +271,93 @@ __global__ __launch_bounds__(256) void k_fast_band(
   uint32_t* bitsMin = bitsIni + bitStride;                      // interior survivors, minTh
   uint8_t* colf = (uint8_t*)(bitsMin + bitStride);              // window edge flags per column
   uint8_t* cellOf = colf + bandElems / 7 + 8;                   // cell of each interior column
-  {
-    // Realigning copy: source dword k of row r = bytes [x0 - LPAD + 4k, +4) of
-    // the row (level 0 rows can start at any byte: caller stride), through a
-    // buffer resource (32-bit offsets) with the row split by a 32-bit
-    // multiply-high instead of a division; each source dword becomes two f16
-    // pairs (v_perm + bias).  All of a thread's loads are issued before the
-    // first LDS store (one HBM round trip per batch).
-    const int nS = P >> 2;  // source dwords per row
-    const int n = R * nS;
+
+  // A workgroup takes bands blockIdx.x, + gridDim.x, ...: the next band's
+  // pixels and cell descriptors are loaded into registers while the current
+  // band is processed, so each band's HBM round trip overlaps the previous
+  // band's work.  Band pixels: source dword k of row r = bytes
+  // [x0 - LPAD + 4k, +4) of the row (level 0 rows can start at any byte:
+  // caller stride), through a buffer resource (32-bit offsets), the row split
+  // by a 32-bit multiply-high instead of a division.  One batch of FAST_LOADS
+  // dwords per thread covers a band (host-checked).
+  uint32_t plo[FAST_LOADS], phi[FAST_LOADS], psft[FAST_LOADS];
+  OrbCellDesc pcell = {};
+  auto issue = [&](const OrbBandDesc& q) {
+    const int ql = q.level, qR = q.y1 - q.y0, qC = q.x1 - q.x0;
+    const uint8_t* qlvl;
+    int qpitch;
+    if (ql == 0) {
+      qlvl = img0 + (long long)img * img0Pitch;
+      qpitch = img0Stride;
+    } else {
+      qlvl = arena + (long long)img * arenaPitch + plan.lv[ql].arenaOff;
+      qpitch = plan.lv[ql].pitch;
+    }
+    const int nS = ((qC + 20) & ~7) >> 2;  // source dwords per row
+    const int n = max(qR * nS, 1);
     const uint32_t magic = (uint32_t)((0xFFFFFFFFull + (uint64_t)nS) / (uint64_t)nS);  // ceil(2^32/nS)
-    const int lh = plan.lv[l].h, lw = plan.lv[l].w;
-    const ImgRsrc im = img_rsrc(lvl, (uint32_t)((lh - 1) * pitch + lw));
-    const uint32_t org = (uint32_t)(bd.y0 * pitch + bd.x0 - FAST_LPAD) + im.sh;
-    for (int i0 = 0; i0 < n; i0 += FAST_LOADS * 256) {
-      uint32_t lo[FAST_LOADS], hi[FAST_LOADS], sft[FAST_LOADS];
+    const ImgRsrc im = img_rsrc(qlvl, (uint32_t)((plan.lv[ql].h - 1) * qpitch + plan.lv[ql].w));
+    const uint32_t org = (uint32_t)(q.y0 * qpitch + q.x0 - FAST_LPAD) + im.sh;
 #pragma unroll
-      for (int q = 0; q < FAST_LOADS; ++q) {
-        const uint32_t i = (uint32_t)min(i0 + q * 256 + tid, n - 1);  // branch-free loads
-        const uint32_t r = __umulhi(i, magic), k = i - r * (uint32_t)nS;
-        const uint32_t o = org + r * (uint32_t)pitch + 4 * k;
-        sft[q] = o & 3u;
-        lo[q] = buf_ld32(im.r, o & ~3u);
-        hi[q] = buf_ld32(im.r, (o & ~3u) + 4);
-      }
+    for (int k8 = 0; k8 < FAST_LOADS; ++k8) {
+      const uint32_t i = (uint32_t)min(k8 * 256 + tid, n - 1);  // branch-free loads
+      const uint32_t r = __umulhi(i, magic), k = i - r * (uint32_t)nS;
+      const uint32_t o = org + r * (uint32_t)qpitch + 4 * k;
+      psft[k8] = o & 3u;
+      plo[k8] = buf_ld32(im.r, o & ~3u);
+      phi[k8] = buf_ld32(im.r, (o & ~3u) + 4);
+    }
+    if (tid < q.nCells) pcell = cells[q.cellBeg + tid];
+  };
+  int b = blockIdx.x;
+  if (b >= nBands) return;
+  OrbBandDesc nbd = bands[b];
+  issue(nbd);
+  for (; b < nBands; b += gridDim.x) {
+  FSTAMP(0);
+  const OrbBandDesc bd = nbd;
+  const OrbCellDesc myCell = pcell;
+  const int R = bd.y1 - bd.y0, C = bd.x1 - bd.x0;
+  const long long slot0 = (long long)img * plan.ncells + bd.cellBeg;
+  const bool tiny = R < 7 || C < 7;
+  const int P = (C + 20) & ~7;  // LDS row pitch (elements): groups read up to element C + 12
+  const int PD = P >> 1;        // dwords per LDS row (f16 pairs)
+  if (!tiny) {
+    // prefetched band -> LDS: each source dword becomes two f16 pairs (v_perm + bias)
+    const int n = R * (P >> 2);
 #pragma unroll
-      for (int q = 0; q < FAST_LOADS; ++q) {
-        const int i = i0 + q * 256 + tid;
-        if (i < n) {
-          const uint32_t w = __builtin_amdgcn_alignbyte(hi[q], lo[q], sft[q]);
-          uint2 h;
-          h.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | FAST_BIAS;
-          h.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | FAST_BIAS;
-          reinterpret_cast<uint2*>(roi32)[i] = h;
-        }
+    for (int k8 = 0; k8 < FAST_LOADS; ++k8) {
+      const int i = k8 * 256 + tid;
+      if (i < n) {
+        const uint32_t w = __builtin_amdgcn_alignbyte(phi[k8], plo[k8], psft[k8]);
+        uint2 h;
+        h.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | FAST_BIAS;
+        h.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | FAST_BIAS;
+        reinterpret_cast<uint2*>(roi32)[i] = h;
       }
     }
+  }
+  if (b + (int)gridDim.x < nBands) {
+    nbd = bands[b + gridDim.x];
+    issue(nbd);
+  }
+  if (tiny) {
+    for (int c = tid; c < bd.nCells; c += 256) cellCount[slot0 + c] = 0;
+    continue;
+  }
+  const int iw = C - 6, ih = R - 6, ni = iw * ih;
+  const int nK = (iw + 7) >> 3;  // 8-pixel groups per interior row
+  const int nBitWords = (ni >> 5) + 3;
+  // cell windows of the band (<= 64 cells, host-checked): they tile the
+  // interior left to right, so cellOf[x] = the last cell starting at or
+  // before x, filled by every thread in parallel after one barrier
+  FSTAMP(1);
+  int cx0 = 0, ww = 0;
+  if (tid < bd.nCells) {
+    cx0 = myCell.x0 - bd.x0;
+    ww = myCell.x1 - myCell.x0 - 6;
+    cellX0[tid] = (int16_t)(ww > 0 ? cx0 : 0x7FFF);
+    cellWW[tid] = (int16_t)ww;
   }
   for (int i = tid; i < nBitWords; i += 256) bitsIni[i] = bitsMin[i] = 0;
   for (int i = tid; i < iw; i += 256) colf[i] = 0;
@@ -329,14 +366,14 @@ __global__ __launch_bounds__(256) void k_fast_band(
     fbMask[0] = fbMask[1] = 0;
   }
   __syncthreads();
-  for (int ci = tid; ci < bd.nCells; ci += 256) {
-    const OrbCellDesc cd = cells[bd.cellBeg + ci];
-    const int cx0 = cd.x0 - bd.x0, ww = cd.x1 - cd.x0 - 6;
-    if (ww > 0) {
-      colf[cx0] |= 1;           // left window edge: x-1 is outside
-      colf[cx0 + ww - 1] |= 2;  // right window edge: x+1 is outside
-      for (int x = 0; x < ww; ++x) cellOf[cx0 + x] = (uint8_t)ci;
-    }
+  if (tid < bd.nCells && ww > 0) {
+    colf[cx0] |= 1;           // left window edge: x-1 is outside
+    colf[cx0 + ww - 1] |= 2;  // right window edge: x+1 is outside
+  }
+  for (int x = tid; x < iw; x += 256) {
+    int c = 0;
+    while (c + 1 < bd.nCells && cellX0[c + 1] <= x) ++c;
+    cellOf[x] = (uint8_t)c;
   }
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
   // Pixels j >= nvLast of a row's last group lie past the interior.  Phase A
@@ -349,7 +386,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
 
   // Group columns pretested by a pass: all of them in phase A, only those
   // touching a fallback cell in phase B (fbK, built before phase B).
-  __shared__ int nFbK;
   uint16_t* fbK = (uint16_t*)(cellOf + bandElems / 7 + 8);
 
   // Score the queued candidates (dense: 256 per pass) and list the corners
@@ -505,8 +541,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
   // Compaction of cell ci from `bits`, one wave, lane = window row (ih <= 64,
   // host-checked).  Returns the cell's key count (wave-uniform).
   auto compact = [&](int ci, const uint32_t* bits) -> int {
-    const OrbCellDesc cd = cells[bd.cellBeg + ci];
-    const int cx0 = cd.x0 - bd.x0, ww = cd.x1 - cd.x0 - 6;
+    const int cx0 = cellX0[ci], ww = cellWW[ci];
     if (ww <= 0) return 0;
     uint32_t* out = cellKeys + (slot0 + ci) * plan.keyCap;
     unsigned long long row = lane < ih ? bit_run(bits, lane * iw + cx0, ww) : 0ull;
@@ -524,9 +559,12 @@ __global__ __launch_bounds__(256) void k_fast_band(
   };
 
   // ---- phase A: every cell at iniThFAST
+  FSTAMP(2);
   fast_pass(ti, std::false_type{});
+  FSTAMP(3);
   nms_pass(ti, bitsIni, false);
   __syncthreads();
+  FSTAMP(4);
   for (int ci = wave; ci < bd.nCells; ci += nw) {
     const int n = compact(ci, bitsIni);
     if (lane == 0) {
@@ -536,7 +574,8 @@ __global__ __launch_bounds__(256) void k_fast_band(
   }
   if (tid == 0) cCount = 0;
   __syncthreads();
-  if ((fbMask[0] | fbMask[1]) == 0) return;
+  FSTAMP(5);
+  if ((fbMask[0] | fbMask[1]) == 0) { FSTAMP(6); continue; }  // LDS free: barrier above
   // ---- phase B: cells without an iniThFAST keypoint, at minThFAST, over the
   // group columns that touch one (wave 0 lists them in order with ballots)
   if (wave == 0) {
@@ -569,7 +608,16 @@ __global__ __launch_bounds__(256) void k_fast_band(
     const int n = compact(ci, bitsMin);
     if (lane == 0) cellCount[slot0 + ci] = n;
   }
+  FSTAMP(7);
+  __syncthreads();  // the next band's pixels overwrite LDS
+  }  // band loop
 }
+
+#ifdef ORB_FAST_STAMPS
+extern "C" hipError_t orb_k_fast_stamps(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fast_stamps), sizeof(g_fast_stamps));
+}
+#endif
 
 // ================================================================ k_octree
 // ExtractorNode::DivideNode + ORBextractor::DistributeOctTree
@@ -1287,9 +1335,13 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
                            uint32_t* cellKeys, int32_t* cellCount, int nimg, hipStream_t s) {
   const size_t lds = orb_k_fast_band_lds(plan->maxBandBytes);
-  dim3 grid(nbands, nimg), block(256);
+  // each workgroup takes ORB_FAST_BANDS_PER_WG bands (default 2; swept 1-8), prefetching the next
+  static const int perWg =
+      getenv("ORB_FAST_BANDS_PER_WG") ? std::max(1, atoi(getenv("ORB_FAST_BANDS_PER_WG"))) : 2;
+  if ((size_t)plan->maxBandBytes > (size_t)4 * FAST_LOADS * 256) return hipErrorInvalidValue;
+  dim3 grid((nbands + perWg - 1) / perWg, nimg), block(256);
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, bands, cells, cellKeys, cellCount);
+                     arenaPitch, *plan, bands, cells, nbands, cellKeys, cellCount);
   return hipGetLastError();
 }
 

@@ -363,7 +363,8 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   std::vector<OrbBandDesc> bands;
   int maxBandBytes = 0;
   static const int bandBudget =
-      getenv("ORB_BAND_BYTES") ? std::max(2048, atoi(getenv("ORB_BAND_BYTES"))) : ORB_BAND_BYTES;
+      getenv("ORB_BAND_BYTES") ? std::min(8192, std::max(2048, atoi(getenv("ORB_BAND_BYTES"))))
+                               : ORB_BAND_BYTES;  // k_fast_band stages <= 8192 elements per pass
   long long arena = 0, blurArena = 0;
   int keyCap = 1, maxRows = 7, maxCols = 7, maxCellsPerLevel = 1, nodeCapMax = 1, slots = 0;
   for (int l = 0; l < L; ++l) {
