@@ -1014,7 +1014,12 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     const int lane = tid & 63;
     // dword start clamped into the row (keeping 4-alignment on aligned levels)
     const int c = min(max(colA + 4 * lane, 0), aligned ? ((L.w - 1) & ~3) : L.w - 1);
-    auto rowOff = [&](int r) { return (uint32_t)(reflect101(td.y0 - 3 + r, L.h) * pitch); };
+    // rows outside the level only for the first / last tile row (uniform test)
+    const bool rowsInside = td.y0 >= 3 && td.y0 + BLUR_SH - 3 <= L.h;
+    auto rowOff = [&](int r) {
+      const int y = td.y0 - 3 + r;
+      return (uint32_t)((rowsInside ? y : reflect101(y, L.h)) * pitch);
+    };
     if (aligned)
       stage_rows<true, (BLUR_SH + 3) / 4>(im, BLUR_SH, BLUR_WROW, (uint32_t)c, &raw[0][0], BLUR_WROW + 1, rowOff);
     else

@@ -171,7 +171,9 @@ __device__ __forceinline__ ImgRsrc img_rsrc(const uint8_t* p, uint32_t bytes) {
 template <bool ALIGNED, int B, class RowOff>
 __device__ __forceinline__ void stage_rows(const ImgRsrc& im, int nR, int nW, uint32_t colOff,
                                            uint32_t* lds, int ldsPitch, RowOff rowOff) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wave index through readfirstlane: the row of each load is wave-uniform,
+  // so rowOff (e.g. a reflect-101 loop) runs on the scalar unit
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int r0 = 0; r0 < nR; r0 += 4 * B) {
     uint32_t lo[B], hi[B], sh[B];
 #pragma unroll
