@@ -29,17 +29,23 @@
 // writes two full 128-byte rows per store.
 #define PYR_TW 128
 #define PYR_TH 32
-#define PYR_SROWS 44  // >= source rows a 32-row output tile can touch (scale <= 1.25), multiple of 4
-#define PYR_SW 44     // >= dwords of source row a 128-column tile touches (+2 read-ahead)
+// Staged source window (rows x dwords): >= the source rows a 32-row output
+// tile touches, multiple of 4, and >= the dwords of source row a 128-column
+// tile touches + 2 read-ahead.  Narrow: scale factors <= 1.25 (every ORB-SLAM2
+// configuration uses 1.2); wide: <= 1.9 (the planner checks every tile).
+#define PYR_SROWS 44
+#define PYR_SW 44
+#define PYR_SROWS_WIDE 64
+#define PYR_SW_WIDE 64
 
-template <bool ALIGNED>
+template <bool ALIGNED, int SROWS = PYR_SROWS, int SW = PYR_SW>
 __global__ __launch_bounds__(256) void k_pyr_resize(
     const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sw, int sh,
     uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
     const int* __restrict__ xofs, const int* __restrict__ alpha,
     const int* __restrict__ yofs, const int* __restrict__ beta) {
   // alpha/beta pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
-  __shared__ __attribute__((aligned(16))) uint32_t tile[PYR_SROWS][PYR_SW];
+  __shared__ __attribute__((aligned(16))) uint32_t tile[SROWS][SW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int tx = tid & 31, ty = tid >> 5;
   const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
@@ -69,7 +75,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   {
     const ImgRsrc im = img_rsrc(src + (long long)blockIdx.z * srcImgPitch,
                                 (uint32_t)((sh - 1) * srcStride + sw));
-    stage_rows<ALIGNED, PYR_SROWS / 4>(im, nR, nW, (uint32_t)(colBase + 4 * lane), &tile[0][0], PYR_SW,
+    stage_rows<ALIGNED, SROWS / 4>(im, nR, nW, (uint32_t)(colBase + 4 * lane), &tile[0][0], SW,
                         [&](int r) { return (uint32_t)((syA + r) * srcStride); });
   }
   __syncthreads();
@@ -1311,18 +1317,20 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             int dh, const int* xofs, const void* alpha, const int* yofs,
                             const void* beta, int xmax, int nimg, hipStream_t s) {
   (void)xmax;  // folded into the alpha table: (2048, 0) past xmax
-  // tile bounds assume a downscale of at most 1.25x per level (checked by the planner)
+  // tile bounds: narrow variant for a per-level downscale <= 1.25, wide <= 1.9
+  const bool wide = (double)sw / dw > 1.25 || (double)sh / dh > 1.25;
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, nimg), block(256);
   // every image base and row start 4-aligned: one load per staged dword
   const bool aligned = (srcStride & 3) == 0 && (((uintptr_t)src) & 3) == 0 && (srcImgPitch & 3) == 0;
-  if (aligned)
-    hipLaunchKernelGGL(k_pyr_resize<true>, grid, block, 0, s, src, srcImgPitch, srcStride, sw, sh,
-                       dst, dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,
-                       (const int*)beta);
-  else
-    hipLaunchKernelGGL(k_pyr_resize<false>, grid, block, 0, s, src, srcImgPitch, srcStride, sw, sh,
-                       dst, dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,
-                       (const int*)beta);
+#define ORB_RESIZE_LAUNCH(AL, R, W)                                                              \
+  hipLaunchKernelGGL((k_pyr_resize<AL, R, W>), grid, block, 0, s, src, srcImgPitch, srcStride, sw, \
+                     sh, dst, dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,      \
+                     (const int*)beta)
+  if (!wide && aligned) ORB_RESIZE_LAUNCH(true, PYR_SROWS, PYR_SW);
+  else if (!wide) ORB_RESIZE_LAUNCH(false, PYR_SROWS, PYR_SW);
+  else if (aligned) ORB_RESIZE_LAUNCH(true, PYR_SROWS_WIDE, PYR_SW_WIDE);
+  else ORB_RESIZE_LAUNCH(false, PYR_SROWS_WIDE, PYR_SW_WIDE);
+#undef ORB_RESIZE_LAUNCH
   return hipGetLastError();
 }
 

@@ -395,10 +395,12 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     const int minBX = 16, minBY = 16, maxBX = d.w - 16, maxBY = d.h - 16;
     const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
     const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
-    if (nCols <= 0 || nRows <= 0) return ORB_EINVAL;
-    const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+    // a level under 30 px of border-free width or height has no cells (the
+    // reference's cell loops run zero times: no keypoints on that level)
+    const int wCell = nCols > 0 ? (int)ceilf(width / nCols) : 0;
+    const int hCell = nRows > 0 ? (int)ceilf(height / nRows) : 0;
     d.cellBeg = (int)cells.size();
-    for (int i = 0; i < nRows; ++i) {
+    for (int i = 0; i < nRows && nCols > 0; ++i) {
       const float iniY = (float)(minBY + i * hCell);
       float maxY = iniY + hCell + 6;
       if (iniY >= maxBY - 3) continue;
@@ -493,6 +495,25 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
         const short b0 = satShort(cvRoundF((1.f - fy) * 2048)), b1 = satShort(cvRoundF(fy * 2048));
         rtab[d.rtabY + dy] = sy;
         rtab[d.rtabY + d.h + dy] = (int32_t)(((uint32_t)(uint16_t)b1 << 16) | (uint16_t)b0);
+      }
+      // k_pyr_resize stages each 128 x 32 output tile's source window in LDS
+      // (narrow 44 x 44 dwords up to a 1.25 downscale, wide 64 x 64 beyond):
+      // every tile of this level must fit the variant orb_k_pyr_resize picks
+      const bool wide = (double)sw / d.w > 1.25 || (double)sh / d.h > 1.25;
+      const int SR = wide ? 64 : 44, SWd = wide ? 64 : 44;
+      const int32_t* xo = &rtab[d.rtabX];
+      const int32_t* yo = &rtab[d.rtabY];
+      for (int x0 = 0; x0 < d.w; x0 += 128) {
+        const int xl = std::min(x0 + 127, d.w - 1), xt = std::min(x0 + 124, d.w - 1);
+        const int colBase = xo[x0] & ~3, sxB = std::min(xo[xl] + 1, sw - 1);
+        const int nW = ((sxB - colBase) >> 2) + 1, lastRead = ((xo[xt] - colBase) >> 2) + 2;
+        if (nW > 64 || nW > SWd || lastRead >= SWd) return ORB_EINVAL;
+      }
+      for (int y0 = 0; y0 < d.h; y0 += 32) {
+        const int yl = std::min(y0 + 31, d.h - 1);
+        const int syA = std::min(std::max(yo[y0], 0), sh - 1);
+        const int syB = std::min(std::max(yo[yl] + 1, 0), sh - 1);
+        if (syB - syA + 1 > SR) return ORB_EINVAL;
       }
     }
   }
@@ -659,9 +680,10 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
                                   int min_th_fast, int device, orb_extractor_t** out) {
   if (!out) return ORB_EINVAL;
   *out = nullptr;
-  // k_pyr_resize stages tiles sized for a per-level downscale of at most 1.25
+  // k_pyr_resize stages tiles sized for a per-level downscale of at most 1.9
+  // (the planner checks every tile of every level)
   if (nfeatures < 0 || nlevels < 1 || nlevels > ORB_MAX_LEVELS || !(scale_factor > 1.0f) ||
-      !(scale_factor <= 1.25f) || nfeatures > 60000)
+      !(scale_factor <= 1.9f) || nfeatures > 60000)
     return ORB_EINVAL;
   orb_status_t st = check_device(device);
   if (st) return st;

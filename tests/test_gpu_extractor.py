@@ -158,3 +158,32 @@ def test_batch_matches_single(gpu):
         assert cnt[f] == len(k1)
         assert kps[f, : cnt[f]].tobytes() == k1.tobytes()
         assert desc[f, : cnt[f]].tobytes() == d1.tobytes()
+
+
+@pytest.mark.parametrize("w,h,nf,sf,nl", [
+    (640, 480, 1000, 1.2, 1),      # single level
+    (1241, 376, 1500, 1.2, 12),    # deep pyramid (level 11: 167 x 51)
+    (640, 480, 800, 1.1, 8),       # finer scale steps
+    (1920, 1080, 2000, 1.5, 6),    # wide resize variant (downscale > 1.25)
+    (1241, 376, 1000, 1.9, 4),     # widest supported downscale
+    (1241, 376, 1000, 1.25, 8),    # narrow variant's limit
+])
+def test_extractor_parameters(gpu, oracle, w, h, nf, sf, nl):
+    """ORBextractor(nfeatures, scaleFactor, nlevels, 20, 7) for parameters other
+    than the yaml defaults: scale tables, quotas, pyramid, keypoints and
+    descriptors all bit-exact."""
+    img = gpu.synth_image(11, 0, w, h)
+    ext = gpu.ORBextractor(nf, sf, nl, 20, 7)
+    k_gpu, d_gpu = ext(img)
+    k_ref, d_ref, _ = oracle.extract(img, nf, sf, nl, 20, 7)
+    assert len(k_gpu) > 0
+    assert k_gpu.tobytes() == k_ref.tobytes(), _diff_report(k_gpu, d_gpu, k_ref, d_ref)
+    assert d_gpu.tobytes() == d_ref.tobytes()
+    ref_pyr = oracle.pyramid(img, sf, nl)
+    for l, lv in enumerate(ext.mvImagePyramid):
+        assert np.ascontiguousarray(lv).tobytes() == ref_pyr[l].tobytes(), f"level {l}"
+
+
+def test_extractor_rejects_unsupported_scale(gpu):
+    with pytest.raises(gpu.OrbError):
+        gpu.ORBextractor(1000, 2.5, 8, 20, 7)
