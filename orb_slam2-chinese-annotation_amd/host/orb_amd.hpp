@@ -16,6 +16,7 @@
 #include <map>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/orb_abi.h"
@@ -488,6 +489,58 @@ class ORBmatcher {
                                         mps.data(), mpDesc.data(), (float)th, vpMatched.data(),
                                         &n),
           "SearchByProjection(KF, Scw)");
+    return n;
+  }
+
+  // SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo),
+  // src/ORBmatcher.cc:718-901.  hasMp[i] = GetMapPoint(i) != NULL; levelSigma2 =
+  // pKF2->mvLevelSigma2; F12 row-major; Cw = pKF1 camera centre; R2w/t2w = pKF2
+  // pose.  vMatchedPairs (out) = (i1, i2) in ascending i1.
+  int SearchForTriangulation(const FrameView& KF1, const std::vector<uint8_t>& hasMp1,
+                             const FeatureVector& fv1, const FrameView& KF2,
+                             const std::vector<uint8_t>& hasMp2, const FeatureVector& fv2,
+                             const std::vector<float>& levelSigma2, const float F12[9],
+                             const orb_camera_t& cam, const float Cw[3], const float R2w[9],
+                             const float t2w[3], bool bOnlyStereo,
+                             std::vector<std::pair<size_t, size_t>>& vMatchedPairs) {
+    const orb_frame_t f1 = KF1.c(), f2 = KF2.c();
+    const CsrFeatureVector a = flatten(fv1), b = flatten(fv2);
+    std::vector<int32_t> m12(KF1.N(), -1);
+    int32_t n = 0;
+    check(orb_search_for_triangulation(h_, &f1, hasMp1.data(), &f2, hasMp2.data(),
+                                       levelSigma2.data(), F12, &cam, Cw, R2w, t2w, a.size(),
+                                       a.nodes.data(), a.offs.data(), a.feats.data(), b.size(),
+                                       b.nodes.data(), b.offs.data(), b.feats.data(),
+                                       bOnlyStereo ? 1 : 0, mbCheckOrientation ? 1 : 0,
+                                       m12.data(), &n),
+          "SearchForTriangulation");
+    vMatchedPairs.clear();
+    vMatchedPairs.reserve(n);
+    for (int i = 0; i < KF1.N(); ++i)
+      if (m12[i] >= 0) vMatchedPairs.emplace_back((size_t)i, (size_t)m12[i]);
+    return n;
+  }
+
+  // SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th), src/ORBmatcher.cc:1212-1458.
+  // mpsX / mpDescX = the MapPoint of keypoint i of KF X (validX[i] = non-NULL),
+  // alreadyX = vbAlreadyMatchedX.  vpMatches12 (out) = idx2 per KF1 keypoint, or -1.
+  int SearchBySim3(const FrameView& KF1, const FrameView& KF2, float logScaleFactor,
+                   const orb_camera_t& cam, const float R1w[9], const float t1w[3],
+                   const float R2w[9], const float t2w[3],
+                   const std::vector<orb_map_point_t>& mps1, const std::vector<uint8_t>& valid1,
+                   const std::vector<uint8_t>& already1, const std::vector<uint8_t>& mpDesc1,
+                   const std::vector<orb_map_point_t>& mps2, const std::vector<uint8_t>& valid2,
+                   const std::vector<uint8_t>& already2, const std::vector<uint8_t>& mpDesc2,
+                   float s12, const float R12[9], const float t12[3], float th,
+                   std::vector<int32_t>& vpMatches12) {
+    const orb_frame_t f1 = KF1.c(), f2 = KF2.c();
+    vpMatches12.assign(KF1.N(), -1);
+    int32_t n = 0;
+    check(orb_search_by_sim3(h_, &f1, &f2, logScaleFactor, &cam, R1w, t1w, R2w, t2w, mps1.data(),
+                             valid1.data(), already1.data(), mpDesc1.data(), mps2.data(),
+                             valid2.data(), already2.data(), mpDesc2.data(), s12, R12, t12, th,
+                             vpMatches12.data(), &n),
+          "SearchBySim3");
     return n;
   }
 
