@@ -591,16 +591,18 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
 static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, size_t stride,
                               size_t imgPitch, orb_keypoint_t* d_kps, uint8_t* d_desc,
                               int capacity, int32_t* d_counts, hipStream_t s) {
-  // Stage DAG: pyramid -> { blur || FAST -> octree } -> orient+desc.  The blur
-  // may run on a side stream beside FAST + octree (ORB_EXTRACT_STREAMS=2;
-  // fork/join by events, graph-capturable).  Both are VALU-bound at batch
-  // sizes that fill the GPU, so by default they run in order on one stream
-  // (measured: no gain from the overlap at B = 512).
+  // Stage DAG: pyramid -> { blur || FAST -> octree } -> orient+desc.  With
+  // ORB_EXTRACT_STREAMS=2 the blur is issued on a side stream after FAST and
+  // runs beside the octree (fork/join by events, graph-capturable).  Measured
+  // at B = 512: no gain (the blur's workgroups hold the CUs and the octree's
+  // 52 KiB-LDS workgroups wait, 0.22 -> 0.78 ms), so by default every stage
+  // runs in order on the caller's stream.
   const OrbPlanDesc& P = h->plan;
   const int32_t* rt = h->dRtab.as<int32_t>();
   uint8_t* arena = h->dArena.as<uint8_t>();
   const long long ap = h->arenaBytes;
-  static const bool sideStream = getenv("ORB_EXTRACT_STREAMS") && atoi(getenv("ORB_EXTRACT_STREAMS")) > 1;
+  static const bool sideStream =
+      getenv("ORB_EXTRACT_STREAMS") && atoi(getenv("ORB_EXTRACT_STREAMS")) > 1;
   hipStream_t s2 = sideStream ? h->stream2 : s;
   StageProfiler& pf = h->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
@@ -618,6 +620,11 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                              rt + d.rtabY + d.h, d.xmax, B, s));
   }
   PROF_REC(ev, pf.e(ev, 0), s);
+  PROF_REC(ev, pf.b(ev, 2), s);
+  HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                          h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
+                          h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
+  PROF_REC(ev, pf.e(ev, 2), s);
   if (s2 != s) {
     HIP_TRY(hipEventRecord(h->evFork, s));
     HIP_TRY(hipStreamWaitEvent(s2, h->evFork, 0));
@@ -628,11 +635,6 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                             s2));
   PROF_REC(ev, pf.e(ev, 1), s2);
   if (s2 != s) HIP_TRY(hipEventRecord(h->evJoin, s2));
-  PROF_REC(ev, pf.b(ev, 2), s);
-  HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                          h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
-                          h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
-  PROF_REC(ev, pf.e(ev, 2), s);
   PROF_REC(ev, pf.b(ev, 3), s);
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
