@@ -1,0 +1,95 @@
+"""Thread-safety of the drop-in boundary (include/orb_abi.h: handles are
+independent; a handle serialises its own calls).  The reference runs two
+ORBextractor instances concurrently for every stereo frame (src/Frame.cc:81-84)
+and builds ORBmatcher objects on the Tracking, LocalMapping and LoopClosing
+threads at once.  ctypes releases the GIL inside every call, so these threads
+really do overlap on the device."""
+import threading
+
+import numpy as np
+import pytest
+
+import scenarios
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_threads(fns):
+    errors = []
+
+    def wrap(fn):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+
+    ts = [threading.Thread(target=wrap, args=(f,)) for f in fns]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+
+
+def test_two_extractors_in_parallel_threads(gpu):
+    # Frame's stereo constructor: left and right extractors on two threads
+    left = [gpu.synth_image(30, f, 1241, 376) for f in range(6)]
+    right = [gpu.synth_image(30, f, 1241, 376, view=1) for f in range(6)]
+    ref_ext = gpu.ORBextractor(2000, 1.2, 8, 20, 7)
+    ref = {("L", i): ref_ext(im) for i, im in enumerate(left)}
+    ref.update({("R", i): ref_ext(im) for i, im in enumerate(right)})
+    got = {}
+    exL, exR = gpu.ORBextractor(2000, 1.2, 8, 20, 7), gpu.ORBextractor(2000, 1.2, 8, 20, 7)
+
+    def run(ext, side, imgs):
+        def f():
+            for i, im in enumerate(imgs):
+                got[(side, i)] = ext(im)
+        return f
+
+    _run_threads([run(exL, "L", left), run(exR, "R", right)])
+    for key, (k, d) in ref.items():
+        assert got[key][0].tobytes() == k.tobytes() and got[key][1].tobytes() == d.tobytes(), key
+
+
+def test_shared_matcher_handle_from_many_threads(gpu):
+    # one handle, four threads (its mutex serialises the calls)
+    w, h = 1241, 376
+    img = gpu.synth_image(5, 0, w, h)
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    k, d = ext(img)
+    scale = np.float32(ext.GetScaleFactors())
+    mps, mpd, locked = gpu.synth_local_map(5, k, d, 3000, w, h)
+    m = gpu.ORBmatcher(0.8)
+    F = gpu.Frame(k, d, scale, w, h)
+    ref = m.SearchByProjection(F, mps, mpd, 1.0, locked)
+    out = [None] * 4
+
+    def job(i):
+        def f():
+            for _ in range(5):
+                out[i] = m.SearchByProjection(F, mps, mpd, 1.0, locked)
+        return f
+
+    _run_threads([job(i) for i in range(4)])
+    for o in out:
+        assert o[0] == ref[0] and np.array_equal(o[1], ref[1])
+
+
+def test_vocabulary_handle_from_many_threads(gpu, oracle):
+    v = scenarios.vocabulary(rng_seed=3, k=10, L=4)
+    voc = gpu.ORBVocabulary(v["k"], v["L"], v["parent"], v["leaf"], v["desc"], v["weight"])
+    feats = [scenarios.vocab_features(v, 1000, rng_seed=i) for i in range(4)]
+    refs = [oracle.vocab_transform(v, f, 4) for f in feats]
+    got = [None] * 4
+
+    def job(i):
+        def f():
+            for _ in range(5):
+                got[i] = voc.transform(feats[i], 4)
+        return f
+
+    _run_threads([job(i) for i in range(4)])
+    for g, r in zip(got, refs):
+        assert np.array_equal(g[0], r[0]) and np.array_equal(g[1].view(np.uint64), r[1].view(np.uint64))
+        assert all(np.array_equal(a, b) for a, b in zip(g[2], r[2:5]))
