@@ -104,12 +104,46 @@ OP3(mad_u16, "v_mad_u16")
 OP3(med3_f16, "v_med3_f16")
 OP3(min3_i32, "v_min3_i32")
 
+#define OP2D(NAME, ASM)                                                                  \
+  __global__ __launch_bounds__(256) void k_##NAME(uint32_t* out, uint32_t seed) {        \
+    double a0 = seed ^ threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, b = seed + 17; \
+    for (int i = 0; i < ITERS; ++i) {                                                    \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a0) : "v"(b));                               \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a1) : "v"(b));                               \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a2) : "v"(b));                               \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a3) : "v"(b));                               \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a0) : "v"(b));                               \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a1) : "v"(b));                               \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a2) : "v"(b));                               \
+      asm volatile(ASM " %0, %0, %1" : "+v"(a3) : "v"(b));                               \
+    }                                                                                    \
+    out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)(a0 + a1 + a2 + a3);                 \
+  }
+OP2D(add_f64, "v_add_f64")
+OP2D(mul_f64, "v_mul_f64")
+#define OP3D(NAME, ASM)                                                                  \
+  __global__ __launch_bounds__(256) void k_##NAME(uint32_t* out, uint32_t seed) {        \
+    double a0 = seed ^ threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, b = seed + 17, c = 3; \
+    for (int i = 0; i < ITERS; ++i) {                                                    \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a0) : "v"(b), "v"(c));                   \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a1) : "v"(b), "v"(c));                   \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a2) : "v"(b), "v"(c));                   \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a3) : "v"(b), "v"(c));                   \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a0) : "v"(b), "v"(c));                   \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a1) : "v"(b), "v"(c));                   \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a2) : "v"(b), "v"(c));                   \
+      asm volatile(ASM " %0, %0, %1, %2" : "+v"(a3) : "v"(b), "v"(c));                   \
+    }                                                                                    \
+    out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)(a0 + a1 + a2 + a3);                 \
+  }
+OP3D(fma_f64, "v_fma_f64")
+
 typedef void (*KFn)(uint32_t*, uint32_t);
 struct Entry { const char* name; KFn fn; };
 
 int main() {
   Entry es[] = {
-      {"v_add_u32", k_add_u32}, {"v_and_b32", k_and_b32}, {"v_lshlrev_b32", k_lshlrev_b32},
+      {"v_add_u32", k_add_u32}, {"v_add_f64", k_add_f64}, {"v_mul_f64", k_mul_f64}, {"v_fma_f64", k_fma_f64}, {"v_and_b32", k_and_b32}, {"v_lshlrev_b32", k_lshlrev_b32},
       {"v_pk_add_f16", k_pk_add_f16}, {"v_pk_min_f16", k_pk_min_f16},
       {"v_pk_max_f16", k_pk_max_f16}, {"v_pk_sub_i16", k_pk_sub_i16},
       {"v_pk_add_u16", k_pk_add_u16}, {"v_pk_min_u16", k_pk_min_u16}, {"v_add_f32", k_add_f32},
