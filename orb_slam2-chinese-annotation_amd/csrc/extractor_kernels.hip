@@ -1129,37 +1129,55 @@ __global__ __launch_bounds__(256) void k_blur_levels(
 }
 
 // =========================================================== k_orient_desc
-// One wave per keypoint.  slot -> (level, index) through plan.lv[].outOff.
-//   IC_Angle (src/ORBextractor.cc:77-113) on the un-blurred level: lanes 0-30
-//   take column u = lane-15 of the centre row and the rows below (+v), lanes
-//   32-62 the rows above (-v); integer moments reduced across the wave.
-//   rBRIEF (:119-164) on the blurred level: lane L evaluates tests L, L+64,
-//   L+128, L+192; one ballot per group of 64 tests is 8 descriptor bytes.
+// Two keypoints per wave: half-wave h (lanes 32h .. 32h+31) takes slot 2p+h
+// of the wave's slot pair p.  Levels own even-sized slot ranges (the planner
+// rounds nodeCap up to even), so both keypoints of a wave are on one level and
+// the level's buffer resources stay wave-uniform; everything per keypoint
+// (IC moments, angle, sincos, 256 tests) runs once per half-wave, so the
+// per-keypoint scalar chain (fastAtan2, the pinned double sincos, address
+// setup, epilogue) is issued once for two keypoints.
+//   IC_Angle (src/ORBextractor.cc:77-113) on the un-blurred level: lane hl
+//   takes row v = hl - 15 (hl < 31) and both 16-byte halves of its 32 columns
+//   at -16..15; integer moments reduced across the half-wave.
+//   rBRIEF (:119-164) on the blurred level: lane hl evaluates tests
+//   hl + 32k (k < 8); ballot k holds tests 32k .. 32k+31 of both keypoints.
+__device__ __forceinline__ int half_sum(int v) {  // sum over the 32 lanes of each half-wave
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_orient_desc(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, const uint8_t* __restrict__ blur,
     long long blurPitch, OrbPlanDesc plan, const uint32_t* __restrict__ outKeys,
     const int32_t* __restrict__ outCount, orb_keypoint_t* __restrict__ kps,
     uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts) {
-  // wave id through readfirstlane: everything derived from it (level, key,
-  // buffer descriptors) is then provably wave-uniform -> SGPRs, no waterfall
+  // wave id through readfirstlane: the level and buffer descriptors derived
+  // from it are provably wave-uniform -> SGPRs, no waterfall
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int half = lane >> 5, hl = lane & 31;
   const int img = blockIdx.y;
-  const int slot = blockIdx.x * 4 + w;
+  const int slot0 = (blockIdx.x * 4 + w) * 2;  // even: first slot of the wave's pair
   const int32_t* cnts = outCount + img * plan.nlevels;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
     counts[img] = tot;
   }
-  if (slot >= plan.slotsPerImage) return;
+  if (slot0 >= plan.slotsPerImage) return;
   int l = 0;
-  while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot) ++l;
-  const int i = slot - plan.lv[l].outOff;
-  if (i >= cnts[l]) return;
+  while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot0) ++l;
+  const int i0 = slot0 - plan.lv[l].outOff, nl = cnts[l];
+  if (i0 >= nl) return;
+  const bool active = i0 + half < nl;  // the pair's second slot may be past the level's count
+  const int i = i0 + (active ? half : 0);
   int base = 0;
   for (int j = 0; j < l; ++j) base += cnts[j];
-  const uint32_t key = outKeys[(long long)img * plan.slotsPerImage + slot];
+  const uint32_t key = outKeys[(long long)img * plan.slotsPerImage + plan.lv[l].outOff + i];
   const int cx = key_x(key), cy = key_y(key);
   const OrbLevelDesc& L = plan.lv[l];
   const uint8_t* lvl;
@@ -1173,43 +1191,41 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   }
   // The blurred 37 x 37 patch the descriptor samples (rotated pattern within
   // +-18 px, max radius 18.38) does not depend on the angle: its loads are
-  // issued first, so they are in flight together with the IC_Angle loads
-  // (one memory round trip per keypoint).
-  __shared__ __attribute__((aligned(16))) uint32_t patch[4][37][ORB_PATCH_DW];
+  // issued first, in flight together with the IC_Angle loads (one memory
+  // round trip per wave).  37 rows x 11 dwords per keypoint, 13 per lane.
+  __shared__ __attribute__((aligned(16))) uint32_t patch[4][2][37][ORB_PATCH_DW];
   const int bp = L.blurPitch;
   const __amdgpu_buffer_rsrc_t rb =
       make_rsrc(blur + (long long)img * blurPitch + L.blurOff, (uint32_t)(L.h * bp));
-  const int colA = cx - 18, psh = colA & 3;  // wave-uniform alignment of the patch
-  uint32_t pv[7];
+  const int colA = cx - 18, psh = colA & 3;  // per-keypoint (half-wave) alignment
+  uint32_t pv[13];
   {
     const uint32_t pbase = (uint32_t)((cy - 18) * bp + (colA & ~3));
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int i = min(lane + 64 * q, 37 * 11 - 1);
-      const int r = i / 11, k = i - r * 11;
+    for (int q = 0; q < 13; ++q) {
+      const int ii = min(hl + 32 * q, 37 * 11 - 1);
+      const int r = ii / 11, k = ii - r * 11;
       pv[q] = buf_ld32(rb, pbase + (uint32_t)(r * bp + 4 * k));
     }
   }
-  // ---- IC_Angle (src/ORBextractor.cc:77-113), exact integer moments.
-  // Lane = (row v = (lane & 31) - 15, half = lane >> 5): 16 bytes at columns
-  // 16*half-16 .. 16*half-1 of row cy+v, masked to |u| <= umax[|v|].  Row sum
-  // and u-moment are v_dot4 products: m10 = sum (u+16)*I - 16*sum I,
-  // m01 = sum v * rowsum.
+  // ---- IC_Angle, exact integer moments.  Row sum and u-moment are v_dot4
+  // products over 16-byte halves masked to |u| <= umax[|v|]:
+  // m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
   int m01 = 0, m10 = 0;
   {
-    const int ri = lane & 31, half = lane >> 5;
+    const int ri = hl;
     if (ri < 31) {
       const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
-      const uint32_t o0 = (uint32_t)((cy + ri - 15) * pitch + cx - 16 + 16 * half) + im.sh;
+      const uint32_t o0 = (uint32_t)((cy + ri - 15) * pitch + cx - 16) + im.sh;
       const uint32_t sh = o0 & 3u, a0 = o0 & ~3u;
-      uint32_t w[5];
+      uint32_t wv[9];
 #pragma unroll
-      for (int k = 0; k < 5; ++k) w[k] = buf_ld32(im.r, a0 + 4 * k);
+      for (int k = 0; k < 9; ++k) wv[k] = buf_ld32(im.r, a0 + 4 * k);
       uint32_t rs = 0, rm = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t d = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh) & c_icmask[ri][4 * half + k];
-        const uint32_t wt = (uint32_t)(16 * half + 4 * k) * 0x01010101u + 0x03020100u;  // u + 16
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t d = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh) & c_icmask[ri][k];
+        const uint32_t wt = (uint32_t)(4 * k) * 0x01010101u + 0x03020100u;  // u + 16
         rs = __builtin_amdgcn_udot4(d, 0x01010101u, rs, false);
         rm = __builtin_amdgcn_udot4(d, wt, rm, false);
       }
@@ -1217,57 +1233,51 @@ __global__ __launch_bounds__(256) void k_orient_desc(
       m01 = (ri - 15) * (int)rs;
     }
   }
-  m01 = wave_sum(m01);
-  m10 = wave_sum(m10);
+  m01 = half_sum(m01);
+  m10 = half_sum(m10);
   const float angle = fast_atan2_deg((float)m01, (float)m10);
   // ---- rBRIEF on the blurred level
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float a, b;
   {
-    float s, c;
-    pinned_sincos(angle * factorPI, &s, &c);
-    a = c;
-    b = s;
+    float sn, cs;
+    pinned_sincos(angle * factorPI, &sn, &cs);
+    a = cs;
+    b = sn;
   }
-  // 512 samples of the blurred level around (cx, cy): the patch (loaded
-  // above, 11 aligned dwords per row, row-contiguous) goes to LDS and the
-  // samples are byte gathers from LDS: scattered byte loads from global memory
-  // cost one L1 tag lookup per distinct line.
 #pragma unroll
-  for (int q = 0; q < 7; ++q) {
-    const int i = lane + 64 * q;
-    if (i < 37 * 11) {
-      const int r = i / 11, k = i - r * 11;
-      patch[w][r][k] = pv[q];
+  for (int q = 0; q < 13; ++q) {
+    const int ii = hl + 32 * q;
+    if (ii < 37 * 11) {
+      const int r = ii / 11, k = ii - r * 11;
+      patch[w][half][r][k] = pv[q];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint8_t* pb = reinterpret_cast<const uint8_t*>(&patch[w][0][0]) + 18 * (ORB_PATCH_DW * 4) + 18 + psh;
-  int v0[4], v1[4];
+  const uint8_t* pb = reinterpret_cast<const uint8_t*>(&patch[w][half][0][0]) +
+                      18 * (ORB_PATCH_DW * 4) + 18 + psh;
+  unsigned long long words[8];
 #pragma unroll
-  for (int kq = 0; kq < 4; ++kq) {
-    const int test = lane + 64 * kq;
-    // one 4-byte load per test (x0, y0, x1, y1 as int8): the whole table is
-    // 1 KB per wave through L1 (a float4 table would be 4 KB)
+  for (int kq = 0; kq < 8; ++kq) {
+    const int test = hl + 32 * kq;
+    // one 4-byte load per test (x0, y0, x1, y1 as int8)
     const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
     const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
-    // |rounded offsets| <= 19: 24-bit multiplies (full rate)
-    v0[kq] = pb[__mul24(cv_round(px0 * b + py0 * a), ORB_PATCH_DW * 4) + cv_round(px0 * a - py0 * b)];
-    v1[kq] = pb[__mul24(cv_round(px1 * b + py1 * a), ORB_PATCH_DW * 4) + cv_round(px1 * a - py1 * b)];
+    // |rounded offsets| <= 19: 24-bit multiplies
+    const int v0 = pb[__mul24(cv_round(px0 * b + py0 * a), ORB_PATCH_DW * 4) + cv_round(px0 * a - py0 * b)];
+    const int v1 = pb[__mul24(cv_round(px1 * b + py1 * a), ORB_PATCH_DW * 4) + cv_round(px1 * a - py1 * b)];
+    words[kq] = __ballot(v0 < v1);
   }
-  unsigned long long words[4];
+  if (active && hl == 0) {
+    const long long o = (long long)img * capacity + base + i;
+    uint32_t d[8];
 #pragma unroll
-  for (int kq = 0; kq < 4; ++kq) words[kq] = __ballot(v0[kq] < v1[kq]);
-  const long long o = (long long)img * capacity + base + i;
-  if (lane == 0) {
-    ulonglong4 d;
-    d.x = words[0];
-    d.y = words[1];
-    d.z = words[2];
-    d.w = words[3];
-    *reinterpret_cast<ulonglong4*>(desc + o * 32) = d;
+    for (int kq = 0; kq < 8; ++kq) d[kq] = (uint32_t)(words[kq] >> (32 * half));
+    uint4* dst = reinterpret_cast<uint4*>(desc + o * 32);
+    dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
     orb_keypoint_t kp;
     kp.x = l ? (float)cx * L.scale : (float)cx;  // pt *= mvScaleFactor[level] (:1157-1165)
     kp.y = l ? (float)cy * L.scale : (float)cy;
@@ -1403,7 +1413,9 @@ hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint32_t* outKeys, const int32_t* outCount,
                              orb_keypoint_t* kps, uint8_t* desc, int capacity, int32_t* counts,
                              int nimg, hipStream_t s) {
-  dim3 grid((plan->slotsPerImage + 3) / 4, nimg), block(256);
+  // 4 waves x 2 slots per workgroup; slotsPerImage and every level's outOff are even
+  if (plan->slotsPerImage & 1) return hipErrorInvalidValue;
+  dim3 grid((plan->slotsPerImage + 7) / 8, nimg), block(256);
   hipLaunchKernelGGL(k_orient_desc, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, blur, blurPitch, *plan, outKeys, outCount, kps, desc, capacity,
                      counts);

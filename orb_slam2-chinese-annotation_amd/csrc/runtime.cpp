@@ -461,7 +461,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     d.nIni = (int)roundf((float)d.Wr / d.Hr);
     if (d.nIni <= 0) return ORB_EINVAL;
     d.hX = (float)d.Wr / d.nIni;
-    d.nodeCap = std::max(d.quota + 4, 4 * d.nIni + 4);
+    d.nodeCap = (std::max(d.quota + 4, 4 * d.nIni + 4) + 1) & ~1;  // even: k_orient_desc slot pairs
     nodeCapMax = std::max(nodeCapMax, d.nodeCap);
     d.outOff = slots;
     slots += d.nodeCap;
