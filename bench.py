@@ -105,6 +105,32 @@ def measured_traffic(kernel, batch):
     return k["traffic_bytes"] * batch / t["batch"], files[-1].name
 
 
+# VALU issue time per wave-instruction per SIMD on gfx950, measured by
+# tools/probe/valu_rates.hip (profiles/r01_valu_rates.txt): plain 32-bit
+# integer / f32 ops ~1.0 ns, packed, 3-input and 24/32-bit multiply ops ~1.8 ns.
+VALU_NS_FAST, VALU_NS_SLOW, N_SIMD = 1.0, 1.8, 1024
+
+
+def valu_issue(kernel, batch, ms_per_launch):
+    """Lower/upper bound on the time the SIMDs need just to issue `kernel`'s
+    VALU instructions (SQ_INSTS_VALU from the newest profiles/rNN_pmc.json,
+    scaled to this batch), as a fraction of its measured launch time."""
+    files = sorted((ROOT / "profiles").glob("r*_pmc.json"))
+    if not files:
+        return None
+    t = json.loads(files[-1].read_text())
+    k = t["kernels"].get(kernel)
+    if k is None or "SQ_INSTS_VALU" not in k:
+        return None
+    n = k["SQ_INSTS_VALU"] * batch / t["batch"]
+    lo, hi = (n / N_SIMD * ns * 1e-6 for ns in (VALU_NS_FAST, VALU_NS_SLOW))
+    return {"valu_instr_per_launch": n, "issue_ms_range": [lo, hi],
+            "frac_range": [lo / ms_per_launch, hi / ms_per_launch],
+            "source": f"profiles/{files[-1].name} SQ_INSTS_VALU x "
+                      f"{VALU_NS_FAST}-{VALU_NS_SLOW} ns per wave-instruction per SIMD "
+                      "(profiles/r01_valu_rates.txt)"}
+
+
 def cpu_baseline(imgs_host, maps, args, scale):
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # CPU oracle: checker / baseline only
@@ -301,6 +327,7 @@ def main():
                               "separate passes, raw KiB x 1024)" if traffic_src else None,
             "bytes_per_launch": dom_bytes,
             "ms_per_launch": dom_ms_per_launch,
+            "valu_issue": valu_issue(dom, B, dom_ms_per_launch),
         },
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
     }

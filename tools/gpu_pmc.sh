@@ -12,4 +12,4 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_S
   -d "$O/pmcA_$TAG" -o run --output-format csv -- python3 "$R/bench.py" $ARGS > "$O/pmcA_$TAG.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU \
   -d "$O/pmcB_$TAG" -o run --output-format csv -- python3 "$R/bench.py" $ARGS > "$O/pmcB_$TAG.log" 2>&1
-echo done
+echo done  # then: tools/pmc_table.py --json profiles/rNN_pmc.json gpurun_out/pmcA_<tag> gpurun_out/pmcB_<tag>
