@@ -43,8 +43,11 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
     const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sw, int sh,
     uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
     const int* __restrict__ xofs, const int* __restrict__ alpha,
-    const int* __restrict__ yofs, const int* __restrict__ beta) {
+    const int* __restrict__ yofs, const int* __restrict__ beta, int nImg) {
   // alpha/beta pack the two 11-bit weights as (w1 << 16) | (w0 & 0xFFFF).
+  // A workgroup takes one output tile of images blockIdx.z, + gridDim.z, ...:
+  // weight tables and the source window are loaded once, and the next image's
+  // window is loaded into registers while the current one is computed.
   __shared__ __attribute__((aligned(16))) uint32_t tile[SROWS][SW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int tx = tid & 31, ty = tid >> 5;
@@ -70,16 +73,18 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   const int syA = min(max(yofs[y0], 0), sh - 1), syB = min(max(yofs[yl] + 1, 0), sh - 1);
   const int colBase = sxA & ~3;
   const int nW = ((sxB - colBase) >> 2) + 1, nR = syB - syA + 1;
-  // staging: lane = dword column, wave = row; ALIGNED sources need one dword
-  // load per LDS dword, others two (realigned with v_alignbyte)
-  {
-    const ImgRsrc im = img_rsrc(src + (long long)blockIdx.z * srcImgPitch,
-                                (uint32_t)((sh - 1) * srcStride + sw));
-    stage_rows<ALIGNED, SROWS / 4>(im, nR, nW, (uint32_t)(colBase + 4 * lane), &tile[0][0], SW,
-                        [&](int r) { return (uint32_t)((syA + r) * srcStride); });
-  }
-  __syncthreads();
-  if (xs >= dw) return;
+  // staging: ALIGNED sources need one dword load per LDS dword, others two
+  // (realigned with v_alignbyte)
+  const uint32_t magic = div_magic(nW);
+  TilePrefetch<(SROWS * SW + 255) / 256> pf;
+  auto issue = [&](int z) {
+    const ImgRsrc im = img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((sh - 1) * srcStride + sw));
+    pf.issue(im, ALIGNED, nR, nW, magic, [&](int r) { return (uint32_t)((syA + r) * srcStride); },
+             [&](int c) { return (uint32_t)(colBase + 4 * c); });
+  };
+  int z = blockIdx.z;
+  if (z >= nImg) return;
+  issue(z);
   // Horizontal taps with v_perm + v_dot2: the thread's 4 columns read source
   // bytes sx0 .. sx0+6 (scale <= 1.25), realigned once per source row into
   // (W0, W1); column j's pair (S[sx], S[sx+1]) is one v_perm into u16 lanes
@@ -107,30 +112,37 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
       h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(W1, W0, sel[j])),
                                     wts[j], 0u, false);
   };
-  // destination: arena level, pitch a multiple of 128 >= dw rounded to 4, so a
-  // whole dword store at xs < dw stays inside the row (padding bytes unused)
-  const __amdgpu_buffer_rsrc_t rd =
-      make_rsrc(dst + (long long)blockIdx.z * dstImgPitch, (uint32_t)(dh * dstStride));
+  for (; z < nImg; z += gridDim.z) {
+    __syncthreads();  // the previous image's taps have read the window
+    pf.commit(&tile[0][0], SW, nR, nW, magic);
+    if (z + (int)gridDim.z < nImg) issue(z + gridDim.z);
+    __syncthreads();
+    if (xs >= dw) continue;
+    // destination: arena level, pitch a multiple of 128 >= dw rounded to 4, so a
+    // whole dword store at xs < dw stays inside the row (padding bytes unused)
+    const __amdgpu_buffer_rsrc_t rd =
+        make_rsrc(dst + (long long)z * dstImgPitch, (uint32_t)(dh * dstStride));
 #pragma unroll
-  for (int rr = 0; rr < PYR_TH / 8; ++rr) {
-    const int y = y0 + (PYR_TH / 8) * ty + rr;
-    if (y >= dh) break;
-    const uint32_t b0 = (uint32_t)be[rr] & 0xFFFFu, b1 = (uint32_t)be[rr] >> 16;
-    uint32_t h0[4], h1[4];
-    hrow(min(max(yo[rr], 0), sh - 1) - syA, h0);
-    hrow(min(max(yo[rr] + 1, 0), sh - 1) - syA, h1);
-    uint32_t packed = 0;
+    for (int rr = 0; rr < PYR_TH / 8; ++rr) {
+      const int y = y0 + (PYR_TH / 8) * ty + rr;
+      if (y >= dh) break;
+      const uint32_t b0 = (uint32_t)be[rr] & 0xFFFFu, b1 = (uint32_t)be[rr] >> 16;
+      uint32_t h0[4], h1[4];
+      hrow(min(max(yo[rr], 0), sh - 1) - syA, h0);
+      hrow(min(max(yo[rr] + 1, 0), sh - 1) - syA, h1);
+      uint32_t packed = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      // h <= 255*2048 and b <= 2048: 24-bit multiplies, sum < 2^31
-      int v = min((int)((__umul24(h0[j], b0) + __umul24(h1[j], b1) + (1u << 21)) >> 22), 255);
-      // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
-      // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
-      // undefined upper half (observed miscompile on gfx950)
-      __asm__ volatile("" : "+v"(v));
-      packed |= (uint32_t)v << (8 * j);
+      for (int j = 0; j < 4; ++j) {
+        // h <= 255*2048 and b <= 2048: 24-bit multiplies, sum < 2^31
+        int v = min((int)((__umul24(h0[j], b0) + __umul24(h1[j], b1) + (1u << 21)) >> 22), 255);
+        // opaque to instruction selection: ROCm 7.2 hipcc fuses shift+clamp+pack of
+        // byte pairs into v_ashr_pk_u8_i32 and then ORs the next bytes into its
+        // undefined upper half (observed miscompile on gfx950)
+        __asm__ volatile("" : "+v"(v));
+        packed |= (uint32_t)v << (8 * j);
+      }
+      buf_st32(rd, (uint32_t)(y * dstStride + xs), packed);
     }
-    buf_st32(rd, (uint32_t)(y * dstStride + xs), packed);
   }
 }
 
@@ -989,48 +1001,59 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 __global__ __launch_bounds__(256) void k_blur_levels(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
-    const OrbTileDesc* __restrict__ tiles, uint8_t* __restrict__ blur, long long blurPitch) {
+    const OrbTileDesc* __restrict__ tiles, uint8_t* __restrict__ blur, long long blurPitch,
+    int nImg) {
   // Source tile staged as aligned dwords, byte b of a row = level column
   // x0-4+b (realigned from any stride); every LDS access is an aligned dword
   // or 8 bytes (unaligned sub-dword LDS reads are replayed by the hardware).
   __shared__ __attribute__((aligned(16))) uint32_t raw[BLUR_SH][BLUR_WROW + 1];
   // row-pass sums, two staged rows per dword: rowp2[p][c] = sum(2p, c) | sum(2p+1, c) << 16
   __shared__ __attribute__((aligned(16))) uint32_t rowp2[BLUR_SH / 2][BLUR_RP2];
-  const int tid = threadIdx.x, img = blockIdx.y;
+  const int tid = threadIdx.x;
   const OrbTileDesc td = tiles[blockIdx.x];
   const int l = td.level;
   const OrbLevelDesc& L = plan.lv[l];
-  const uint8_t* lvl;
-  int pitch;
-  if (l == 0) {
-    lvl = img0 + (long long)img * img0Pitch;
-    pitch = img0Stride;
-  } else {
-    lvl = arena + (long long)img * arenaPitch + L.arenaOff;
-    pitch = L.pitch;
-  }
-  // Staging (all loads in flight at once).  Rows outside the level are
-  // reflected (REFLECT_101) when addressed; columns are loaded with the dword
-  // start clamped into the row, and the few bytes a border tile needs outside
-  // [0, w) are patched from their reflected columns afterwards.
+  // A workgroup blurs one tile of images blockIdx.y, + gridDim.y, ...; the
+  // next image's source rows are loaded into registers while the current one
+  // is computed (RowPrefetch), so its HBM round trip overlaps this image's work.
+  // Staging: rows outside the level are reflected (REFLECT_101) when
+  // addressed; columns are loaded with the dword start clamped into the row,
+  // and the few bytes a border tile needs outside [0, w) are patched from
+  // their reflected columns afterwards.
   const int colA = td.x0 - 4;  // level column of staged byte 0
-  {
+  // rows outside the level only for the first / last tile row (uniform test)
+  const bool rowsInside = td.y0 >= 3 && td.y0 + BLUR_SH - 3 <= L.h;
+  auto level_of = [&](int im, int* pitch) -> const uint8_t* {
+    if (l == 0) {
+      *pitch = img0Stride;
+      return img0 + (long long)im * img0Pitch;
+    }
+    *pitch = L.pitch;
+    return arena + (long long)im * arenaPitch + L.arenaOff;
+  };
+  TilePrefetch<(BLUR_SH * BLUR_WROW + 255) / 256> pf;
+  const uint32_t magic = div_magic(BLUR_WROW);
+  auto issue = [&](int im) {
+    int pitch;
+    const uint8_t* lvl = level_of(im, &pitch);
     const bool aligned = l > 0 || ((pitch & 3) == 0 && (((uintptr_t)lvl) & 3) == 0);
-    const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
-    const int lane = tid & 63;
-    // dword start clamped into the row (keeping 4-alignment on aligned levels)
-    const int c = min(max(colA + 4 * lane, 0), aligned ? ((L.w - 1) & ~3) : L.w - 1);
-    // rows outside the level only for the first / last tile row (uniform test)
-    const bool rowsInside = td.y0 >= 3 && td.y0 + BLUR_SH - 3 <= L.h;
-    auto rowOff = [&](int r) {
-      const int y = td.y0 - 3 + r;
-      return (uint32_t)((rowsInside ? y : reflect101(y, L.h)) * pitch);
-    };
-    if (aligned)
-      stage_rows<true, (BLUR_SH + 3) / 4>(im, BLUR_SH, BLUR_WROW, (uint32_t)c, &raw[0][0], BLUR_WROW + 1, rowOff);
-    else
-      stage_rows<false, (BLUR_SH + 3) / 4>(im, BLUR_SH, BLUR_WROW, (uint32_t)c, &raw[0][0], BLUR_WROW + 1, rowOff);
-  }
+    const ImgRsrc ir = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
+    const int cmax = aligned ? ((L.w - 1) & ~3) : L.w - 1;
+    pf.issue(ir, aligned, BLUR_SH, BLUR_WROW, magic,
+             [&](int r) {
+               const int y = td.y0 - 3 + r;
+               return (uint32_t)((rowsInside ? y : reflect101(y, L.h)) * pitch);
+             },
+             // dword start clamped into the row (keeping 4-alignment on aligned levels)
+             [&](int c) { return (uint32_t)min(max(colA + 4 * c, 0), cmax); });
+  };
+  int img = blockIdx.y;
+  if (img >= nImg) return;
+  issue(img);
+  for (; img < nImg; img += gridDim.y) {
+  // raw is free: the previous image's row pass ended before its second barrier
+  pf.commit(&raw[0][0], BLUR_WROW + 1, BLUR_SH, BLUR_WROW, magic);
+  if (img + (int)gridDim.y < nImg) issue(img + gridDim.y);
   const bool leftB = colA < 0, rightB = td.x0 + ORB_BLUR_TW + 3 > L.w;
   if (leftB || rightB) {  // uniform per workgroup
     __syncthreads();
@@ -1126,6 +1149,7 @@ __global__ __launch_bounds__(256) void k_blur_levels(
       }
     }
   }
+  }  // image loop
 }
 
 // =========================================================== k_orient_desc
@@ -1329,13 +1353,17 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   (void)xmax;  // folded into the alpha table: (2048, 0) past xmax
   // tile bounds: narrow variant for a per-level downscale <= 1.25, wide <= 1.9
   const bool wide = (double)sw / dw > 1.25 || (double)sh / dh > 1.25;
-  dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, nimg), block(256);
+  // each workgroup resizes one tile of ORB_RESIZE_IMAGES_PER_WG images (default 4)
+  static const int perWg =
+      getenv("ORB_RESIZE_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_RESIZE_IMAGES_PER_WG"))) : 4;
+  dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, (nimg + perWg - 1) / perWg),
+      block(256);
   // every image base and row start 4-aligned: one load per staged dword
   const bool aligned = (srcStride & 3) == 0 && (((uintptr_t)src) & 3) == 0 && (srcImgPitch & 3) == 0;
 #define ORB_RESIZE_LAUNCH(AL, R, W)                                                              \
   hipLaunchKernelGGL((k_pyr_resize<AL, R, W>), grid, block, 0, s, src, srcImgPitch, srcStride, sw, \
                      sh, dst, dstImgPitch, dstStride, dw, dh, xofs, (const int*)alpha, yofs,      \
-                     (const int*)beta)
+                     (const int*)beta, nimg)
   if (!wide && aligned) ORB_RESIZE_LAUNCH(true, PYR_SROWS, PYR_SW);
   else if (!wide) ORB_RESIZE_LAUNCH(false, PYR_SROWS, PYR_SW);
   else if (aligned) ORB_RESIZE_LAUNCH(true, PYR_SROWS_WIDE, PYR_SW_WIDE);
@@ -1401,9 +1429,12 @@ hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
                              int nimg, hipStream_t s) {
-  dim3 grid(plan->nBlurTiles, nimg), block(256);
+  // each workgroup blurs one tile of ORB_BLUR_IMAGES_PER_WG images (default 4)
+  static const int perWg =
+      getenv("ORB_BLUR_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_BLUR_IMAGES_PER_WG"))) : 4;
+  dim3 grid(plan->nBlurTiles, (nimg + perWg - 1) / perWg), block(256);
   hipLaunchKernelGGL(k_blur_levels, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, tiles, blur, blurPitch);
+                     arenaPitch, *plan, tiles, blur, blurPitch, nimg);
   return hipGetLastError();
 }
 

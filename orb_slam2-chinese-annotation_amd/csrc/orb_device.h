@@ -197,6 +197,57 @@ __device__ __forceinline__ void stage_rows(const ImgRsrc& im, int nR, int nW, ui
   }
 }
 
+// Staging split in two for software pipelining: issue() puts the loads of a
+// tile of nR rows x rowW dwords (nR * rowW <= NQ * 256) in flight into
+// registers, NQ dwords per thread of a 256-thread workgroup (element
+// i = q*256 + tid -> row i / rowW, dword i % rowW, the division by a
+// multiply-high: i / d = umulhi(2i, ceil(2^31 / d)) for i < 2^20, d >= 1 --
+// 2^31 rather than 2^32 so that d = 1 has a 32-bit magic); commit() realigns them into
+// LDS.  A workgroup walking several images issues the next image's tile before
+// it computes the current one, so the HBM round trip overlaps that work.
+// rowOff(r) / colOff(c) give byte offsets (per lane); aligned (wave-uniform)
+// tiles skip the second load and realign by 0.  Elements past the tile repeat
+// its last one (branch-free loads) and are not committed.
+__device__ __forceinline__ uint32_t div_magic(int d) {
+  return (uint32_t)((0x7FFFFFFFull + (uint64_t)d) / (uint64_t)d);
+}
+template <int NQ>
+struct TilePrefetch {
+  uint32_t lo[NQ], hi[NQ], sh[NQ];
+  // the thread index is laundered through an empty asm so that the per-element
+  // offsets are recomputed per image instead of being hoisted out of the image
+  // loop (which would hold 2 x NQ more registers across it)
+  __device__ __forceinline__ static int opaque_tid() {
+    int t = (int)threadIdx.x;
+    __asm__ volatile("" : "+v"(t));
+    return t;
+  }
+  template <class RowOff, class ColOff>
+  __device__ __forceinline__ void issue(const ImgRsrc& im, bool aligned, int nR, int rowW,
+                                        uint32_t magic, RowOff rowOff, ColOff colOff) {
+    const int tid = opaque_tid(), n = nR * rowW;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t i = (uint32_t)min(q * 256 + tid, n - 1);
+      const uint32_t r = __umulhi(i << 1, magic), c = i - r * (uint32_t)rowW;
+      const uint32_t o = rowOff((int)r) + colOff((int)c) + im.sh;
+      sh[q] = o & 3u;
+      lo[q] = buf_ld32(im.r, o & ~3u);
+      hi[q] = aligned ? 0u : buf_ld32(im.r, (o & ~3u) + 4);
+    }
+  }
+  __device__ __forceinline__ void commit(uint32_t* lds, int ldsPitch, int nR, int rowW,
+                                         uint32_t magic) const {
+    const int tid = opaque_tid(), n = nR * rowW;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t i = (uint32_t)(q * 256 + tid);
+      const uint32_t r = __umulhi(i << 1, magic), c = i - r * (uint32_t)rowW;
+      if ((int)i < n) lds[r * ldsPitch + c] = __builtin_amdgcn_alignbyte(hi[q], lo[q], sh[q]);
+    }
+  }
+};
+
 // Bytes b and b+1 (b < 11) of the 12-byte little-endian window (w0, w1, w2),
 // as the low 16 bits of the result.
 __device__ __forceinline__ uint32_t byte_pair(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
