@@ -366,9 +366,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
   const int iw = C - 6, ih = R - 6, ni = iw * ih;
   const int nK = (iw + 7) >> 3;  // 8-pixel groups per interior row
   const int nBitWords = (ni >> 5) + 3;
-  // cell windows of the band (<= 64 cells, host-checked): they tile the
-  // interior left to right, so cellOf[x] = the last cell starting at or
-  // before x, filled by every thread in parallel after one barrier
+  // cell windows of the band (<= 64 cells, host-checked)
   FSTAMP(1);
   int cx0 = 0, ww = 0;
   if (tid < bd.nCells) {
@@ -377,7 +375,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
     cellX0[tid] = (int16_t)(ww > 0 ? cx0 : 0x7FFF);
     cellWW[tid] = (int16_t)ww;
   }
-  for (int i = tid; i < nBitWords; i += 256) bitsIni[i] = bitsMin[i] = 0;
+  for (int i = tid; i < nBitWords; i += 256) bitsIni[i] = 0;
   for (int i = tid; i < iw; i += 256) colf[i] = 0;
   if (tid == 0) {
     qCount = cCount = 0;
@@ -387,11 +385,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
   if (tid < bd.nCells && ww > 0) {
     colf[cx0] |= 1;           // left window edge: x-1 is outside
     colf[cx0 + ww - 1] |= 2;  // right window edge: x+1 is outside
-  }
-  for (int x = tid; x < iw; x += 256) {
-    int c = 0;
-    while (c + 1 < bd.nCells && cellX0[c + 1] <= x) ++c;
-    cellOf[x] = (uint8_t)c;
   }
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
   // Pixels j >= nvLast of a row's last group lie past the interior.  Phase A
@@ -595,7 +588,16 @@ __global__ __launch_bounds__(256) void k_fast_band(
   FSTAMP(5);
   if ((fbMask[0] | fbMask[1]) == 0) { FSTAMP(6); continue; }  // LDS free: barrier above
   // ---- phase B: cells without an iniThFAST keypoint, at minThFAST, over the
-  // group columns that touch one (wave 0 lists them in order with ballots)
+  // group columns that touch one (wave 0 lists them in order with ballots).
+  // The cell of each interior column is only needed here: the cells tile the
+  // interior left to right, so cellOf[x] = the last cell starting at or before x.
+  for (int x = tid; x < iw; x += 256) {
+    int c = 0;
+    while (c + 1 < bd.nCells && cellX0[c + 1] <= x) ++c;
+    cellOf[x] = (uint8_t)c;
+  }
+  for (int i = tid; i < nBitWords; i += 256) bitsMin[i] = 0;
+  __syncthreads();
   if (wave == 0) {
     int cnt = 0;
     for (int k0 = 0; k0 < nK; k0 += 64) {
@@ -1073,10 +1075,14 @@ __global__ __launch_bounds__(256) void k_blur_levels(
   }
   __syncthreads();
   // Integer 7-tap kernel [18,34,49,55,49,34,18] (sums to 257 per axis).  Row
-  // pass: a 7-tap sum is two v_dot4_u32_u8 on the byte window realigned with
-  // v_alignbyte; column pass: four v_dot2_u32_u16 over row pairs.
-  constexpr uint32_t K0123 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
-  constexpr uint32_t K456 = 49u | (34u << 8) | (18u << 16);
+  // pass: the 7-tap sum at byte offset s of a dword triple (w0, w1, w2) is
+  // v_dot4_u32_u8 of each dword with the kernel shifted to that offset (2 or 3
+  // dot4, no byte realignment); column pass: four v_dot2_u32_u16 over row pairs.
+  constexpr uint32_t k0 = 18, k1 = 34, k2 = 49, k3 = 55, k4 = 49, k5 = 34, k6 = 18;
+  constexpr uint32_t S0a = (k0 << 8) | (k1 << 16) | (k2 << 24), S0b = k3 | (k4 << 8) | (k5 << 16) | (k6 << 24);
+  constexpr uint32_t S1a = (k0 << 16) | (k1 << 24), S1b = k2 | (k3 << 8) | (k4 << 16) | (k5 << 24), S1c = k6;
+  constexpr uint32_t S2a = k0 << 24, S2b = k1 | (k2 << 8) | (k3 << 16) | (k4 << 24), S2c = k5 | (k6 << 8);
+  constexpr uint32_t S3b = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), S3c = k4 | (k5 << 8) | (k6 << 16);
   // row pass: task (row pair p, group g) -> sums of columns 4g..4g+3 of staged
   // rows 2p, 2p+1 (output column x0+4g+i reads staged bytes 4g+i+1 .. 4g+i+7)
   constexpr int G = ORB_BLUR_TW / 4;
@@ -1087,13 +1093,12 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     for (int h = 0; h < 2; ++h) {
       const uint32_t* rw = raw[2 * pr + h] + g;
       const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
-      o[h][0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), K0123,
-                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), K456, 0u, false), false);
-      o[h][1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), K0123,
-                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), K456, 0u, false), false);
-      o[h][2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), K0123,
-                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), K456, 0u, false), false);
-      o[h][3] = __builtin_amdgcn_udot4(w1, K0123, __builtin_amdgcn_udot4(w2, K456, 0u, false), false);
+      o[h][0] = __builtin_amdgcn_udot4(w0, S0a, __builtin_amdgcn_udot4(w1, S0b, 0u, false), false);
+      o[h][1] = __builtin_amdgcn_udot4(w0, S1a, __builtin_amdgcn_udot4(w1, S1b,
+                                       __builtin_amdgcn_udot4(w2, S1c, 0u, false), false), false);
+      o[h][2] = __builtin_amdgcn_udot4(w0, S2a, __builtin_amdgcn_udot4(w1, S2b,
+                                       __builtin_amdgcn_udot4(w2, S2c, 0u, false), false), false);
+      o[h][3] = __builtin_amdgcn_udot4(w1, S3b, __builtin_amdgcn_udot4(w2, S3c, 0u, false), false);
     }
     uint4 pk;
     pk.x = o[0][0] | (o[1][0] << 16);
@@ -1165,12 +1170,17 @@ __global__ __launch_bounds__(256) void k_blur_levels(
 //   at -16..15; integer moments reduced across the half-wave.
 //   rBRIEF (:119-164) on the blurred level: lane hl evaluates tests
 //   hl + 32k (k < 8); ballot k holds tests 32k .. 32k+31 of both keypoints.
-__device__ __forceinline__ int half_sum(int v) {  // sum over the 32 lanes of each half-wave
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  v += __shfl_xor(v, 16, 64);
+// Sum over the 32 lanes of each half-wave: quad, 8- and 16-lane steps as DPP
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: each pairs a
+// lane with one holding the other half of its group), then lane ^ 16 by one
+// ds_swizzle in bitmask mode (and 0x1F, xor 0x10) -- one LDS-path op where
+// __shfl_xor would take five ds_bpermute round trips.
+__device__ __forceinline__ int half_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);
+  v += __builtin_amdgcn_ds_swizzle(v, 0x401F);
   return v;
 }
 
