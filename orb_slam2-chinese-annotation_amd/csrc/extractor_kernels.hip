@@ -728,7 +728,10 @@ __global__ __launch_bounds__(512) void k_octree(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int tmp[17];
   __shared__ int sh[8];
-  const int l = blockIdx.x, img = blockIdx.y, T = blockDim.x, t = threadIdx.x;
+  // grid (images, levels): the dispatcher walks x first, so every image's level 0
+  // (the most keys, the longest workgroups) starts before any level 1, and the
+  // short upper levels fill the tail
+  const int l = blockIdx.y, img = blockIdx.x, T = blockDim.x, t = threadIdx.x;
   const OrbLevelDesc& L = plan.lv[l];
   const int NC = nodeCapMax;
   int n2 = 1;
@@ -1429,7 +1432,7 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  dim3 grid(plan->nlevels, nimg), block(512);
+  dim3 grid(nimg, plan->nlevels), block(512);
   hipLaunchKernelGGL(k_octree, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys, gNid,
                      ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag);
   return hipGetLastError();
