@@ -22,7 +22,8 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "lib" / "liborb_amd.so"
+# ORB_AMD_LIB selects another build of the same library (A/B kernel experiments)
+LIB_PATH = Path(os.environ.get("ORB_AMD_LIB", PKG_DIR / "lib" / "liborb_amd.so"))
 
 ORB_OK, ORB_EEMPTY, ORB_EINVAL, ORB_ENOMEM, ORB_EDEVICE, ORB_ECAPACITY, ORB_ENODEV = 0, 1, -1, -2, -3, -4, -5
 

@@ -1036,21 +1036,30 @@ __global__ __launch_bounds__(256) void k_blur_levels(
     *pitch = L.pitch;
     return arena + (long long)im * arenaPitch + L.arenaOff;
   };
-  TilePrefetch<(BLUR_SH * BLUR_WROW + 255) / 256> pf;
+  constexpr int NQ = (BLUR_SH * BLUR_WROW + 255) / 256;
+  TilePrefetch<NQ> pf;
   const uint32_t magic = div_magic(BLUR_WROW);
+  // Staged element q of this thread sits at the same offset in every image of
+  // the tile: row (reflected on border tiles) x pitch + dword start clamped
+  // into the row (4-aligned on aligned levels), computed once.  Level 0 is
+  // staged as unaligned unless every image base and row start is 4-aligned.
+  int pitch0;
+  level_of(0, &pitch0);
+  const bool alignedAll =
+      l > 0 || ((img0Stride & 3) == 0 && (img0Pitch & 3) == 0 && (((uintptr_t)img0) & 3) == 0);
+  const int cmax = alignedAll ? ((L.w - 1) & ~3) : L.w - 1;
+  uint32_t eoff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint32_t i = (uint32_t)min(q * 256 + tid, BLUR_SH * BLUR_WROW - 1);
+    const int r = (int)__umulhi(i << 1, magic), c = (int)i - r * BLUR_WROW;
+    const int y = td.y0 - 3 + r;
+    eoff[q] = (uint32_t)((rowsInside ? y : reflect101(y, L.h)) * pitch0 + min(max(colA + 4 * c, 0), cmax));
+  }
   auto issue = [&](int im) {
     int pitch;
     const uint8_t* lvl = level_of(im, &pitch);
-    const bool aligned = l > 0 || ((pitch & 3) == 0 && (((uintptr_t)lvl) & 3) == 0);
-    const ImgRsrc ir = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
-    const int cmax = aligned ? ((L.w - 1) & ~3) : L.w - 1;
-    pf.issue(ir, aligned, BLUR_SH, BLUR_WROW, magic,
-             [&](int r) {
-               const int y = td.y0 - 3 + r;
-               return (uint32_t)((rowsInside ? y : reflect101(y, L.h)) * pitch);
-             },
-             // dword start clamped into the row (keeping 4-alignment on aligned levels)
-             [&](int c) { return (uint32_t)min(max(colA + 4 * c, 0), cmax); });
+    pf.issue_at(img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w)), alignedAll, eoff);
   };
   int img = blockIdx.y;
   if (img >= nImg) return;

@@ -236,6 +236,18 @@ struct TilePrefetch {
       hi[q] = aligned ? 0u : buf_ld32(im.r, (o & ~3u) + 4);
     }
   }
+  // the same loads at per-element byte offsets computed once by the caller
+  // (off[q] = row + column offset of element q; a workgroup walking the same
+  // tile of several images keeps them across images)
+  __device__ __forceinline__ void issue_at(const ImgRsrc& im, bool aligned, const uint32_t* off) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t o = off[q] + im.sh;
+      sh[q] = o & 3u;
+      lo[q] = buf_ld32(im.r, o & ~3u);
+      hi[q] = aligned ? 0u : buf_ld32(im.r, (o & ~3u) + 4);
+    }
+  }
   __device__ __forceinline__ void commit(uint32_t* lds, int ldsPitch, int nR, int rowW,
                                          uint32_t magic) const {
     const int tid = opaque_tid(), n = nR * rowW;
