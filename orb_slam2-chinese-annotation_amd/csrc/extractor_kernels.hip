@@ -76,11 +76,19 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   // staging: ALIGNED sources need one dword load per LDS dword, others two
   // (realigned with v_alignbyte)
   const uint32_t magic = div_magic(nW);
-  TilePrefetch<(SROWS * SW + 255) / 256> pf;
+  constexpr int NQ = (SROWS * SW + 255) / 256;
+  TilePrefetch<NQ> pf;
+  // staged element q of this thread: the same offset in every image, computed once
+  uint32_t eoff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint32_t i = (uint32_t)min(q * 256 + tid, nR * nW - 1);
+    const uint32_t r = __umulhi(i << 1, magic), c = i - r * (uint32_t)nW;
+    eoff[q] = (syA + r) * (uint32_t)srcStride + (uint32_t)colBase + 4 * c;
+  }
   auto issue = [&](int z) {
-    const ImgRsrc im = img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((sh - 1) * srcStride + sw));
-    pf.issue(im, ALIGNED, nR, nW, magic, [&](int r) { return (uint32_t)((syA + r) * srcStride); },
-             [&](int c) { return (uint32_t)(colBase + 4 * c); });
+    pf.issue_at(img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((sh - 1) * srcStride + sw)),
+                ALIGNED, eoff);
   };
   int z = blockIdx.z;
   if (z >= nImg) return;
