@@ -187,3 +187,39 @@ def test_extractor_parameters(gpu, oracle, w, h, nf, sf, nl):
 def test_extractor_rejects_unsupported_scale(gpu):
     with pytest.raises(gpu.OrbError):
         gpu.ORBextractor(1000, 2.5, 8, 20, 7)
+
+
+@pytest.mark.parametrize("w,h,stride,pitch,B", [
+    (640, 480, 640, 640 * 480, 6),          # aligned rows and images
+    (640, 480, 644, 644 * 480 + 2, 5),      # aligned rows, images at alternating alignment
+    (641, 479, 641, 641 * 479, 3),          # odd stride and odd image pitch
+    (1241, 376, 1241, 1241 * 376, 9),       # 9 images: uneven images per workgroup
+])
+def test_batch_layouts_vs_oracle(gpu, oracle, w, h, stride, pitch, B):
+    """extract_batch over B images packed at (stride, pitch): the resize and blur
+    workgroups walk several images each (prefetching the next), so every image
+    and every alignment case is checked against the CPU oracle."""
+    torch = pytest.importorskip("torch")
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    imgs = [gpu.synth_image(30 + B, f, w, h) for f in range(B)]
+    buf = np.zeros(pitch * B + stride, np.uint8)
+    for f, im in enumerate(imgs):
+        for y in range(h):
+            buf[f * pitch + y * stride: f * pitch + y * stride + w] = im[y]
+    cap = ext.capacity(w, h)
+    d_img = torch.from_numpy(buf).cuda()
+    d_kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ext.extract_batch(d_img.data_ptr(), B, w, h, stride, pitch, d_kps.data_ptr(),
+                      d_desc.data_ptr(), cap, d_cnt.data_ptr())
+    torch.cuda.synchronize()
+    kps = d_kps.cpu().numpy().view(gpu.KEYPOINT_DTYPE).reshape(B, cap)
+    desc = d_desc.cpu().numpy()
+    cnt = d_cnt.cpu().numpy()
+    for f in range(B):
+        kr, dr, _ = oracle.extract(imgs[f], 1000, 1.2, 8, 20, 7)
+        assert cnt[f] == len(kr), (f, cnt[f], len(kr))
+        assert kps[f, : cnt[f]].tobytes() == kr.tobytes(), f
+        assert desc[f, : cnt[f]].tobytes() == dr.tobytes(), f
