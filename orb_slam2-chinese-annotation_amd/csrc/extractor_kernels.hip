@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   // weight tables and the source window are loaded once, and the next image's
   // window is loaded into registers while the current one is computed.
   __shared__ __attribute__((aligned(16))) uint32_t tile[SROWS][SW];
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x;
   const int tx = tid & 31, ty = tid >> 5;
   const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
   const int xs = x0 + 4 * tx;
@@ -87,8 +87,8 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
     eoff[q] = (syA + r) * (uint32_t)srcStride + (uint32_t)colBase + 4 * c;
   }
   auto issue = [&](int z) {
-    pf.issue_at(img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((sh - 1) * srcStride + sw)),
-                ALIGNED, eoff);
+    pf.issue(img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((sh - 1) * srcStride + sw)),
+             ALIGNED, eoff);
   };
   int z = blockIdx.z;
   if (z >= nImg) return;
@@ -1028,7 +1028,7 @@ __global__ __launch_bounds__(256) void k_blur_levels(
   const OrbLevelDesc& L = plan.lv[l];
   // A workgroup blurs one tile of images blockIdx.y, + gridDim.y, ...; the
   // next image's source rows are loaded into registers while the current one
-  // is computed (RowPrefetch), so its HBM round trip overlaps this image's work.
+  // is computed (TilePrefetch), so its HBM round trip overlaps this image's work.
   // Staging: rows outside the level are reflected (REFLECT_101) when
   // addressed; columns are loaded with the dword start clamped into the row,
   // and the few bytes a border tile needs outside [0, w) are patched from
@@ -1067,7 +1067,7 @@ __global__ __launch_bounds__(256) void k_blur_levels(
   auto issue = [&](int im) {
     int pitch;
     const uint8_t* lvl = level_of(im, &pitch);
-    pf.issue_at(img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w)), alignedAll, eoff);
+    pf.issue(img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w)), alignedAll, eoff);
   };
   int img = blockIdx.y;
   if (img >= nImg) return;

@@ -111,31 +111,6 @@ __device__ __forceinline__ double pinned_log(double x) {
   return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
 }
 
-// --------------------------------------------------- realigning byte loads
-// Bytes [p, p+4) as one dword for any alignment of p, from the aligned dwords
-// covering them.  `last` = the last byte that may be read: the second aligned
-// dword is replaced by the first when it starts past `last`, so no read
-// leaves the page of a valid byte.  Split in two halves so that a loop can
-// issue every load (branch-free, no wait) before assembling any dword:
-//   RawDw r = raw_u32_any(p, last);  ...  uint32_t v = r.get();
-struct RawDw {
-  uint32_t lo, hi, sh;
-  __device__ __forceinline__ uint32_t get() const { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
-};
-__device__ __forceinline__ RawDw raw_u32_any(const uint8_t* p, const uint8_t* last) {
-  const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
-  const uint32_t* a = (const uint32_t*)(p - sh);
-  const uint32_t* b = ((const uint8_t*)(a + 1) <= last) ? a + 1 : a;
-  RawDw r;
-  r.lo = a[0];
-  r.hi = b[0];
-  r.sh = sh;
-  return r;
-}
-__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p, const uint8_t* last) {
-  return raw_u32_any(p, last).get();
-}
-
 // Buffer resources: 32-bit per-lane offsets (no 64-bit address VALU) and a
 // hardware range check per dword (a dword load that ends past `bytes` reads
 // as 0, a store past it is dropped).  Build only from wave-uniform values.
@@ -162,84 +137,25 @@ __device__ __forceinline__ ImgRsrc img_rsrc(const uint8_t* p, uint32_t bytes) {
   return ir;
 }
 
-// Stage image rows into LDS, lane = dword column, wave = row (4 waves, B rows
-// per wave in flight per batch): lds[r * ldsPitch + lane] = image bytes
-// [rowOff(r) + colOff, +4) for r < nR and lane < nW (nW <= 64; colOff is this
-// lane's column byte offset).  ALIGNED: every such offset (plus the base
-// misalignment) is a multiple of 4 -- one load per dword; otherwise two,
-// realigned with v_alignbyte.  Bytes past the image read as 0.
-template <bool ALIGNED, int B, class RowOff>
-__device__ __forceinline__ void stage_rows(const ImgRsrc& im, int nR, int nW, uint32_t colOff,
-                                           uint32_t* lds, int ldsPitch, RowOff rowOff) {
-  // wave index through readfirstlane: the row of each load is wave-uniform,
-  // so rowOff (e.g. a reflect-101 loop) runs on the scalar unit
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int r0 = 0; r0 < nR; r0 += 4 * B) {
-    uint32_t lo[B], hi[B], sh[B];
-#pragma unroll
-    for (int q = 0; q < B; ++q) {
-      const int r = min(r0 + wv + 4 * q, nR - 1);
-      const uint32_t o = rowOff(r) + colOff + im.sh;
-      if (ALIGNED) {
-        lo[q] = buf_ld32(im.r, o);
-      } else {
-        sh[q] = o & 3u;
-        lo[q] = buf_ld32(im.r, o & ~3u);
-        hi[q] = buf_ld32(im.r, (o & ~3u) + 4);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < B; ++q) {
-      const int r = r0 + wv + 4 * q;
-      if (r < nR && lane < nW)
-        lds[r * ldsPitch + lane] = ALIGNED ? lo[q] : __builtin_amdgcn_alignbyte(hi[q], lo[q], sh[q]);
-    }
-  }
-}
-
-// Staging split in two for software pipelining: issue() puts the loads of a
-// tile of nR rows x rowW dwords (nR * rowW <= NQ * 256) in flight into
-// registers, NQ dwords per thread of a 256-thread workgroup (element
-// i = q*256 + tid -> row i / rowW, dword i % rowW, the division by a
-// multiply-high: i / d = umulhi(2i, ceil(2^31 / d)) for i < 2^20, d >= 1 --
-// 2^31 rather than 2^32 so that d = 1 has a 32-bit magic); commit() realigns them into
-// LDS.  A workgroup walking several images issues the next image's tile before
-// it computes the current one, so the HBM round trip overlaps that work.
-// rowOff(r) / colOff(c) give byte offsets (per lane); aligned (wave-uniform)
-// tiles skip the second load and realign by 0.  Elements past the tile repeat
-// its last one (branch-free loads) and are not committed.
+// Staging split in two for software pipelining.  A workgroup walking the same
+// tile of several images (resize, blur) stages, per thread, NQ dwords of a
+// tile of nR rows x rowW dwords (nR * rowW <= NQ * 256; element
+// i = q*256 + tid -> row i / rowW, dword i % rowW).  The caller computes the
+// element byte offsets once (they are the same in every image), issue() puts
+// one image's loads in flight into registers, and commit() realigns them into
+// LDS.  The next image's tile is issued before the current one is computed,
+// so its HBM round trip overlaps that work.  Aligned (wave-uniform) tiles skip
+// the second load and realign by 0.  The division by rowW is a multiply-high:
+// i / d = umulhi(2i, ceil(2^31 / d)) for i < 2^20, d >= 1 (2^31 rather than
+// 2^32 so that d = 1 has a 32-bit magic).
 __device__ __forceinline__ uint32_t div_magic(int d) {
   return (uint32_t)((0x7FFFFFFFull + (uint64_t)d) / (uint64_t)d);
 }
 template <int NQ>
 struct TilePrefetch {
   uint32_t lo[NQ], hi[NQ], sh[NQ];
-  // the thread index is laundered through an empty asm so that the per-element
-  // offsets are recomputed per image instead of being hoisted out of the image
-  // loop (which would hold 2 x NQ more registers across it)
-  __device__ __forceinline__ static int opaque_tid() {
-    int t = (int)threadIdx.x;
-    __asm__ volatile("" : "+v"(t));
-    return t;
-  }
-  template <class RowOff, class ColOff>
-  __device__ __forceinline__ void issue(const ImgRsrc& im, bool aligned, int nR, int rowW,
-                                        uint32_t magic, RowOff rowOff, ColOff colOff) {
-    const int tid = opaque_tid(), n = nR * rowW;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const uint32_t i = (uint32_t)min(q * 256 + tid, n - 1);
-      const uint32_t r = __umulhi(i << 1, magic), c = i - r * (uint32_t)rowW;
-      const uint32_t o = rowOff((int)r) + colOff((int)c) + im.sh;
-      sh[q] = o & 3u;
-      lo[q] = buf_ld32(im.r, o & ~3u);
-      hi[q] = aligned ? 0u : buf_ld32(im.r, (o & ~3u) + 4);
-    }
-  }
-  // the same loads at per-element byte offsets computed once by the caller
-  // (off[q] = row + column offset of element q; a workgroup walking the same
-  // tile of several images keeps them across images)
-  __device__ __forceinline__ void issue_at(const ImgRsrc& im, bool aligned, const uint32_t* off) {
+  // off[q] = byte offset of element q inside the image
+  __device__ __forceinline__ void issue(const ImgRsrc& im, bool aligned, const uint32_t* off) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint32_t o = off[q] + im.sh;
@@ -250,7 +166,11 @@ struct TilePrefetch {
   }
   __device__ __forceinline__ void commit(uint32_t* lds, int ldsPitch, int nR, int rowW,
                                          uint32_t magic) const {
-    const int tid = opaque_tid(), n = nR * rowW;
+    // the thread index is laundered through an empty asm so that the LDS
+    // addresses are recomputed per image instead of held across the image loop
+    int tid = (int)threadIdx.x;
+    __asm__ volatile("" : "+v"(tid));
+    const int n = nR * rowW;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const uint32_t i = (uint32_t)(q * 256 + tid);
@@ -259,14 +179,6 @@ struct TilePrefetch {
     }
   }
 };
-
-// Bytes b and b+1 (b < 11) of the 12-byte little-endian window (w0, w1, w2),
-// as the low 16 bits of the result.
-__device__ __forceinline__ uint32_t byte_pair(uint32_t w0, uint32_t w1, uint32_t w2, int b) {
-  const uint32_t lo = b < 4 ? w0 : (b < 8 ? w1 : w2);
-  const uint32_t hi = b < 4 ? w1 : (b < 8 ? w2 : 0u);
-  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(b & 3));
-}
 
 // ------------------------------------------------------------- Hamming
 // DescriptorDistance (src/ORBmatcher.cc:1814-1830) == popcount(a ^ b) over 256 bits.
