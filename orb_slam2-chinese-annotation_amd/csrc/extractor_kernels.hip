@@ -1383,9 +1383,9 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   (void)xmax;  // folded into the alpha table: (2048, 0) past xmax
   // tile bounds: narrow variant for a per-level downscale <= 1.25, wide <= 1.9
   const bool wide = (double)sw / dw > 1.25 || (double)sh / dh > 1.25;
-  // each workgroup resizes one tile of ORB_RESIZE_IMAGES_PER_WG images (default 4)
+  // each workgroup resizes one tile of ORB_RESIZE_IMAGES_PER_WG images (default 8; swept 2-16)
   static const int perWg =
-      getenv("ORB_RESIZE_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_RESIZE_IMAGES_PER_WG"))) : 4;
+      getenv("ORB_RESIZE_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_RESIZE_IMAGES_PER_WG"))) : 8;
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, (nimg + perWg - 1) / perWg),
       block(256);
   // every image base and row start 4-aligned: one load per staged dword
@@ -1459,9 +1459,9 @@ hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
                              int nimg, hipStream_t s) {
-  // each workgroup blurs one tile of ORB_BLUR_IMAGES_PER_WG images (default 4)
+  // each workgroup blurs one tile of ORB_BLUR_IMAGES_PER_WG images (default 8; swept 2-16)
   static const int perWg =
-      getenv("ORB_BLUR_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_BLUR_IMAGES_PER_WG"))) : 4;
+      getenv("ORB_BLUR_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_BLUR_IMAGES_PER_WG"))) : 8;
   dim3 grid(plan->nBlurTiles, (nimg + perWg - 1) / perWg), block(256);
   hipLaunchKernelGGL(k_blur_levels, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, *plan, tiles, blur, blurPitch, nimg);
