@@ -566,13 +566,21 @@ __global__ __launch_bounds__(256) void k_fast_band(
     unsigned long long row = lane < ih ? bit_run(bits, lane * iw + cx0, ww) : 0ull;
     const int cnt = __popcll(row);
     const int incl = wave_incl_scan(cnt);
-    const int total = __shfl(incl, 63, 64);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
     int o = incl - cnt;
+    // two keys per iteration: both strength reads are in flight together
+    const uint8_t* srow = sc + (lane + 3) * P + cx0 + 8;
+    const uint32_t kx = (uint32_t)(bd.x0 + 3 + cx0), ky = (uint32_t)(bd.y0 + 3 + lane);
     while (row) {
-      const int x = __builtin_ctzll(row);
+      const int x0 = __builtin_ctzll(row);
       row &= row - 1;
-      const int m = sc[(lane + 3) * P + cx0 + x + 8];
-      out[o++] = pack_key(bd.x0 + 3 + cx0 + x, bd.y0 + 3 + lane, m - 1);
+      const bool two = row != 0;
+      const int x1 = two ? __builtin_ctzll(row) : x0;
+      if (two) row &= row - 1;
+      const int m0 = srow[x0], m1 = srow[x1];
+      out[o] = pack_key(kx + x0, ky, m0 - 1);
+      if (two) out[o + 1] = pack_key(kx + x1, ky, m1 - 1);
+      o += two ? 2 : 1;
     }
     return total;
   };
