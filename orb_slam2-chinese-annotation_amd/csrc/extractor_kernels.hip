@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
   const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = blockDim.x >> 6;
   const int bandElems = plan.maxBandBytes;
-  const int bitStride = (bandElems >> 5) + 3;
+  const int bitStride = ((bandElems >> 5) + 4) & ~1;  // even: colf / fbCol stay 8-aligned
   uint32_t* roi32 = (uint32_t*)smem;                            // R x P f16 band pixels
   const _Float16* roih = (const _Float16*)smem;
   uint8_t* sc = smem + 2 * bandElems;                           // R x P arc strengths
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
   uint32_t* bitsIni = (uint32_t*)(corners + FAST_CORNERS);      // interior survivors, iniTh
   uint32_t* bitsMin = bitsIni + bitStride;                      // interior survivors, minTh
   uint8_t* colf = (uint8_t*)(bitsMin + bitStride);              // window edge flags per column
-  uint8_t* cellOf = colf + bandElems / 7 + 8;                   // cell of each interior column
+  uint8_t* fbCol = colf + ((bandElems / 7 + 15) & ~7);          // 1: column in a fallback cell
 
   // A workgroup takes bands blockIdx.x, + gridDim.x, ...: the next band's
   // pixels and cell descriptors are loaded into registers while the current
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
 
   // Group columns pretested by a pass: all of them in phase A, only those
   // touching a fallback cell in phase B (fbK, built before phase B).
-  uint16_t* fbK = (uint16_t*)(cellOf + bandElems / 7 + 8);
+  uint16_t* fbK = (uint16_t*)(fbCol + ((bandElems / 7 + 15) & ~7));
 
   // Score the queued candidates (dense: 256 per pass) and list the corners
   // (m > t).  In phase B strengths already known from phase A are kept.
@@ -467,17 +467,12 @@ __global__ __launch_bounds__(256) void k_fast_band(
           rp[i] = pretest_pair(D[i + 2], U[i], q4, Dn[i], q12, T);
         }
         if (FB) {
-          // only pixels of fallback cells (and of the interior)
+          // only pixels of fallback cells (fbCol is 0 past the interior): one
+          // 8-byte read of the group's column flags
+          const unsigned long long fm = *reinterpret_cast<const unsigned long long*>(fbCol + 8 * k);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int x = 8 * k + j;
-            bool in = x < iw;
-            if (in) {
-              const int cc = cellOf[x];
-              in = (fbMask[cc >> 5] >> (cc & 31)) & 1u;
-            }
-            if (!in) rp[j >> 1] |= (j & 1) ? 0x80000000u : 0x8000u;
-          }
+          for (int j = 0; j < 8; ++j)
+            if (!((fm >> (8 * j)) & 0xFFull)) rp[j >> 1] |= (j & 1) ? 0x80000000u : 0x8000u;
         } else {
           // strengths start at 0 (8 bytes, 8-aligned), FAST_OUTSIDE past the interior
           const unsigned long long z = k == nK - 1 ? outsideLast : 0ull;
@@ -529,10 +524,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
         y = (int)(((float)j + 0.5f) / (float)iw);
         x = j - y * iw;
         off = (y + 3) * P + (x + 8);
-        if (fallbackOnly) {
-          const int c = cellOf[x];
-          if (!((fbMask[c >> 5] >> (c & 31)) & 1u)) continue;
-        }
+        if (fallbackOnly && !fbCol[x]) continue;
       } else {
         off = corners[j];
         const int ry = (int)(((float)off + 0.5f) / (float)P);
@@ -605,12 +597,17 @@ __global__ __launch_bounds__(256) void k_fast_band(
   if ((fbMask[0] | fbMask[1]) == 0) { FSTAMP(6); continue; }  // LDS free: barrier above
   // ---- phase B: cells without an iniThFAST keypoint, at minThFAST, over the
   // group columns that touch one (wave 0 lists them in order with ballots).
-  // The cell of each interior column is only needed here: the cells tile the
-  // interior left to right, so cellOf[x] = the last cell starting at or before x.
-  for (int x = tid; x < iw; x += 256) {
-    int c = 0;
-    while (c + 1 < bd.nCells && cellX0[c + 1] <= x) ++c;
-    cellOf[x] = (uint8_t)c;
+  // Column flags fbCol[x] (x < 8 nK) = column x lies in a fallback cell: the
+  // cells tile the interior left to right, so x's cell is the last one
+  // starting at or before x.
+  for (int x = tid; x < 8 * nK; x += 256) {
+    uint8_t f = 0;
+    if (x < iw) {
+      int c = 0;
+      while (c + 1 < bd.nCells && cellX0[c + 1] <= x) ++c;
+      f = (uint8_t)((fbMask[c >> 5] >> (c & 31)) & 1u);
+    }
+    fbCol[x] = f;
   }
   for (int i = tid; i < nBitWords; i += 256) bitsMin[i] = 0;
   __syncthreads();
@@ -619,16 +616,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
     for (int k0 = 0; k0 < nK; k0 += 64) {
       const int k = k0 + lane;
       bool hit = false;
-      if (k < nK) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int x = 8 * k + j;
-          if (x < iw) {
-            const int c = cellOf[x];
-            hit = hit || ((fbMask[c >> 5] >> (c & 31)) & 1u);
-          }
-        }
-      }
+      if (k < nK) hit = *reinterpret_cast<const unsigned long long*>(fbCol + 8 * k) != 0ull;
       const unsigned long long b = __ballot(hit);
       if (hit) fbK[cnt + __popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)k;
       cnt += __popcll(b);
@@ -1414,9 +1402,9 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
 // element pitch): f16 pixels, strengths, queue, corner list, two interior
 // bitmaps, per-column flags / cells, phase-B group list.
 size_t orb_k_fast_band_lds(int bandElems) {
-  const size_t bitBytes = 4 * (size_t)((bandElems >> 5) + 3);
+  const size_t bitBytes = 4 * (size_t)(((bandElems >> 5) + 4) & ~1);
   return (size_t)bandElems * 3 + FAST_QCAP * 2 + FAST_CORNERS * 2 + 2 * bitBytes +
-         2 * ((size_t)bandElems / 7 + 8) + 2 * ((size_t)bandElems / 28 + 8);
+         2 * (size_t)((bandElems / 7 + 15) & ~7) + 2 * ((size_t)bandElems / 28 + 8);
 }
 
 hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
