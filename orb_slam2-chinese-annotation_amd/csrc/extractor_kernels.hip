@@ -409,17 +409,30 @@ __global__ __launch_bounds__(256) void k_fast_band(
 
   // Score the queued candidates (dense: 256 per pass) and list the corners
   // (m > t).  In phase B strengths already known from phase A are kept.
-  auto flush = [&](int t, int nq) {
+  // Phase A (fresh): nothing is scored yet, so the arc strength is computed
+  // unconditionally and its 16 ring reads go out together with the strength
+  // byte read (which only tells FAST_OUTSIDE pixels apart).
+  auto flush = [&](int t, int nq, bool fresh) {
     for (int j0 = 0; j0 < nq; j0 += 256) {
       const int j = j0 + tid;
       bool corner = false;
       int off = 0;
       if (j < nq) {
         off = queue[j];
-        int m = sc[off];  // 0: not scored yet; phase B keeps phase-A strengths
-        if (m == 0) {
-          m = min(max(fast_score(roih + off, P), 0), 255);
-          sc[off] = (uint8_t)m;
+        int m;
+        if (fresh) {
+          const int s = min(max(fast_score(roih + off, P), 0), 255);
+          m = sc[off];
+          if (m == 0) {
+            m = s;
+            sc[off] = (uint8_t)m;
+          }
+        } else {
+          m = sc[off];  // 0: not scored yet; phase B keeps phase-A strengths
+          if (m == 0) {
+            m = min(max(fast_score(roih + off, P), 0), 255);
+            sc[off] = (uint8_t)m;
+          }
         }
         corner = m > t && m >= 2;
       }
@@ -506,7 +519,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
       // every wave reads the count before any wave appends again: the flush
       // synchronises; a round without one takes a second barrier
       const int nq = qCount;
-      if (nq > FAST_QFLUSH || g0 + FAST_GROUPS >= nG) flush(t, nq);
+      if (nq > FAST_QFLUSH || g0 + FAST_GROUPS >= nG) flush(t, nq, !FB);
       else __syncthreads();
     }
   };
