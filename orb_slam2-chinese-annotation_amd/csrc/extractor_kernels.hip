@@ -544,14 +544,17 @@ __global__ __launch_bounds__(256) void k_fast_band(
         y = ry - 3;
         x = off - ry * P - 8;
       }
+      // the strength, the column's window-edge flags and all 8 neighbours are
+      // read in one LDS round trip (every neighbour element lies inside the
+      // band); neighbours outside the cell window count as 0 (cv::FAST's border)
       const uint8_t* c = sc + off;
-      const int m = c[0];
+      const int m = c[0], cf = colf[x];
+      const int r0 = c[-P - 1], r1 = c[-P], r2 = c[-P + 1], r3 = c[-1], r4 = c[1], r5 = c[P - 1],
+                r6 = c[P], r7 = c[P + 1];
       if (m <= t || m < 2) continue;
-      const int cf = colf[x];
       const bool L = !(cf & 1), Rt = !(cf & 2), U = y > 0, D = y < ih - 1;
-      const int nb[8] = {(U && L) ? c[-P - 1] : 0, U ? c[-P] : 0, (U && Rt) ? c[-P + 1] : 0,
-                         L ? c[-1] : 0, Rt ? c[1] : 0, (D && L) ? c[P - 1] : 0,
-                         D ? c[P] : 0, (D && Rt) ? c[P + 1] : 0};
+      const int nb[8] = {(U && L) ? r0 : 0, U ? r1 : 0, (U && Rt) ? r2 : 0, L ? r3 : 0,
+                         Rt ? r4 : 0, (D && L) ? r5 : 0, D ? r6 : 0, (D && Rt) ? r7 : 0};
       bool ok = true;
 #pragma unroll
       for (int k = 0; k < 8; ++k) ok = ok && !(nb[k] > t && nb[k] >= m);
