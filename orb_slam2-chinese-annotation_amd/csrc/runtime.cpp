@@ -186,6 +186,29 @@ struct DevBuf {
   T* as() const { return (T*)p; }
 };
 
+// Pinned host staging for the host-buffer API: one contiguous DMA each way
+// (a 2-D copy from pageable memory goes row by row, ~7 us per row).
+struct HostBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  orb_status_t ensure(size_t n) {
+    if (n <= bytes) return ORB_OK;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return ORB_ENOMEM;
+    bytes = n;
+    return ORB_OK;
+  }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T* as() const { return (T*)p; }
+};
+
 // HIP-event timing of kernel stages on the stream they are launched on.  Each
 // profiled call takes a fresh set of events from a pool (no synchronisation in
 // the launch path); read() drains every recorded set and accumulates per-stage
@@ -295,6 +318,7 @@ struct orb_extractor {
   DevBuf dArena, dBlur, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
   // single-image API scratch
   DevBuf dImg, dKps, dDesc, dCounts;
+  HostBuf hImg, hOut;  // pinned staging: image in, counts + keypoints + descriptors out
   int lastW = 0, lastH = 0;
   size_t lastImgStride = 0;
   const uint8_t* lastImg0 = nullptr;  // level 0 of the last batch (device)
@@ -737,6 +761,8 @@ void orb_extractor_destroy(orb_extractor_t* h) {
                     &h->dGKeys, &h->dGNid, &h->dOutKeys, &h->dOutCount, &h->dErr,
                     &h->dImg, &h->dKps, &h->dDesc, &h->dCounts};
   for (DevBuf* b : bufs) b->release();
+  h->hImg.release();
+  h->hOut.release();
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
@@ -814,15 +840,25 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   if ((st = h->dKps.ensure((size_t)cap * sizeof(orb_keypoint_t)))) return st;
   if ((st = h->dDesc.ensure((size_t)cap * 32))) return st;
   if ((st = h->dCounts.ensure(16))) return st;
-  HIP_TRY(hipMemcpy2DAsync(h->dImg.p, dstride, image, stride, width, height,
-                           hipMemcpyHostToDevice, h->stream));
+  // image -> pinned staging at the device row pitch -> one DMA
+  if ((st = h->hImg.ensure(pitch))) return st;
+  for (int y = 0; y < height; ++y)
+    memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
+  HIP_TRY(hipMemcpyAsync(h->dImg.p, h->hImg.p, pitch, hipMemcpyHostToDevice, h->stream));
   st = run_batch(h, h->dImg.as<uint8_t>(), 1, dstride, pitch, h->dKps.as<orb_keypoint_t>(),
                  h->dDesc.as<uint8_t>(), cap, h->dCounts.as<int32_t>(), h->stream);
   if (st) return st;
-  int32_t n = 0, err = 0;
-  HIP_TRY(hipMemcpyAsync(&n, h->dCounts.p, 4, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipMemcpyAsync(&err, h->dErr.p, 4, hipMemcpyDeviceToHost, h->stream));
+  // counts, error flag, then as many records as the capacity allows, in one
+  // round trip: the pinned block holds [n, err, pad, pad | cap keypoints | cap x 32]
+  const size_t kOff = 16, dOff = kOff + (size_t)cap * sizeof(orb_keypoint_t);
+  if ((st = h->hOut.ensure(dOff + (size_t)cap * 32))) return st;
+  uint8_t* ho = h->hOut.as<uint8_t>();
+  HIP_TRY(hipMemcpyAsync(ho, h->dCounts.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipMemcpyAsync(ho + 4, h->dErr.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  int32_t n = 0, err = 0;
+  memcpy(&n, ho, 4);
+  memcpy(&err, ho + 4, 4);
   h->lastW = width;
   h->lastH = height;
   if (err) {
@@ -832,10 +868,13 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   *n_keypoints = n;
   if (n > capacity) return ORB_ECAPACITY;
   if (n > 0) {
-    HIP_TRY(hipMemcpy(keypoints, h->dKps.p, (size_t)n * sizeof(orb_keypoint_t),
-                      hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(ho + kOff, h->dKps.p, (size_t)n * sizeof(orb_keypoint_t),
+                           hipMemcpyDeviceToHost, h->stream));
     if (descriptors)
-      HIP_TRY(hipMemcpy(descriptors, h->dDesc.p, (size_t)n * 32, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpyAsync(ho + dOff, h->dDesc.p, (size_t)n * 32, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    memcpy(keypoints, ho + kOff, (size_t)n * sizeof(orb_keypoint_t));
+    if (descriptors) memcpy(descriptors, ho + dOff, (size_t)n * 32);
   }
   return ORB_OK;
 }
