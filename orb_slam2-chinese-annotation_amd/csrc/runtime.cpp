@@ -1045,6 +1045,7 @@ struct orb_matcher {
   // stereo / frame / BoW scratch
   DevBuf dRKeys, dRDesc, dNR, dPyr, dPairLv, dDepth, dSad, dBowA, dBowB, dBowC, dBowD, dBowE,
       dBowF, dBowG, dBowH, dBowI, dBowJ, dBowK;
+  HostBuf hPyr;  // pinned staging of the host stereo pyramids (one DMA)
   // frustum scratch
   DevBuf dMapPts, dPose, dTracks, dNInView;
   // SearchForInitialization / ComputeDistinctiveDescriptors scratch
@@ -1113,6 +1114,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dOffs, &m->dObsDesc, &m->dBest, &m->dBestDesc, &m->dInitQ,
                     &m->dInitStage, &m->dInitCounts};
   for (DevBuf* b : bufs) b->release();
+  m->hPyr.release();
   for (DevBuf& b : m->sx) b.release();
   m->prof.destroy();
   hipStreamDestroy(m->stream);
@@ -1394,16 +1396,22 @@ orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in, fl
   StereoPairLevelsHost lv;
   memset(&lv, 0, sizeof(lv));
   uint8_t* base = m->dPyr.as<uint8_t>();
+  // both pyramids -> pinned staging in the device layout -> one DMA (2-D copies
+  // from pageable memory go row by row)
+  if ((st = m->hPyr.ensure(total))) return st;
+  uint8_t* hb = m->hPyr.as<uint8_t>();
   for (int l = 0; l < L; ++l) {
-    uint8_t* dl = base + off[l];
-    uint8_t* dr = dl + (size_t)P.strideL[l] * P.h[l];
-    HIP_TRY(hipMemcpy2DAsync(dl, P.strideL[l], in->left_levels[l], (size_t)in->level_stride[l],
-                             P.w[l], P.h[l], hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpy2DAsync(dr, P.strideR[l], in->right_levels[l], (size_t)in->level_stride[l],
-                             P.w[l], P.h[l], hipMemcpyHostToDevice, s));
-    lv.L[l] = dl;
-    lv.R[l] = dr;
+    const size_t rowsL = (size_t)P.strideL[l] * P.h[l];
+    for (int y = 0; y < P.h[l]; ++y) {
+      memcpy(hb + off[l] + (size_t)y * P.strideL[l],
+             in->left_levels[l] + (size_t)y * in->level_stride[l], (size_t)P.w[l]);
+      memcpy(hb + off[l] + rowsL + (size_t)y * P.strideR[l],
+             in->right_levels[l] + (size_t)y * in->level_stride[l], (size_t)P.w[l]);
+    }
+    lv.L[l] = base + off[l];
+    lv.R[l] = base + off[l] + rowsL;
   }
+  HIP_TRY(hipMemcpyAsync(base, hb, total, hipMemcpyHostToDevice, s));
   if ((st = upload(m->dPairLv, &lv, sizeof(lv), s))) return st;
   if ((st = m->dUr.ensure((size_t)stride * 4))) return st;
   if ((st = m->dDepth.ensure((size_t)stride * 4))) return st;

@@ -38,3 +38,18 @@ for _ in range(N):
 t1 = time.perf_counter()
 print(f"SearchByProjection (host buffers, 5000 MPs): {N / (t1 - t0):.0f} calls/s, "
       f"{1e3 * (t1 - t0) / N:.3f} ms/call")
+# Frame::ComputeStereoMatches on host buffers (both 8-level pyramids uploaded per call)
+el, er = orb.ORBextractor(2000, 1.2, 8, 20, 7), orb.ORBextractor(2000, 1.2, 8, 20, 7)
+kl, dl = el(orb.synth_image(1, 0, W, H, 0))
+kr, dr = er(orb.synth_image(1, 0, W, H, 1))
+lp, rp = el.mvImagePyramid, er.mvImagePyramid
+inv = el.GetInverseScaleFactors()
+F2 = orb.Frame(kl, dl, np.float32(el.GetScaleFactors()), W, H)
+for _ in range(5):
+    m.ComputeStereoMatches(F2, kr, dr, lp, rp, inv, 386.1448, 718.856)
+t0 = time.perf_counter()
+for _ in range(100):
+    m.ComputeStereoMatches(F2, kr, dr, lp, rp, inv, 386.1448, 718.856)
+t1 = time.perf_counter()
+print(f"ComputeStereoMatches (host buffers, 2000 + 2000 kps, pyramids uploaded): "
+      f"{100 / (t1 - t0):.0f} pairs/s, {1e3 * (t1 - t0) / 100:.3f} ms/pair")
