@@ -897,6 +897,20 @@ orb_status_t orb_extractor_batch_level(orb_extractor_t* h, int image, int level,
   return ORB_OK;
 }
 
+// Device level -> caller's host rows through the pinned staging block: a 2-D
+// copy straight into pageable memory goes row by row.
+static orb_status_t copy_level_to_host(orb_extractor_t* h, uint8_t* dst, size_t dst_stride,
+                                       const uint8_t* src, size_t src_stride, int w, int hh) {
+  orb_status_t st = h->hOut.ensure((size_t)w * hh);
+  if (st) return st;
+  uint8_t* ho = h->hOut.as<uint8_t>();
+  HIP_TRY(hipMemcpy2DAsync(ho, (size_t)w, src, src_stride, (size_t)w, hh, hipMemcpyDeviceToHost,
+                           h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  for (int y = 0; y < hh; ++y) memcpy(dst + (size_t)y * dst_stride, ho + (size_t)y * w, (size_t)w);
+  return ORB_OK;
+}
+
 orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t* dst,
                                          size_t dst_stride, int* width, int* height) {
   if (!h) return ORB_EINVAL;
@@ -912,8 +926,7 @@ orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t*
   if (dst_stride < (size_t)w) return ORB_EINVAL;
   hipSetDevice(h->device);
   HIP_TRY(hipStreamSynchronize(h->stream));
-  HIP_TRY(hipMemcpy2D(dst, dst_stride, src, sstride, w, hh, hipMemcpyDeviceToHost));
-  return ORB_OK;
+  return copy_level_to_host(h, dst, dst_stride, src, sstride, w, hh);
 }
 
 orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t* dst,
@@ -928,9 +941,8 @@ orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t*
   if (dst_stride < (size_t)L.w) return ORB_EINVAL;
   hipSetDevice(h->device);
   HIP_TRY(hipStreamSynchronize(h->stream));
-  HIP_TRY(hipMemcpy2D(dst, dst_stride, h->dBlur.as<uint8_t>() + L.blurOff, L.blurPitch, L.w, L.h,
-                      hipMemcpyDeviceToHost));
-  return ORB_OK;
+  return copy_level_to_host(h, dst, dst_stride, h->dBlur.as<uint8_t>() + L.blurOff, L.blurPitch,
+                            L.w, L.h);
 }
 
 orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable) {
