@@ -784,10 +784,9 @@ __global__ __launch_bounds__(512) void k_octree(
     K = gKeys + cellSlot0 * plan.keyCap;  // this level's slot range, reused compacted
     NID = gNid + cellSlot0 * plan.keyCap;
   }
-  if (n > 65535) {  // node/key labels are 16-bit
-    if (t == 0) { atomicOr(errFlag, 1); outCount[img * plan.nlevels + l] = 0; }
-    return;
-  }
+  // n < 2^24 (x, y < 4096): node labels NID are node indices (< nodeCap <= 65535),
+  // the final-phase sort key packs (size: 24 bits, creation order: 24 bits, node: 16 bits)
+  errFlag += img;  // per-image status (read back through the image's count)
   for (int c = t; c < nc; c += T) {
     const int cnt = cellCount[cellSlot0 + c], base = cellBase[c];
     const uint32_t* src = cellKeys + (cellSlot0 + c) * plan.keyCap;
@@ -897,6 +896,10 @@ __global__ __launch_bounds__(512) void k_octree(
       if (alive + nToExpand * 3 > N) finalPhase = true;      // :692
     } else {
       // ================= final phase pass (:695-756)
+      if (seqNext >= (1 << 24)) {  // creation order no longer fits the sort key (24 bits)
+        if (t == 0) atomicOr(errFlag, 8);
+        break;
+      }
       for (int a = t; a < alive; a += T) g0[a] = A[a].cnt > 1 ? 1 : 0;
       __syncthreads();
       const int ncand = block_scan_array(g0, alive, tmp);
@@ -908,7 +911,7 @@ __global__ __launch_bounds__(512) void k_octree(
       for (int a = t; a < alive; a += T) {
         const OctNode nd = A[a];
         if (nd.cnt > 1)  // sort key (size, creation order); node index rides in the low bits
-          sortBuf[g0[a]] = ((unsigned long long)nd.cnt << 48) |
+          sortBuf[g0[a]] = ((unsigned long long)nd.cnt << 40) |
                            ((unsigned long long)(uint32_t)nd.seq << 16) | (unsigned)a;
         q4[a * 4 + 0] = q4[a * 4 + 1] = q4[a * 4 + 2] = q4[a * 4 + 3] = 0;
         rk[a] = 0x7fffffff;
@@ -1216,12 +1219,13 @@ __device__ __forceinline__ int half_sum(int v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_orient_desc(
+__global__ __launch_bounds__(256) void k_orient_desc_split(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, const uint8_t* __restrict__ blur,
     long long blurPitch, OrbPlanDesc plan, const uint32_t* __restrict__ outKeys,
-    const int32_t* __restrict__ outCount, orb_keypoint_t* __restrict__ kps,
-    uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts) {
+    const int32_t* __restrict__ outCount, const int32_t* __restrict__ errFlag,
+    orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc, int capacity,
+    int32_t* __restrict__ counts) {
   // wave id through readfirstlane: the level and buffer descriptors derived
   // from it are provably wave-uniform -> SGPRs, no waterfall
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1232,7 +1236,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
-    counts[img] = tot;
+    counts[img] = errFlag[img] ? (int32_t)ORB_EDEVICE : tot;  // failed image: negative count
   }
   if (slot0 >= plan.slotsPerImage) return;
   int l = 0;
@@ -1334,6 +1338,261 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     // |rounded offsets| <= 19: 24-bit multiplies
     const int v0 = pb[__mul24(cv_round(px0 * b + py0 * a), ORB_PATCH_DW * 4) + cv_round(px0 * a - py0 * b)];
     const int v1 = pb[__mul24(cv_round(px1 * b + py1 * a), ORB_PATCH_DW * 4) + cv_round(px1 * a - py1 * b)];
+    words[kq] = __ballot(v0 < v1);
+  }
+  if (active && hl == 0) {
+    const long long o = (long long)img * capacity + base + i;
+    uint32_t d[8];
+#pragma unroll
+    for (int kq = 0; kq < 8; ++kq) d[kq] = (uint32_t)(words[kq] >> (32 * half));
+    uint4* dst = reinterpret_cast<uint4*>(desc + o * 32);
+    dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    orb_keypoint_t kp;
+    kp.x = l ? (float)cx * L.scale : (float)cx;  // pt *= mvScaleFactor[level] (:1157-1165)
+    kp.y = l ? (float)cy * L.scale : (float)cy;
+    kp.size = L.sizeF;
+    kp.angle = angle;
+    kp.response = (float)key_s(key);
+    kp.octave = l;
+    kp.class_id = -1;
+    kps[o] = kp;
+  }
+}
+
+// ===================================================== k_orient_desc (fused)
+// IC_Angle + GaussianBlur 7x7 + rBRIEF + rescale in one pass, two keypoints
+// per wave (half-wave per keypoint, slot pairing as in k_orient_desc_split).
+// The blurred level is never materialised: descriptors sample only the 37 x 37
+// blurred patch around a keypoint (rotated pattern within +-18 px), and that
+// patch depends only on the 43 x 43 raw window around it, so each keypoint
+// blurs its own window in LDS (src/ORBextractor.cc:1141-1151 blurs the whole
+// level, then samples it; the bytes sampled are identical).
+//   staging: raw rows cy-21 .. cy+21 (lane hl: rows hl, hl + 32), realigned
+//     so byte b of LDS row r is column cx-21+b; rows outside the level are
+//     reflected (REFLECT_101) when addressed, columns outside it patched
+//     bytewise from their reflected columns (keypoints sit >= 19 px inside,
+//     so a window overhangs by at most 2 columns / rows per side).
+//   IC_Angle (:77-113) from the staged rows in registers (rows 6..36).
+//   row pass: task (row pair, 4-column group): u16 row sums of both rows,
+//     packed (row 2p | row 2p+1 << 16) per column: 2.5 v_dot4 per sum.
+//   column pass: task (output row pair, group): four v_dot2 per output over
+//     the packed row pairs, (sum + 2^15) >> 16 saturated -> the blurred patch,
+//     written over the raw rows it no longer needs.
+//   rBRIEF (:119-164): 512 byte reads from the patch, ballots.
+#define DESC_RAW_DW 12   // raw / patch row pitch (dwords)
+#define DESC_RAW_ROWS 44 // 43 staged rows + the odd row of the last row-sum pair
+#define DESC_RS_DW 40    // row-sum pair row pitch (dwords): 10 groups of 4 columns
+#define DESC_RS_PAIRS 22
+struct DescWaveLds {
+  uint32_t raw[2][DESC_RAW_ROWS][DESC_RAW_DW];
+  uint32_t rsp[2][DESC_RS_PAIRS][DESC_RS_DW];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void k_orient_desc(
+    const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
+    const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
+    const uint32_t* __restrict__ outKeys, const int32_t* __restrict__ outCount,
+    const int32_t* __restrict__ errFlag, orb_keypoint_t* __restrict__ kps,
+    uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts) {
+  __shared__ __attribute__((aligned(16))) DescWaveLds sm[4];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int half = lane >> 5, hl = lane & 31;
+  const int img = blockIdx.y;
+  const int slot0 = (blockIdx.x * 4 + w) * 2;
+  const int32_t* cnts = outCount + img * plan.nlevels;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int tot = 0;
+    for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
+    counts[img] = errFlag[img] ? (int32_t)ORB_EDEVICE : tot;  // failed image: negative count
+  }
+  if (slot0 >= plan.slotsPerImage) return;
+  int l = 0;
+  while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot0) ++l;
+  const int i0 = slot0 - plan.lv[l].outOff, nl = cnts[l];
+  if (i0 >= nl) return;
+  const bool active = i0 + half < nl;
+  const int i = i0 + (active ? half : 0);
+  int base = 0;
+  for (int j = 0; j < l; ++j) base += cnts[j];
+  const uint32_t key = outKeys[(long long)img * plan.slotsPerImage + plan.lv[l].outOff + i];
+  const int cx = key_x(key), cy = key_y(key);
+  const OrbLevelDesc& L = plan.lv[l];
+  const uint8_t* lvl;
+  int pitch;
+  if (l == 0) {
+    lvl = img0 + (long long)img * img0Pitch;
+    pitch = img0Stride;
+  } else {
+    lvl = arena + (long long)img * arenaPitch + L.arenaOff;
+    pitch = L.pitch;
+  }
+  uint32_t (*raw)[DESC_RAW_DW] = sm[w].raw[half];
+  uint32_t (*rsp)[DESC_RS_DW] = sm[w].rsp[half];
+  // ---- staging: 12 dwords (3 x 16-byte loads) per row, realigned
+  const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
+  const int colA = cx - 21;
+  const bool second = hl < 43 - 32;  // this lane also stages row hl + 32
+  uint32_t ra[12], rb[12];
+  auto load_row = [&](int r, uint32_t* d) {
+    int y = cy - 21 + r;
+    y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
+    const uint32_t o = (uint32_t)(y * pitch + colA) + im.sh;
+    const uint32_t a0 = o & ~3u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(im.r, (int)(a0 + 16 * k), 0, 0);
+      d[4 * k] = (uint32_t)v[0];
+      d[4 * k + 1] = (uint32_t)v[1];
+      d[4 * k + 2] = (uint32_t)v[2];
+      d[4 * k + 3] = (uint32_t)v[3];
+    }
+    return o & 3u;
+  };
+  const uint32_t sha = load_row(hl, ra);
+  uint32_t shb = 0;
+  if (second) shb = load_row(hl + 32, rb);
+  auto realign = [&](uint32_t* d, uint32_t sh) {
+#pragma unroll
+    for (int k = 0; k < 11; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    d[11] = __builtin_amdgcn_alignbyte(0u, d[11], sh);
+  };
+  auto store_row = [&](int r, const uint32_t* d) {
+    uint4* dst = reinterpret_cast<uint4*>(raw[r]);
+    dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    dst[2] = make_uint4(d[8], d[9], d[10], d[11]);
+  };
+  realign(ra, sha);
+  store_row(hl, ra);
+  if (second) {
+    realign(rb, shb);
+    store_row(hl + 32, rb);
+  }
+  if (colA < 0 || cx + 21 >= L.w) {
+    // window overhangs a level column edge: bytes of columns < 0 or >= w take
+    // their REFLECT_101 column (in range and inside the window); each lane
+    // patches the rows it staged
+    wave_lds_sync();
+    for (int s = 0; s < (second ? 2 : 1); ++s) {
+      uint8_t* rp = reinterpret_cast<uint8_t*>(raw[hl + 32 * s]);
+      for (int b = 0; b < -colA; ++b) rp[b] = rp[-(colA + b) - colA];
+      for (int b = max(L.w - colA, 0); b < 43; ++b) rp[b] = rp[2 * L.w - 2 - (colA + b) - colA];
+    }
+  }
+  // ---- IC_Angle from the rows in registers: row v = ri - 15 is staged row
+  // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
+  // by one byte).  m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
+  int m01 = 0, m10 = 0;
+  {
+    const bool useA = hl >= 6;
+    const int ri = useA ? hl - 6 : hl + 26;
+    if (hl != 5) {
+      uint32_t rs = 0, rm = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t lo = useA ? ra[k + 1] : rb[k + 1], hi = useA ? ra[k + 2] : rb[k + 2];
+        const uint32_t d = __builtin_amdgcn_alignbyte(hi, lo, 1) & c_icmask[ri][k];
+        const uint32_t wt = (uint32_t)(4 * k) * 0x01010101u + 0x03020100u;
+        rs = __builtin_amdgcn_udot4(d, 0x01010101u, rs, false);
+        rm = __builtin_amdgcn_udot4(d, wt, rm, false);
+      }
+      m10 = (int)rm - 16 * (int)rs;
+      m01 = (ri - 15) * (int)rs;
+    }
+  }
+  wave_lds_sync();
+  // ---- row pass: output column c of row-sum row r = sum_i k_i * byte(r, c + i)
+  constexpr uint32_t k0 = 18, k1 = 34, k2 = 49, k3 = 55, k4 = 49, k5 = 34, k6 = 18;
+  constexpr uint32_t T0a = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), T0b = k4 | (k5 << 8) | (k6 << 16);
+  constexpr uint32_t T1a = (k0 << 8) | (k1 << 16) | (k2 << 24), T1b = k3 | (k4 << 8) | (k5 << 16) | (k6 << 24);
+  constexpr uint32_t T2a = (k0 << 16) | (k1 << 24), T2b = k2 | (k3 << 8) | (k4 << 16) | (k5 << 24), T2c = k6;
+  constexpr uint32_t T3a = k0 << 24, T3b = k1 | (k2 << 8) | (k3 << 16) | (k4 << 24), T3c = k5 | (k6 << 8);
+#pragma unroll
+  for (int it = 0; it < (DESC_RS_PAIRS * 10 + 31) / 32; ++it) {
+    const int t = hl + 32 * it;
+    if (t < DESC_RS_PAIRS * 10) {
+      const int p = t / 10, g = t - 10 * p;
+      uint32_t o[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t* rw = raw[2 * p + h] + g;
+        const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
+        o[h][0] = __builtin_amdgcn_udot4(w0, T0a, __builtin_amdgcn_udot4(w1, T0b, 0u, false), false);
+        o[h][1] = __builtin_amdgcn_udot4(w0, T1a, __builtin_amdgcn_udot4(w1, T1b, 0u, false), false);
+        o[h][2] = __builtin_amdgcn_udot4(w0, T2a, __builtin_amdgcn_udot4(w1, T2b,
+                                         __builtin_amdgcn_udot4(w2, T2c, 0u, false), false), false);
+        o[h][3] = __builtin_amdgcn_udot4(w0, T3a, __builtin_amdgcn_udot4(w1, T3b,
+                                         __builtin_amdgcn_udot4(w2, T3c, 0u, false), false), false);
+      }
+      *reinterpret_cast<uint4*>(&rsp[p][4 * g]) =
+          make_uint4(o[0][0] | (o[1][0] << 16), o[0][1] | (o[1][1] << 16),
+                     o[0][2] | (o[1][2] << 16), o[0][3] | (o[1][3] << 16));
+    }
+  }
+  m01 = half_sum(m01);
+  m10 = half_sum(m10);
+  const float angle = fast_atan2_deg((float)m01, (float)m10);
+  wave_lds_sync();
+  // ---- column pass: blurred patch row y (level row cy-18+y) reads row-sum
+  // rows y .. y+6 = pairs y/2 .. y/2+3, weights (k0,k1)(k2,k3)(k4,k5)(k6,0)
+  // for even y, (0,k0)(k1,k2)(k3,k4)(k5,k6) for odd y
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 E0 = {18, 34}, E1 = {49, 55}, E2 = {49, 34}, E3 = {18, 0};
+  const u16x2 O0 = {0, 18}, O1 = {34, 49}, O2 = {55, 49}, O3 = {34, 18};
+#pragma unroll
+  for (int it = 0; it < (19 * 10 + 31) / 32; ++it) {
+    const int t = hl + 32 * it;
+    if (t < 19 * 10) {
+      const int q = t / 10, g = t - 10 * q;
+      uint4 pv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pv[k] = *reinterpret_cast<const uint4*>(&rsp[q + k][4 * g]);
+      uint32_t packedE = 0, packedO = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t se = 1u << 15, so = 1u << 15;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t wv = c == 0 ? pv[k].x : (c == 1 ? pv[k].y : (c == 2 ? pv[k].z : pv[k].w));
+          const u16x2 v = __builtin_bit_cast(u16x2, wv);
+          se = __builtin_amdgcn_udot2(v, k == 0 ? E0 : (k == 1 ? E1 : (k == 2 ? E2 : E3)), se, false);
+          so = __builtin_amdgcn_udot2(v, k == 0 ? O0 : (k == 1 ? O1 : (k == 2 ? O2 : O3)), so, false);
+        }
+        int ve = min((int)(se >> 16), 255), vo = min((int)(so >> 16), 255);
+        __asm__ volatile("" : "+v"(ve), "+v"(vo));  // see k_pyr_resize: keep the byte pack opaque
+        packedE |= (uint32_t)ve << (8 * c);
+        packedO |= (uint32_t)vo << (8 * c);
+      }
+      raw[2 * q][g] = packedE;
+      if (2 * q + 1 < 37) raw[2 * q + 1][g] = packedO;
+    }
+  }
+  const float factorPI = (float)(3.14159265358979323846 / 180.f);
+  float a, b;
+  {
+    float sn, cs;
+    pinned_sincos(angle * factorPI, &sn, &cs);
+    a = cs;
+    b = sn;
+  }
+  wave_lds_sync();
+  // ---- rBRIEF: the patch centre (0, 0) is patch row 18, column 18
+  const uint8_t* pb = reinterpret_cast<const uint8_t*>(&raw[18][0]) + 18;
+  unsigned long long words[8];
+#pragma unroll
+  for (int kq = 0; kq < 8; ++kq) {
+    const int test = hl + 32 * kq;
+    const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
+    const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
+    const int v0 = pb[__mul24(cv_round(px0 * b + py0 * a), DESC_RAW_DW * 4) + cv_round(px0 * a - py0 * b)];
+    const int v1 = pb[__mul24(cv_round(px1 * b + py1 * a), DESC_RAW_DW * 4) + cv_round(px1 * a - py1 * b)];
     words[kq] = __ballot(v0 < v1);
   }
   if (active && hl == 0) {
@@ -1480,18 +1739,30 @@ hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0S
   return hipGetLastError();
 }
 
-hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
-                             const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
-                             long long blurPitch, const OrbPlanDesc* plan,
-                             const uint32_t* outKeys, const int32_t* outCount,
-                             orb_keypoint_t* kps, uint8_t* desc, int capacity, int32_t* counts,
-                             int nimg, hipStream_t s) {
+hipError_t orb_k_orient_desc_split(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                                   const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
+                                   long long blurPitch, const OrbPlanDesc* plan,
+                                   const uint32_t* outKeys, const int32_t* outCount,
+                                   const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
+                                   int capacity, int32_t* counts, int nimg, hipStream_t s) {
   // 4 waves x 2 slots per workgroup; slotsPerImage and every level's outOff are even
   if (plan->slotsPerImage & 1) return hipErrorInvalidValue;
   dim3 grid((plan->slotsPerImage + 7) / 8, nimg), block(256);
+  hipLaunchKernelGGL(k_orient_desc_split, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
+                     arenaPitch, blur, blurPitch, *plan, outKeys, outCount, errFlag, kps, desc,
+                     capacity, counts);
+  return hipGetLastError();
+}
+
+hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                             const uint32_t* outKeys, const int32_t* outCount,
+                             const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
+                             int capacity, int32_t* counts, int nimg, hipStream_t s) {
+  if (plan->slotsPerImage & 1) return hipErrorInvalidValue;
+  dim3 grid((plan->slotsPerImage + 7) / 8, nimg), block(256);
   hipLaunchKernelGGL(k_orient_desc, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, blur, blurPitch, *plan, outKeys, outCount, kps, desc, capacity,
-                     counts);
+                     arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts);
   return hipGetLastError();
 }
 

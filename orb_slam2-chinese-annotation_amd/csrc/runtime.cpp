@@ -41,12 +41,17 @@ hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
                              int nimg, hipStream_t s);
+hipError_t orb_k_orient_desc_split(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                                   const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
+                                   long long blurPitch, const OrbPlanDesc* plan,
+                                   const uint32_t* outKeys, const int32_t* outCount,
+                                   const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
+                                   int capacity, int32_t* counts, int nimg, hipStream_t s);
 hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
-                             const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
-                             long long blurPitch, const OrbPlanDesc* plan,
+                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const uint32_t* outKeys, const int32_t* outCount,
-                             orb_keypoint_t* kps, uint8_t* desc, int capacity, int32_t* counts,
-                             int nimg, hipStream_t s);
+                             const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
+                             int capacity, int32_t* counts, int nimg, hipStream_t s);
 hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out, hipStream_t s);
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
@@ -249,6 +254,7 @@ struct StageProfiler {
       if (hipEventSynchronize(ev[2 * nStages + 1]) != hipSuccess) continue;
       for (int i = 0; i < nStages; ++i) {
         float t = 0.f;
+        if (launchesPerCall[i] == 0) continue;  // stage not run in this configuration
         if (hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]) == hipSuccess) {
           ms[i] += t;
           launches[i] += launchesPerCall[i];
@@ -302,6 +308,7 @@ struct orb_extractor {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // side stream: blur runs beside FAST + octree
   hipEvent_t evFork = nullptr, evJoin = nullptr;
+  hipEvent_t evBatch = nullptr;  // recorded at the end of every run_batch on its stream
   bool ownStream = false;
   std::mutex mu;
 
@@ -594,20 +601,30 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   return ORB_OK;
 }
 
+// ORB_SPLIT_BLUR=1: the round-1 split path (k_blur_levels writes every blurred
+// level, k_orient_desc_split samples them) for A/B runs; default is the fused
+// k_orient_desc, which blurs each keypoint's window in LDS.
+static bool split_blur() {
+  static const bool v = getenv("ORB_SPLIT_BLUR") && atoi(getenv("ORB_SPLIT_BLUR")) > 0;
+  return v;
+}
+
 static orb_status_t ensure_batch(orb_extractor* h, int B) {
   if (B <= h->batchCap) return ORB_OK;
   const OrbPlanDesc& P = h->plan;
   const size_t cellSlots = (size_t)B * P.ncells * P.keyCap;
   orb_status_t st;
   if ((st = h->dArena.ensure((size_t)B * h->arenaBytes))) return st;
-  if ((st = h->dBlur.ensure((size_t)B * h->blurBytes))) return st;
+  // the blurred levels are materialised only in the split A/B mode
+  // (ORB_SPLIT_BLUR=1); orb_extractor_blurred_level blurs one image on demand
+  if (split_blur() && (st = h->dBlur.ensure((size_t)B * h->blurBytes))) return st;
   if ((st = h->dCellKeys.ensure(cellSlots * 4))) return st;
   if ((st = h->dGKeys.ensure(cellSlots * 4))) return st;
   if ((st = h->dGNid.ensure(cellSlots * 2))) return st;
   if ((st = h->dCellCount.ensure((size_t)B * P.ncells * 4))) return st;
   if ((st = h->dOutKeys.ensure((size_t)B * P.slotsPerImage * 4))) return st;
   if ((st = h->dOutCount.ensure((size_t)B * P.nlevels * 4))) return st;
-  if ((st = h->dErr.ensure(16))) return st;
+  if ((st = h->dErr.ensure((size_t)B * 4))) return st;
   h->batchCap = B;
   return ORB_OK;
 }
@@ -615,12 +632,10 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
 static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, size_t stride,
                               size_t imgPitch, orb_keypoint_t* d_kps, uint8_t* d_desc,
                               int capacity, int32_t* d_counts, hipStream_t s) {
-  // Stage DAG: pyramid -> { blur || FAST -> octree } -> orient+desc.  With
-  // ORB_EXTRACT_STREAMS=2 the blur is issued on a side stream after FAST and
-  // runs beside the octree (fork/join by events, graph-capturable).  Measured
-  // at B = 512: no gain (the blur's workgroups hold the CUs and the octree's
-  // 52 KiB-LDS workgroups wait, 0.22 -> 0.78 ms), so by default every stage
-  // runs in order on the caller's stream.
+  // Stage chain: pyramid -> FAST -> octree -> orient + blur + descriptors
+  // (k_orient_desc blurs each keypoint's window in LDS).  Split A/B mode
+  // (ORB_SPLIT_BLUR=1): k_blur_levels writes every blurred level after FAST,
+  // optionally on a side stream (ORB_EXTRACT_STREAMS=2, fork/join by events).
   const OrbPlanDesc& P = h->plan;
   const int32_t* rt = h->dRtab.as<int32_t>();
   uint8_t* arena = h->dArena.as<uint8_t>();
@@ -631,7 +646,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   StageProfiler& pf = h->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
-  HIP_TRY(hipMemsetAsync(h->dErr.p, 0, 16, s));
+  HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
   PROF_REC(ev, pf.b(ev, 0), s);
   for (int l = 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
@@ -649,29 +664,39 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                           h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
                           h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
-  if (s2 != s) {
-    HIP_TRY(hipEventRecord(h->evFork, s));
-    HIP_TRY(hipStreamWaitEvent(s2, h->evFork, 0));
+  const bool split = split_blur();
+  if (split) {
+    if (s2 != s) {
+      HIP_TRY(hipEventRecord(h->evFork, s));
+      HIP_TRY(hipStreamWaitEvent(s2, h->evFork, 0));
+    }
+    PROF_REC(ev, pf.b(ev, 1), s2);
+    HIP_TRY(orb_k_blur_levels(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                              h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, B,
+                              s2));
+    PROF_REC(ev, pf.e(ev, 1), s2);
+    if (s2 != s) HIP_TRY(hipEventRecord(h->evJoin, s2));
   }
-  PROF_REC(ev, pf.b(ev, 1), s2);
-  HIP_TRY(orb_k_blur_levels(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                            h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, B,
-                            s2));
-  PROF_REC(ev, pf.e(ev, 1), s2);
-  if (s2 != s) HIP_TRY(hipEventRecord(h->evJoin, s2));
   PROF_REC(ev, pf.b(ev, 3), s);
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                        h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
                        h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), B, s));
   PROF_REC(ev, pf.e(ev, 3), s);
-  if (s2 != s) HIP_TRY(hipStreamWaitEvent(s, h->evJoin, 0));
+  if (split && s2 != s) HIP_TRY(hipStreamWaitEvent(s, h->evJoin, 0));
   PROF_REC(ev, pf.b(ev, 4), s);
-  HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap,
-                            h->dBlur.as<uint8_t>(), h->blurBytes, &P, h->dOutKeys.as<uint32_t>(),
-                            h->dOutCount.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
+  if (split)
+    HIP_TRY(orb_k_orient_desc_split(d_images, (long long)imgPitch, (int)stride, arena, ap,
+                                    h->dBlur.as<uint8_t>(), h->blurBytes, &P,
+                                    h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
+                                    h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
+  else
+    HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                              h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
+                              h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
   PROF_REC(ev, pf.e(ev, 4), s);
   PROF_REC(ev, pf.t1(ev), s);
+  HIP_TRY(hipEventRecord(h->evBatch, s));  // readbacks on the handle stream wait for it
   h->lastImg0 = d_images;
   h->lastImg0Pitch = imgPitch;
   h->lastImg0Stride = (int)stride;
@@ -726,11 +751,13 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->evBatch, hipEventDisableTiming) != hipSuccess) {
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->stream2) hipStreamDestroy(h->stream2);
     if (h->evFork) hipEventDestroy(h->evFork);
     if (h->evJoin) hipEventDestroy(h->evJoin);
+    if (h->evBatch) hipEventDestroy(h->evBatch);
     delete h;
     return ORB_EDEVICE;
   }
@@ -743,6 +770,7 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
     h->prof.launchesPerCall[i] = 1;
   }
   h->prof.launchesPerCall[0] = std::max(nlevels - 1, 0);
+  h->prof.launchesPerCall[1] = split_blur() ? 1 : 0;  // k_blur_levels: split A/B mode only
   if (orb_k_upload_constants(h->stream) != hipSuccess ||
       orb_k_upload_umax(h->umax, h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -768,6 +796,7 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   if (h->stream2) hipStreamDestroy(h->stream2);
   if (h->evFork) hipEventDestroy(h->evFork);
   if (h->evJoin) hipEventDestroy(h->evJoin);
+  if (h->evBatch) hipEventDestroy(h->evBatch);
   delete h;
 }
 
@@ -861,7 +890,7 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   memcpy(&err, ho + 4, 4);
   h->lastW = width;
   h->lastH = height;
-  if (err) {
+  if (n < 0) {  // the octree hit an internal limit (errFlag bits: 2 node cap, 4 passes, 8 sort key)
     if (getenv("ORB_AMD_DEBUG")) fprintf(stderr, "[orb_amd] kernel error flag %d\n", err);
     return ORB_EDEVICE;
   }
@@ -925,7 +954,7 @@ orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t*
   if (!dst) return ORB_OK;
   if (dst_stride < (size_t)w) return ORB_EINVAL;
   hipSetDevice(h->device);
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));  // the batch may have run on a caller stream
   return copy_level_to_host(h, dst, dst_stride, src, sstride, w, hh);
 }
 
@@ -940,7 +969,19 @@ orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t*
   if (!dst) return ORB_OK;
   if (dst_stride < (size_t)L.w) return ORB_EINVAL;
   hipSetDevice(h->device);
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  // The extraction never materialises blurred levels (k_orient_desc blurs
+  // each keypoint's window in LDS; in the split A/B mode they are in dBlur
+  // already): blur image 0 of the last call on demand with k_blur_levels.
+  HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));
+  if (!split_blur()) {
+    if (!h->lastImg0) return ORB_EINVAL;
+    orb_status_t st = h->dBlur.ensure((size_t)h->blurBytes);
+    if (st) return st;
+    HIP_TRY(orb_k_blur_levels(h->lastImg0, (long long)h->lastImg0Pitch, h->lastImg0Stride,
+                              h->dArena.as<uint8_t>(), h->arenaBytes, &h->plan,
+                              h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, 1,
+                              h->stream));
+  }
   return copy_level_to_host(h, dst, dst_stride, h->dBlur.as<uint8_t>() + L.blurOff, L.blurPitch,
                             L.w, L.h);
 }
