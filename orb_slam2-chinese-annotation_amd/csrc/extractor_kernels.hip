@@ -1395,6 +1395,8 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#define DESC_PPW 4  // slot pairs per wave (software-pipelined: the next pair's window loads overlap this one)
+
 __global__ __launch_bounds__(256) void k_orient_desc(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
@@ -1405,59 +1407,85 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31;
   const int img = blockIdx.y;
-  const int slot0 = (blockIdx.x * 4 + w) * 2;
   const int32_t* cnts = outCount + img * plan.nlevels;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
     counts[img] = errFlag[img] ? (int32_t)ORB_EDEVICE : tot;  // failed image: negative count
   }
-  if (slot0 >= plan.slotsPerImage) return;
-  int l = 0;
-  while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot0) ++l;
-  const int i0 = slot0 - plan.lv[l].outOff, nl = cnts[l];
-  if (i0 >= nl) return;
-  const bool active = i0 + half < nl;
-  const int i = i0 + (active ? half : 0);
-  int base = 0;
-  for (int j = 0; j < l; ++j) base += cnts[j];
-  const uint32_t key = outKeys[(long long)img * plan.slotsPerImage + plan.lv[l].outOff + i];
-  const int cx = key_x(key), cy = key_y(key);
-  const OrbLevelDesc& L = plan.lv[l];
-  const uint8_t* lvl;
-  int pitch;
-  if (l == 0) {
-    lvl = img0 + (long long)img * img0Pitch;
-    pitch = img0Stride;
-  } else {
-    lvl = arena + (long long)img * arenaPitch + L.arenaOff;
-    pitch = L.pitch;
+  // this wave's slot pairs: pairBase + 4 j, j < DESC_PPW (the workgroup's four
+  // waves interleave); lane 2 j + h holds the packed key of slot 2 (pairBase + 4 j) + h
+  const int pairBase = blockIdx.x * 4 * DESC_PPW + w;
+  if (2 * pairBase >= plan.slotsPerImage) return;
+  const uint32_t* imgKeys = outKeys + (long long)img * plan.slotsPerImage;
+  uint32_t keyv = 0;
+  if (lane < 2 * DESC_PPW) {
+    const int slot = 2 * (pairBase + 4 * (lane >> 1)) + (lane & 1);
+    if (slot < plan.slotsPerImage) keyv = imgKeys[slot];
   }
   uint32_t (*raw)[DESC_RAW_DW] = sm[w].raw[half];
   uint32_t (*rsp)[DESC_RS_DW] = sm[w].rsp[half];
-  // ---- staging: 12 dwords (3 x 16-byte loads) per row, realigned
-  const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
-  const int colA = cx - 21;
   const bool second = hl < 43 - 32;  // this lane also stages row hl + 32
-  uint32_t ra[12], rb[12];
-  auto load_row = [&](int r, uint32_t* d) {
-    int y = cy - 21 + r;
-    y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
-    const uint32_t o = (uint32_t)(y * pitch + colA) + im.sh;
-    const uint32_t a0 = o & ~3u;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(im.r, (int)(a0 + 16 * k), 0, 0);
-      d[4 * k] = (uint32_t)v[0];
-      d[4 * k + 1] = (uint32_t)v[1];
-      d[4 * k + 2] = (uint32_t)v[2];
-      d[4 * k + 3] = (uint32_t)v[3];
-    }
-    return o & 3u;
+  // A pair is valid when its first slot holds a keypoint of its level; the
+  // second half-wave duplicates the first when the level's count is odd.
+  struct Pair {
+    bool valid, active;
+    int l, i, cx, cy;
+    uint32_t key;
   };
-  const uint32_t sha = load_row(hl, ra);
-  uint32_t shb = 0;
-  if (second) shb = load_row(hl + 32, rb);
+  auto setup = [&](int j) {
+    Pair P;
+    P.valid = false;
+    const int slot0 = 2 * (pairBase + 4 * j);
+    if (slot0 >= plan.slotsPerImage) return P;
+    int l = 0;
+    while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot0) ++l;
+    const int i0 = slot0 - plan.lv[l].outOff, nl = cnts[l];
+    if (i0 >= nl) return P;
+    P.valid = true;
+    P.l = l;
+    P.active = i0 + half < nl;
+    P.i = i0 + (P.active ? half : 0);
+    const uint32_t k0 = __builtin_amdgcn_readlane(keyv, 2 * j);
+    const uint32_t k1 = __builtin_amdgcn_readlane(keyv, 2 * j + 1);
+    P.key = (half && P.active) ? k1 : k0;
+    P.cx = key_x(P.key);
+    P.cy = key_y(P.key);
+    return P;
+  };
+  // ---- staging: raw rows cy-21+r (REFLECT_101 rows), 12 dwords (3 x 16-byte
+  // loads) from the 4-aligned byte at or below column cx-21
+  uint32_t ra[12], rb[12], sha = 0, shb = 0;
+  auto issue = [&](const Pair& P) {
+    const OrbLevelDesc& L = plan.lv[P.l];
+    const uint8_t* lvl;
+    int pitch;
+    if (P.l == 0) {
+      lvl = img0 + (long long)img * img0Pitch;
+      pitch = img0Stride;
+    } else {
+      lvl = arena + (long long)img * arenaPitch + L.arenaOff;
+      pitch = L.pitch;
+    }
+    const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
+    auto load_row = [&](int r, uint32_t* d) {
+      int y = P.cy - 21 + r;
+      y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
+      const uint32_t o = (uint32_t)(y * pitch + P.cx - 21) + im.sh;
+      const uint32_t a0 = o & ~3u;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(im.r, (int)(a0 + 16 * k), 0, 0);
+        d[4 * k] = (uint32_t)v[0];
+        d[4 * k + 1] = (uint32_t)v[1];
+        d[4 * k + 2] = (uint32_t)v[2];
+        d[4 * k + 3] = (uint32_t)v[3];
+      }
+      return o & 3u;
+    };
+    sha = load_row(hl, ra);
+    if (second) shb = load_row(hl + 32, rb);
+  };
   auto realign = [&](uint32_t* d, uint32_t sh) {
 #pragma unroll
     for (int k = 0; k < 11; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
@@ -1469,31 +1497,34 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
     dst[2] = make_uint4(d[8], d[9], d[10], d[11]);
   };
-  realign(ra, sha);
-  store_row(hl, ra);
-  if (second) {
-    realign(rb, shb);
-    store_row(hl + 32, rb);
-  }
-  if (colA < 0 || cx + 21 >= L.w) {
-    // window overhangs a level column edge: bytes of columns < 0 or >= w take
-    // their REFLECT_101 column (in range and inside the window); each lane
-    // patches the rows it staged
-    wave_lds_sync();
-    for (int s = 0; s < (second ? 2 : 1); ++s) {
-      uint8_t* rp = reinterpret_cast<uint8_t*>(raw[hl + 32 * s]);
-      for (int b = 0; b < -colA; ++b) rp[b] = rp[-(colA + b) - colA];
-      for (int b = max(L.w - colA, 0); b < 43; ++b) rp[b] = rp[2 * L.w - 2 - (colA + b) - colA];
+  constexpr uint32_t k0 = 18, k1 = 34, k2 = 49, k3 = 55, k4 = 49, k5 = 34, k6 = 18;
+  constexpr uint32_t T0a = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), T0b = k4 | (k5 << 8) | (k6 << 16);
+  constexpr uint32_t T1a = (k0 << 8) | (k1 << 16) | (k2 << 24), T1b = k3 | (k4 << 8) | (k5 << 16) | (k6 << 24);
+  constexpr uint32_t T2a = (k0 << 16) | (k1 << 24), T2b = k2 | (k3 << 8) | (k4 << 16) | (k5 << 24), T2c = k6;
+  constexpr uint32_t T3a = k0 << 24, T3b = k1 | (k2 << 8) | (k3 << 16) | (k4 << 24), T3c = k5 | (k6 << 8);
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 E0 = {18, 34}, E1 = {49, 55}, E2 = {49, 34}, E3 = {18, 0};
+  const u16x2 O0 = {0, 18}, O1 = {34, 49}, O2 = {55, 49}, O3 = {34, 18};
+
+  Pair cur = setup(0);
+  if (cur.valid) issue(cur);
+  for (int j = 0; j < DESC_PPW; ++j) {
+    const Pair P = cur;
+    if (P.valid) {
+      realign(ra, sha);
+      store_row(hl, ra);
+      if (second) {
+        realign(rb, shb);
+        store_row(hl + 32, rb);
+      }
     }
-  }
-  // ---- IC_Angle from the rows in registers: row v = ri - 15 is staged row
-  // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
-  // by one byte).  m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
-  int m01 = 0, m10 = 0;
-  {
-    const bool useA = hl >= 6;
-    const int ri = useA ? hl - 6 : hl + 26;
-    if (hl != 5) {
+    // ---- IC_Angle from the rows in registers: row v = ri - 15 is staged row
+    // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
+    // by one byte).  m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
+    int m01 = 0, m10 = 0;
+    if (P.valid && hl != 5) {
+      const bool useA = hl >= 6;
+      const int ri = useA ? hl - 6 : hl + 26;
       uint32_t rs = 0, rm = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -1506,112 +1537,127 @@ __global__ __launch_bounds__(256) void k_orient_desc(
       m10 = (int)rm - 16 * (int)rs;
       m01 = (ri - 15) * (int)rs;
     }
-  }
-  wave_lds_sync();
-  // ---- row pass: output column c of row-sum row r = sum_i k_i * byte(r, c + i)
-  constexpr uint32_t k0 = 18, k1 = 34, k2 = 49, k3 = 55, k4 = 49, k5 = 34, k6 = 18;
-  constexpr uint32_t T0a = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), T0b = k4 | (k5 << 8) | (k6 << 16);
-  constexpr uint32_t T1a = (k0 << 8) | (k1 << 16) | (k2 << 24), T1b = k3 | (k4 << 8) | (k5 << 16) | (k6 << 24);
-  constexpr uint32_t T2a = (k0 << 16) | (k1 << 24), T2b = k2 | (k3 << 8) | (k4 << 16) | (k5 << 24), T2c = k6;
-  constexpr uint32_t T3a = k0 << 24, T3b = k1 | (k2 << 8) | (k3 << 16) | (k4 << 24), T3c = k5 | (k6 << 8);
-#pragma unroll
-  for (int it = 0; it < (DESC_RS_PAIRS * 10 + 31) / 32; ++it) {
-    const int t = hl + 32 * it;
-    if (t < DESC_RS_PAIRS * 10) {
-      const int p = t / 10, g = t - 10 * p;
-      uint32_t o[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t* rw = raw[2 * p + h] + g;
-        const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
-        o[h][0] = __builtin_amdgcn_udot4(w0, T0a, __builtin_amdgcn_udot4(w1, T0b, 0u, false), false);
-        o[h][1] = __builtin_amdgcn_udot4(w0, T1a, __builtin_amdgcn_udot4(w1, T1b, 0u, false), false);
-        o[h][2] = __builtin_amdgcn_udot4(w0, T2a, __builtin_amdgcn_udot4(w1, T2b,
-                                         __builtin_amdgcn_udot4(w2, T2c, 0u, false), false), false);
-        o[h][3] = __builtin_amdgcn_udot4(w0, T3a, __builtin_amdgcn_udot4(w1, T3b,
-                                         __builtin_amdgcn_udot4(w2, T3c, 0u, false), false), false);
-      }
-      *reinterpret_cast<uint4*>(&rsp[p][4 * g]) =
-          make_uint4(o[0][0] | (o[1][0] << 16), o[0][1] | (o[1][1] << 16),
-                     o[0][2] | (o[1][2] << 16), o[0][3] | (o[1][3] << 16));
+    // the next pair's window loads go out now and land during this pair's work
+    if (j + 1 < DESC_PPW) {
+      cur = setup(j + 1);
+      if (cur.valid) issue(cur);
     }
-  }
-  m01 = half_sum(m01);
-  m10 = half_sum(m10);
-  const float angle = fast_atan2_deg((float)m01, (float)m10);
-  wave_lds_sync();
-  // ---- column pass: blurred patch row y (level row cy-18+y) reads row-sum
-  // rows y .. y+6 = pairs y/2 .. y/2+3, weights (k0,k1)(k2,k3)(k4,k5)(k6,0)
-  // for even y, (0,k0)(k1,k2)(k3,k4)(k5,k6) for odd y
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  const u16x2 E0 = {18, 34}, E1 = {49, 55}, E2 = {49, 34}, E3 = {18, 0};
-  const u16x2 O0 = {0, 18}, O1 = {34, 49}, O2 = {55, 49}, O3 = {34, 18};
+    if (!P.valid) continue;  // wave-uniform
+    const OrbLevelDesc& L = plan.lv[P.l];
+    const int cx = P.cx, cy = P.cy, colA = cx - 21;
+    if (colA < 0 || cx + 21 >= L.w) {
+      // window overhangs a level column edge: bytes of columns < 0 or >= w take
+      // their REFLECT_101 column (in range and inside the window); each lane
+      // patches the rows it staged
+      wave_lds_sync();
+      for (int s = 0; s < (second ? 2 : 1); ++s) {
+        uint8_t* rp = reinterpret_cast<uint8_t*>(raw[hl + 32 * s]);
+        for (int b = 0; b < -colA; ++b) rp[b] = rp[-(colA + b) - colA];
+        for (int b = max(L.w - colA, 0); b < 43; ++b) rp[b] = rp[2 * L.w - 2 - (colA + b) - colA];
+      }
+    }
+    wave_lds_sync();
+    // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
 #pragma unroll
-  for (int it = 0; it < (19 * 10 + 31) / 32; ++it) {
-    const int t = hl + 32 * it;
-    if (t < 19 * 10) {
-      const int q = t / 10, g = t - 10 * q;
-      uint4 pv[4];
+    for (int it = 0; it < (DESC_RS_PAIRS * 10 + 31) / 32; ++it) {
+      const int t = hl + 32 * it;
+      if (t < DESC_RS_PAIRS * 10) {
+        const int p = t / 10, g = t - 10 * p;
+        uint32_t o[2][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pv[k] = *reinterpret_cast<const uint4*>(&rsp[q + k][4 * g]);
-      uint32_t packedE = 0, packedO = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint32_t se = 1u << 15, so = 1u << 15;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t wv = c == 0 ? pv[k].x : (c == 1 ? pv[k].y : (c == 2 ? pv[k].z : pv[k].w));
-          const u16x2 v = __builtin_bit_cast(u16x2, wv);
-          se = __builtin_amdgcn_udot2(v, k == 0 ? E0 : (k == 1 ? E1 : (k == 2 ? E2 : E3)), se, false);
-          so = __builtin_amdgcn_udot2(v, k == 0 ? O0 : (k == 1 ? O1 : (k == 2 ? O2 : O3)), so, false);
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t* rw = raw[2 * p + h] + g;
+          const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
+          o[h][0] = __builtin_amdgcn_udot4(w0, T0a, __builtin_amdgcn_udot4(w1, T0b, 0u, false), false);
+          o[h][1] = __builtin_amdgcn_udot4(w0, T1a, __builtin_amdgcn_udot4(w1, T1b, 0u, false), false);
+          o[h][2] = __builtin_amdgcn_udot4(w0, T2a, __builtin_amdgcn_udot4(w1, T2b,
+                                           __builtin_amdgcn_udot4(w2, T2c, 0u, false), false), false);
+          o[h][3] = __builtin_amdgcn_udot4(w0, T3a, __builtin_amdgcn_udot4(w1, T3b,
+                                           __builtin_amdgcn_udot4(w2, T3c, 0u, false), false), false);
         }
-        int ve = min((int)(se >> 16), 255), vo = min((int)(so >> 16), 255);
-        __asm__ volatile("" : "+v"(ve), "+v"(vo));  // see k_pyr_resize: keep the byte pack opaque
-        packedE |= (uint32_t)ve << (8 * c);
-        packedO |= (uint32_t)vo << (8 * c);
+        *reinterpret_cast<uint4*>(&rsp[p][4 * g]) =
+            make_uint4(o[0][0] | (o[1][0] << 16), o[0][1] | (o[1][1] << 16),
+                       o[0][2] | (o[1][2] << 16), o[0][3] | (o[1][3] << 16));
       }
-      raw[2 * q][g] = packedE;
-      if (2 * q + 1 < 37) raw[2 * q + 1][g] = packedO;
     }
-  }
-  const float factorPI = (float)(3.14159265358979323846 / 180.f);
-  float a, b;
-  {
-    float sn, cs;
-    pinned_sincos(angle * factorPI, &sn, &cs);
-    a = cs;
-    b = sn;
-  }
-  wave_lds_sync();
-  // ---- rBRIEF: the patch centre (0, 0) is patch row 18, column 18
-  const uint8_t* pb = reinterpret_cast<const uint8_t*>(&raw[18][0]) + 18;
-  unsigned long long words[8];
+    m01 = half_sum(m01);
+    m10 = half_sum(m10);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    wave_lds_sync();
+    // ---- column pass: blurred patch row y (level row cy-18+y) reads row-sum
+    // rows y .. y+6 = pairs y/2 .. y/2+3, weights (k0,k1)(k2,k3)(k4,k5)(k6,0)
+    // for even y, (0,k0)(k1,k2)(k3,k4)(k5,k6) for odd y
 #pragma unroll
-  for (int kq = 0; kq < 8; ++kq) {
-    const int test = hl + 32 * kq;
-    const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
-    const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
-    const int v0 = pb[__mul24(cv_round(px0 * b + py0 * a), DESC_RAW_DW * 4) + cv_round(px0 * a - py0 * b)];
-    const int v1 = pb[__mul24(cv_round(px1 * b + py1 * a), DESC_RAW_DW * 4) + cv_round(px1 * a - py1 * b)];
-    words[kq] = __ballot(v0 < v1);
-  }
-  if (active && hl == 0) {
-    const long long o = (long long)img * capacity + base + i;
-    uint32_t d[8];
+    for (int it = 0; it < (19 * 10 + 31) / 32; ++it) {
+      const int t = hl + 32 * it;
+      if (t < 19 * 10) {
+        const int q = t / 10, g = t - 10 * q;
+        uint4 pv[4];
 #pragma unroll
-    for (int kq = 0; kq < 8; ++kq) d[kq] = (uint32_t)(words[kq] >> (32 * half));
-    uint4* dst = reinterpret_cast<uint4*>(desc + o * 32);
-    dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
-    dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
-    orb_keypoint_t kp;
-    kp.x = l ? (float)cx * L.scale : (float)cx;  // pt *= mvScaleFactor[level] (:1157-1165)
-    kp.y = l ? (float)cy * L.scale : (float)cy;
-    kp.size = L.sizeF;
-    kp.angle = angle;
-    kp.response = (float)key_s(key);
-    kp.octave = l;
-    kp.class_id = -1;
-    kps[o] = kp;
+        for (int k = 0; k < 4; ++k) pv[k] = *reinterpret_cast<const uint4*>(&rsp[q + k][4 * g]);
+        uint32_t packedE = 0, packedO = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          uint32_t se = 1u << 15, so = 1u << 15;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t wv = c == 0 ? pv[k].x : (c == 1 ? pv[k].y : (c == 2 ? pv[k].z : pv[k].w));
+            const u16x2 v = __builtin_bit_cast(u16x2, wv);
+            se = __builtin_amdgcn_udot2(v, k == 0 ? E0 : (k == 1 ? E1 : (k == 2 ? E2 : E3)), se, false);
+            so = __builtin_amdgcn_udot2(v, k == 0 ? O0 : (k == 1 ? O1 : (k == 2 ? O2 : O3)), so, false);
+          }
+          int ve = min((int)(se >> 16), 255), vo = min((int)(so >> 16), 255);
+          __asm__ volatile("" : "+v"(ve), "+v"(vo));  // see k_pyr_resize: keep the byte pack opaque
+          packedE |= (uint32_t)ve << (8 * c);
+          packedO |= (uint32_t)vo << (8 * c);
+        }
+        raw[2 * q][g] = packedE;
+        if (2 * q + 1 < 37) raw[2 * q + 1][g] = packedO;
+      }
+    }
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    float a, b;
+    {
+      float sn, cs;
+      pinned_sincos(angle * factorPI, &sn, &cs);
+      a = cs;
+      b = sn;
+    }
+    wave_lds_sync();
+    // ---- rBRIEF: the patch centre (0, 0) is patch row 18, column 18
+    const uint8_t* pb = reinterpret_cast<const uint8_t*>(&raw[18][0]) + 18;
+    unsigned long long words[8];
+#pragma unroll
+    for (int kq = 0; kq < 8; ++kq) {
+      const int test = hl + 32 * kq;
+      const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
+      const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
+      const int v0 = pb[__mul24(cv_round(px0 * b + py0 * a), DESC_RAW_DW * 4) + cv_round(px0 * a - py0 * b)];
+      const int v1 = pb[__mul24(cv_round(px1 * b + py1 * a), DESC_RAW_DW * 4) + cv_round(px1 * a - py1 * b)];
+      words[kq] = __ballot(v0 < v1);
+    }
+    if (P.active && hl == 0) {
+      int base = 0;
+      for (int jl = 0; jl < P.l; ++jl) base += cnts[jl];
+      const long long o = (long long)img * capacity + base + P.i;
+      uint32_t d[8];
+#pragma unroll
+      for (int kq = 0; kq < 8; ++kq) d[kq] = (uint32_t)(words[kq] >> (32 * half));
+      uint4* dst = reinterpret_cast<uint4*>(desc + o * 32);
+      dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
+      dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
+      orb_keypoint_t kp;
+      kp.x = P.l ? (float)cx * L.scale : (float)cx;  // pt *= mvScaleFactor[level] (:1157-1165)
+      kp.y = P.l ? (float)cy * L.scale : (float)cy;
+      kp.size = L.sizeF;
+      kp.angle = angle;
+      kp.response = (float)key_s(P.key);
+      kp.octave = P.l;
+      kp.class_id = -1;
+      kps[o] = kp;
+    }
+    // the next pair's staging overwrites raw: every lane's patch reads are done
+    wave_lds_sync();
   }
 }
 
@@ -1760,7 +1806,7 @@ hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0S
                              const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
                              int capacity, int32_t* counts, int nimg, hipStream_t s) {
   if (plan->slotsPerImage & 1) return hipErrorInvalidValue;
-  dim3 grid((plan->slotsPerImage + 7) / 8, nimg), block(256);
+  dim3 grid((plan->slotsPerImage + 8 * DESC_PPW - 1) / (8 * DESC_PPW), nimg), block(256);
   hipLaunchKernelGGL(k_orient_desc, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts);
   return hipGetLastError();
