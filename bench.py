@@ -1,15 +1,16 @@
 #!/usr/bin/env python3
 """bench.py -- frames/s of ORB extract + match (BASELINE.json metric) on N MI355X GPUs.
 
-One step = one batch of B synthetic KITTI-shaped 1241x376 frames per GPU through
-the whole hot path, resident in HBM: ORBextractor (1000 features, 8 levels,
-FAST 20/7) + SearchByProjection(F, local map) against a 5,000-point synthetic
-local map per frame (the headline workload).  Frames shard
-one batch per rank (weak scaling); the only collective is an RCCL all-gather of
-the per-frame keypoint counts each step and of the per-rank times at the end.
-Steps are pipelined over two HIP streams and two buffer sets: step k's matcher
-overlaps step k+1's extraction (every step still does all of its work; the
-timed region ends with a device synchronize).
+Each GPU holds a resident sequence of D distinct synthetic KITTI-shaped
+1241x376 frames (default 8192) in HBM; one step = one pass of the whole hot
+path over all D frames, in launches of B = 512: ORBextractor (1000 features,
+8 levels, FAST 20/7) + SearchByProjection(F, local map) against each frame's
+own 5,000-point synthetic local map (the headline
+workload).  Frames shard per rank (weak scaling); the only collective is an
+RCCL all-gather of the per-frame keypoint counts per launch and of the per-rank
+times at the end.  Launches are pipelined over two HIP streams and two buffer
+sets: launch g's matcher overlaps launch g+1's extraction (every launch does
+all of its work; the timed region ends with a device synchronize).
 
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant
 kernel, HIP-event timed over the timed region) and `cpu_baseline` (the C++ CPU
@@ -71,10 +72,10 @@ def algorithmic_bytes(w, h, scale, nlevels, n_kp, n_mp):
             "frame_total_survey": (2 * sum(P) - P[0]) + 60 * n_kp + match}
 
 
-def shard_frames(rank, batch):
+def shard_frames(rank, frames):
     """Frame ids this rank processes in each step: a contiguous block of the
     synthetic sequence per rank (weak scaling, no data-path collective)."""
-    return [rank * batch + i for i in range(batch)]
+    return [rank * frames + i for i in range(frames)]
 
 
 def gather_counts(dist, counts, out):
@@ -131,34 +132,185 @@ def valu_issue(kernel, batch, ms_per_launch):
                       "(profiles/r01_valu_rates.txt)"}
 
 
+def parallel_map(fn, items, threads):
+    """fn over items on host threads (the library's ctypes calls release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        return list(ex.map(fn, items))
+
+
+def synth_images(orb, seed, frame_ids, W, H, threads, view=0):
+    """(len(frame_ids), H, W) synthetic frames, rendered straight into one array."""
+    imgs = np.empty((len(frame_ids), H, W), np.uint8)
+    lib = orb.lib()
+
+    def one(i):
+        lib.orb_synth_image(seed, frame_ids[i], view, W, H, imgs[i].ctypes.data, W)
+
+    parallel_map(one, range(len(frame_ids)), threads)
+    return imgs
+
+
+def host_cpu():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
 def cpu_baseline(imgs_host, maps, args, scale):
+    """The CPU oracle (same C++ restatement the parity tests use; the reference
+    itself cannot be built here) on a bounded sample of the same workload: one
+    thread pinned to one core, each frame timed alone (extract + match), the
+    median frame time reported as frames/s (SURVEY §8(d) method)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # CPU oracle: checker / baseline only
 
+    aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    core = min(aff) if aff else None
+    if core is not None:
+        os.sched_setaffinity(0, {core})
+    try:
+        times = []
+        t_start = time.perf_counter()
+        n = 0
+        while True:
+            i = n % len(imgs_host)
+            t0 = time.perf_counter()
+            k, d, _ = oracle.extract(imgs_host[i], args.features, 1.2, 8, 20, 7)
+            mps, mpd, locked = maps[i]
+            oracle.match_projection_local(k, d, scale, args.width, args.height, mps, mpd, 1.0, 0.8,
+                                          locked[: len(k)])
+            t1 = time.perf_counter()
+            n += 1
+            if n > 3:  # 3 warm-up frames
+                times.append(t1 - t0)
+            el = t1 - t_start
+            if (el >= args.cpu_seconds and len(times) >= 20) or len(times) >= args.cpu_max_frames:
+                break
+    finally:
+        if aff is not None:
+            os.sched_setaffinity(0, aff)
+    med = float(np.median(times))
+    model, ncpu = host_cpu()
+    return {"value": 1.0 / med, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{len(times)} timed frames (after 3 warm-up) of the same {args.width}x"
+                      f"{args.height} stream: oracle ORBextractor ({args.features} feat) + "
+                      f"SearchByProjection vs {args.mappoints} map points, C++ -O3 "
+                      f"-march=x86-64-v3 -ffp-contract=off, scalar, 1 thread pinned to core "
+                      f"{core}; median {med * 1e3:.2f} ms/frame (mean "
+                      f"{np.mean(times) * 1e3:.2f}), {el:.1f} s",
+            "host_cpu": model, "host_nproc": ncpu}
+
+
+def secondary_configs(orb, torch, args, dev, threads):
+    """C3 (stereo pairs/s) and C5 (problems/s at M = 50k), GPU rates only (their
+    parity is tests/test_gpu_matchers_more.py and tests/test_gpu_matcher.py)."""
+    out = {}
+    s = torch.cuda.current_stream(dev).cuda_stream
+    # ---- C3: 1241x376 pairs, 2000 feat/img, extraction x2 + ComputeStereoMatches
+    W, H, P, NF = 1241, 376, 256, 2000
+    bf, fx = 386.1448, 718.856
+    L = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
+    R = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
+    cap = L.capacity(W, H)
+    ids = list(range(P))  # frame ids: the ego-motion offset walks over every earlier frame
+    dl = torch.from_numpy(synth_images(orb, args.seed ^ 3, ids, W, H, threads, 0)).to(dev)
+    dr = torch.from_numpy(synth_images(orb, args.seed ^ 3, ids, W, H, threads, 1)).to(dev)
+    z = lambda *sh, dt=torch.int32: torch.zeros(sh, dtype=dt, device=dev)
+    kl, dsl, nl = z(P, cap, 7), z(P, cap, 32, dt=torch.uint8), z(P)
+    kr, dsr, nr = z(P, cap, 7), z(P, cap, 32, dt=torch.uint8), z(P)
+    ur, dp, sad = z(P, cap, dt=torch.float32), z(P, cap, dt=torch.float32), z(P, cap)
+    m = orb.ORBmatcher(device=dev.index)
+
+    def c3():
+        L.extract_batch(dl.data_ptr(), P, W, H, W, W * H, kl.data_ptr(), dsl.data_ptr(), cap,
+                        nl.data_ptr(), s)
+        R.extract_batch(dr.data_ptr(), P, W, H, W, W * H, kr.data_ptr(), dsr.data_ptr(), cap,
+                        nr.data_ptr(), s)
+        m.stereo_match_batch(P, L, R, kl.data_ptr(), dsl.data_ptr(), nl.data_ptr(), kr.data_ptr(),
+                             dsr.data_ptr(), nr.data_ptr(), cap, bf, fx, ur.data_ptr(),
+                             dp.data_ptr(), sad.data_ptr(), s)
+
+    sec = timed_loop(c3, 20, 3, torch)
+    if int(torch.minimum(nl, nr).min().item()) < 0:
+        raise RuntimeError("C3: an extraction reported failure (negative count)")
+    out["C3_stereo_pairs_per_s"] = {"value": P / sec, "unit": "pairs/s", "pairs_per_step": P,
+                                    "ms_per_step": sec * 1e3,
+                                    "workload": "1241x376 stereo pairs, 2000 feat/img, "
+                                                "extraction x2 + ComputeStereoMatches"}
+    del dl, dr, kl, dsl, kr, dsr, ur, dp, sad
+    # ---- C5: 1920x1080, 4000 feat + SearchByProjection vs 50,000 map points, th 1, nnratio 0.8
+    W, H, NF, M, B = 1920, 1080, 4000, 50000, 16
+    ext = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
+    scale = np.float32(ext.GetScaleFactors())
+    cap = ext.capacity(W, H)
+    d = torch.from_numpy(synth_images(orb, 5, list(range(B)), W, H, threads)).to(dev)
+    k, de, n = z(B, cap, 7), z(B, cap, 32, dt=torch.uint8), z(B)
+    ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
+                      n.data_ptr(), s)
+    torch.cuda.synchronize()
+    kh = k.cpu().numpy().view(orb.KEYPOINT_DTYPE).reshape(B, cap)
+    dh, nh = de.cpu().numpy(), n.cpu().numpy()
+    maps = parallel_map(lambda i: orb.synth_local_map(5 + i, kh[i, :nh[i]], dh[i, :nh[i]], M, W, H),
+                        range(B), threads)
+    mps = np.stack([mm[0] for mm in maps])
+    mpd = np.stack([mm[1] for mm in maps])
+    lk = np.zeros((B, cap), np.uint8)
+    for i in range(B):
+        lk[i, :nh[i]] = maps[i][2]
+    d_mps = torch.from_numpy(mps.view(np.uint8).reshape(B, -1)).to(dev)
+    d_mpd = torch.from_numpy(mpd).to(dev)
+    d_lk = torch.from_numpy(lk).to(dev)
+    d_nm = torch.full((B,), M, dtype=torch.int32, device=dev)
+    d_km, d_nmatch = z(B, cap), z(B)
+    mt = orb.ORBmatcher(0.8, device=dev.index)
+
+    def c5():
+        ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
+                          n.data_ptr(), s)
+        mt.search_by_projection_batch(B, k.data_ptr(), de.data_ptr(), n.data_ptr(), d_lk.data_ptr(),
+                                      cap, d_mps.data_ptr(), d_mpd.data_ptr(), d_nm.data_ptr(), M,
+                                      W, H, scale, 1.0, d_km.data_ptr(), d_nmatch.data_ptr(), s)
+
+    sec = timed_loop(c5, 20, 3, torch)
+    if int(n.min().item()) < 0:
+        raise RuntimeError("C5: an extraction reported failure (negative count)")
+    out["C5_problems_per_s"] = {"value": B / sec, "unit": "problems/s", "problems_per_step": B,
+                                "ms_per_step": sec * 1e3,
+                                "mean_keypoints": float(n.float().mean().item()),
+                                "mean_matches": float(d_nmatch.float().mean().item()),
+                                "workload": "1920x1080, 4000 feat, extraction + "
+                                            "SearchByProjection vs 50,000 map points"}
+    return out
+
+
+def timed_loop(fn, steps, warmup, torch):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n = 0
-    while True:
-        i = n % len(imgs_host)
-        k, d, _ = oracle.extract(imgs_host[i], args.features, 1.2, 8, 20, 7)
-        mps, mpd, locked = maps[i]
-        oracle.match_projection_local(k, d, scale, args.width, args.height, mps, mpd, 1.0, 0.8,
-                                      locked[: len(k)])
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= args.cpu_seconds and n >= 3) or n >= args.cpu_max_frames:
-            break
-    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} frames {args.width}x{args.height}: oracle ORBextractor "
-                      f"({args.features} feat) + SearchByProjection vs {args.mappoints} map "
-                      f"points, C++ -O3 scalar, 1 thread, {el:.1f} s"}
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
 
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="frames per GPU per step")
+    ap.add_argument("--steps", type=int, default=60,
+                    help="timed steps; one step = one pass over the --frames resident frames")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=8192,
+                    help="distinct resident frames per GPU (a step processes each once)")
+    ap.add_argument("--batch", type=int, default=512, help="frames per extraction launch")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--features", type=int, default=1000)
@@ -166,6 +318,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-max-frames", type=int, default=400)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C3 / C5 extra keys")
+    ap.add_argument("--threads", type=int, default=16, help="host threads for input synthesis")
     ap.add_argument("--seed", type=int, default=0x4B495454)
     args = ap.parse_args()
 
@@ -181,18 +335,22 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     orb = load_package()
     W, H, B, NF, M = args.width, args.height, args.batch, args.features, args.mappoints
+    D = args.frames
+    if D % B:
+        raise SystemExit("--frames must be a multiple of --batch")
+    NB = D // B
 
     # ---------------- inputs: this rank's shard of the synthetic sequence, in HBM
-    frames = shard_frames(rank, B)
-    imgs = np.stack([orb.synth_image(args.seed, f, W, H) for f in frames])
+    frames = shard_frames(rank, D)
+    imgs = synth_images(orb, args.seed, frames, W, H, args.threads)
     ext = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=local)
     scale = np.float32(ext.GetScaleFactors())
     cap = ext.capacity(W, H)
     dev = torch.device("cuda", local)
-    # Two streams, two buffer sets: step k's SearchByProjection (matcher
-    # stream) overlaps step k+1's extraction (extract stream).  Step k's
-    # extraction writes buffer set k % 2 once the matcher of step k - 2 (the
-    # set's previous reader) has finished; its matcher starts once it is done.
+    # Two streams, two buffer sets: launch g's SearchByProjection (matcher
+    # stream) overlaps launch g+1's extraction (extract stream).  Launch g
+    # writes buffer set g % 2 once the matcher of launch g - 2 (the set's
+    # previous reader) has finished; its matcher starts once it is done.
     ext_stream = torch.cuda.Stream(dev)
     match_stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(ext_stream)
@@ -206,52 +364,65 @@ def main():
             for _ in range(2)]
     extracted = [torch.cuda.Event(), torch.cuda.Event()]
     matched = [torch.cuda.Event(), torch.cuda.Event()]
+    frame_bytes = W * H
 
-    def extract(st, stream):
-        ext.extract_batch(d_img.data_ptr(), B, W, H, W, W * H, st["kps"].data_ptr(),
-                          st["desc"].data_ptr(), cap, st["cnt"].data_ptr(), stream.cuda_stream)
+    def extract(st, batch, stream):
+        ext.extract_batch(d_img.data_ptr() + batch * B * frame_bytes, B, W, H, W, frame_bytes,
+                          st["kps"].data_ptr(), st["desc"].data_ptr(), cap, st["cnt"].data_ptr(),
+                          stream.cuda_stream)
 
-    extract(sets[0], ext_stream)  # untimed: derive each frame's local map from its own keypoints
-    torch.cuda.synchronize()
-    kps_h = sets[0]["kps"].cpu().numpy().view(orb.KEYPOINT_DTYPE).reshape(B, cap)
-    desc_h = sets[0]["desc"].cpu().numpy()
-    cnt_h = sets[0]["cnt"].cpu().numpy()
-    mps_all = np.zeros((B, M), orb.MP_TRACK_DTYPE)
-    mpd_all = np.zeros((B, M, 32), np.uint8)
-    lock_all = np.zeros((B, cap), np.uint8)
-    maps = []
-    for i in range(B):
-        n = int(cnt_h[i])
-        mps, mpd, lk = orb.synth_local_map(args.seed + frames[i], kps_h[i, :n], desc_h[i, :n], M, W, H)
-        mps_all[i], mpd_all[i], lock_all[i, :n] = mps, mpd, lk
-        maps.append((mps, mpd, lk))
-    d_mps = torch.from_numpy(mps_all.view(np.uint8).reshape(B, -1)).to(dev)
+    # untimed pass: every frame's local map is derived from its own keypoints
+    kps_h = np.zeros((D, cap), orb.KEYPOINT_DTYPE)
+    desc_h = np.zeros((D, cap, 32), np.uint8)
+    cnt_h = np.zeros(D, np.int32)
+    for b in range(NB):
+        extract(sets[0], b, ext_stream)
+        torch.cuda.synchronize()
+        kps_h[b * B:(b + 1) * B] = sets[0]["kps"].cpu().numpy().view(orb.KEYPOINT_DTYPE).reshape(B, cap)
+        desc_h[b * B:(b + 1) * B] = sets[0]["desc"].cpu().numpy()
+        cnt_h[b * B:(b + 1) * B] = sets[0]["cnt"].cpu().numpy()
+    if cnt_h.min() < 0:  # the extractor marks an image it could not finish with a negative count
+        raise RuntimeError(f"extraction failed on {int((cnt_h < 0).sum())} frame(s)")
+    maps = parallel_map(lambda i: orb.synth_local_map(args.seed + frames[i], kps_h[i, :cnt_h[i]],
+                                                      desc_h[i, :cnt_h[i]], M, W, H),
+                        range(D), args.threads)
+    mps_all = np.stack([mm[0] for mm in maps])
+    mpd_all = np.stack([mm[1] for mm in maps])
+    lock_all = np.zeros((D, cap), np.uint8)
+    for i in range(D):
+        lock_all[i, :cnt_h[i]] = maps[i][2]
+    d_mps = torch.from_numpy(mps_all.view(np.uint8).reshape(D, -1)).to(dev)
     d_mpd = torch.from_numpy(mpd_all).to(dev)
     d_lock = torch.from_numpy(lock_all).to(dev)
     d_nmps = torch.full((B,), M, dtype=torch.int32, device=dev)
+    del mpd_all, lock_all
     matcher = orb.ORBmatcher(0.8, device=local)
     torch.cuda.synchronize()
 
-    def step(k):
-        j = k % 2
+    def launch(g):
+        j, b = g % 2, g % NB
         st = sets[j]
-        if k >= 2:
+        if g >= 2:
             ext_stream.wait_event(matched[j])
-        extract(st, ext_stream)
+        extract(st, b, ext_stream)
         extracted[j].record(ext_stream)
         match_stream.wait_event(extracted[j])
         matcher.search_by_projection_batch(B, st["kps"].data_ptr(), st["desc"].data_ptr(),
-                                           st["cnt"].data_ptr(), d_lock.data_ptr(), cap,
-                                           d_mps.data_ptr(), d_mpd.data_ptr(), d_nmps.data_ptr(),
-                                           M, W, H, scale, 1.0, st["match"].data_ptr(),
-                                           st["nmatch"].data_ptr(), match_stream.cuda_stream)
+                                           st["cnt"].data_ptr(), d_lock[b * B].data_ptr(), cap,
+                                           d_mps[b * B].data_ptr(), d_mpd[b * B].data_ptr(),
+                                           d_nmps.data_ptr(), M, W, H, scale, 1.0,
+                                           st["match"].data_ptr(), st["nmatch"].data_ptr(),
+                                           match_stream.cuda_stream)
         if dist is not None:  # RCCL: gather every frame's keypoint count
             with torch.cuda.stream(match_stream):
                 gather_counts(dist, st["cnt"], st["gathered"])
         matched[j].record(match_stream)
 
+    g = 0
     for k in range(args.warmup):
-        step(k)
+        for _ in range(NB):
+            launch(g)
+            g += 1
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -259,7 +430,9 @@ def main():
     matcher.profile(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k)
+        for _ in range(NB):
+            launch(g)
+            g += 1
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -267,14 +440,19 @@ def main():
     elapsed = t1 - t0
     if dist is not None:
         elapsed = max_over_ranks(dist, elapsed, dev)
+    for st in sets:
+        if int(st["cnt"].min().item()) < 0:
+            raise RuntimeError("extraction reported a failed frame (negative count)")
 
     # per-kernel HIP-event times over the timed region, each on its own stream.
     # The extract stream is the critical path (the matcher stream runs in its
     # shadow, so matcher kernel times include time-sharing with the next
-    # step's extraction): the roofline kernel is the longest extraction kernel.
+    # launch's extraction): the roofline kernel is the longest extraction kernel.
     kern, ext_kern = {}, []
     for st in range(5):
         name, ms, n = ext.profile_read(st)
+        if n == 0:
+            continue  # stage not run (k_blur_levels: split A/B mode only)
         kern[name] = (ms, n)
         ext_kern.append(name)
     for st in range(3):
@@ -282,18 +460,41 @@ def main():
         kern[name] = (ms, n)
     ext.profile(False)
     matcher.profile(False)
-    n_kp = float(sets[0]["cnt"].float().mean().item())
+    n_kp = float(cnt_h.mean())
     nmatch = float(sets[0]["nmatch"].float().mean().item())
     alg = algorithmic_bytes(W, H, scale, 8, n_kp, M)
     dom = max(ext_kern, key=lambda k: kern[k][0])
     dom_ms_per_launch = kern[dom][0] / max(kern[dom][1], 1)
-    # bytes one launch of the dominant kernel processes
-    launches_per_step = kern[dom][1] / args.steps
-    dom_bytes = alg[dom] * B / launches_per_step
-    achieved = dom_bytes / (dom_ms_per_launch * 1e-3) / 1e9
-
+    # bytes one launch of the dominant kernel processes (B frames; the resize
+    # runs nlevels-1 launches per extraction)
+    launches_per_extract = kern[dom][1] / (args.steps * NB)
+    dom_bytes = alg[dom] * B / launches_per_extract
+    hbm_gbs = dom_bytes / (dom_ms_per_launch * 1e-3) / 1e9
     traffic, traffic_src = measured_traffic(dom, B)
-    total_frames = B * args.steps * world
+    valu = valu_issue(dom, B, dom_ms_per_launch)
+    total_frames = D * args.steps * world
+    if valu is not None:
+        # VALU issue: the roofline that binds this integer kernel (its HBM
+        # fraction is reported beside it)
+        rate = valu["valu_instr_per_launch"] / (dom_ms_per_launch * 1e-3) / 1e9
+        peak = N_SIMD / VALU_NS_FAST
+        roof = {"kernel": dom, "bound": "valu", "achieved": rate, "peak": peak,
+                "unit": "G VALU wave-instructions/s", "frac": rate / peak,
+                "note": "peak = 1024 SIMDs x one plain 32-bit VALU wave-instruction per ns "
+                        "(profiles/r01_valu_rates.txt); SQ_INSTS_VALU per launch from "
+                        + valu["source"].split(" ")[0],
+                "valu_issue": valu}
+    else:
+        roof = {"kernel": dom, "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS}
+    roof.update({
+        "traffic": traffic,
+        "traffic_source": f"profiles/{traffic_src} (rocprofv3 FETCH_SIZE+WRITE_SIZE, "
+                          "separate passes)" if traffic_src else None,
+        "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_launch": dom_bytes},
+        "ms_per_launch": dom_ms_per_launch,
+    })
     result = {
         "metric": METRIC,
         "value": total_frames / elapsed,
@@ -310,29 +511,23 @@ def main():
         "config": {
             "workload": f"C4: {W}x{H} KITTI-shaped synthetic stream, {NF} feat/frame, "
                         f"SearchByProjection vs {M}-point local map per frame",
-            "frames_per_gpu_per_step": B,
+            "frames_per_gpu_per_step": D,
+            "distinct_frames_per_gpu": D,
+            "frames_per_launch": B,
+            "timed_region_s": elapsed,
             "parallelism": f"frames sharded over {world} rank(s), RCCL all-gather of counts",
             "mean_keypoints_per_frame": n_kp,
             "mean_matches_per_frame": nmatch,
         },
-        "roofline": {
-            "kernel": dom,
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": f"profiles/{traffic_src} (rocprofv3 FETCH_SIZE+WRITE_SIZE, "
-                              "separate passes, raw KiB x 1024)" if traffic_src else None,
-            "bytes_per_launch": dom_bytes,
-            "ms_per_launch": dom_ms_per_launch,
-            "valu_issue": valu_issue(dom, B, dom_ms_per_launch),
-        },
-        "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
+        "roofline": roof,
+        "kernels_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kern.items()},
+        "extraction_stream_ms_per_launch": sum(kern[k][0] for k in ext_kern) / (args.steps * NB),
     }
+    if rank == 0 and world == 1 and not args.no_secondary:
+        del d_img
+        result.update(secondary_configs(orb, torch, args, dev, args.threads))
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(imgs, maps, args, scale)
+        result["cpu_baseline"] = cpu_baseline(imgs[:64], maps[:64], args, scale)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
