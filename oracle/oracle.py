@@ -8,13 +8,17 @@ header of orb_oracle.cpp and DESIGN.md §2).
 from __future__ import annotations
 
 import ctypes
+import os
 import subprocess
 from pathlib import Path
 
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "liborb_oracle.so"
+# ORB_ORACLE_VARIANT=glibc (read at import) selects the build with the
+# reference's own glibc cosf/sinf/logf calls instead of the pins (tools/parity_libm.py)
+LIB_PATH = HERE / ("liborb_oracle_glibc.so" if os.environ.get("ORB_ORACLE_VARIANT") == "glibc"
+                   else "liborb_oracle.so")
 
 KEYPOINT_DTYPE = np.dtype(
     [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),

@@ -38,6 +38,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <list>
 #include <utility>
 #include <vector>
@@ -529,7 +530,7 @@ static Img gaussian_blur7(const Img& src) {
 }
 
 // A.6 pinned sin/cos: fdlibm-style reduction and kernels in double, rounded to float.
-static void pinned_sincos(float angle, float* s_out, float* c_out) {
+[[maybe_unused]] static void pinned_sincos(float angle, float* s_out, float* c_out) {
   const double x = (double)angle;
   const double invpio2 = 6.36619772367581382433e-01;
   const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
@@ -559,6 +560,19 @@ static void pinned_sincos(float angle, float* s_out, float* c_out) {
   *c_out = (float)c;
 }
 
+// ORB_ORACLE_GLIBC_MATH (oracle/Makefile target liborb_oracle_glibc.so; used
+// only by tools/parity_libm.py to measure what the A.6/A.7 pins change): the
+// reference's own calls instead of the pins -- cos/sin of a float under
+// `using namespace std` (src/ORBextractor.cc:67-68,125), i.e. glibc cosf/sinf.
+static inline void desc_sincos(float angle, float* s, float* c) {
+#ifdef ORB_ORACLE_GLIBC_MATH
+  *s = std::sin(angle);
+  *c = std::cos(angle);
+#else
+  pinned_sincos(angle, s, c);
+#endif
+}
+
 // a8: computeOrbDescriptor, src/ORBextractor.cc:119-164
 static void orb_descriptor(const KP& kpt, const Img& blurred, uint8_t* desc) {
   const float factorPI = (float)(M_PI / 180.f);
@@ -566,7 +580,7 @@ static void orb_descriptor(const KP& kpt, const Img& blurred, uint8_t* desc) {
   float a, b;
   {
     float s, c;
-    pinned_sincos(angle, &s, &c);
+    desc_sincos(angle, &s, &c);
     a = c;
     b = s;
   }
@@ -794,6 +808,16 @@ static double pinned_log(double x) {
   return k == 0 ? f - sv * (f - R) : dk * ln2_hi - ((sv * (f - R) - dk * ln2_lo) - f);
 }
 
+// log(ratio) of MapPoint::PredictScale (src/MapPoint.cc:443): pinned, or glibc
+// logf under ORB_ORACLE_GLIBC_MATH (see desc_sincos)
+static inline float scale_log(float ratio) {
+#ifdef ORB_ORACLE_GLIBC_MATH
+  return std::log(ratio);
+#else
+  return (float)pinned_log((double)ratio);
+#endif
+}
+
 struct FrustumCfg {
   orb_camera_t cam;
   float minX, maxX, minY, maxY, cosLimit, logScale;
@@ -835,7 +859,7 @@ static bool frustum_one(const orb_map_point_t& mp, const orb_pose_t& T, const Fr
   const float viewCos = (float)(dot / (double)dist);            // :351
   if (viewCos < c.cosLimit) return false;                       // :353-354
   const float ratio = mp.max_distance / dist;                   // PredictScale
-  const float lr = (float)pinned_log((double)ratio);
+  const float lr = scale_log(ratio);
   const float q = ceilf(lr / c.logScale);
   int level;
   if (q < 0.f) level = 0;
@@ -1247,7 +1271,7 @@ static inline double dot3(const float* a, const float* b) {
 // MapPoint::PredictScale (src/MapPoint.cc:417-450), logf pinned
 static inline int predict_scale(float maxDistance, float dist, float logScale, int nLevels) {
   const float ratio = maxDistance / dist;
-  const float q = ceilf((float)pinned_log((double)ratio) / logScale);
+  const float q = ceilf(scale_log(ratio) / logScale);
   if (q < 0.f) return 0;
   if (q >= (float)nLevels) return nLevels - 1;
   return (int)q;
@@ -1762,7 +1786,7 @@ int oracle_fast(const uint8_t* img, int w, int h, int threshold, orb_keypoint_t*
 
 float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
 
-void oracle_sincos(float angle, float* s, float* c) { pinned_sincos(angle, s, c); }
+void oracle_sincos(float angle, float* s, float* c) { desc_sincos(angle, s, c); }
 
 int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
 
