@@ -311,6 +311,21 @@ orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor
                                     int kp_stride, float bf, float fx, float* d_u_right,
                                     float* d_depth, int32_t* d_sad, void* stream);
 
+/* Frame::ComputeStereoMatches (src/Frame.cc:516-704) for the pair whose left
+ * and right images were extracted last by orb_extractor_extract on left_ext and
+ * right_ext (the stereo Frame constructor's two ExtractORB calls,
+ * src/Frame.cc:81-93): keypoints, descriptors and both pyramids are read where
+ * the extractions left them in device memory, so only mvuRight / mvDepth
+ * (-1 = no match) are copied back.  *n_left = the left keypoint count; the
+ * outputs need n_left entries (ORB_ECAPACITY if capacity is smaller; both
+ * outputs NULL = size query).
+ * ORB_EINVAL if either handle's last call was not orb_extractor_extract.
+ * Synchronous. */
+orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_ext,
+                                        orb_extractor_t* right_ext, float bf, float fx,
+                                        float* u_right, float* depth, int capacity,
+                                        int* n_left);
+
 /* SearchByProjection(CurrentFrame, LastFrame, th, bMono) with ORBmatcher(nnratio, checkOri).
  * The last frame's map points are given already projected with the current
  * pose (the float camera-space coordinates xc, yc and invzc computed exactly

@@ -123,6 +123,7 @@ def lib() -> ctypes.CDLL:
             i32, [vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, f32, f32, f32, f32, i32, vp,
                   f32, f32, vp, vp, vp]),
         "orb_stereo_match": (i32, [vp, vp, vp, vp]),
+        "orb_stereo_match_extracted": (i32, [vp, vp, vp, f32, f32, vp, vp, i32, vp]),
         "orb_stereo_match_batch": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32,
                                          vp, vp, vp, vp]),
         "orb_match_projection_frame": (i32, [vp, vp, vp, i32, vp, vp, vp, f32, f32, i32, i32, vp,
@@ -469,6 +470,23 @@ class ORBmatcher:
 
 
     # ---------------------------------------------------- Frame::ComputeStereoMatches
+    def ComputeStereoMatchesExtracted(self, left_ext, right_ext, bf: float, fx: float):
+        """Frame::ComputeStereoMatches for the pair last extracted by the two
+        handles' __call__ (orb_stereo_match_extracted): nothing but mvuRight /
+        mvDepth crosses PCIe.  Returns (mvuRight, mvDepth)."""
+        n = ctypes.c_int(0)
+        L = lib()
+        _check(L.orb_stereo_match_extracted(self._h, left_ext.handle, right_ext.handle, bf, fx,
+                                            None, None, 0, ctypes.byref(n)),
+               "orb_stereo_match_extracted")
+        ur = np.full(n.value, -1, np.float32)
+        dp = np.full(n.value, -1, np.float32)
+        if n.value:
+            _check(L.orb_stereo_match_extracted(self._h, left_ext.handle, right_ext.handle, bf,
+                                                fx, _ptr(ur), _ptr(dp), n.value, ctypes.byref(n)),
+                   "orb_stereo_match_extracted")
+        return ur, dp
+
     def ComputeStereoMatches(self, left: Frame, right_keys, right_desc, left_pyramid,
                              right_pyramid, inv_scale_factors, bf: float, fx: float):
         """Frame::ComputeStereoMatches (src/Frame.cc:516-704): (mvuRight, mvDepth)."""

@@ -324,8 +324,17 @@ struct orb_extractor {
   int batchCap = 0;
   DevBuf dArena, dBlur, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
   // single-image API scratch
-  DevBuf dImg, dKps, dDesc, dCounts;
-  HostBuf hImg, hOut;  // pinned staging: image in, counts + keypoints + descriptors out
+  // single-image API: dImg (the image at a 64-B row pitch) and dOne = [count,
+  // pad x3 | cap keypoints | cap x 32 descriptors], mirrored by the pinned
+  // hImg / hOut so each call is one DMA in and one DMA out
+  DevBuf dImg, dOne;
+  HostBuf hImg, hOut, hLvl;  // hLvl: staging of orb_extractor_pyramid_level / _blurred_level
+  int oneCap = 0;            // capacity of the dOne layout
+  bool lastSingle = false;   // the last call was orb_extractor_extract (dOne is current)
+  // the whole single-image call (H2D, every kernel, D2H) as one hipGraph per
+  // plan; keyed by the buffers it captured (any reallocation re-captures)
+  hipGraphExec_t oneExec = nullptr;
+  std::vector<const void*> oneKey;
   int lastW = 0, lastH = 0;
   size_t lastImgStride = 0;
   const uint8_t* lastImg0 = nullptr;  // level 0 of the last batch (device)
@@ -631,7 +640,8 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
 
 static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, size_t stride,
                               size_t imgPitch, orb_keypoint_t* d_kps, uint8_t* d_desc,
-                              int capacity, int32_t* d_counts, hipStream_t s) {
+                              int capacity, int32_t* d_counts, hipStream_t s,
+                              bool capturing = false) {
   // Stage chain: pyramid -> FAST -> octree -> orient + blur + descriptors
   // (k_orient_desc blurs each keypoint's window in LDS).  Split A/B mode
   // (ORB_SPLIT_BLUR=1): k_blur_levels writes every blurred level after FAST,
@@ -696,7 +706,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                               h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
   PROF_REC(ev, pf.e(ev, 4), s);
   PROF_REC(ev, pf.t1(ev), s);
-  HIP_TRY(hipEventRecord(h->evBatch, s));  // readbacks on the handle stream wait for it
+  if (!capturing) HIP_TRY(hipEventRecord(h->evBatch, s));  // readbacks on the handle stream wait for it
   h->lastImg0 = d_images;
   h->lastImg0Pitch = imgPitch;
   h->lastImg0Stride = (int)stride;
@@ -787,10 +797,12 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   DevBuf* bufs[] = {&h->dCells, &h->dRtab, &h->dTiles, &h->dBlur, &h->dArena, &h->dCellKeys, &h->dCellCount,
                     &h->dGKeys, &h->dGNid, &h->dOutKeys, &h->dOutCount, &h->dErr,
-                    &h->dImg, &h->dKps, &h->dDesc, &h->dCounts};
+                    &h->dImg, &h->dOne};
   for (DevBuf* b : bufs) b->release();
   h->hImg.release();
   h->hOut.release();
+  h->hLvl.release();
+  if (h->oneExec) hipGraphExecDestroy(h->oneExec);
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
@@ -846,6 +858,7 @@ orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_im
   st = run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors, capacity,
                  d_counts, s);
   if (st) return st;
+  h->lastSingle = false;
   h->lastW = width;
   h->lastH = height;
   return ORB_OK;
@@ -864,44 +877,72 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   const int cap = h->plan.slotsPerImage;
   const size_t dstride = ((size_t)width + 63) & ~(size_t)63;
   const size_t pitch = dstride * height;
+  const size_t kOff = 16, dOff = kOff + (size_t)cap * sizeof(orb_keypoint_t);
+  const size_t outBytes = dOff + (size_t)cap * 32;
   if ((st = ensure_batch(h, 1))) return st;
   if ((st = h->dImg.ensure(pitch))) return st;
-  if ((st = h->dKps.ensure((size_t)cap * sizeof(orb_keypoint_t)))) return st;
-  if ((st = h->dDesc.ensure((size_t)cap * 32))) return st;
-  if ((st = h->dCounts.ensure(16))) return st;
-  // image -> pinned staging at the device row pitch -> one DMA
+  if ((st = h->dOne.ensure(outBytes))) return st;
   if ((st = h->hImg.ensure(pitch))) return st;
+  if ((st = h->hOut.ensure(outBytes))) return st;
+  // image -> pinned staging at the device row pitch
   for (int y = 0; y < height; ++y)
     memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
-  HIP_TRY(hipMemcpyAsync(h->dImg.p, h->hImg.p, pitch, hipMemcpyHostToDevice, h->stream));
-  st = run_batch(h, h->dImg.as<uint8_t>(), 1, dstride, pitch, h->dKps.as<orb_keypoint_t>(),
-                 h->dDesc.as<uint8_t>(), cap, h->dCounts.as<int32_t>(), h->stream);
-  if (st) return st;
-  // counts, error flag, then as many records as the capacity allows, in one
-  // round trip: the pinned block holds [n, err, pad, pad | cap keypoints | cap x 32]
-  const size_t kOff = 16, dOff = kOff + (size_t)cap * sizeof(orb_keypoint_t);
-  if ((st = h->hOut.ensure(dOff + (size_t)cap * 32))) return st;
-  uint8_t* ho = h->hOut.as<uint8_t>();
-  HIP_TRY(hipMemcpyAsync(ho, h->dCounts.p, 4, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipMemcpyAsync(ho + 4, h->dErr.p, 4, hipMemcpyDeviceToHost, h->stream));
+  uint8_t* d1 = h->dOne.as<uint8_t>();
+  // one DMA in, the extraction, one DMA out of the count and every record slot
+  auto enqueue = [&](bool capturing) -> orb_status_t {
+    HIP_TRY(hipMemcpyAsync(h->dImg.p, h->hImg.p, pitch, hipMemcpyHostToDevice, h->stream));
+    orb_status_t r = run_batch(h, h->dImg.as<uint8_t>(), 1, dstride, pitch,
+                               reinterpret_cast<orb_keypoint_t*>(d1 + kOff), d1 + dOff, cap,
+                               reinterpret_cast<int32_t*>(d1), h->stream, capturing);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(h->hOut.p, d1, outBytes, hipMemcpyDeviceToHost, h->stream));
+    return ORB_OK;
+  };
+  static const bool noGraph = getenv("ORB_NO_GRAPH") && atoi(getenv("ORB_NO_GRAPH")) > 0;
+  if (h->prof.enabled || noGraph) {
+    if ((st = enqueue(false))) return st;
+  } else {
+    const std::vector<const void*> key = {
+        h->dImg.p, h->dOne.p, h->hImg.p, h->hOut.p, h->dArena.p, h->dCellKeys.p, h->dGKeys.p,
+        h->dGNid.p, h->dCellCount.p, h->dOutKeys.p, h->dOutCount.p, h->dErr.p, h->dRtab.p,
+        h->dBands.p, h->dCells.p, (const void*)(intptr_t)width, (const void*)(intptr_t)height,
+        (const void*)(intptr_t)cap};
+    if (!h->oneExec || key != h->oneKey) {
+      if (h->oneExec) hipGraphExecDestroy(h->oneExec);
+      h->oneExec = nullptr;
+      hipGraph_t graph = nullptr;
+      HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+      st = enqueue(true);
+      hipError_t ce = hipStreamEndCapture(h->stream, &graph);
+      if (st) {
+        if (graph) hipGraphDestroy(graph);
+        return st;
+      }
+      if (ce != hipSuccess) return ORB_EDEVICE;
+      hipError_t ie = hipGraphInstantiate(&h->oneExec, graph, nullptr, nullptr, 0);
+      hipGraphDestroy(graph);
+      if (ie != hipSuccess) {
+        h->oneExec = nullptr;
+        return ORB_EDEVICE;
+      }
+      h->oneKey = key;
+    }
+    HIP_TRY(hipGraphLaunch(h->oneExec, h->stream));
+    HIP_TRY(hipEventRecord(h->evBatch, h->stream));
+  }
   HIP_TRY(hipStreamSynchronize(h->stream));
-  int32_t n = 0, err = 0;
+  h->oneCap = cap;
+  h->lastSingle = true;
+  const uint8_t* ho = h->hOut.as<uint8_t>();
+  int32_t n = 0;
   memcpy(&n, ho, 4);
-  memcpy(&err, ho + 4, 4);
   h->lastW = width;
   h->lastH = height;
-  if (n < 0) {  // the octree hit an internal limit (errFlag bits: 2 node cap, 4 passes, 8 sort key)
-    if (getenv("ORB_AMD_DEBUG")) fprintf(stderr, "[orb_amd] kernel error flag %d\n", err);
-    return ORB_EDEVICE;
-  }
+  // a negative count: the octree hit an internal limit (never at ORB-SLAM2 settings)
+  if (n < 0) return ORB_EDEVICE;
   *n_keypoints = n;
   if (n > capacity) return ORB_ECAPACITY;
   if (n > 0) {
-    HIP_TRY(hipMemcpyAsync(ho + kOff, h->dKps.p, (size_t)n * sizeof(orb_keypoint_t),
-                           hipMemcpyDeviceToHost, h->stream));
-    if (descriptors)
-      HIP_TRY(hipMemcpyAsync(ho + dOff, h->dDesc.p, (size_t)n * 32, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
     memcpy(keypoints, ho + kOff, (size_t)n * sizeof(orb_keypoint_t));
     if (descriptors) memcpy(descriptors, ho + dOff, (size_t)n * 32);
   }
@@ -930,9 +971,9 @@ orb_status_t orb_extractor_batch_level(orb_extractor_t* h, int image, int level,
 // copy straight into pageable memory goes row by row.
 static orb_status_t copy_level_to_host(orb_extractor_t* h, uint8_t* dst, size_t dst_stride,
                                        const uint8_t* src, size_t src_stride, int w, int hh) {
-  orb_status_t st = h->hOut.ensure((size_t)w * hh);
+  orb_status_t st = h->hLvl.ensure((size_t)w * hh);
   if (st) return st;
-  uint8_t* ho = h->hOut.as<uint8_t>();
+  uint8_t* ho = h->hLvl.as<uint8_t>();
   HIP_TRY(hipMemcpy2DAsync(ho, (size_t)w, src, src_stride, (size_t)w, hh, hipMemcpyDeviceToHost,
                            h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1528,6 +1569,95 @@ orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor
                        n_pairs, s));
   // the pair-level pointer table must outlive the asynchronous launch
   HIP_TRY(hipStreamSynchronize(s));
+  return ORB_OK;
+}
+
+// Frame::ComputeStereoMatches for the pair the two handles extracted last with
+// orb_extractor_extract (src/Frame.cc:81-93 runs the two ExtractORB threads,
+// then ComputeStereoMatches): keypoints, descriptors and both pyramids are
+// read where the extractions left them in HBM; only mvuRight / mvDepth travel.
+orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_ext,
+                                        orb_extractor_t* right_ext, float bf, float fx,
+                                        float* u_right, float* depth, int capacity,
+                                        int* n_left) {
+  if (!m || !left_ext || !right_ext || left_ext == right_ext || !(fx > 0) || !n_left)
+    return ORB_EINVAL;
+  // both handles stay locked while their last-call state is read and used
+  orb_extractor* a = left_ext < right_ext ? left_ext : right_ext;
+  orb_extractor* b = left_ext < right_ext ? right_ext : left_ext;
+  std::lock_guard<std::mutex> ga(a->mu), gb(b->mu);
+  if (!left_ext->lastSingle || !right_ext->lastSingle) return ORB_EINVAL;
+  const int L = left_ext->nlevels;
+  if (L != right_ext->nlevels || left_ext->planW != right_ext->planW ||
+      left_ext->planH != right_ext->planH)
+    return ORB_EINVAL;
+  int32_t nL = 0, nR = 0;
+  memcpy(&nL, left_ext->hOut.p, 4);
+  memcpy(&nR, right_ext->hOut.p, 4);
+  if (nL < 0 || nR < 0) return ORB_EDEVICE;
+  *n_left = nL;
+  if (!u_right && !depth) return ORB_OK;  // size query
+  if (nL > capacity) return ORB_ECAPACITY;
+  if (nL == 0) return ORB_OK;
+  if (!u_right || !depth) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  hipSetDevice(m->device);
+  hipStream_t s = m->stream;
+  HIP_TRY(hipStreamWaitEvent(s, left_ext->evBatch, 0));
+  HIP_TRY(hipStreamWaitEvent(s, right_ext->evBatch, 0));
+  StereoParamsHost P;
+  memset(&P, 0, sizeof(P));
+  P.nLevels = L;
+  P.bf = bf;
+  P.fx = fx;
+  std::copy(left_ext->scale.begin(), left_ext->scale.end(), P.scale);
+  std::copy(left_ext->invScale.begin(), left_ext->invScale.end(), P.invScale);
+  StereoPairLevelsHost lv;
+  memset(&lv, 0, sizeof(lv));
+  for (int l = 0; l < L; ++l) {
+    const OrbLevelDesc& dl = left_ext->plan.lv[l];
+    const OrbLevelDesc& dr = right_ext->plan.lv[l];
+    P.w[l] = dl.w;
+    P.h[l] = dl.h;
+    if (l == 0) {  // level 0 = the image staged by orb_extractor_extract
+      lv.L[0] = left_ext->dImg.as<uint8_t>();
+      lv.R[0] = right_ext->dImg.as<uint8_t>();
+      P.strideL[0] = (int)(((size_t)dl.w + 63) & ~(size_t)63);
+      P.strideR[0] = (int)(((size_t)dr.w + 63) & ~(size_t)63);
+    } else {
+      lv.L[l] = left_ext->dArena.as<uint8_t>() + dl.arenaOff;
+      lv.R[l] = right_ext->dArena.as<uint8_t>() + dr.arenaOff;
+      P.strideL[l] = dl.pitch;
+      P.strideR[l] = dr.pitch;
+    }
+  }
+  orb_status_t st;
+  if ((st = m->dPairLv.ensure(sizeof(lv)))) return st;
+  if ((st = m->dUr.ensure((size_t)nL * 4))) return st;
+  if ((st = m->dDepth.ensure((size_t)nL * 4))) return st;
+  if ((st = m->dSad.ensure((size_t)nL * 4))) return st;
+  if ((st = m->hPyr.ensure((size_t)nL * 8 + sizeof(lv)))) return st;
+  memcpy(m->hPyr.as<uint8_t>() + (size_t)nL * 8, &lv, sizeof(lv));
+  HIP_TRY(hipMemcpyAsync(m->dPairLv.p, m->hPyr.as<uint8_t>() + (size_t)nL * 8, sizeof(lv),
+                         hipMemcpyHostToDevice, s));
+  const uint8_t* l1 = left_ext->dOne.as<uint8_t>();
+  const uint8_t* r1 = right_ext->dOne.as<uint8_t>();
+  const int stride = std::max(left_ext->oneCap, right_ext->oneCap);
+  // the two records blocks have their own capacities: pair 0 only, so the
+  // shared kpStride of the kernel is never applied
+  HIP_TRY(orb_k_stereo(reinterpret_cast<const orb_keypoint_t*>(l1 + 16),
+                       l1 + 16 + (size_t)left_ext->oneCap * sizeof(orb_keypoint_t),
+                       reinterpret_cast<const int32_t*>(l1),
+                       reinterpret_cast<const orb_keypoint_t*>(r1 + 16),
+                       r1 + 16 + (size_t)right_ext->oneCap * sizeof(orb_keypoint_t),
+                       reinterpret_cast<const int32_t*>(r1), stride, nL, m->dPairLv.p, &P,
+                       m->dUr.as<float>(), m->dDepth.as<float>(), m->dSad.as<int32_t>(), 1, s));
+  HIP_TRY(hipMemcpyAsync(m->hPyr.p, m->dUr.p, (size_t)nL * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(m->hPyr.as<uint8_t>() + (size_t)nL * 4, m->dDepth.p, (size_t)nL * 4,
+                         hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  memcpy(u_right, m->hPyr.p, (size_t)nL * 4);
+  memcpy(depth, m->hPyr.as<uint8_t>() + (size_t)nL * 4, (size_t)nL * 4);
   return ORB_OK;
 }
 

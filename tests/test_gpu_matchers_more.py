@@ -100,3 +100,33 @@ def test_search_by_bow(gpu, oracle, seed, nnratio, check_ori):
     assert n_ref > 50
     assert n_gpu == n_ref
     assert np.array_equal(fm, fm_ref)
+
+
+@pytest.mark.parametrize("seed", [1, 3])
+def test_stereo_from_extracted_handles(gpu, oracle, seed):
+    """Frame's stereo path with nothing but mvuRight / mvDepth leaving the GPU:
+    both handles' last orb_extractor_extract feeds orb_stereo_match_extracted."""
+    sp = scenarios.stereo_pair(oracle, seed)
+    L = gpu.ORBextractor(2000, 1.2, 8, 20, 7)
+    R = gpu.ORBextractor(2000, 1.2, 8, 20, 7)
+    kl, dl = L(oracle.synth_image(seed, 0, sp["w"], sp["h"], 0))
+    kr, dr = R(oracle.synth_image(seed, 0, sp["w"], sp["h"], 1))
+    assert kl.tobytes() == sp["kl"].tobytes() and kr.tobytes() == sp["kr"].tobytes()
+    ur_ref, dp_ref = oracle.stereo_match(sp["kl"], sp["dl"], sp["scale"], sp["kr"], sp["dr"],
+                                         sp["lpyr"], sp["rpyr"], sp["inv"], scenarios.BF,
+                                         scenarios.FX, sp["w"], sp["h"])
+    ur, dp = gpu.ORBmatcher().ComputeStereoMatchesExtracted(L, R, scenarios.BF, scenarios.FX)
+    assert (ur_ref > 0).sum() > 50
+    assert ur.tobytes() == ur_ref.tobytes() and dp.tobytes() == dp_ref.tobytes()
+    # a batch call on a handle invalidates its single-image state
+    with pytest.raises(gpu.OrbError):
+        torch = pytest.importorskip("torch")
+        img = torch.from_numpy(oracle.synth_image(seed, 1, sp["w"], sp["h"])).cuda()
+        cap = L.capacity(sp["w"], sp["h"])
+        k = torch.zeros((1, cap, 7), dtype=torch.int32, device="cuda")
+        d = torch.zeros((1, cap, 32), dtype=torch.uint8, device="cuda")
+        n = torch.zeros(1, dtype=torch.int32, device="cuda")
+        L.extract_batch(img.data_ptr(), 1, sp["w"], sp["h"], sp["w"], sp["w"] * sp["h"],
+                        k.data_ptr(), d.data_ptr(), cap, n.data_ptr())
+        torch.cuda.synchronize()
+        gpu.ORBmatcher().ComputeStereoMatchesExtracted(L, R, scenarios.BF, scenarios.FX)
