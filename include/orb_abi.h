@@ -124,8 +124,10 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
                                    int height, size_t stride, orb_keypoint_t* keypoints,
                                    uint8_t* descriptors, int capacity, int* n_keypoints);
 
-/* Host copy of mvImagePyramid[level] from the last orb_extractor_extract call.
- * dst may be NULL to query the size. */
+/* Host copy of mvImagePyramid[level] of the first image of the last call
+ * (orb_extractor_extract, or image 0 of orb_extractor_extract_batch, whose
+ * level 0 is read from the caller's d_images: keep it alive until then).
+ * The copy waits for the last call's stream.  dst may be NULL to query the size. */
 orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t* dst,
                                          size_t dst_stride, int* width, int* height);
 /* The 7x7 Gaussian-blurred copy of level `level` of the first image of the
@@ -145,7 +147,10 @@ orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_im
                                          int32_t* d_counts, void* stream);
 
 /* Device pointer to pyramid level `level` of batch image `image` after
- * orb_extractor_extract_batch (valid until the next call on this handle). */
+ * orb_extractor_extract_batch (valid until the next call on this handle).
+ * Level 0 is the caller's own image memory (d_images of that call): it is
+ * valid only while the caller keeps it.  Readers on another stream must order
+ * themselves after the batch's stream. */
 orb_status_t orb_extractor_batch_level(orb_extractor_t* h, int image, int level,
                                        const uint8_t** d_level, int* width, int* height,
                                        size_t* stride);

@@ -1455,6 +1455,13 @@ orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in, fl
       !in->inv_scale_factors || !in->left_levels || !in->right_levels || !in->level_width ||
       !in->level_height || !in->level_stride || !(in->fx > 0))
     return ORB_EINVAL;
+  // every level must be a real image: rows at least as long as the level
+  // (the staging copy reads w bytes of each row at y * stride)
+  for (int l = 0; l < L; ++l)
+    if (in->level_width[l] <= 0 || in->level_height[l] <= 0 ||
+        in->level_stride[l] < (int64_t)in->level_width[l] || !in->left_levels[l] ||
+        !in->right_levels[l])
+      return ORB_EINVAL;
   for (int i = 0; i < NL; ++i) { u_right[i] = -1.0f; depth[i] = -1.0f; }
   if (NL == 0) return ORB_OK;
   std::lock_guard<std::mutex> g(m->mu);

@@ -76,3 +76,32 @@ def test_product_does_not_link_the_oracle(orb):
     assert "oracle" not in out
     syms = exported(orb.LIB_PATH)
     assert not any(s.startswith("oracle_") for s in syms)
+
+
+def test_stereo_rejects_short_level_stride(orb):
+    """orb_stereo_match validates every level's stride before staging (a stride
+    shorter than the width would read rows past their end)."""
+    import ctypes
+    import numpy as np
+    L = orb.lib()
+    lvl = np.zeros((8, 8), np.uint8)
+    ptrs = (ctypes.c_void_p * 1)(lvl.ctypes.data)
+    w = np.array([64], np.int32)
+    h = np.array([8], np.int32)
+    st = np.array([8], np.int64)  # < width
+    inv = np.ones(1, np.float32)
+    keys = np.zeros(1, orb.KEYPOINT_DTYPE)
+    desc = np.zeros((1, 32), np.uint8)
+    f = orb.Frame(keys, desc, np.ones(1, np.float32), 64, 8)._c()
+    s = orb._StereoInput()
+    s.left = ctypes.addressof(f)
+    s.n_right = 0
+    s.n_levels = 1
+    s.left_levels = s.right_levels = ctypes.addressof(ptrs)
+    s.level_width, s.level_height, s.level_stride = (orb._ptr(w), orb._ptr(h), orb._ptr(st))
+    s.inv_scale_factors = orb._ptr(inv)
+    s.bf, s.fx = 40.0, 500.0
+    ur = np.zeros(1, np.float32)
+    dp = np.zeros(1, np.float32)
+    # validation happens before any device work (no GPU needed)
+    assert L.orb_stereo_match(ctypes.c_void_p(1), ctypes.byref(s), orb._ptr(ur), orb._ptr(dp)) == orb.ORB_EINVAL
