@@ -1,0 +1,101 @@
+// integration/ORBextractor.cc -- drop-in replacement for src/ORBextractor.cc of
+// ORB_SLAM2 (yg838457845/ORB_SLAM2-Chinese-annotation): every member of
+// include/ORBextractor.h:45-114 forwards to the MI355X C ABI
+// (include/orb_abi.h, lib/liborb_amd.so).
+//
+// Header change: include/ORBextractor.h gains
+//   #include "orb_abi.h"
+//   public:  orb_extractor_t* gpu() const { return mpGpu; }
+//   protected: orb_extractor_t* mpGpu = nullptr;
+// and its inline destructor becomes `~ORBextractor(){ orb_extractor_destroy(mpGpu); }`.
+// Frame.cc and Tracking.cc compile unchanged.
+//
+// mvImagePyramid (public, read by Frame::ComputeStereoMatches,
+// src/Frame.cc:524,619,633,639) is refreshed from the device after each call.
+// With ORB_AMD_GPU_STEREO defined (and integration/FrameStereo.cc replacing
+// Frame::ComputeStereoMatches) nothing reads it on the host, and the copy is
+// skipped: keypoints, descriptors and pyramids then stay in HBM for stereo.
+#include "ORBextractor.h"
+
+#include <cassert>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <opencv2/core/core.hpp>
+#include <opencv2/features2d/features2d.hpp>
+#include <opencv2/imgproc/imgproc.hpp>
+
+#include "orb_abi.h"
+
+using namespace cv;
+using namespace std;
+
+namespace ORB_SLAM2 {
+
+static_assert(sizeof(cv::KeyPoint) == sizeof(orb_keypoint_t), "cv::KeyPoint is 28 bytes");
+
+static void check(orb_status_t st, const char* what) {
+  if (st != ORB_OK)
+    throw std::runtime_error(std::string("ORBextractor::") + what + ": " + orb_status_string(st));
+}
+
+// src/ORBextractor.cc:428-489: the scale tables, per-level quotas and umax are
+// computed by the library with the reference's float/double expressions and
+// read back through the getters.
+ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST,
+                           int _minThFAST)
+    : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels),
+      iniThFAST(_iniThFAST), minThFAST(_minThFAST) {
+  const char* dev = getenv("ORB_AMD_DEVICE");
+  check(orb_extractor_create(nfeatures, (float)scaleFactor, nlevels, iniThFAST, minThFAST,
+                             dev ? atoi(dev) : 0, &mpGpu),
+        "ORBextractor");
+  mvScaleFactor.resize(nlevels);
+  orb_extractor_get_scale_factors(mpGpu, mvScaleFactor.data());
+  mvInvScaleFactor.resize(nlevels);
+  orb_extractor_get_inverse_scale_factors(mpGpu, mvInvScaleFactor.data());
+  mvLevelSigma2.resize(nlevels);
+  orb_extractor_get_scale_sigma_squares(mpGpu, mvLevelSigma2.data());
+  mvInvLevelSigma2.resize(nlevels);
+  orb_extractor_get_inverse_scale_sigma_squares(mpGpu, mvInvLevelSigma2.data());
+  mnFeaturesPerLevel.resize(nlevels);
+  orb_extractor_get_features_per_level(mpGpu, mnFeaturesPerLevel.data());
+  mvImagePyramid.resize(nlevels);
+}
+
+// src/ORBextractor.cc:1091-1169.  The mask is ignored, as in the reference.
+void ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoint>& _keypoints,
+                              OutputArray _descriptors) {
+  (void)_mask;
+  if (_image.empty()) return;  // :1095-1096, outputs untouched
+  Mat image = _image.getMat();
+  assert(image.type() == CV_8UC1);  // :1100
+  const int cap = orb_extractor_capacity(mpGpu, image.cols, image.rows);
+  if (cap < 0) throw std::runtime_error("ORBextractor::operator(): unsupported image size");
+  _keypoints.resize(cap);
+  Mat desc(cap, 32, CV_8U);
+  int n = 0;
+  check(orb_extractor_extract(mpGpu, image.ptr<uint8_t>(), image.cols, image.rows, image.step,
+                              reinterpret_cast<orb_keypoint_t*>(_keypoints.data()),
+                              desc.ptr<uint8_t>(), cap, &n),
+        "operator()");
+  _keypoints.resize(n);  // :1127-1128 clears and refills
+  if (n == 0)
+    _descriptors.release();  // :1118-1121
+  else
+    desc.rowRange(0, n).copyTo(_descriptors);
+#ifndef ORB_AMD_GPU_STEREO
+  for (int l = 0; l < nlevels; ++l) {
+    int w = 0, h = 0;
+    check(orb_extractor_pyramid_level(mpGpu, l, nullptr, 0, &w, &h), "mvImagePyramid");
+    mvImagePyramid[l].create(h, w, CV_8U);
+    check(orb_extractor_pyramid_level(mpGpu, l, mvImagePyramid[l].ptr<uint8_t>(),
+                                      mvImagePyramid[l].step, nullptr, nullptr),
+          "mvImagePyramid");
+  }
+#endif
+}
+
+}  // namespace ORB_SLAM2

@@ -1,0 +1,107 @@
+"""The reference-typed drop-ins (integration/*.cc) compile, and their stubs match
+the reference headers.
+
+integration/ORBmatcher.cc, ORBextractor.cc and FrameStereo.cc replace
+src/ORBmatcher.cc, src/ORBextractor.cc and Frame::ComputeStereoMatches.  OpenCV
+is not installed, so they are syntax-checked against
+tests/integration_stub/orb_slam2_decls.h (declarations only; nothing is linked
+and no reference source is compiled).  When the reference tree is present, the
+stub's ORB_SLAM2 declarations are checked against the reference headers:
+ORBmatcher's declarations are exactly include/ORBmatcher.h's, and every other
+stub declaration (Frame, KeyFrame, MapPoint, ORBextractor members the drop-ins
+use) appears in the reference header, except the documented additions marked
+INTEGRATION CHANGE."""
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from conftest import REFERENCE
+
+ROOT = Path(__file__).resolve().parents[1]
+STUB = ROOT / "tests" / "integration_stub"
+SOURCES = ["ORBmatcher.cc", "ORBextractor.cc", "FrameStereo.cc"]
+
+
+@pytest.mark.parametrize("src", SOURCES)
+def test_drop_in_compiles(src):
+    r = subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+                        "-I", str(STUB), "-I", str(ROOT / "include"),
+                        str(ROOT / "integration" / src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def _strip_comments(s):
+    s = re.sub(r"/\*.*?\*/", "", s, flags=re.S)
+    return re.sub(r"//[^\n]*", "", s)
+
+
+def _class_body(text, name):
+    m = re.search(r"\bclass\s+" + name + r"\b[^;{]*\{", text)
+    assert m, name
+    i, depth = m.end(), 1
+    j = i
+    while depth:
+        depth += {"{": 1, "}": -1}.get(text[j], 0)
+        j += 1
+    return text[i:j - 1]
+
+
+def _decls(body):
+    """Normalised member declarations: inline bodies removed, access
+    specifiers dropped, whitespace and std:: removed."""
+    prev = None
+    while prev != body:  # innermost {...} (function bodies, enum lists kept as text)
+        prev = body
+        body = re.sub(r"\)\s*(const\s*)?\{[^{}]*\}", r") \1;", body)
+    body = re.sub(r"\b(public|protected|private)\s*:", "", body)
+    out = set()
+    for d in body.split(";"):
+        d = re.sub(r"\s+", "", d.replace("std::", ""))
+        d = d.replace("inline", "")
+        if d:
+            out.add(d)
+    return out
+
+
+def _stub_decls(name, keep_changes=False):
+    raw = (STUB / "orb_slam2_decls.h").read_text()
+    body = _class_body(raw, name)
+    if not keep_changes:
+        body = "\n".join(l for l in body.splitlines() if "INTEGRATION CHANGE" not in l)
+    return _decls(_strip_comments(body))
+
+
+def _ref_decls(header, name):
+    return _decls(_class_body(_strip_comments((REFERENCE / "include" / header).read_text()), name))
+
+
+needs_ref = pytest.mark.skipif(not (REFERENCE / "include" / "ORBmatcher.h").exists(),
+                               reason="reference tree not mounted")
+
+
+@needs_ref
+def test_orbmatcher_declarations_are_the_references():
+    assert _stub_decls("ORBmatcher") == _ref_decls("ORBmatcher.h", "ORBmatcher")
+
+
+@needs_ref
+@pytest.mark.parametrize("name,header", [("ORBextractor", "ORBextractor.h"), ("Frame", "Frame.h"),
+                                         ("KeyFrame", "KeyFrame.h"), ("MapPoint", "MapPoint.h")])
+def test_stub_members_exist_in_reference(name, header):
+    missing = _stub_decls(name) - _ref_decls(header, name)
+    assert not missing, missing
+
+
+def test_every_orbmatcher_member_is_defined():
+    """One definition per declared overload (12 search/fuse members + the
+    constructor, DescriptorDistance and the three protected helpers)."""
+    src = _strip_comments((ROOT / "integration" / "ORBmatcher.cc").read_text())
+    defs = re.findall(r"\bORBmatcher::(\w+)\s*\(", src)
+    counts = {n: defs.count(n) for n in set(defs)}
+    assert counts == {"ORBmatcher": 1, "SearchByProjection": 4, "SearchByBoW": 2,
+                      "SearchForInitialization": 1, "SearchForTriangulation": 1,
+                      "SearchBySim3": 1, "Fuse": 2, "DescriptorDistance": 1,
+                      "RadiusByViewingCos": 1, "CheckDistEpipolarLine": 1,
+                      "ComputeThreeMaxima": 1}
