@@ -66,7 +66,8 @@ def algorithmic_bytes(w, h, scale, nlevels, n_kp, n_mp):
     match = 60 * n_mp + 48 * n_kp + 24576                  # SURVEY §8(d) B_lm
     octree = 8 * n_kp                                      # selected keys in, out (4 B each)
     blur = 2 * sum(P)                                      # read + write every level
-    return {"k_pyr_resize": pyr, "k_blur_levels": blur, "k_fast_band": fast, "k_octree": octree,
+    return {"k_pyr_resize": pyr, "k_blur_levels": blur, "k_fast_band": fast, "k_fast_cells": fast,
+            "k_octree": octree,
             "k_orient_desc": desc, "k_proj_candidates": match, "k_proj_resolve": 24 * n_mp,
             "k_grid_build": 32 * n_kp,
             "frame_total_survey": (2 * sum(P) - P[0]) + 60 * n_kp + match}

@@ -653,6 +653,293 @@ __global__ __launch_bounds__(256) void k_fast_band(
   }  // band loop
 }
 
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ============================================================ k_fast_cells
+// FAST per cell, one wave per cell (src/ORBextractor.cc:816-865), no
+// workgroup barriers: a wave stages its cell's ROI (cell + the 3-px FAST
+// border) as biased f16 in its own LDS slice, pretests 8 pixels per lane
+// (compass test, as k_fast_band), queues the candidates with wave ballots,
+// scores them (arc strengths), lists the corners (m > t), runs the cell-local
+// 3x3 NMS into a row bitmap and compacts it row by row (lane = window row).
+// A cell without a keypoint at iniThFAST reruns the same at minThFAST over
+// its window, keeping the strengths already computed (:846-850).  Output per
+// cell: keys in row-major window order (cv::FAST's order), packed
+// x | y << 12 | score << 24 in level coordinates, and their count.
+#define FC_WAVES 2      // waves per workgroup (LDS slices)
+#define FC_CPW 4        // cells per wave (software-pipelined ROI loads)
+#define FC_QCAP 1024    // candidate queue per wave (one pretest round adds <= 512)
+#define FC_CCAP 512     // corner list per wave; beyond it the NMS runs densely
+
+__host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
+  return maxRows * ((maxCols + 20) & ~7);
+}
+__host__ __device__ inline int fc_wave_bytes(int tileElems) {
+  // f16 tile + strengths + queue + corners + 64 rows x 64-bit bitmap
+  return ((3 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + 512) + 15) & ~15;
+}
+
+__global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
+    const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
+    const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
+    const OrbCellDesc* __restrict__ cells, uint32_t* __restrict__ cellKeys,
+    int32_t* __restrict__ cellCount, int tileElems) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int img = blockIdx.y;
+  unsigned char* wbase = smem + wave * fc_wave_bytes(tileElems);
+  uint32_t* tile32 = (uint32_t*)wbase;
+  const _Float16* tileh = (const _Float16*)wbase;
+  uint8_t* sc = wbase + 2 * tileElems;
+  uint16_t* queue = (uint16_t*)(sc + tileElems);
+  uint16_t* corners = queue + FC_QCAP;
+  uint32_t* bits = (uint32_t*)(corners + FC_CCAP);  // row y: words 2y, 2y+1
+  // this wave's cells: (blockIdx.x * FC_CPW + j) * FC_WAVES + wave, j < FC_CPW;
+  // the next cell's ROI is loaded into registers while this one is processed
+  auto cell_of = [&](int j) { return (blockIdx.x * FC_CPW + j) * FC_WAVES + wave; };
+  // ---- staging: lane r loads ROI row r, bytes [x0 - LPAD, x0 - LPAD + P)
+  // of level row y0 + r, as four 16-byte loads from the 4-aligned byte at or
+  // below its start (any caller stride), realigned in registers; every byte
+  // becomes a biased f16 (one v_perm per f16 pair: the bias byte comes from
+  // the constant operand)
+  uint32_t raw[16], rsh = 0;
+  auto issue = [&](const OrbCellDesc& q) {
+    const int ql = q.level, qR = q.y1 - q.y0;
+    const uint8_t* lvl;
+    int pitch;
+    if (ql == 0) {
+      lvl = img0 + (long long)img * img0Pitch;
+      pitch = img0Stride;
+    } else {
+      lvl = arena + (long long)img * arenaPitch + plan.lv[ql].arenaOff;
+      pitch = plan.lv[ql].pitch;
+    }
+    const ImgRsrc im = img_rsrc(lvl, (uint32_t)((plan.lv[ql].h - 1) * pitch + plan.lv[ql].w));
+    const int r = min(lane, max(qR - 1, 0));
+    const uint32_t o = (uint32_t)((q.y0 + r) * pitch + q.x0 - FAST_LPAD) + im.sh;
+    rsh = o & 3u;
+    const uint32_t a0 = o & ~3u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(im.r, (int)(a0 + 16 * k), 0, 0);
+      raw[4 * k] = (uint32_t)v[0];
+      raw[4 * k + 1] = (uint32_t)v[1];
+      raw[4 * k + 2] = (uint32_t)v[2];
+      raw[4 * k + 3] = (uint32_t)v[3];
+    }
+  };
+  int ci = cell_of(0);
+  if (ci >= plan.ncells) return;
+  OrbCellDesc ncd = cells[ci];
+  issue(ncd);
+  for (int jc = 0; jc < FC_CPW && ci < plan.ncells; ++jc) {
+  const OrbCellDesc cd = ncd;
+  const int R = cd.y1 - cd.y0, C = cd.x1 - cd.x0;
+  const long long slot = (long long)img * plan.ncells + ci;
+  const bool tiny = R < 7 || C < 7;
+  const int P = (C + 20) & ~7, PD = P >> 1;
+  if (!tiny && lane < R) {
+    const int nS = P >> 2;  // source dwords per row (<= 14, host-checked)
+    uint4* dst = reinterpret_cast<uint4*>(tile32 + lane * PD);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (2 * k < nS) {
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(raw[2 * k + 1], raw[2 * k], rsh);
+        const uint32_t w1 = __builtin_amdgcn_alignbyte(raw[2 * k + 2], raw[2 * k + 1], rsh);
+        uint4 h;
+        h.x = __builtin_amdgcn_perm(0x64646464u, w0, 0x04010400u);
+        h.y = __builtin_amdgcn_perm(0x64646464u, w0, 0x04030402u);
+        h.z = __builtin_amdgcn_perm(0x64646464u, w1, 0x04010400u);
+        h.w = __builtin_amdgcn_perm(0x64646464u, w1, 0x04030402u);
+        dst[k] = h;
+      }
+    }
+  }
+  const int ciNext = jc + 1 < FC_CPW ? cell_of(jc + 1) : plan.ncells;
+  if (ciNext < plan.ncells) {
+    ncd = cells[ciNext];
+    issue(ncd);
+  }
+  if (tiny) {
+    if (lane == 0) cellCount[slot] = 0;
+    ci = ciNext;
+    continue;
+  }
+  const int iw = C - 6, ih = R - 6;
+  const int nK = (iw + 7) >> 3;  // 8-pixel groups per interior row
+  const int nvLast = iw - 8 * (nK - 1);
+  const unsigned long long outsideLast =
+      nvLast >= 8 ? 0ull : (0x0101010101010101ull << (8 * nvLast));
+  const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
+  const float invK = 1.0f / (float)nK, invP = 1.0f / (float)P, invW = 1.0f / (float)iw;
+  wave_lds_sync();
+
+  int nq = 0, nc = 0;  // wave-uniform queue / corner counts
+  // score the queued candidates, list the corners (m > t)
+  auto flush = [&](int t, bool fresh) {
+    for (int j0 = 0; j0 < nq; j0 += 64) {
+      const int j = j0 + lane;
+      bool corner = false;
+      int off = 0;
+      if (j < nq) {
+        off = queue[j];
+        int m;
+        if (fresh) {  // the 16 ring reads go out with the strength read
+          const int s = min(max(fast_score(tileh + off, P), 0), 255);
+          m = sc[off];
+          if (m == 0) {
+            m = s;
+            sc[off] = (uint8_t)m;
+          }
+        } else {
+          m = sc[off];  // 0: not scored yet; phase B keeps phase-A strengths
+          if (m == 0) {
+            m = min(max(fast_score(tileh + off, P), 0), 255);
+            sc[off] = (uint8_t)m;
+          }
+        }
+        corner = m > t && m >= 2;
+      }
+      const unsigned long long bal = __ballot(corner);
+      const int pos = nc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      if (corner && pos < FC_CCAP) corners[pos] = (uint16_t)off;
+      nc += __popcll(bal);
+    }
+    nq = 0;
+  };
+  // one FAST pass at threshold t over the window: pretest, queue, strengths, corners
+  auto fast_pass = [&](int t, bool fresh) {
+    h16x2 T;
+    T.x = T.y = (_Float16)(float)(t + 1);
+    const int nG = ih * nK;
+    for (int g0 = 0; g0 < nG; g0 += 64) {
+      const int gi = g0 + lane;
+      uint32_t rp[4] = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+      int off = 0;
+      if (gi < nG) {
+        const int rr = (int)(((float)gi + 0.5f) * invK), k = gi - rr * nK;
+        const int r = rr + 3;
+        off = r * P + 8 + 8 * k;  // element of interior column 8k
+        const uint32_t* row = tile32 + r * PD + 4 + 4 * k;
+        const uint2 a = *reinterpret_cast<const uint2*>(row - 2);
+        const uint4 b = *reinterpret_cast<const uint4*>(row);
+        const uint2 c = *reinterpret_cast<const uint2*>(row + 4);
+        const uint4 u = *reinterpret_cast<const uint4*>(row + 3 * PD);  // circle 0 (y + 3)
+        const uint4 d = *reinterpret_cast<const uint4*>(row - 3 * PD);  // circle 8 (y - 3)
+        const uint32_t D[8] = {a.x, a.y, b.x, b.y, b.z, b.w, c.x, c.y};
+        const uint32_t U[4] = {u.x, u.y, u.z, u.w}, Dn[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t q4 = __builtin_amdgcn_alignbyte(D[i + 4], D[i + 3], 2);   // x + 3
+          const uint32_t q12 = __builtin_amdgcn_alignbyte(D[i + 1], D[i], 2);      // x - 3
+          rp[i] = pretest_pair(D[i + 2], U[i], q4, Dn[i], q12, T);
+        }
+        if (fresh) {  // strengths start at 0, FAST_OUTSIDE past the interior
+          const unsigned long long z = k == nK - 1 ? outsideLast : 0ull;
+          *reinterpret_cast<unsigned long long*>(sc + off) = z;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t w = rp[j >> 1];
+        const bool pass = (j & 1) ? ((int)w >= 0) : ((short)(w & 0xFFFFu) >= 0);
+        const unsigned long long bj = __ballot(pass);
+        const int pos = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bj, 0u));
+        if (pass) queue[pos] = (uint16_t)(off + j);
+        nq += __popcll(bj);
+      }
+      if (nq > FC_QCAP - 512 || g0 + 64 >= nG) {
+        wave_lds_sync();
+        flush(t, fresh);
+        wave_lds_sync();
+      }
+    }
+  };
+  // cell-local NMS at t into the row bitmap: a corner survives iff no
+  // neighbour inside the window has nb > t && nb >= m (outside counts as 0)
+  auto nms = [&](int t) {
+    for (int i = lane; i < 2 * ih; i += 64) bits[i] = 0;
+    wave_lds_sync();
+    const bool dense = nc > FC_CCAP;
+    const int nItems = dense ? ih * iw : nc;
+    for (int j = lane; j < nItems; j += 64) {
+      int x, y, off;
+      if (dense) {
+        y = (int)(((float)j + 0.5f) * invW);
+        x = j - y * iw;
+        off = (y + 3) * P + (x + 8);
+      } else {
+        off = corners[j];
+        const int ry = (int)(((float)off + 0.5f) * invP);
+        y = ry - 3;
+        x = off - ry * P - 8;
+      }
+      const uint8_t* cp = sc + off;
+      const int m = cp[0];
+      const int r0 = cp[-P - 1], r1 = cp[-P], r2 = cp[-P + 1], r3 = cp[-1], r4 = cp[1],
+                r5 = cp[P - 1], r6 = cp[P], r7 = cp[P + 1];
+      if (m <= t || m < 2) continue;
+      const bool L = x > 0, Rt = x < iw - 1, U = y > 0, D = y < ih - 1;
+      const int nb[8] = {(U && L) ? r0 : 0, U ? r1 : 0, (U && Rt) ? r2 : 0, L ? r3 : 0,
+                         Rt ? r4 : 0, (D && L) ? r5 : 0, D ? r6 : 0, (D && Rt) ? r7 : 0};
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ok = ok && !(nb[k] > t && nb[k] >= m);
+      if (ok) atomicOr(&bits[2 * y + (x >> 5)], 1u << (x & 31));
+    }
+    wave_lds_sync();
+  };
+  // keys of the window in row-major order (lane = window row, ih <= 64)
+  uint32_t* out = cellKeys + slot * plan.keyCap;
+  auto compact = [&]() -> int {
+    unsigned long long row = 0ull;
+    if (lane < ih) {
+      const uint2 w = *reinterpret_cast<const uint2*>(bits + 2 * lane);
+      row = (unsigned long long)w.x | ((unsigned long long)w.y << 32);
+    }
+    const int cnt = __popcll(row);
+    const int incl = wave_incl_scan(cnt);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    int o = incl - cnt;
+    const uint8_t* srow = sc + (lane + 3) * P + 8;
+    const uint32_t kx = (uint32_t)(cd.x0 + 3), ky = (uint32_t)(cd.y0 + 3 + lane);
+    while (row) {
+      const int x0 = __builtin_ctzll(row);
+      row &= row - 1;
+      const bool two = row != 0;
+      const int x1 = two ? __builtin_ctzll(row) : x0;
+      if (two) row &= row - 1;
+      const int m0 = srow[x0], m1 = srow[x1];
+      out[o] = pack_key(kx + x0, ky, m0 - 1);
+      if (two) out[o + 1] = pack_key(kx + x1, ky, m1 - 1);
+      o += two ? 2 : 1;
+    }
+    return total;
+  };
+  // ---- phase A at iniThFAST
+  fast_pass(ti, true);
+  nms(ti);
+  int n = compact();
+  if (n == 0 && tm != ti) {
+    // ---- phase B: no keypoint at iniThFAST -> minThFAST (:846-850)
+    nc = 0;
+    fast_pass(tm, false);
+    nms(tm);
+    n = compact();
+  }
+  if (lane == 0) cellCount[slot] = n;
+  ci = ciNext;
+  wave_lds_sync();  // the next cell's staging overwrites the tile
+  }  // cell loop
+}
+
 #ifdef ORB_FAST_STAMPS
 extern "C" hipError_t orb_k_fast_stamps(void* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fast_stamps), sizeof(g_fast_stamps));
@@ -1389,11 +1676,6 @@ struct DescWaveLds {
   uint32_t rsp[2][DESC_RS_PAIRS][DESC_RS_DW];
 };
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 #define DESC_PPW 4  // slot pairs per wave (software-pipelined: the next pair's window loads overlap this one)
 
@@ -1740,6 +2022,37 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
   dim3 grid((nbands + perWg - 1) / perWg, nimg), block(256);
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, *plan, bands, cells, nbands, cellKeys, cellCount);
+  return hipGetLastError();
+}
+
+// k_fast_cells: LDS per workgroup for cells of at most maxRows x maxCols
+// (ROI incl. the 3-px border)
+// k_fast_cells stages one ROI row per lane (every ORB-SLAM2 configuration;
+// the larger cells of tiny levels go to k_fast_band)
+bool orb_k_fast_cells_fits(const OrbPlanDesc* plan) {
+  // lane = ROI row (<= 64 rows); a row's P <= 56 bytes (+3 realign) in four 16-byte loads
+  return plan->maxCellRows <= 64 && ((plan->maxCellCols + 20) & ~7) <= 56;
+}
+
+size_t orb_k_fast_cells_lds(int maxRows, int maxCols) {
+  return (size_t)FC_WAVES * fc_wave_bytes(fc_tile_elems(maxRows, maxCols));
+}
+
+hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                            const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
+                            int nimg, hipStream_t s) {
+  const int tileElems = fc_tile_elems(plan->maxCellRows, plan->maxCellCols);
+  const size_t lds = orb_k_fast_cells_lds(plan->maxCellRows, plan->maxCellCols);
+  if (!orb_k_fast_cells_fits(plan)) return hipErrorInvalidValue;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fast_cells,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  dim3 grid((plan->ncells + FC_WAVES * FC_CPW - 1) / (FC_WAVES * FC_CPW), nimg), block(64 * FC_WAVES);
+  hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
+                     arenaPitch, *plan, cells, cellKeys, cellCount, tileElems);
   return hipGetLastError();
 }
 

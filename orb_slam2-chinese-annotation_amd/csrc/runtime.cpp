@@ -28,6 +28,12 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             int dh, const int* xofs, const void* alpha, const int* yofs,
                             const void* beta, int xmax, int nimg, hipStream_t s);
 size_t orb_k_fast_band_lds(int bandElems);
+size_t orb_k_fast_cells_lds(int maxRows, int maxCols);
+bool orb_k_fast_cells_fits(const OrbPlanDesc* plan);
+hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
+                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
+                            const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
+                            int nimg, hipStream_t s);
 hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
@@ -670,9 +676,19 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   }
   PROF_REC(ev, pf.e(ev, 0), s);
   PROF_REC(ev, pf.b(ev, 2), s);
-  HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                          h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
-                          h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
+  static const bool bandFast = getenv("ORB_FAST_BANDS") && atoi(getenv("ORB_FAST_BANDS")) > 0;
+  // k_fast_cells (one wave per cell) unless a tiny level's cells outgrow its
+  // staging; k_fast_band (one workgroup per run of cells) otherwise or on request
+  const bool useBands = bandFast || !orb_k_fast_cells_fits(&P);
+  pf.names[2] = useBands ? "k_fast_band" : "k_fast_cells";
+  if (useBands)
+    HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                            h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
+                            h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
+  else
+    HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                             h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
+                             h->dCellCount.as<int32_t>(), B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
   const bool split = split_blur();
   if (split) {
