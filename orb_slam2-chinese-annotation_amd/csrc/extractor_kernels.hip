@@ -670,8 +670,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // its window, keeping the strengths already computed (:846-850).  Output per
 // cell: keys in row-major window order (cv::FAST's order), packed
 // x | y << 12 | score << 24 in level coordinates, and their count.
-#define FC_WAVES 2      // waves per workgroup (LDS slices)
+#ifndef FC_WAVES
+#define FC_WAVES 1      // waves per workgroup (LDS slices; swept 1-4)
+#endif
+#ifndef FC_CPW
 #define FC_CPW 4        // cells per wave (software-pipelined ROI loads)
+#endif
 #define FC_QCAP 1024    // candidate queue per wave (one pretest round adds <= 512)
 #define FC_CCAP 512     // corner list per wave; beyond it the NMS runs densely
 
@@ -1663,10 +1667,11 @@ __global__ __launch_bounds__(256) void k_orient_desc_split(
 //   IC_Angle (:77-113) from the staged rows in registers (rows 6..36).
 //   row pass: task (row pair, 4-column group): u16 row sums of both rows,
 //     packed (row 2p | row 2p+1 << 16) per column: 2.5 v_dot4 per sum.
-//   column pass: task (output row pair, group): four v_dot2 per output over
-//     the packed row pairs, (sum + 2^15) >> 16 saturated -> the blurred patch,
-//     written over the raw rows it no longer needs.
-//   rBRIEF (:119-164): 512 byte reads from the patch, ballots.
+//   rBRIEF (:119-164): each of the 512 samples takes the column pass of its
+//     own pixel -- four v_dot2 over the packed row-sum pairs (the weights of
+//     the row's parity), (sum + 2^15) >> 16 saturated -- instead of a column
+//     pass over the whole 37 x 37 patch (about a third of its pixels are
+//     sampled); ballots.
 #define DESC_RAW_DW 12   // raw / patch row pitch (dwords)
 #define DESC_RAW_ROWS 44 // 43 staged rows + the odd row of the last row-sum pair
 #define DESC_RS_DW 40    // row-sum pair row pitch (dwords): 10 groups of 4 columns
@@ -1866,37 +1871,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     m10 = half_sum(m10);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
     wave_lds_sync();
-    // ---- column pass: blurred patch row y (level row cy-18+y) reads row-sum
-    // rows y .. y+6 = pairs y/2 .. y/2+3, weights (k0,k1)(k2,k3)(k4,k5)(k6,0)
-    // for even y, (0,k0)(k1,k2)(k3,k4)(k5,k6) for odd y
-#pragma unroll
-    for (int it = 0; it < (19 * 10 + 31) / 32; ++it) {
-      const int t = hl + 32 * it;
-      if (t < 19 * 10) {
-        const int q = t / 10, g = t - 10 * q;
-        uint4 pv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) pv[k] = *reinterpret_cast<const uint4*>(&rsp[q + k][4 * g]);
-        uint32_t packedE = 0, packedO = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          uint32_t se = 1u << 15, so = 1u << 15;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t wv = c == 0 ? pv[k].x : (c == 1 ? pv[k].y : (c == 2 ? pv[k].z : pv[k].w));
-            const u16x2 v = __builtin_bit_cast(u16x2, wv);
-            se = __builtin_amdgcn_udot2(v, k == 0 ? E0 : (k == 1 ? E1 : (k == 2 ? E2 : E3)), se, false);
-            so = __builtin_amdgcn_udot2(v, k == 0 ? O0 : (k == 1 ? O1 : (k == 2 ? O2 : O3)), so, false);
-          }
-          int ve = min((int)(se >> 16), 255), vo = min((int)(so >> 16), 255);
-          __asm__ volatile("" : "+v"(ve), "+v"(vo));  // see k_pyr_resize: keep the byte pack opaque
-          packedE |= (uint32_t)ve << (8 * c);
-          packedO |= (uint32_t)vo << (8 * c);
-        }
-        raw[2 * q][g] = packedE;
-        if (2 * q + 1 < 37) raw[2 * q + 1][g] = packedO;
-      }
-    }
+    // ---- rBRIEF sampling the blur directly: blurred pixel (ry, rx) of the
+    // patch = column pass of row-sum rows 18+ry .. 24+ry at column 18+rx,
+    // i.e. the four pairs (18+ry)/2 .. +3 with the parity's weights
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float a, b;
     {
@@ -1905,17 +1882,29 @@ __global__ __launch_bounds__(256) void k_orient_desc(
       a = cs;
       b = sn;
     }
-    wave_lds_sync();
-    // ---- rBRIEF: the patch centre (0, 0) is patch row 18, column 18
-    const uint8_t* pb = reinterpret_cast<const uint8_t*>(&raw[18][0]) + 18;
+    const uint32_t wE[4] = {__builtin_bit_cast(uint32_t, E0), __builtin_bit_cast(uint32_t, E1),
+                            __builtin_bit_cast(uint32_t, E2), __builtin_bit_cast(uint32_t, E3)};
+    const uint32_t wO[4] = {__builtin_bit_cast(uint32_t, O0), __builtin_bit_cast(uint32_t, O1),
+                            __builtin_bit_cast(uint32_t, O2), __builtin_bit_cast(uint32_t, O3)};
+    auto blurred = [&](int ry, int rx) -> int {
+      const int y = ry + 18;
+      const uint32_t* p = &rsp[y >> 1][rx + 18];
+      uint32_t s = 1u << 15;
+      const bool odd = y & 1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        s = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p[k * DESC_RS_DW]),
+                                   __builtin_bit_cast(u16x2, odd ? wO[k] : wE[k]), s, false);
+      return min((int)(s >> 16), 255);
+    };
     unsigned long long words[8];
 #pragma unroll
     for (int kq = 0; kq < 8; ++kq) {
       const int test = hl + 32 * kq;
       const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
       const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
-      const int v0 = pb[__mul24(cv_round(px0 * b + py0 * a), DESC_RAW_DW * 4) + cv_round(px0 * a - py0 * b)];
-      const int v1 = pb[__mul24(cv_round(px1 * b + py1 * a), DESC_RAW_DW * 4) + cv_round(px1 * a - py1 * b)];
+      const int v0 = blurred(cv_round(px0 * b + py0 * a), cv_round(px0 * a - py0 * b));
+      const int v1 = blurred(cv_round(px1 * b + py1 * a), cv_round(px1 * a - py1 * b));
       words[kq] = __ballot(v0 < v1);
     }
     if (P.active && hl == 0) {
