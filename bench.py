@@ -80,7 +80,13 @@ def shard_frames(rank, frames):
 
 
 def gather_counts(dist, counts, out):
-    """RCCL all-gather of every frame's keypoint count (int32 per frame)."""
+    """RCCL all-gather of every frame's keypoint count (int32 per frame).  With
+    the gloo backend (the multi-process test on one GPU) through host copies."""
+    if dist.get_backend() == "gloo":
+        parts = [c.cpu() for c in out.chunk(dist.get_world_size())]
+        dist.all_gather(parts, counts.cpu())
+        out.copy_(__import__("torch").cat(parts))
+        return out
     dist.all_gather_into_tensor(out, counts)
     return out
 
@@ -322,6 +328,9 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3 / C5 extra keys")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input synthesis")
     ap.add_argument("--seed", type=int, default=0x4B495454)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the measured path); gloo only for the multi-rank test "
+                         "on one GPU (ORB_BENCH_DEVICE pins every rank to one device)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,11 +338,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
+    if os.environ.get("ORB_BENCH_DEVICE") is not None:
+        local = int(os.environ["ORB_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     orb = load_package()
     W, H, B, NF, M = args.width, args.height, args.batch, args.features, args.mappoints
     D = args.frames
@@ -440,10 +454,20 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     if dist is not None:
-        elapsed = max_over_ranks(dist, elapsed, dev)
+        elapsed = max_over_ranks(dist, elapsed, dev if args.dist_backend == "nccl" else "cpu")
     for st in sets:
         if int(st["cnt"].min().item()) < 0:
             raise RuntimeError("extraction reported a failed frame (negative count)")
+    gather_ok = None
+    if dist is not None:  # the gathered counts of this rank's last launch are its own
+        j = (g - 1) % 2
+        mine = sets[j]["gathered"][rank * B:(rank + 1) * B]
+        gather_ok = bool(torch.equal(mine, sets[j]["cnt"]))
+        ok = torch.tensor([1 if gather_ok else 0], dtype=torch.int32)
+        if args.dist_backend == "nccl":
+            ok = ok.to(dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        gather_ok = bool(ok.item())
 
     # per-kernel HIP-event times over the timed region, each on its own stream.
     # The extract stream is the critical path (the matcher stream runs in its
@@ -516,7 +540,9 @@ def main():
             "distinct_frames_per_gpu": D,
             "frames_per_launch": B,
             "timed_region_s": elapsed,
-            "parallelism": f"frames sharded over {world} rank(s), RCCL all-gather of counts",
+            "parallelism": f"frames sharded over {world} rank(s), "
+                           f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-gather of counts",
+            "count_gather_verified": gather_ok,
             "mean_keypoints_per_frame": n_kp,
             "mean_matches_per_frame": nmatch,
         },

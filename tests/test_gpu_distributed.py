@@ -1,0 +1,41 @@
+"""The sharded bench path with two ranks on the GPU box: each
+rank extracts and matches its own block of the synthetic sequence and the
+per-frame keypoint counts are all-gathered every launch.  The box has one GPU,
+so both ranks are pinned to it (ORB_BENCH_DEVICE) and the collective runs on
+gloo (RCCL does not take two ranks on one device); the 8-GPU RCCL run is the
+driver's scaling bench."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_ranks_shard_and_gather(gpu):
+    env = dict(os.environ, ORB_BENCH_DEVICE="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--dist-backend", "gloo", "--frames", "512", "--steps", "2", "--warmup", "1",
+           "--no-cpu", "--no-secondary", "--threads", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["scaling"] == "weak"
+    assert res["config"]["frames_per_gpu_per_step"] == 512
+    assert res["config"]["count_gather_verified"] is True
+    # whole-job value = frames of both ranks / the slowest rank's time
+    assert abs(res["value"] - 2 * 512 * res["steps"] / (res["ms_per_step"] * 1e-3 * res["steps"])) \
+        < 1e-6 * res["value"]
