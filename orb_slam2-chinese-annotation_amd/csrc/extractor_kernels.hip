@@ -1657,30 +1657,28 @@ __global__ __launch_bounds__(256) void k_orient_desc_split(
 // The blurred level is never materialised: descriptors sample only the 37 x 37
 // blurred patch around a keypoint (rotated pattern within +-18 px), and that
 // patch depends only on the 43 x 43 raw window around it, so each keypoint
-// blurs its own window in LDS (src/ORBextractor.cc:1141-1151 blurs the whole
-// level, then samples it; the bytes sampled are identical).
-//   staging: raw rows cy-21 .. cy+21 (lane hl: rows hl, hl + 32), realigned
-//     so byte b of LDS row r is column cx-21+b; rows outside the level are
-//     reflected (REFLECT_101) when addressed, columns outside it patched
-//     bytewise from their reflected columns (keypoints sit >= 19 px inside,
-//     so a window overhangs by at most 2 columns / rows per side).
-//   IC_Angle (:77-113) from the staged rows in registers (rows 6..36).
-//   row pass: task (row pair, 4-column group): u16 row sums of both rows,
-//     packed (row 2p | row 2p+1 << 16) per column: 2.5 v_dot4 per sum.
+// blurs its own window (src/ORBextractor.cc:1141-1151 blurs the whole level,
+// then samples it; the bytes sampled are identical).
+//   staging: lane hl < 22 loads raw rows cy-21+2hl and cy-21+2hl+1 (three
+//     16-byte loads each) and realigns them in registers so byte b is column
+//     cx-21+b; rows outside the level are reflected (REFLECT_101) when
+//     addressed, columns outside it patched bytewise from their reflected
+//     columns through LDS (keypoints sit >= 19 px inside, so a window
+//     overhangs by at most 2 columns / rows per side).
+//   IC_Angle (:77-113) from the rows in registers (rows 6..36).
+//   row pass, from registers: the lane's two rows, ten 4-column groups of
+//     u16 row sums (2.5 v_dot4 per sum), packed (row 2p | row 2p+1 << 16) and
+//     stored as row-sum pair p in LDS (the only LDS the kernel uses).
 //   rBRIEF (:119-164): each of the 512 samples takes the column pass of its
 //     own pixel -- four v_dot2 over the packed row-sum pairs (the weights of
 //     the row's parity), (sum + 2^15) >> 16 saturated -- instead of a column
 //     pass over the whole 37 x 37 patch (about a third of its pixels are
 //     sampled); ballots.
-#define DESC_RAW_DW 12   // raw / patch row pitch (dwords)
-#define DESC_RAW_ROWS 44 // 43 staged rows + the odd row of the last row-sum pair
 #define DESC_RS_DW 40    // row-sum pair row pitch (dwords): 10 groups of 4 columns
-#define DESC_RS_PAIRS 22
+#define DESC_RS_PAIRS 22 // 43 rows + the unused odd row of the last pair
 struct DescWaveLds {
-  uint32_t raw[2][DESC_RAW_ROWS][DESC_RAW_DW];
   uint32_t rsp[2][DESC_RS_PAIRS][DESC_RS_DW];
 };
-
 
 #define DESC_PPW 4  // slot pairs per wave (software-pipelined: the next pair's window loads overlap this one)
 
@@ -1710,9 +1708,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const int slot = 2 * (pairBase + 4 * (lane >> 1)) + (lane & 1);
     if (slot < plan.slotsPerImage) keyv = imgKeys[slot];
   }
-  uint32_t (*raw)[DESC_RAW_DW] = sm[w].raw[half];
   uint32_t (*rsp)[DESC_RS_DW] = sm[w].rsp[half];
-  const bool second = hl < 43 - 32;  // this lane also stages row hl + 32
+  // lane hl < 22 holds rows 2 hl and 2 hl + 1 (row 43 only feeds a zero weight)
+  const bool second = hl < DESC_RS_PAIRS;
   // A pair is valid when its first slot holds a keypoint of its level; the
   // second half-wave duplicates the first when the level's count is odd.
   struct Pair {
@@ -1770,16 +1768,18 @@ __global__ __launch_bounds__(256) void k_orient_desc(
       }
       return o & 3u;
     };
-    sha = load_row(hl, ra);
-    if (second) shb = load_row(hl + 32, rb);
+    if (second) {
+      sha = load_row(2 * hl, ra);
+      shb = load_row(2 * hl + 1, rb);
+    }
   };
   auto realign = [&](uint32_t* d, uint32_t sh) {
 #pragma unroll
     for (int k = 0; k < 11; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
     d[11] = __builtin_amdgcn_alignbyte(0u, d[11], sh);
   };
-  auto store_row = [&](int r, const uint32_t* d) {
-    uint4* dst = reinterpret_cast<uint4*>(raw[r]);
+  auto store_row = [&](uint32_t* rowp, const uint32_t* d) {
+    uint4* dst = reinterpret_cast<uint4*>(rowp);
     dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
     dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
     dst[2] = make_uint4(d[8], d[9], d[10], d[11]);
@@ -1797,35 +1797,33 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   if (cur.valid) issue(cur);
   for (int j = 0; j < DESC_PPW; ++j) {
     const Pair P = cur;
-    if (P.valid) {
+    if (P.valid && second) {
       realign(ra, sha);
-      store_row(hl, ra);
-      if (second) {
-        realign(rb, shb);
-        store_row(hl + 32, rb);
-      }
+      realign(rb, shb);
     }
     // ---- IC_Angle from the rows in registers: row v = ri - 15 is staged row
     // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
     // by one byte).  m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
     int m01 = 0, m10 = 0;
-    if (P.valid && hl != 5) {
-      const bool useA = hl >= 6;
-      const int ri = useA ? hl - 6 : hl + 26;
+    auto ic_row = [&](const uint32_t* d, int ri) {  // staged row ri + 6, ri in [0, 31)
       uint32_t rs = 0, rm = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const uint32_t lo = useA ? ra[k + 1] : rb[k + 1], hi = useA ? ra[k + 2] : rb[k + 2];
-        const uint32_t d = __builtin_amdgcn_alignbyte(hi, lo, 1) & c_icmask[ri][k];
+        const uint32_t dd = __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], 1) & c_icmask[ri][k];
         const uint32_t wt = (uint32_t)(4 * k) * 0x01010101u + 0x03020100u;
-        rs = __builtin_amdgcn_udot4(d, 0x01010101u, rs, false);
-        rm = __builtin_amdgcn_udot4(d, wt, rm, false);
+        rs = __builtin_amdgcn_udot4(dd, 0x01010101u, rs, false);
+        rm = __builtin_amdgcn_udot4(dd, wt, rm, false);
       }
-      m10 = (int)rm - 16 * (int)rs;
-      m01 = (ri - 15) * (int)rs;
+      m10 += (int)rm - 16 * (int)rs;
+      m01 += (ri - 15) * (int)rs;
+    };
+    if (P.valid && second) {
+      if (2 * hl >= 6 && 2 * hl <= 36) ic_row(ra, 2 * hl - 6);
+      if (2 * hl + 1 >= 6 && 2 * hl + 1 <= 36) ic_row(rb, 2 * hl + 1 - 6);
     }
-    // the next pair's window loads go out now and land during this pair's work
-    if (j + 1 < DESC_PPW) {
+    // (the rows stay in registers through the row pass: the next pair's loads
+    // go out after it)
+    if (!P.valid && j + 1 < DESC_PPW) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
@@ -1833,28 +1831,35 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const OrbLevelDesc& L = plan.lv[P.l];
     const int cx = P.cx, cy = P.cy, colA = cx - 21;
     if (colA < 0 || cx + 21 >= L.w) {
-      // window overhangs a level column edge: bytes of columns < 0 or >= w take
-      // their REFLECT_101 column (in range and inside the window); each lane
-      // patches the rows it staged
-      wave_lds_sync();
-      for (int s = 0; s < (second ? 2 : 1); ++s) {
-        uint8_t* rp = reinterpret_cast<uint8_t*>(raw[hl + 32 * s]);
-        for (int b = 0; b < -colA; ++b) rp[b] = rp[-(colA + b) - colA];
-        for (int b = max(L.w - colA, 0); b < 43; ++b) rp[b] = rp[2 * L.w - 2 - (colA + b) - colA];
-      }
-    }
-    wave_lds_sync();
-    // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
+      // window overhangs a level column edge: the lane's two rows go through
+      // the (not yet used) row-sum area, where the bytes of columns < 0 or >= w
+      // take their REFLECT_101 column, and come back patched
+      uint32_t* scr = &rsp[0][0] + 24 * hl;  // rows 2 hl, 2 hl + 1: 12 dwords each
+      if (second) {
+        store_row(scr, ra);
+        store_row(scr + 12, rb);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          uint8_t* rp = reinterpret_cast<uint8_t*>(scr + 12 * s2);
+          for (int b = 0; b < -colA; ++b) rp[b] = rp[-(colA + b) - colA];
+          for (int b = max(L.w - colA, 0); b < 43; ++b) rp[b] = rp[2 * L.w - 2 - (colA + b) - colA];
+        }
 #pragma unroll
-    for (int it = 0; it < (DESC_RS_PAIRS * 10 + 31) / 32; ++it) {
-      const int t = hl + 32 * it;
-      if (t < DESC_RS_PAIRS * 10) {
-        const int p = t / 10, g = t - 10 * p;
+        for (int k = 0; k < 12; ++k) {
+          ra[k] = scr[k];
+          rb[k] = scr[12 + k];
+        }
+      }
+      wave_lds_sync();
+    }
+    // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
+    if (second) {  // the lane's row pair from registers, group by group
+#pragma unroll
+      for (int g = 0; g < 10; ++g) {
         uint32_t o[2][4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const uint32_t* rw = raw[2 * p + h] + g;
-          const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
+          const uint32_t* rw = h ? rb : ra;
+          const uint32_t w0 = rw[g], w1 = rw[g + 1], w2 = rw[g + 2];
           o[h][0] = __builtin_amdgcn_udot4(w0, T0a, __builtin_amdgcn_udot4(w1, T0b, 0u, false), false);
           o[h][1] = __builtin_amdgcn_udot4(w0, T1a, __builtin_amdgcn_udot4(w1, T1b, 0u, false), false);
           o[h][2] = __builtin_amdgcn_udot4(w0, T2a, __builtin_amdgcn_udot4(w1, T2b,
@@ -1862,10 +1867,14 @@ __global__ __launch_bounds__(256) void k_orient_desc(
           o[h][3] = __builtin_amdgcn_udot4(w0, T3a, __builtin_amdgcn_udot4(w1, T3b,
                                            __builtin_amdgcn_udot4(w2, T3c, 0u, false), false), false);
         }
-        *reinterpret_cast<uint4*>(&rsp[p][4 * g]) =
+        *reinterpret_cast<uint4*>(&rsp[hl][4 * g]) =
             make_uint4(o[0][0] | (o[1][0] << 16), o[0][1] | (o[1][1] << 16),
                        o[0][2] | (o[1][2] << 16), o[0][3] | (o[1][3] << 16));
       }
+    }
+    if (j + 1 < DESC_PPW) {
+      cur = setup(j + 1);
+      if (cur.valid) issue(cur);
     }
     m01 = half_sum(m01);
     m10 = half_sum(m10);
