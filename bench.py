@@ -514,8 +514,9 @@ def main():
                 "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS}
     roof.update({
         "traffic": traffic,
-        "traffic_source": f"profiles/{traffic_src} (rocprofv3 FETCH_SIZE+WRITE_SIZE, "
-                          "separate passes)" if traffic_src else None,
+        "traffic_source": f"profiles/{traffic_src} (rocprofv3 FETCH_SIZE x 2 (gfx950 "
+                          "calibration, profiles/r02_fetch_calib.txt) + WRITE_SIZE, separate "
+                          "passes)" if traffic_src else None,
         "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_launch": dom_bytes},
         "ms_per_launch": dom_ms_per_launch,

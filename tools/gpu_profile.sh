@@ -21,6 +21,8 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$O/pmcw_$TAG" -o run --output-f
   -- python3 "$R/bench.py" --no-cpu --no-secondary --frames 512 --steps 2 --warmup 1 > "$O/pmcw_$TAG.json" 2> "$O/pmcw_$TAG.err"
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib_$TAG" -o run --output-format csv \
   -- "$R/tools/probe/fetch_calib" > "$O/calib_$TAG.log" 2>&1
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d "$O/calibw_$TAG" -o run --output-format csv \
+  -- "$R/tools/probe/fetch_calib" > "$O/calibw_$TAG.log" 2>&1
 cd "$R"
 bash tools/gpu_pmc.sh "$TAG" --frames 512 --no-secondary
 echo done

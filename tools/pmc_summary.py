@@ -4,11 +4,11 @@ bytes per launch, the `traffic` figure bench.py reports.
 
 Usage: tools/pmc_summary.py <fetch_dir> <write_dir> <batch> <out.json>
 
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Values are reported raw (no
-x2 correction): the gfx950 halving applies to 16-B/lane streaming loads, and our
-kernels load bytes and dwords; on k_pyr_resize (dword loads, known byte count)
-raw FETCH_SIZE matches the algorithmic read bytes within a few per cent
-(DESIGN.md §5).
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  FETCH_SIZE is doubled: on
+gfx950 it reports half the bytes of every load shape the kernels use --
+dword, 16-B and 64-B-per-lane reads of a known 1 GiB all read back as 0.5 GiB
+(tools/probe/fetch_calib.hip, profiles/r02_fetch_calib.txt).  WRITE_SIZE is
+used raw (exact for the same probe's dword and 16-B stores).
 """
 import collections
 import csv
@@ -28,7 +28,8 @@ def per_kernel(d, counter):
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(Path(d) / "run_counter_collection.csv")):
         if r["Counter_Name"] == counter:
-            vals[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+            scale = 2.0 if counter == "FETCH_SIZE" else 1.0  # calibrated, see above
+            vals[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0 * scale)
     return vals
 
 

@@ -1,4 +1,4 @@
-// FETCH_SIZE calibration (development probe): rocprofv3 --pmc FETCH_SIZE over
+// FETCH_SIZE / WRITE_SIZE calibration (development probe): rocprofv3 --pmc FETCH_SIZE over
 // kernels that each read a known, disjoint 1 GiB once, with the load shapes
 // the extractor uses.  MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes
 // of 16-B/lane coalesced streaming reads and is uncalibrated for other widths.
@@ -7,7 +7,8 @@
 //   row64      64 B per lane (four 16-B loads), lane = row of a 1 KiB-pitch
 //              image: k_fast_cells' ROI staging (one row per lane), 64-B aligned
 //   row64u     the same starting 4 bytes past alignment (caller strides)
-// Run: rocprofv3 --pmc FETCH_SIZE -d <dir> -o run --output-format csv -- tools/probe/fetch_calib
+//   wr32 / wr128  dword / 16-B stores, coalesced (WRITE_SIZE)
+// Run: rocprofv3 --pmc FETCH_SIZE (or WRITE_SIZE) -d <dir> -o run --output-format csv -- tools/probe/fetch_calib
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -29,6 +30,14 @@ __global__ void rd128(const uint4* __restrict__ a, size_t n, uint32_t* out) {
     acc ^= v.x ^ v.y ^ v.z ^ v.w;
   }
   if (acc == 0x12345678u) out[0] = acc;
+}
+__global__ void wr32(uint32_t* __restrict__ a, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    a[i] = (uint32_t)i;
+}
+__global__ void wr128(uint4* __restrict__ a, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    a[i] = make_uint4((uint32_t)i, 0u, 1u, 2u);
 }
 // image: rows x 1024 B; lane (row r, window j) reads bytes [r*1024 + 64 j + s, +64)
 __global__ void row64(const uint8_t* __restrict__ img, int rows, int s, uint32_t* out) {
@@ -62,7 +71,9 @@ int main() {
   const int waves = rows / 64 * 16;
   hipLaunchKernelGGL(row64, dim3(waves / 4), dim3(256), 0, 0, a, rows, 0, o);
   hipLaunchKernelGGL(row64, dim3(waves / 4), dim3(256), 0, 0, a, rows, 4, o);
+  hipLaunchKernelGGL(wr32, dim3(8192), dim3(256), 0, 0, (uint32_t*)a, bytes / 4);
+  hipLaunchKernelGGL(wr128, dim3(8192), dim3(256), 0, 0, (uint4*)a, bytes / 16);
   hipDeviceSynchronize();
-  printf("each kernel reads %zu bytes once (row64 with s=4 reads 4 bytes past the end of its last row)\n", bytes);
+  printf("each kernel reads (rd*, row64) or writes (wr*)  %zu bytes once (row64 with s=4 reads 4 bytes past the end of its last row)\n", bytes);
   return 0;
 }
