@@ -676,8 +676,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef FC_CPW
 #define FC_CPW 4        // cells per wave (software-pipelined ROI loads)
 #endif
+#ifndef FC_QCAP
 #define FC_QCAP 1024    // candidate queue per wave (one pretest round adds <= 512)
+#endif
+#ifndef FC_CCAP
 #define FC_CCAP 512     // corner list per wave; beyond it the NMS runs densely
+#endif
 
 __host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
   return maxRows * ((maxCols + 20) & ~7);
@@ -691,7 +695,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbCellDesc* __restrict__ cells, uint32_t* __restrict__ cellKeys,
-    int32_t* __restrict__ cellCount, int tileElems) {
+    int32_t* __restrict__ cellCount, int tileElems, int cellBeg, int cellEnd) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -705,7 +709,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   uint32_t* bits = (uint32_t*)(corners + FC_CCAP);  // row y: words 2y, 2y+1
   // this wave's cells: (blockIdx.x * FC_CPW + j) * FC_WAVES + wave, j < FC_CPW;
   // the next cell's ROI is loaded into registers while this one is processed
-  auto cell_of = [&](int j) { return (blockIdx.x * FC_CPW + j) * FC_WAVES + wave; };
+  auto cell_of = [&](int j) { return cellBeg + (blockIdx.x * FC_CPW + j) * FC_WAVES + wave; };
   // ---- staging: lane r loads ROI row r, bytes [x0 - LPAD, x0 - LPAD + P)
   // of level row y0 + r, as four 16-byte loads from the 4-aligned byte at or
   // below its start (any caller stride), realigned in registers; every byte
@@ -738,10 +742,10 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     }
   };
   int ci = cell_of(0);
-  if (ci >= plan.ncells) return;
+  if (ci >= cellEnd) return;
   OrbCellDesc ncd = cells[ci];
   issue(ncd);
-  for (int jc = 0; jc < FC_CPW && ci < plan.ncells; ++jc) {
+  for (int jc = 0; jc < FC_CPW && ci < cellEnd; ++jc) {
   const OrbCellDesc cd = ncd;
   const int R = cd.y1 - cd.y0, C = cd.x1 - cd.x0;
   const long long slot = (long long)img * plan.ncells + ci;
@@ -764,8 +768,8 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       }
     }
   }
-  const int ciNext = jc + 1 < FC_CPW ? cell_of(jc + 1) : plan.ncells;
-  if (ciNext < plan.ncells) {
+  const int ciNext = jc + 1 < FC_CPW ? cell_of(jc + 1) : cellEnd;
+  if (ciNext < cellEnd) {
     ncd = cells[ciNext];
     issue(ncd);
   }
@@ -2036,10 +2040,13 @@ size_t orb_k_fast_cells_lds(int maxRows, int maxCols) {
   return (size_t)FC_WAVES * fc_wave_bytes(fc_tile_elems(maxRows, maxCols));
 }
 
+// cells [cellBeg, cellEnd) of every image (the level-0 cells can run beside the
+// resize chain, which levels >= 1 wait for)
 hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
-                            int nimg, hipStream_t s) {
+                            int cellBeg, int cellEnd, int nimg, hipStream_t s) {
+  if (cellEnd <= cellBeg) return hipSuccess;
   const int tileElems = fc_tile_elems(plan->maxCellRows, plan->maxCellCols);
   const size_t lds = orb_k_fast_cells_lds(plan->maxCellRows, plan->maxCellCols);
   if (!orb_k_fast_cells_fits(plan)) return hipErrorInvalidValue;
@@ -2048,9 +2055,10 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  dim3 grid((plan->ncells + FC_WAVES * FC_CPW - 1) / (FC_WAVES * FC_CPW), nimg), block(64 * FC_WAVES);
+  const int n = cellEnd - cellBeg;
+  dim3 grid((n + FC_WAVES * FC_CPW - 1) / (FC_WAVES * FC_CPW), nimg), block(64 * FC_WAVES);
   hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, cells, cellKeys, cellCount, tileElems);
+                     arenaPitch, *plan, cells, cellKeys, cellCount, tileElems, cellBeg, cellEnd);
   return hipGetLastError();
 }
 

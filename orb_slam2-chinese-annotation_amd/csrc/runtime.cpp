@@ -33,7 +33,7 @@ bool orb_k_fast_cells_fits(const OrbPlanDesc* plan);
 hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
-                            int nimg, hipStream_t s);
+                            int cellBeg, int cellEnd, int nimg, hipStream_t s);
 hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
@@ -233,6 +233,7 @@ struct StageProfiler {
   int nStages = 0;
   const char* names[kMaxStages] = {};
   std::vector<std::vector<hipEvent_t>> pool;  // each: 2 * nStages + 2 events
+  std::vector<unsigned> ran;                   // per call: stages whose events were recorded
   size_t used = 0;
   double ms[kMaxStages + 1] = {};
   long launches[kMaxStages + 1] = {};
@@ -247,9 +248,12 @@ struct StageProfiler {
     if (used == pool.size()) {
       pool.emplace_back(2 * nStages + 2);
       for (hipEvent_t& e : pool.back()) hipEventCreate(&e);
+      ran.push_back(0);
     }
+    ran[used] = ~0u;
     return &pool[used++];
   }
+  void not_run(int stage) { ran[used - 1] &= ~(1u << stage); }  // of the current call
   hipEvent_t b(std::vector<hipEvent_t>* ev, int stage) const { return (*ev)[2 * stage]; }
   hipEvent_t e(std::vector<hipEvent_t>* ev, int stage) const { return (*ev)[2 * stage + 1]; }
   hipEvent_t t0(std::vector<hipEvent_t>* ev) const { return (*ev)[2 * nStages]; }
@@ -260,10 +264,12 @@ struct StageProfiler {
       if (hipEventSynchronize(ev[2 * nStages + 1]) != hipSuccess) continue;
       for (int i = 0; i < nStages; ++i) {
         float t = 0.f;
-        if (launchesPerCall[i] == 0) continue;  // stage not run in this configuration
+        if (launchesPerCall[i] == 0 || !(ran[c] >> i & 1)) continue;  // stage not run
         if (hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]) == hipSuccess) {
           ms[i] += t;
           launches[i] += launchesPerCall[i];
+        } else {
+          (void)hipGetLastError();  // clear it: torch checks the last error after its launches
         }
       }
       float t = 0.f;
@@ -278,6 +284,7 @@ struct StageProfiler {
     for (auto& v : pool)
       for (hipEvent_t ev : v) hipEventDestroy(ev);
     pool.clear();
+    ran.clear();
     used = 0;
   }
 };
@@ -314,6 +321,7 @@ struct orb_extractor {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // side stream: blur runs beside FAST + octree
   hipEvent_t evFork = nullptr, evJoin = nullptr;
+  hipEvent_t evL0Fork = nullptr, evL0Join = nullptr;  // level-0 FAST beside the resize chain
   hipEvent_t evBatch = nullptr;  // recorded at the end of every run_batch on its stream
   bool ownStream = false;
   std::mutex mu;
@@ -663,6 +671,29 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
   HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
+  static const bool bandFast = getenv("ORB_FAST_BANDS") && atoi(getenv("ORB_FAST_BANDS")) > 0;
+  static const bool noL0Overlap = getenv("ORB_FAST_L0_INLINE") && atoi(getenv("ORB_FAST_L0_INLINE")) > 0;
+  // k_fast_cells (one wave per cell) unless a tiny level's cells outgrow its
+  // staging; k_fast_band (one workgroup per run of cells) otherwise or on request
+  const bool useBands = bandFast || !orb_k_fast_cells_fits(&P);
+  pf.names[2] = useBands ? "k_fast_band" : "k_fast_cells";
+  // Level 0 is the caller's image: its FAST cells need no pyramid, so they run
+  // on the side stream beside the latency-bound resize chain (fork / join by
+  // events, graph-capturable); levels >= 1 follow the chain on the main stream.
+  const int l0End = P.lv[0].cellEnd;
+  const bool l0Side = !useBands && !noL0Overlap && l0End > 0 && P.nlevels > 1;
+  if (l0Side) {
+    HIP_TRY(hipEventRecord(h->evL0Fork, s));
+    HIP_TRY(hipStreamWaitEvent(h->stream2, h->evL0Fork, 0));
+    PROF_REC(ev, pf.b(ev, 5), h->stream2);
+    HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                             h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
+                             h->dCellCount.as<int32_t>(), 0, l0End, B, h->stream2));
+    PROF_REC(ev, pf.e(ev, 5), h->stream2);
+    HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
+  } else if (ev) {
+    pf.not_run(5);
+  }
   PROF_REC(ev, pf.b(ev, 0), s);
   for (int l = 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
@@ -676,11 +707,6 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   }
   PROF_REC(ev, pf.e(ev, 0), s);
   PROF_REC(ev, pf.b(ev, 2), s);
-  static const bool bandFast = getenv("ORB_FAST_BANDS") && atoi(getenv("ORB_FAST_BANDS")) > 0;
-  // k_fast_cells (one wave per cell) unless a tiny level's cells outgrow its
-  // staging; k_fast_band (one workgroup per run of cells) otherwise or on request
-  const bool useBands = bandFast || !orb_k_fast_cells_fits(&P);
-  pf.names[2] = useBands ? "k_fast_band" : "k_fast_cells";
   if (useBands)
     HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                             h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
@@ -688,8 +714,9 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   else
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), B, s));
+                             h->dCellCount.as<int32_t>(), l0Side ? l0End : 0, P.ncells, B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
+  if (l0Side) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));
   const bool split = split_blur();
   if (split) {
     if (s2 != s) {
@@ -778,20 +805,24 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
       hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->evL0Fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->evL0Join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evBatch, hipEventDisableTiming) != hipSuccess) {
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->stream2) hipStreamDestroy(h->stream2);
     if (h->evFork) hipEventDestroy(h->evFork);
     if (h->evJoin) hipEventDestroy(h->evJoin);
+    if (h->evL0Fork) hipEventDestroy(h->evL0Fork);
+    if (h->evL0Join) hipEventDestroy(h->evL0Join);
     if (h->evBatch) hipEventDestroy(h->evBatch);
     delete h;
     return ORB_EDEVICE;
   }
   h->ownStream = true;
-  h->prof.nStages = 5;
-  const char* names[5] = {"k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree",
-                          "k_orient_desc"};
-  for (int i = 0; i < 5; ++i) {
+  h->prof.nStages = 6;
+  const char* names[6] = {"k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree",
+                          "k_orient_desc", "k_fast_cells_l0"};
+  for (int i = 0; i < 6; ++i) {
     h->prof.names[i] = names[i];
     h->prof.launchesPerCall[i] = 1;
   }
@@ -824,6 +855,8 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   if (h->stream2) hipStreamDestroy(h->stream2);
   if (h->evFork) hipEventDestroy(h->evFork);
   if (h->evJoin) hipEventDestroy(h->evJoin);
+  if (h->evL0Fork) hipEventDestroy(h->evL0Fork);
+  if (h->evL0Join) hipEventDestroy(h->evL0Join);
   if (h->evBatch) hipEventDestroy(h->evBatch);
   delete h;
 }
@@ -1053,7 +1086,7 @@ orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable) {
   return ORB_OK;
 }
 
-// stage 0..4 = kernels, stage 5 = whole extraction call
+// stage 0..5 = kernels, stage 6 = whole extraction call
 orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
                                         int* launches, const char** name) {
   if (!h || stage < 0 || stage > h->prof.nStages) return ORB_EINVAL;

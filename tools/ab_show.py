@@ -7,4 +7,4 @@ for line in open(sys.argv[1]):
     r = json.loads(line)
     b = r["bench"]
     k = {n: round(v, 3) for n, v in b["kernels_ms_per_launch"].items()}
-    print(f'{r["variant"]:>10} {b["value"]:10.0f} fr/s  ext {b["extraction_stream_ms_per_launch"]:.3f} ms  {k}')
+    print(f'{r["variant"]:>10} {b["value"]:10.0f} fr/s  call {b.get("extraction_call_ms_per_launch", 0):.3f} ms  {k}')

@@ -2,7 +2,9 @@
 # Round profile recipe (run on the GPU box through gpurun from the repo root):
 #   the default bench line, a rocprofv3 kernel-trace/stats pass, two HBM PMC
 #   passes (FETCH_SIZE and WRITE_SIZE cannot share a pass), the FETCH_SIZE
-#   calibration probe, and the two SQ passes of tools/gpu_pmc.sh.
+#   calibration probe, and the two SQ passes of tools/gpu_pmc.sh.  The PMC
+#   passes run FAST as one launch per call (ORB_FAST_L0_INLINE=1; counters are
+#   per dispatch and the level-0 split changes no instruction or byte counts).
 # Usage: tools/gpu_profile.sh <tag>
 set -eo pipefail
 TAG=${1:-r02}
@@ -15,9 +17,9 @@ cd /tmp && export TMPDIR=/tmp
 SMALL="--no-cpu --no-secondary --frames 1024 --steps 10 --warmup 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$TAG" -o run --output-format csv \
   -- python3 "$R/bench.py" $SMALL > "$O/prof_$TAG.json" 2> "$O/prof_$TAG.err"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$O/pmcf_$TAG" -o run --output-format csv \
+ORB_FAST_L0_INLINE=1 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$O/pmcf_$TAG" -o run --output-format csv \
   -- python3 "$R/bench.py" --no-cpu --no-secondary --frames 512 --steps 2 --warmup 1 > "$O/pmcf_$TAG.json" 2> "$O/pmcf_$TAG.err"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$O/pmcw_$TAG" -o run --output-format csv \
+ORB_FAST_L0_INLINE=1 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$O/pmcw_$TAG" -o run --output-format csv \
   -- python3 "$R/bench.py" --no-cpu --no-secondary --frames 512 --steps 2 --warmup 1 > "$O/pmcw_$TAG.json" 2> "$O/pmcw_$TAG.err"
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib_$TAG" -o run --output-format csv \
   -- "$R/tools/probe/fetch_calib" > "$O/calib_$TAG.log" 2>&1

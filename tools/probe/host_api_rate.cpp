@@ -55,7 +55,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 50; ++i)
     CHECK(orb_extractor_extract(ext, imgs[i % 16].data(), W, H, W, kps.data(), desc.data(), cap, &n));
   printf("  kernels per call (HIP events, 50 calls):");
-  for (int st = 0; st <= 5; ++st) {
+  for (int st = 0; st <= 6; ++st) {
     double ms = 0;
     int launches = 0;
     const char* name = nullptr;
