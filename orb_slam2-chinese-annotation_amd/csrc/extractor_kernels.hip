@@ -19,6 +19,29 @@
 #include "orb_pattern_data.h"
 #include "../../include/orb_abi.h"
 
+// Workgroups are dispatched round-robin over the 8 XCDs (linear id L runs on
+// XCD L % 8), and each XCD has its own L2.  With a (work item, image) grid that
+// spreads one image's neighbouring cells / keypoint runs over all eight L2s, so
+// every XCD fetches every image.  xcd_swizzle remaps the linear id so that XCD
+// k runs one contiguous range of (blockIdx.x, blockIdx.y): the workgroups in
+// flight on an XCD cover a couple of images, whose rows its L2 then serves.
+#ifndef ORB_XCD_SWIZZLE
+#define ORB_XCD_SWIZZLE 1
+#endif
+__device__ __forceinline__ void xcd_swizzle(int& bx, int& by) {
+  const int gx = gridDim.x, n = gx * gridDim.y;
+  const int L = blockIdx.x + gx * blockIdx.y;
+  if (!ORB_XCD_SWIZZLE) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    return;
+  }
+  const int xcd = L & 7, pos = L >> 3, q = n >> 3, r = n & 7;
+  const int logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  by = logical / gx;
+  bx = logical - by * gx;
+}
+
 // ============================================================ k_pyr_resize
 // cv::resize(prev, level, sz, 0, 0, INTER_LINEAR) on 8U with OpenCV's 11-bit
 // fixed-point weights.  The weight tables are computed
@@ -699,7 +722,8 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int img = blockIdx.y;
+  int bx, img;
+  xcd_swizzle(bx, img);
   unsigned char* wbase = smem + wave * fc_wave_bytes(tileElems);
   uint32_t* tile32 = (uint32_t*)wbase;
   const _Float16* tileh = (const _Float16*)wbase;
@@ -707,9 +731,9 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   uint16_t* queue = (uint16_t*)(sc + tileElems);
   uint16_t* corners = queue + FC_QCAP;
   uint32_t* bits = (uint32_t*)(corners + FC_CCAP);  // row y: words 2y, 2y+1
-  // this wave's cells: (blockIdx.x * FC_CPW + j) * FC_WAVES + wave, j < FC_CPW;
-  // the next cell's ROI is loaded into registers while this one is processed
-  auto cell_of = [&](int j) { return cellBeg + (blockIdx.x * FC_CPW + j) * FC_WAVES + wave; };
+  // this wave's cells: (bx * FC_CPW + j) * FC_WAVES + wave, j < FC_CPW; the
+  // next cell's ROI is loaded into registers while this one is processed
+  auto cell_of = [&](int j) { return cellBeg + (bx * FC_CPW + j) * FC_WAVES + wave; };
   // ---- staging: lane r loads ROI row r, bytes [x0 - LPAD, x0 - LPAD + P)
   // of level row y0 + r, as four 16-byte loads from the 4-aligned byte at or
   // below its start (any caller stride), realigned in registers; every byte
@@ -1695,16 +1719,17 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   __shared__ __attribute__((aligned(16))) DescWaveLds sm[4];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31;
-  const int img = blockIdx.y;
+  int bx, img;
+  xcd_swizzle(bx, img);
   const int32_t* cnts = outCount + img * plan.nlevels;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bx == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
     counts[img] = errFlag[img] ? (int32_t)ORB_EDEVICE : tot;  // failed image: negative count
   }
   // this wave's slot pairs: pairBase + 4 j, j < DESC_PPW (the workgroup's four
   // waves interleave); lane 2 j + h holds the packed key of slot 2 (pairBase + 4 j) + h
-  const int pairBase = blockIdx.x * 4 * DESC_PPW + w;
+  const int pairBase = bx * 4 * DESC_PPW + w;
   if (2 * pairBase >= plan.slotsPerImage) return;
   const uint32_t* imgKeys = outKeys + (long long)img * plan.slotsPerImage;
   uint32_t keyv = 0;

@@ -672,10 +672,14 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   PROF_REC(ev, pf.t0(ev), s);
   HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
   static const bool bandFast = getenv("ORB_FAST_BANDS") && atoi(getenv("ORB_FAST_BANDS")) > 0;
+  static const int kCellsMinBatch =
+      getenv("ORB_FAST_CELLS_MIN_BATCH") ? atoi(getenv("ORB_FAST_CELLS_MIN_BATCH")) : 4;
   static const bool noL0Overlap = getenv("ORB_FAST_L0_INLINE") && atoi(getenv("ORB_FAST_L0_INLINE")) > 0;
   // k_fast_cells (one wave per cell) unless a tiny level's cells outgrow its
   // staging; k_fast_band (one workgroup per run of cells) otherwise or on request
-  const bool useBands = bandFast || !orb_k_fast_cells_fits(&P);
+  // (a frame or two per call: the band kernel's fewer, larger workgroups and a
+  // single stream give the lower latency)
+  const bool useBands = bandFast || B < kCellsMinBatch || !orb_k_fast_cells_fits(&P);
   pf.names[2] = useBands ? "k_fast_band" : "k_fast_cells";
   // Level 0 is the caller's image: its FAST cells need no pyramid, so they run
   // on the side stream beside the latency-bound resize chain (fork / join by

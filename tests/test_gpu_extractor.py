@@ -223,3 +223,52 @@ def test_batch_layouts_vs_oracle(gpu, oracle, w, h, stride, pitch, B):
         assert cnt[f] == len(kr), (f, cnt[f], len(kr))
         assert kps[f, : cnt[f]].tobytes() == kr.tobytes(), f
         assert desc[f, : cnt[f]].tobytes() == dr.tobytes(), f
+
+
+def _batch_vs_oracle(gpu, oracle, imgs, nf=1000, sf=1.2, nl=8):
+    torch = pytest.importorskip("torch")
+    B = len(imgs)
+    h, w = imgs[0].shape
+    ext = gpu.ORBextractor(nf, sf, nl, 20, 7)
+    cap = ext.capacity(w, h)
+    d_img = torch.from_numpy(np.stack(imgs)).cuda()
+    d_kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ext.extract_batch(d_img.data_ptr(), B, w, h, w, w * h, d_kps.data_ptr(), d_desc.data_ptr(),
+                      cap, d_cnt.data_ptr())
+    torch.cuda.synchronize()
+    kps = d_kps.cpu().numpy().view(gpu.KEYPOINT_DTYPE).reshape(B, cap)
+    desc = d_desc.cpu().numpy()
+    cnt = d_cnt.cpu().numpy()
+    for f in range(B):
+        kr, dr, _ = oracle.extract(imgs[f], nf, sf, nl, 20, 7)
+        assert cnt[f] == len(kr), (f, cnt[f], len(kr))
+        assert kps[f, : cnt[f]].tobytes() == kr.tobytes(), \
+            (f, _diff_report(kps[f, : cnt[f]], desc[f, : cnt[f]], kr, dr))
+        assert desc[f, : cnt[f]].tobytes() == dr.tobytes(), f
+
+
+def test_batch_hard_cases_vs_oracle(gpu, oracle):
+    """Batches of >= 4 frames take the one-wave-per-cell FAST kernel (level 0 on
+    the side stream); single frames take the band kernel.  The hard single-frame
+    cases above, as one batch: noise, low contrast (minThFAST fallback), flat."""
+    rng = np.random.default_rng(3)
+    noise = rng.integers(0, 256, (480, 640), dtype=np.uint8)
+    rng = np.random.default_rng(4)
+    base = gpu.synth_image(9, 0, 640, 480).astype(np.int32)
+    low = (128 + (base - 128) // 12 + rng.integers(-3, 4, base.shape)).clip(0, 255).astype(np.uint8)
+    flat = np.full((480, 640), 128, np.uint8)
+    _batch_vs_oracle(gpu, oracle, [noise, low, flat, gpu.synth_image(2, 0, 640, 480)])
+
+
+@pytest.mark.parametrize("w,h,nf,sf,nl", [
+    (1241, 376, 1500, 1.2, 12),
+    (640, 480, 800, 1.1, 8),
+    (1920, 1080, 2000, 1.5, 6),
+    (1241, 376, 1000, 1.9, 4),
+    (640, 480, 1000, 1.2, 1),
+])
+def test_batch_parameters_vs_oracle(gpu, oracle, w, h, nf, sf, nl):
+    _batch_vs_oracle(gpu, oracle, [gpu.synth_image(40, f, w, h) for f in range(4)], nf, sf, nl)

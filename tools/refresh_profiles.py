@@ -3,7 +3,7 @@
 profiles/<tag>_*: HBM traffic and SQ PMC summaries, rocprofv3 kernel stats,
 the GPU test log and the bench line (roofline.traffic / valu_issue re-derived
 from the new PMC files).  Prints the per-kernel figures DESIGN.md §4 tabulates.
-Usage: tools/refresh_profiles.py [tag] [--docs]"""
+Usage: tools/refresh_profiles.py [tag]  (DESIGN.md §4 is edited by hand from its output)"""
 import csv
 import json
 import shutil
@@ -50,62 +50,20 @@ for _ in range(7):
 alg = bench.algorithmic_bytes(1241, 376, np.float32(sc), 8, b["config"]["mean_keypoints_per_frame"], 5000)
 h = json.loads((P / f"{tag}_hbm_traffic.json").read_text())["kernels"]
 pm = json.loads((P / f"{tag}_pmc.json").read_text())["kernels"]
-for k in ["k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree", "k_orient_desc"]:
-    n_launch = 7 if k == "k_pyr_resize" else 1
+# dispatches per extraction call, from the trace itself: k_pyr_resize runs
+# nlevels-1 launches, k_fast_cells two (level 0 on the side stream, then levels
+# >= 1); the PMC passes run FAST inline (one dispatch), so their per-dispatch
+# counters are already per call
+calls = {k: agg[k][0] / agg["k_octree"][0] for k in agg}
+for k in [k for k in ["k_pyr_resize", "k_blur_levels", "k_fast_band", "k_fast_cells", "k_octree",
+                      "k_orient_desc"] if k in agg and k in pm]:
+    n_launch = round(calls[k])
     ms = agg[k][1] / agg[k][0] / 1e6 * n_launch
     a = alg[k] * 512
-    t = h[k]["traffic_bytes"] * n_launch
+    t = h[k]["traffic_bytes"] * (7 if k == "k_pyr_resize" else 1)
     d = pm[k]
     w = d["SQ_WAVE_CYCLES"]
-    print(f"{k:16s} {ms:.3f} ms/step  {a / ms / 1e6:6.0f} GB/s  frac {a / ms / 1e6 / 8000:.3f}  "
-          f"traffic/alg {t / a:.2f}  wait/inst/active "
+    print(f"{k:16s} {ms:.3f} ms/call ({n_launch} dispatches)  {a / ms / 1e6:6.0f} GB/s  "
+          f"frac {a / ms / 1e6 / 8000:.3f}  traffic/alg {t / a:.2f}  wait/inst/active "
           f"{100 * d['SQ_WAIT_ANY'] / w:.0f}/{100 * d['SQ_WAIT_INST_ANY'] / w:.0f}/"
           f"{100 * d['SQ_ACTIVE_INST_ANY'] / w:.0f} %  valu {d['SQ_INSTS_VALU']:.3g}")
-
-# ---- --docs: rewrite the measured figures quoted in DESIGN.md / BASELINE.md / README.md
-if "--docs" in sys.argv:
-    import re
-
-    v, ms_step, cpu, kk = b["value"], b["ms_per_step"], b["cpu_baseline"]["value"], b["kernels_ms_per_step"]
-    ext = ["k_pyr_resize", "k_fast_band", "k_blur_levels", "k_octree", "k_orient_desc"]
-    s = (ROOT / "DESIGN.md").read_text()
-    for k in ["k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree", "k_orient_desc"]:
-        n_launch = 7 if k == "k_pyr_resize" else 1
-        ms = agg[k][1] / agg[k][0] / 1e6 * n_launch
-        a = alg[k] * 512
-        t = h[k]["traffic_bytes"] * n_launch
-        g = a / ms / 1e6
-        pat = re.compile(r"(\| `" + k + r"` \|[^\n]*?\| )([0-9.]+) \| ([0-9]+) \| ([0-9.]+) \| ([^|]+) \|\n")
-        mo = pat.search(s)
-        fd = 3 if g / 8000 < 0.01 else 2
-        tc = mo.group(5) if k in ("k_octree", "k_orient_desc") else f"{t / a:.2f}"
-        s = s[:mo.start()] + f"{mo.group(1)}{ms:.2f} | {g:.0f} | {g / 8000:.{fd}f} | {tc} |\n" + s[mo.end():]
-    s = re.sub(r"The step is then [0-9.]+ ms =\n\*\*[0-9.]+k frames/s\*\* on one MI355X. The cpu_baseline is [0-9.]+ frames/s on one core, so\nthe GPU is [0-9,]+× faster. The critical path is the extraction stream: resize [0-9.]+,\nFAST [0-9.]+, blur [0-9.]+, octree [0-9.]+ and orient_desc [0-9.]+ ms, [0-9.]+ ms in all.",
-               lambda _: f"The step is then {ms_step:.2f} ms =\n**{v / 1e3:.1f}k frames/s** on one MI355X. The cpu_baseline is {cpu:.1f} frames/s on one core, so\nthe GPU is {v / cpu:,.0f}× faster. The critical path is the extraction stream: resize {kk['k_pyr_resize']:.2f},\nFAST {kk['k_fast_band']:.2f}, blur {kk['k_blur_levels']:.2f}, octree {kk['k_octree']:.2f} and orient_desc {kk['k_orient_desc']:.2f} ms, {sum(kk[x] for x in ext):.2f} ms in all.", s)
-    fast_prof = agg["k_fast_band"][1] / agg["k_fast_band"][0] / 1e6
-    s = re.sub(r"pipelined step is [0-9.]+ ms, and rocprofv3's average for it is [0-9.]+ ms",
-               f"pipelined step is {r['ms_per_launch']:.2f} ms, and rocprofv3's average for it is {fast_prof:.2f} ms", s)
-    lo, hi = r["valu_issue"]["issue_ms_range"]
-    flo, fhi = r["valu_issue"]["frac_range"]
-    s = re.sub(r"issue time of `k_fast_band` at [0-9.]+–[0-9.]+ ms of its [0-9.]+ ms, i.e. [0-9]+–[0-9]+ %",
-               f"issue time of `k_fast_band` at {lo:.2f}–{hi:.2f} ms of its {r['ms_per_launch']:.2f} ms, i.e. {100 * flo:.0f}–{100 * fhi:.0f} %", s)
-
-    def fr(n):
-        d = pm[n]
-        w = d["SQ_WAVE_CYCLES"]
-        return "%d / %d / %d %%" % tuple(round(100 * d[c] / w) for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"))
-    s = re.sub(r"`k_fast_band`\n[0-9]+ / [0-9]+ / [0-9]+ %, `k_blur_levels` [0-9]+ / [0-9]+ / [0-9]+ %, `k_pyr_resize` [0-9]+ / [0-9]+ / [0-9]+ %,\n`k_orient_desc` [0-9]+ / [0-9]+ / [0-9]+ %, `k_octree` [0-9]+ / [0-9]+ / [0-9]+ %",
-               lambda _: f"`k_fast_band`\n{fr('k_fast_band')}, `k_blur_levels` {fr('k_blur_levels')}, `k_pyr_resize` {fr('k_pyr_resize')},\n`k_orient_desc` {fr('k_orient_desc')}, `k_octree` {fr('k_octree')}", s)
-    (ROOT / "DESIGN.md").write_text(s)
-    s = (ROOT / "BASELINE.md").read_text()
-    s = re.sub(r"\| \*\*[0-9,]+ frames/s\*\* \([0-9.]+ ms per 512 frames, pipelined steps\) \|",
-               lambda _: f"| **{v:,.0f} frames/s** ({ms_step:.2f} ms per 512 frames, pipelined steps) |", s)
-    s = re.sub(r"\| \*\*C4 headline\*\* extract \+ SearchByProjection \(5k MPs\) \| [0-9.]+ frames/s \|",
-               lambda _: f"| **C4 headline** extract + SearchByProjection (5k MPs) | {cpu:.1f} frames/s |", s)
-    s = re.sub(r"C4 at 1 GPU is [0-9,]+× the single-thread", lambda _: f"C4 at 1 GPU is {v / cpu:,.0f}× the single-thread", s)
-    (ROOT / "BASELINE.md").write_text(s)
-    s = (ROOT / "README.md").read_text()
-    s = re.sub(r"is \*\*[0-9.]+k frames/s\*\*", lambda _: f"is **{v / 1e3:.1f}k frames/s**", s)
-    s = re.sub(r"runs the same workload at [0-9.]+ frames/s", lambda _: f"runs the same workload at {cpu:.1f} frames/s", s)
-    (ROOT / "README.md").write_text(s)
-    print("docs updated")
