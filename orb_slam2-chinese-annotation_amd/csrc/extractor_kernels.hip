@@ -1,14 +1,18 @@
 // extractor_kernels.hip -- gfx950 kernels of the ORB extractor (ORBextractor::operator()).
 //
-// Pipeline for a batch of B images (one launch per stage, every launch covers
-// all B images; HBM layout in DESIGN.md §3):
-//   k_pyr_resize   x (nlevels-1)  bilinear level l from level l-1   src/ORBextractor.cc:1172-1207
-//   k_fast_band    x 1            FAST-9/16 score over a band of      src/ORBextractor.cc:816-865
-//                                 cells, cell-local NMS, iniTh -> minTh fallback, ordered compaction
-//   k_octree       x 1            DistributeOctTree, one workgroup   src/ORBextractor.cc:558-782
+// Pipeline for a batch of B images (every launch covers all B images; HBM
+// layout in DESIGN.md §3):
+//   k_pyr_resize   x (nlevels-1)  bilinear level l from level l-1    src/ORBextractor.cc:1172-1207
+//   k_fast_cells   x 2            FAST-9/16 + cell-local NMS + iniTh  src/ORBextractor.cc:785-865
+//                                 -> minTh fallback, one wave per cell; level 0's cells
+//                                 on a side stream beside the resize chain, then levels >= 1
+//   (k_fast_band   x 1            the same per band of cells; single frames, oversized cells)
+//   k_octree       x 1            DistributeOctTree, one workgroup    src/ORBextractor.cc:558-782
 //                                 per (image, level), list order emulated exactly
-//   k_orient_desc  x 1            IC_Angle + 7x7 blur + rBRIEF-256,   src/ORBextractor.cc:77-164,
-//                                 one wave per keypoint, rescale       1131-1167
+//   k_orient_desc  x 1            IC_Angle + rBRIEF-256 with the 7x7  src/ORBextractor.cc:77-164,
+//                                 blur fused (each sample blurred     1131-1167
+//                                 from LDS row sums), two keypoints per wave, rescale
+//   (k_blur_levels + k_orient_desc_split: blurred levels on demand / split A/B mode)
 // Bit-exactness contract: every output byte equals the CPU oracle
 // (oracle/orb_oracle.cpp) on the same image.
 #include <stdlib.h>
