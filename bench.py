@@ -476,20 +476,21 @@ def main():
     kern, ext_kern = {}, []
     for st in range(6):
         name, ms, n = ext.profile_read(st)
-        if n == 0 or ms == 0.0:
+        if n == 0:
             continue  # stage not run (k_blur_levels: split A/B mode only)
         kern[name] = (ms, n)
         ext_kern.append(name)
-    if "k_fast_cells_l0" in kern and "k_fast_cells" in kern:
-        # level 0's cells run as their own launch beside the resize chain: one
-        # FAST pass = both launches (summed durations, counted once per call)
-        ms0, _ = kern.pop("k_fast_cells_l0")
-        ext_kern.remove("k_fast_cells_l0")
-        ms1, n1 = kern["k_fast_cells"]
-        kern["k_fast_cells"] = (ms0 + ms1, n1)
-        fast_l0_ms = ms0
-    else:
-        fast_l0_ms = None
+    # level 0's FAST runs as its own launch on the side stream (beside the
+    # resize chain): one pass of a kernel = both launches (summed durations, counted once per call)
+    side_ms = {}
+    for name in [k for k in ext_kern if k.endswith("_l0")]:
+        ms0, _ = kern.pop(name)
+        ext_kern.remove(name)
+        side_ms[name] = ms0 / (args.steps * NB)
+        base = name[:-3]
+        if base in kern:
+            ms1, n1 = kern[base]
+            kern[base] = (ms0 + ms1, n1)
     _, call_ms, call_n = ext.profile_read(6)  # whole extraction call, start to join
     for st in range(3):
         name, ms, n = matcher.profile_read(st)
@@ -562,8 +563,7 @@ def main():
         "kernels_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kern.items()},
         "extraction_kernels_ms_per_launch": sum(kern[k][0] for k in ext_kern) / (args.steps * NB),
         "extraction_call_ms_per_launch": call_ms / max(call_n, 1),
-        "fast_level0_side_stream_ms_per_launch": (fast_l0_ms / (args.steps * NB)
-                                                  if fast_l0_ms is not None else None),
+        "level0_side_stream_ms_per_launch": side_ms,
     }
     if rank == 0 and world == 1 and not args.no_secondary:
         del d_img

@@ -165,8 +165,8 @@ void* orb_extractor_stream(orb_extractor_t* h);
  * 0 k_pyr_resize (nlevels-1 launches per call), 1 k_blur_levels (split mode
  * only), 2 FAST (k_fast_cells on levels >= 1, or k_fast_band on all levels),
  * 3 k_octree, 4 k_orient_desc, 5 k_fast_cells_l0 (level 0's cells on the side
- * stream, beside the resize chain; 0 ms when not split off), 6 = the whole
- * extraction call. */
+ * stream, beside the resize chain; 0 launches when not split off), 6 = the
+ * whole extraction call. */
 orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable);
 orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
                                         int* launches, const char** name);

@@ -1067,14 +1067,14 @@ __global__ __launch_bounds__(512) void k_octree(
     OrbPlanDesc plan, const int32_t* __restrict__ cellCount, const uint32_t* __restrict__ cellKeys,
     uint32_t* __restrict__ gKeys, uint16_t* __restrict__ gNid, int ldsKeyCap, int nodeCapMax,
     int maxCellsPerLevel, uint32_t* __restrict__ outKeys, int32_t* __restrict__ outCount,
-    int32_t* __restrict__ errFlag) {
+    int32_t* __restrict__ errFlag, int levelBeg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int tmp[17];
   __shared__ int sh[8];
-  // grid (images, levels): the dispatcher walks x first, so every image's level 0
-  // (the most keys, the longest workgroups) starts before any level 1, and the
-  // short upper levels fill the tail
-  const int l = blockIdx.y, img = blockIdx.x, T = blockDim.x, t = threadIdx.x;
+  // grid (images, levels levelBeg..): the dispatcher walks x first, so every
+  // image's lowest level (the most keys, the longest workgroups) starts before
+  // the next, and the short upper levels fill the tail
+  const int l = levelBeg + blockIdx.y, img = blockIdx.x, T = blockDim.x, t = threadIdx.x;
   const OrbLevelDesc& L = plan.lv[l];
   const int NC = nodeCapMax;
   int n2 = 1;
@@ -2107,16 +2107,18 @@ size_t orb_k_octree_node_bytes(int nodeCapMax, int maxCellsPerLevel) {
 hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
                         int nodeCapMax, int maxCellsPerLevel, uint32_t* outKeys,
-                        int32_t* outCount, int32_t* errFlag, int nimg, hipStream_t s) {
+                        int32_t* outCount, int32_t* errFlag, int levelBeg, int levelEnd, int nimg,
+                        hipStream_t s) {
+  if (levelEnd <= levelBeg || nimg <= 0) return hipSuccess;
   const size_t lds = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, ldsKeyCap);
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k_octree,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  dim3 grid(nimg, plan->nlevels), block(512);
+  dim3 grid(nimg, levelEnd - levelBeg), block(512);
   hipLaunchKernelGGL(k_octree, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys, gNid,
-                     ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag);
+                     ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, levelBeg);
   return hipGetLastError();
 }
 

@@ -42,7 +42,7 @@ size_t orb_k_octree_lds(int nodeCapMax, int maxCellsPerLevel, int ldsKeyCap);
 hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
                         int nodeCapMax, int maxCellsPerLevel, uint32_t* outKeys,
-                        int32_t* outCount, int32_t* errFlag, int nimg, hipStream_t s);
+                        int32_t* outCount, int32_t* errFlag, int levelBeg, int levelEnd, int nimg, hipStream_t s);
 hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0Stride,
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
@@ -228,7 +228,7 @@ struct StageProfiler {
   // Per call: a (begin, end) event pair per stage, recorded on whichever stream
   // runs that stage (stages may overlap), plus a (begin, end) pair for the
   // whole call on the caller's stream.
-  static const int kMaxStages = 6;
+  static const int kMaxStages = 8;
   bool enabled = false;
   int nStages = 0;
   const char* names[kMaxStages] = {};
@@ -720,6 +720,8 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
                              h->dCellCount.as<int32_t>(), l0Side ? l0End : 0, P.ncells, B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
+  // (level 0's octree on the side stream as well measured no gain: the octree's
+  // time is its per-workgroup pass latency, not level 0's size)
   if (l0Side) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));
   const bool split = split_blur();
   if (split) {
@@ -738,7 +740,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                        h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
-                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), B, s));
+                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, P.nlevels, B, s));
   PROF_REC(ev, pf.e(ev, 3), s);
   if (split && s2 != s) HIP_TRY(hipStreamWaitEvent(s, h->evJoin, 0));
   PROF_REC(ev, pf.b(ev, 4), s);

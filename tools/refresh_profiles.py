@@ -54,7 +54,7 @@ pm = json.loads((P / f"{tag}_pmc.json").read_text())["kernels"]
 # nlevels-1 launches, k_fast_cells two (level 0 on the side stream, then levels
 # >= 1); the PMC passes run FAST inline (one dispatch), so their per-dispatch
 # counters are already per call
-calls = {k: agg[k][0] / agg["k_octree"][0] for k in agg}
+calls = {k: agg[k][0] / agg["k_orient_desc"][0] for k in agg}
 for k in [k for k in ["k_pyr_resize", "k_blur_levels", "k_fast_band", "k_fast_cells", "k_octree",
                       "k_orient_desc"] if k in agg and k in pm]:
     n_launch = round(calls[k])
