@@ -65,6 +65,56 @@ __device__ __forceinline__ void xcd_swizzle(int& bx, int& by) {
 #define PYR_SROWS_WIDE 64
 #define PYR_SW_WIDE 64
 
+// Source-window staging in 16-byte groups: element i of a window of nR rows x
+// nG groups (4 dwords each) is row i / nG, group i % nG.  One b128 load per
+// group (+ one dword for the realignment of an unaligned source) instead of
+// one or two dword loads per dword, one b128 LDS store.  The window's dword
+// pitch is a multiple of 4 and >= 4 nG, so a group never crosses a row.
+#ifndef PYR_LOAD16
+#define PYR_LOAD16 1
+#endif
+template <int NQ>
+struct TilePrefetch16 {
+  uint32_t w[NQ][5], sh[NQ];
+  __device__ __forceinline__ void issue(const ImgRsrc& im, bool aligned, const uint32_t* off) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t o = off[q] + im.sh;
+      sh[q] = o & 3u;
+      const uint32_t a = o & ~3u;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(im.r, (int)a, 0, 0);
+      w[q][0] = (uint32_t)v[0];
+      w[q][1] = (uint32_t)v[1];
+      w[q][2] = (uint32_t)v[2];
+      w[q][3] = (uint32_t)v[3];
+      w[q][4] = aligned ? 0u : buf_ld32(im.r, a + 16);
+    }
+  }
+  __device__ __forceinline__ void commit(uint32_t* lds, int ldsPitch, int nR, int nG,
+                                         uint32_t magic, bool aligned) const {
+    int tid = (int)threadIdx.x;
+    __asm__ volatile("" : "+v"(tid));  // see TilePrefetch::commit
+    const int n = nR * nG;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t i = (uint32_t)(q * 256 + tid);
+      const uint32_t r = __umulhi(i << 1, magic), g = i - r * (uint32_t)nG;
+      if ((int)i < n) {
+        uint4 d;
+        if (aligned) {
+          d = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
+        } else {
+          d.x = __builtin_amdgcn_alignbyte(w[q][1], w[q][0], sh[q]);
+          d.y = __builtin_amdgcn_alignbyte(w[q][2], w[q][1], sh[q]);
+          d.z = __builtin_amdgcn_alignbyte(w[q][3], w[q][2], sh[q]);
+          d.w = __builtin_amdgcn_alignbyte(w[q][4], w[q][3], sh[q]);
+        }
+        *reinterpret_cast<uint4*>(lds + r * ldsPitch + 4 * g) = d;
+      }
+    }
+  }
+};
+
 template <bool ALIGNED, int SROWS = PYR_SROWS, int SW = PYR_SW>
 __global__ __launch_bounds__(256) void k_pyr_resize(
     const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sw, int sh,
@@ -101,17 +151,19 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   const int colBase = sxA & ~3;
   const int nW = ((sxB - colBase) >> 2) + 1, nR = syB - syA + 1;
   // staging: ALIGNED sources need one dword load per LDS dword, others two
-  // (realigned with v_alignbyte)
-  const uint32_t magic = div_magic(nW);
-  constexpr int NQ = (SROWS * SW + 255) / 256;
-  TilePrefetch<NQ> pf;
+  // (realigned with v_alignbyte); PYR_LOAD16: one b128 (+ one dword) per 4
+  static_assert(SW % 4 == 0, "window pitch must hold whole 16-byte groups");
+  const int nStage = PYR_LOAD16 ? (nW + 3) >> 2 : nW;  // staged elements per row
+  const uint32_t magic = div_magic(nStage);
+  constexpr int NQ = PYR_LOAD16 ? (SROWS * (SW / 4) + 255) / 256 : (SROWS * SW + 255) / 256;
+  typename std::conditional<PYR_LOAD16, TilePrefetch16<NQ>, TilePrefetch<NQ>>::type pf;
   // staged element q of this thread: the same offset in every image, computed once
   uint32_t eoff[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const uint32_t i = (uint32_t)min(q * 256 + tid, nR * nW - 1);
-    const uint32_t r = __umulhi(i << 1, magic), c = i - r * (uint32_t)nW;
-    eoff[q] = (syA + r) * (uint32_t)srcStride + (uint32_t)colBase + 4 * c;
+    const uint32_t i = (uint32_t)min(q * 256 + tid, nR * nStage - 1);
+    const uint32_t r = __umulhi(i << 1, magic), c = i - r * (uint32_t)nStage;
+    eoff[q] = (syA + r) * (uint32_t)srcStride + (uint32_t)colBase + (PYR_LOAD16 ? 16 : 4) * c;
   }
   auto issue = [&](int z) {
     pf.issue(img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((sh - 1) * srcStride + sw)),
@@ -149,7 +201,11 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   };
   for (; z < nImg; z += gridDim.z) {
     __syncthreads();  // the previous image's taps have read the window
-    pf.commit(&tile[0][0], SW, nR, nW, magic);
+#if PYR_LOAD16
+    pf.commit(&tile[0][0], SW, nR, nStage, magic, ALIGNED);
+#else
+    pf.commit(&tile[0][0], SW, nR, nStage, magic);
+#endif
     if (z + (int)gridDim.z < nImg) issue(z + gridDim.z);
     __syncthreads();
     if (xs >= dw) continue;

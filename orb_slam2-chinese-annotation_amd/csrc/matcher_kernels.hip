@@ -98,7 +98,9 @@ __global__ __launch_bounds__(64) void k_grid_build(const orb_keypoint_t* __restr
 // with more than PROJ_STAGE keypoints scan the global grid instead.
 #define PROJ_STAGE 2048
 
-#define PROJ_WG 1024
+#ifndef PROJ_WG
+#define PROJ_WG 512  // map points per workgroup (grid staged once per workgroup; swept 256-1024)
+#endif
 __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked, int kpStride,
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
     const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
     uint32_t* __restrict__ topk, int32_t* __restrict__ ncand) {
   __shared__ int sCS[GRID_CELLS + 1];
-  __shared__ __attribute__((aligned(16))) uint4 sKp[PROJ_STAGE];
+  extern __shared__ __attribute__((aligned(16))) uint4 sKp[];  // min(kpStride, PROJ_STAGE)
   __shared__ float sScale[ORB_MAX_LEVELS];
   const int p = blockIdx.y;
   const int tid = threadIdx.x;
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
   const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
   const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
   const int32_t* ci = cellIdx + (size_t)p * kpStride;
-  const bool staged = N <= PROJ_STAGE;
+  const bool staged = N <= min(kpStride, PROJ_STAGE);
 #pragma unroll
   for (int i = 0; i < ORB_MAX_LEVELS; ++i)
     if (tid == i) sScale[i] = P.scale[i];
@@ -385,8 +387,10 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
                                  int nproblems, hipStream_t s) {
   const ProjParams P = *(const ProjParams*)params;
   if (mpMax <= 0 || nproblems <= 0) return hipSuccess;
+  // dynamic LDS: the staged keypoints of a frame, sized to the key capacity
+  const size_t lds = (size_t)std::min(kpStride, PROJ_STAGE) * sizeof(uint4);
   hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems),
-                     dim3(PROJ_WG), 0, s,
+                     dim3(PROJ_WG), lds, s,
                      keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
                      cellStart, cellIdx, P, topk, ncand);
   return hipGetLastError();
