@@ -361,13 +361,15 @@ __global__ __launch_bounds__(256) void k_fast_band(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbBandDesc* __restrict__ bands, const OrbCellDesc* __restrict__ cells, int nBands,
-    uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount) {
+    uint32_t* __restrict__ cellKeys, int32_t* __restrict__ cellCount, int32_t* __restrict__ errFlag) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qCount, cCount;
   __shared__ uint32_t fbMask[2];  // cells (of this band) that fall back to minThFAST
   __shared__ int16_t cellX0[64], cellWW[64];  // cell windows: first interior column, width
   __shared__ int nFbK;
   const int img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the image's status starts clean (k_octree may flag it, k_orient_desc reads it)
+  if (blockIdx.x == 0 && tid == 0) errFlag[img] = 0;
   const int nw = blockDim.x >> 6;
   const int bandElems = plan.maxBandBytes;
   const int bitStride = ((bandElems >> 5) + 4) & ~1;  // even: colf / fbCol stay 8-aligned
@@ -778,12 +780,15 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbCellDesc* __restrict__ cells, uint32_t* __restrict__ cellKeys,
-    int32_t* __restrict__ cellCount, int tileElems, int cellBeg, int cellEnd) {
+    int32_t* __restrict__ cellCount, int tileElems, int cellBeg, int cellEnd,
+    int32_t* __restrict__ errFlag) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bx, img;
   xcd_swizzle(bx, img);
+  // the image's status starts clean (k_octree may flag it, k_orient_desc reads it)
+  if (bx == 0 && threadIdx.x == 0) errFlag[img] = 0;
   unsigned char* wbase = smem + wave * fc_wave_bytes(tileElems);
   uint32_t* tile32 = (uint32_t*)wbase;
   const _Float16* tileh = (const _Float16*)wbase;
@@ -2100,7 +2105,8 @@ size_t orb_k_fast_band_lds(int bandElems) {
 hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
-                           uint32_t* cellKeys, int32_t* cellCount, int nimg, hipStream_t s) {
+                           uint32_t* cellKeys, int32_t* cellCount, int32_t* errFlag, int nimg,
+                           hipStream_t s) {
   const size_t lds = orb_k_fast_band_lds(plan->maxBandBytes);
   // each workgroup takes ORB_FAST_BANDS_PER_WG bands (default 2; swept 1-8), prefetching the next
   static const int perWg =
@@ -2108,7 +2114,7 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
   if ((size_t)plan->maxBandBytes > (size_t)4 * FAST_LOADS * 256) return hipErrorInvalidValue;
   dim3 grid((nbands + perWg - 1) / perWg, nimg), block(256);
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, bands, cells, nbands, cellKeys, cellCount);
+                     arenaPitch, *plan, bands, cells, nbands, cellKeys, cellCount, errFlag);
   return hipGetLastError();
 }
 
@@ -2130,7 +2136,7 @@ size_t orb_k_fast_cells_lds(int maxRows, int maxCols) {
 hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
-                            int cellBeg, int cellEnd, int nimg, hipStream_t s) {
+                            int32_t* errFlag, int cellBeg, int cellEnd, int nimg, hipStream_t s) {
   if (cellEnd <= cellBeg) return hipSuccess;
   const int tileElems = fc_tile_elems(plan->maxCellRows, plan->maxCellCols);
   const size_t lds = orb_k_fast_cells_lds(plan->maxCellRows, plan->maxCellCols);
@@ -2143,7 +2149,8 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
   const int n = cellEnd - cellBeg;
   dim3 grid((n + FC_WAVES * FC_CPW - 1) / (FC_WAVES * FC_CPW), nimg), block(64 * FC_WAVES);
   hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, cells, cellKeys, cellCount, tileElems, cellBeg, cellEnd);
+                     arenaPitch, *plan, cells, cellKeys, cellCount, tileElems, cellBeg, cellEnd,
+                     errFlag);
   return hipGetLastError();
 }
 

@@ -33,11 +33,12 @@ bool orb_k_fast_cells_fits(const OrbPlanDesc* plan);
 hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
-                            int cellBeg, int cellEnd, int nimg, hipStream_t s);
+                            int32_t* errFlag, int cellBeg, int cellEnd, int nimg, hipStream_t s);
 hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Stride,
                            const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                            const OrbBandDesc* bands, int nbands, const OrbCellDesc* cells,
-                           uint32_t* cellKeys, int32_t* cellCount, int nimg, hipStream_t s);
+                           uint32_t* cellKeys, int32_t* cellCount, int32_t* errFlag, int nimg,
+                           hipStream_t s);
 size_t orb_k_octree_lds(int nodeCapMax, int maxCellsPerLevel, int ldsKeyCap);
 hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
@@ -670,7 +671,9 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   StageProfiler& pf = h->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
-  HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
+  // the FAST kernels clear each image's status flag (one launch fewer per call);
+  // a plan without cells launches no FAST kernel
+  if (P.ncells == 0) HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
   static const bool bandFast = getenv("ORB_FAST_BANDS") && atoi(getenv("ORB_FAST_BANDS")) > 0;
   static const int kCellsMinBatch =
       getenv("ORB_FAST_CELLS_MIN_BATCH") ? atoi(getenv("ORB_FAST_CELLS_MIN_BATCH")) : 4;
@@ -692,7 +695,8 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     PROF_REC(ev, pf.b(ev, 5), h->stream2);
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), 0, l0End, B, h->stream2));
+                             h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, l0End, B,
+                             h->stream2));
     PROF_REC(ev, pf.e(ev, 5), h->stream2);
     HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
   } else if (ev) {
@@ -714,11 +718,13 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   if (useBands)
     HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                             h->dBands.as<OrbBandDesc>(), P.nBands, h->dCells.as<OrbCellDesc>(),
-                            h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(), B, s));
+                            h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(),
+                            h->dErr.as<int32_t>(), B, s));
   else
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), l0Side ? l0End : 0, P.ncells, B, s));
+                             h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(),
+                             l0Side ? l0End : 0, P.ncells, B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
   // (level 0's octree on the side stream as well measured no gain: the octree's
   // time is its per-workgroup pass latency, not level 0's size)
