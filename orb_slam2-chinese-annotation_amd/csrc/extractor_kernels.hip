@@ -1123,6 +1123,7 @@ __device__ void block_bitonic_desc(unsigned long long* v, int n2) {
 }
 
 #define OCT_MAX_PASSES 512
+#define OCT_RANK_MAX 512  // final-phase candidates ranked by counting (multiple of the 512 threads)
 
 __global__ __launch_bounds__(512) void k_octree(
     OrbPlanDesc plan, const int32_t* __restrict__ cellCount, const uint32_t* __restrict__ cellKeys,
@@ -1301,7 +1302,32 @@ __global__ __launch_bounds__(512) void k_octree(
         rk[a] = 0x7fffffff;
       }
       __syncthreads();
-      block_bitonic_desc(sortBuf, m2);  // largest (size, seq) first == reverse of std::sort
+      // largest (size, seq) first == reverse of std::sort.  Keys are distinct
+      // (creation order is unique), so up to OCT_RANK_MAX candidates are ranked
+      // by counting (every thread scans the keys as LDS broadcasts: two
+      // barriers) instead of the bitonic network's log^2 barrier steps.
+      if (ncand <= OCT_RANK_MAX) {
+        unsigned long long mine[OCT_RANK_MAX / 512];
+        int rank[OCT_RANK_MAX / 512];
+#pragma unroll
+        for (int q = 0; q < OCT_RANK_MAX / 512; ++q) {
+          const int j = t + q * T;
+          mine[q] = j < ncand ? sortBuf[j] : 0ull;
+          rank[q] = 0;
+        }
+        for (int i = 0; i < ncand; ++i) {
+          const unsigned long long k = sortBuf[i];
+#pragma unroll
+          for (int q = 0; q < OCT_RANK_MAX / 512; ++q) rank[q] += k > mine[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < OCT_RANK_MAX / 512; ++q)
+          if (t + q * T < ncand) sortBuf[rank[q]] = mine[q];
+        __syncthreads();
+      } else {
+        block_bitonic_desc(sortBuf, m2);
+      }
       for (int j = t; j < ncand; j += T) rk[(int)(sortBuf[j] & 0xFFFF)] = j;
       for (int k = t; k < n; k += T) {
         const int a = NID[k];
