@@ -1103,6 +1103,55 @@ __device__ int block_scan_array(int* a, int n, int* tmp) {
   return total;
 }
 
+// Two in-place chunked exclusive scans (a[0..na), b[0..nb)) plus the block
+// sum of one value per thread, sharing one round of barriers (four, against
+// eleven for three separate scans).  tmp: >= 51 ints of LDS.  Must be called
+// by all threads; the arrays' writers need no barrier before the call.
+__device__ void block_scan2(int* a, int na, int* b, int nb, int extra, int* tmp, int* totA,
+                            int* totB, int* totX) {
+  const int T = blockDim.x, t = threadIdx.x;
+  const int pa = (na + T - 1) / T, pb = (nb + T - 1) / T;
+  const int ba = min(t * pa, na), ea = min(ba + pa, na);
+  const int bb = min(t * pb, nb), eb = min(bb + pb, nb);
+  __syncthreads();
+  int sa = 0, sb = 0;
+  for (int i = ba; i < ea; ++i) sa += a[i];
+  for (int i = bb; i < eb; ++i) sb += b[i];
+  const int l = lane_id(), w = t >> 6, nw = (T + 63) >> 6;
+  const int ia = wave_incl_scan(sa), ib = wave_incl_scan(sb), ix = wave_incl_scan(extra);
+  if (l == 63) {
+    tmp[w] = ia;
+    tmp[16 + w] = ib;
+    tmp[32 + w] = ix;
+  }
+  __syncthreads();
+  if (t < 3) {
+    int acc = 0;
+    for (int i = 0; i < nw; ++i) {
+      const int v = tmp[16 * t + i];
+      tmp[16 * t + i] = acc;
+      acc += v;
+    }
+    tmp[48 + t] = acc;
+  }
+  __syncthreads();
+  int xa = tmp[w] + ia - sa, xb = tmp[16 + w] + ib - sb;
+  *totA = tmp[48];
+  *totB = tmp[49];
+  *totX = tmp[50];
+  for (int i = ba; i < ea; ++i) {
+    const int v = a[i];
+    a[i] = xa;
+    xa += v;
+  }
+  for (int i = bb; i < eb; ++i) {
+    const int v = b[i];
+    b[i] = xb;
+    xb += v;
+  }
+  __syncthreads();
+}
+
 __device__ void block_bitonic_desc(unsigned long long* v, int n2) {
   for (int k = 2; k <= n2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -1131,7 +1180,7 @@ __global__ __launch_bounds__(512) void k_octree(
     int maxCellsPerLevel, uint32_t* __restrict__ outKeys, int32_t* __restrict__ outCount,
     int32_t* __restrict__ errFlag, int levelBeg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int tmp[17];
+  __shared__ int tmp[52];
   __shared__ int sh[8];
   // grid (images, levels levelBeg..): the dispatcher walks x first, so every
   // image's lowest level (the most keys, the longest workgroups) starts before
@@ -1239,10 +1288,8 @@ __global__ __launch_bounds__(512) void k_octree(
         g0[a] = nce;
         g1[a] = A[a].cnt > 1 ? 0 : 1;
       }
-      int nToExpand;
-      block_excl_scan(nteLocal, tmp, &nToExpand);
-      const int S = block_scan_array(g0, alive, tmp);
-      const int NM = block_scan_array(g1, alive, tmp);
+      int nToExpand, S, NM;
+      block_scan2(g0, alive, g1, alive, nteLocal, tmp, &S, &NM, &nToExpand);
       if (S + NM > NC) {
         if (t == 0) atomicOr(errFlag, 2);
         break;
@@ -1353,11 +1400,10 @@ __global__ __launch_bounds__(512) void k_octree(
       const int jstop = sh[1];
       for (int j = t; j < ncand; j += T)
         if (j > jstop) g1[j] = 0;
-      __syncthreads();
-      const int S = block_scan_array(g1, ncand, tmp);  // child base per divided node
       for (int a = t; a < alive; a += T) g2[a] = (rk[a] <= jstop) ? 0 : 1;
-      __syncthreads();
-      const int keep = block_scan_array(g2, alive, tmp);
+      // child base per divided node, position of each kept node
+      int S, keep, unused;
+      block_scan2(g1, ncand, g2, alive, 0, tmp, &S, &keep, &unused);
       if (S + keep > NC) {
         if (t == 0) atomicOr(errFlag, 2);
         break;
