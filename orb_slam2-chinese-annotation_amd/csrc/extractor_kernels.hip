@@ -1874,6 +1874,10 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     const int slot = 2 * (pairBase + 4 * (lane >> 1)) + (lane & 1);
     if (slot < plan.slotsPerImage) keyv = imgKeys[slot];
   }
+  // the image's per-level keypoint counts, lane l = level l, and their
+  // exclusive prefix (output offsets): loaded once, read by v_readlane
+  const int cntv = lane < plan.nlevels ? cnts[lane] : 0;
+  const int cntx = wave_incl_scan(cntv) - cntv;
   uint32_t (*rsp)[DESC_RS_DW] = sm[w].rsp[half];
   // lane hl < 22 holds rows 2 hl and 2 hl + 1 (row 43 only feeds a zero weight)
   const bool second = hl < DESC_RS_PAIRS;
@@ -1891,7 +1895,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     if (slot0 >= plan.slotsPerImage) return P;
     int l = 0;
     while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot0) ++l;
-    const int i0 = slot0 - plan.lv[l].outOff, nl = cnts[l];
+    const int i0 = slot0 - plan.lv[l].outOff, nl = __builtin_amdgcn_readlane(cntv, l);
     if (i0 >= nl) return P;
     P.valid = true;
     P.l = l;
@@ -1959,6 +1963,17 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   const u16x2 E0 = {18, 34}, E1 = {49, 55}, E2 = {49, 34}, E3 = {18, 0};
   const u16x2 O0 = {0, 18}, O1 = {34, 49}, O2 = {55, 49}, O3 = {34, 18};
 
+  // IC_Angle byte masks of the lane's two rows (the rows are the same for
+  // every keypoint pair): loaded once instead of per pair
+  uint32_t mka[8], mkb[8];
+  {
+    const int ria = 2 * hl - 6, rib = 2 * hl + 1 - 6;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      mka[k] = (ria >= 0 && ria <= 30) ? c_icmask[ria][k] : 0u;
+      mkb[k] = (rib >= 0 && rib <= 30) ? c_icmask[rib][k] : 0u;
+    }
+  }
   Pair cur = setup(0);
   if (cur.valid) issue(cur);
   for (int j = 0; j < DESC_PPW; ++j) {
@@ -1971,11 +1986,11 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
     // by one byte).  m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
     int m01 = 0, m10 = 0;
-    auto ic_row = [&](const uint32_t* d, int ri) {  // staged row ri + 6, ri in [0, 31)
+    auto ic_row = [&](const uint32_t* d, const uint32_t* mk, int ri) {  // staged row ri + 6, ri in [0, 31)
       uint32_t rs = 0, rm = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const uint32_t dd = __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], 1) & c_icmask[ri][k];
+        const uint32_t dd = __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], 1) & mk[k];
         const uint32_t wt = (uint32_t)(4 * k) * 0x01010101u + 0x03020100u;
         rs = __builtin_amdgcn_udot4(dd, 0x01010101u, rs, false);
         rm = __builtin_amdgcn_udot4(dd, wt, rm, false);
@@ -1984,8 +1999,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(
       m01 += (ri - 15) * (int)rs;
     };
     if (P.valid && second) {
-      if (2 * hl >= 6 && 2 * hl <= 36) ic_row(ra, 2 * hl - 6);
-      if (2 * hl + 1 >= 6 && 2 * hl + 1 <= 36) ic_row(rb, 2 * hl + 1 - 6);
+      if (2 * hl >= 6 && 2 * hl <= 36) ic_row(ra, mka, 2 * hl - 6);
+      if (2 * hl + 1 >= 6 && 2 * hl + 1 <= 36) ic_row(rb, mkb, 2 * hl + 1 - 6);
     }
     // (the rows stay in registers through the row pass: the next pair's loads
     // go out after it)
@@ -2083,8 +2098,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
       words[kq] = __ballot(v0 < v1);
     }
     if (P.active && hl == 0) {
-      int base = 0;
-      for (int jl = 0; jl < P.l; ++jl) base += cnts[jl];
+      const int base = __builtin_amdgcn_readlane(cntx, P.l);
       const long long o = (long long)img * capacity + base + P.i;
       uint32_t d[8];
 #pragma unroll
