@@ -272,3 +272,21 @@ def test_batch_hard_cases_vs_oracle(gpu, oracle):
 ])
 def test_batch_parameters_vs_oracle(gpu, oracle, w, h, nf, sf, nl):
     _batch_vs_oracle(gpu, oracle, [gpu.synth_image(40, f, w, h) for f in range(4)], nf, sf, nl)
+
+
+def test_noise_720p_dense_levels(gpu, oracle):
+    """1280x720 uniform noise: level 0 holds tens of thousands of FAST
+    candidates (about 10 % of its pixels), well past any 16-bit key label, so
+    the octree's global-scratch path and its node / key capacities are
+    exercised at a size the reference handles without limits
+    (src/ORBextractor.cc:558-782).  Single frame (band FAST) and a batch of
+    four (cell FAST) against the oracle."""
+    rng = np.random.default_rng(720)
+    imgs = [rng.integers(0, 256, (720, 1280), dtype=np.uint8) for _ in range(4)]
+    k_gpu, d_gpu = gpu.ORBextractor(2000, 1.2, 8, 20, 7)(imgs[0])
+    k_ref, d_ref, _ = oracle.extract(imgs[0], 2000, 1.2, 8, 20, 7)
+    assert k_gpu.tobytes() == k_ref.tobytes(), _diff_report(k_gpu, d_gpu, k_ref, d_ref)
+    assert d_gpu.tobytes() == d_ref.tobytes()
+    cand, _ = oracle.candidates(imgs[0], 2000, 1.2, 8, 20, 7)
+    assert (cand["octave"] == 0).sum() > 65535 // 4, "noise frame not dense enough to matter"
+    _batch_vs_oracle(gpu, oracle, imgs, 2000)
