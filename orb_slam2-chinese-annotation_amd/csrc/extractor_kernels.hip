@@ -1172,8 +1172,10 @@ __device__ void block_bitonic_desc(unsigned long long* v, int n2) {
 }
 
 #define OCT_MAX_PASSES 512
-#define OCT_RANK_MAX 512  // final-phase candidates ranked by counting (multiple of the 512 threads)
+#define OCT_RANK_MAX 512
+#define OCT_REG_KEYS 8  // keys per thread held in registers (n <= 8 x 512), small batches  // final-phase candidates ranked by counting (multiple of the 512 threads)
 
+template <bool REG>
 __global__ __launch_bounds__(512) void k_octree(
     OrbPlanDesc plan, const int32_t* __restrict__ cellCount, const uint32_t* __restrict__ cellKeys,
     uint32_t* __restrict__ gKeys, uint16_t* __restrict__ gNid, int ldsKeyCap, int nodeCapMax,
@@ -1226,17 +1228,52 @@ __global__ __launch_bounds__(512) void k_octree(
     const uint32_t* src = cellKeys + (cellSlot0 + c) * plan.keyCap;
     for (int i = 0; i < cnt; ++i) K[base + i] = src[i];
   }
+  // REG (a frame or two per call, one workgroup per level): each thread's keys
+  // k = t, t + T, ... live in registers (key and node id) for the whole
+  // distribution when the level has at most OCT_REG_KEYS * T of them: a pass's
+  // per-key steps are then independent register work with only the node
+  // lookups in LDS, instead of dependent LDS round trips per key.  Batches keep
+  // K / NID in memory: the registers would cost them occupancy (6 -> 4 waves
+  // per SIMD, 0.129 -> 0.167 ms per 512 frames).
+  const bool inReg = REG && n <= OCT_REG_KEYS * T;
+  uint32_t kr[OCT_REG_KEYS];
+  int nr[OCT_REG_KEYS];
+  auto each_key = [&](auto&& f) {
+    if (inReg) {
+#pragma unroll
+      for (int i = 0; i < OCT_REG_KEYS; ++i) {
+        const int k = t + i * T;
+        if (k < n) f(kr[i], nr[i], k);
+      }
+    } else {
+      for (int k = t; k < n; k += T) {
+        const uint32_t key = K[k];
+        int nid = NID[k];
+        f(key, nid, k);
+        NID[k] = (uint16_t)nid;
+      }
+    }
+  };
+  __syncthreads();  // K complete
+  if (inReg) {
+#pragma unroll
+    for (int i = 0; i < OCT_REG_KEYS; ++i) {
+      const int k = t + i * T;
+      kr[i] = k < n ? K[k] : 0u;
+      nr[i] = 0;
+    }
+  }
   // ---- roots (src/ORBextractor.cc:562-604)
   const int nIni = L.nIni;
   const float hX = L.hX;
   for (int i = t; i < nIni; i += T) g0[i] = 0;
   __syncthreads();
-  for (int k = t; k < n; k += T) {
-    const float xr = (float)(key_x(K[k]) - 16);
+  each_key([&](uint32_t key, int& nid, int) {
+    const float xr = (float)(key_x(key) - 16);
     const int r = min((int)__fdiv_rn(xr, hX), nIni - 1);  // vpIniNodes[kp.pt.x/hX]
-    NID[k] = (uint16_t)r;
+    nid = r;
     atomicAdd(&g0[r], 1);
-  }
+  });
   __syncthreads();
   if (t == 0) {
     int a = 0;
@@ -1256,7 +1293,7 @@ __global__ __launch_bounds__(512) void k_octree(
     sh[0] = a;
   }
   __syncthreads();
-  for (int k = t; k < n; k += T) NID[k] = (uint16_t)g1[NID[k]];
+  each_key([&](uint32_t, int& nid, int) { nid = g1[nid]; });
   int alive = sh[0];
   const int N = L.quota;
   int seqNext = nIni;
@@ -1269,10 +1306,10 @@ __global__ __launch_bounds__(512) void k_octree(
       // ================= regular pass: divide every node with > 1 key (:625-684)
       for (int i = t; i < alive * 4; i += T) q4[i] = 0;
       __syncthreads();
-      for (int k = t; k < n; k += T) {
-        const int a = NID[k];
-        if (A[a].cnt > 1) atomicAdd(&q4[a * 4 + oct_quad(K[k], A[a])], 1);
-      }
+      each_key([&](uint32_t key, int& nid, int) {
+        const OctNode nd = A[nid];
+        if (nd.cnt > 1) atomicAdd(&q4[nid * 4 + oct_quad(key, nd)], 1);
+      });
       __syncthreads();
       int nteLocal = 0;
       for (int a = t; a < alive; a += T) {
@@ -1315,11 +1352,10 @@ __global__ __launch_bounds__(512) void k_octree(
         }
       }
       __syncthreads();
-      for (int k = t; k < n; k += T) {
-        const int a = NID[k];
-        const OctNode& nd = A[a];
-        NID[k] = (uint16_t)q4[a * 4 + (nd.cnt > 1 ? oct_quad(K[k], nd) : 0)];
-      }
+      each_key([&](uint32_t key, int& nid, int) {
+        const OctNode nd = A[nid];
+        nid = q4[nid * 4 + (nd.cnt > 1 ? oct_quad(key, nd) : 0)];
+      });
       __syncthreads();
       OctNode* sw = A; A = B; B = sw;
       alive = S + NM;
@@ -1376,10 +1412,10 @@ __global__ __launch_bounds__(512) void k_octree(
         block_bitonic_desc(sortBuf, m2);
       }
       for (int j = t; j < ncand; j += T) rk[(int)(sortBuf[j] & 0xFFFF)] = j;
-      for (int k = t; k < n; k += T) {
-        const int a = NID[k];
-        if (A[a].cnt > 1) atomicAdd(&q4[a * 4 + oct_quad(K[k], A[a])], 1);
-      }
+      each_key([&](uint32_t key, int& nid, int) {
+        const OctNode nd = A[nid];
+        if (nd.cnt > 1) atomicAdd(&q4[nid * 4 + oct_quad(key, nd)], 1);
+      });
       if (t == 0) sh[1] = ncand - 1;
       __syncthreads();
       // node j in sorted order adds (non-empty children - 1) nodes; stop after
@@ -1430,11 +1466,10 @@ __global__ __launch_bounds__(512) void k_octree(
         }
       }
       __syncthreads();
-      for (int k = t; k < n; k += T) {
-        const int a = NID[k];
-        const OctNode& nd = A[a];
-        NID[k] = (uint16_t)q4[a * 4 + (rk[a] <= jstop ? oct_quad(K[k], nd) : 0)];
-      }
+      each_key([&](uint32_t key, int& nid, int) {
+        const OctNode nd = A[nid];
+        nid = q4[nid * 4 + (rk[nid] <= jstop ? oct_quad(key, nd) : 0)];
+      });
       __syncthreads();
       OctNode* sw = A; A = B; B = sw;
       alive = S + keep;
@@ -1447,8 +1482,9 @@ __global__ __launch_bounds__(512) void k_octree(
   uint32_t* best = (uint32_t*)g0;
   for (int a = t; a < alive; a += T) best[a] = 0u;
   __syncthreads();
-  for (int k = t; k < n; k += T)
-    atomicMax(&best[NID[k]], ((uint32_t)key_s(K[k]) << 24) | (uint32_t)(0xFFFFFF - k));
+  each_key([&](uint32_t key, int& nid, int k) {
+    atomicMax(&best[nid], ((uint32_t)key_s(key) << 24) | (uint32_t)(0xFFFFFF - k));
+  });
   __syncthreads();
   uint32_t* out = outKeys + (long long)img * plan.slotsPerImage + L.outOff;
   for (int a = t; a < alive; a += T) out[a] = K[0xFFFFFF - (int)(best[a] & 0xFFFFFF)];
@@ -1847,12 +1883,18 @@ struct DescWaveLds {
 
 #define DESC_PPW 4  // slot pairs per wave (software-pipelined: the next pair's window loads overlap this one)
 
+template <int PPW>
 __global__ __launch_bounds__(256) void k_orient_desc(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const uint32_t* __restrict__ outKeys, const int32_t* __restrict__ outCount,
     const int32_t* __restrict__ errFlag, orb_keypoint_t* __restrict__ kps,
-    uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts) {
+    uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts, int ppwRt) {
+  // PPW > 0: compile-time pairs per wave (batches); PPW == 0: ppwRt (small calls;
+  // an instantiation with a compile-time single pair, k_orient_desc<1>, wrote
+  // keypoints to the wrong slots under ROCm 7.2 hipcc while the same source with
+  // the count at run time is bit-exact)
+  const int ppw = PPW ? PPW : ppwRt;
   __shared__ __attribute__((aligned(16))) DescWaveLds sm[4];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31;
@@ -1864,13 +1906,13 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
     counts[img] = errFlag[img] ? (int32_t)ORB_EDEVICE : tot;  // failed image: negative count
   }
-  // this wave's slot pairs: pairBase + 4 j, j < DESC_PPW (the workgroup's four
-  // waves interleave); lane 2 j + h holds the packed key of slot 2 (pairBase + 4 j) + h
-  const int pairBase = bx * 4 * DESC_PPW + w;
+  // this wave's slot pairs: pairBase + 4 j, j < ppw <= DESC_PPW (the workgroup's
+  // four waves interleave); lane 2 j + h holds the packed key of slot 2 (pairBase + 4 j) + h
+  const int pairBase = bx * 4 * ppw + w;
   if (2 * pairBase >= plan.slotsPerImage) return;
   const uint32_t* imgKeys = outKeys + (long long)img * plan.slotsPerImage;
   uint32_t keyv = 0;
-  if (lane < 2 * DESC_PPW) {
+  if (lane < 2 * ppw) {
     const int slot = 2 * (pairBase + 4 * (lane >> 1)) + (lane & 1);
     if (slot < plan.slotsPerImage) keyv = imgKeys[slot];
   }
@@ -1976,7 +2018,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
   }
   Pair cur = setup(0);
   if (cur.valid) issue(cur);
-  for (int j = 0; j < DESC_PPW; ++j) {
+  for (int j = 0; j < ppw; ++j) {
     const Pair P = cur;
     if (P.valid && second) {
       realign(ra, sha);
@@ -2004,7 +2046,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     }
     // (the rows stay in registers through the row pass: the next pair's loads
     // go out after it)
-    if (!P.valid && j + 1 < DESC_PPW) {
+    if (!P.valid && j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
@@ -2053,7 +2095,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(
                        o[0][2] | (o[1][2] << 16), o[0][3] | (o[1][3] << 16));
       }
     }
-    if (j + 1 < DESC_PPW) {
+    if (j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
@@ -2195,8 +2237,11 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
                            hipStream_t s) {
   const size_t lds = orb_k_fast_band_lds(plan->maxBandBytes);
   // each workgroup takes ORB_FAST_BANDS_PER_WG bands (default 2; swept 1-8), prefetching the next
-  static const int perWg =
-      getenv("ORB_FAST_BANDS_PER_WG") ? std::max(1, atoi(getenv("ORB_FAST_BANDS_PER_WG"))) : 2;
+  // (one band per workgroup for a frame or two per call: the grid is small and
+  // the per-workgroup band chain is the latency)
+  static const int perWgEnv =
+      getenv("ORB_FAST_BANDS_PER_WG") ? std::max(1, atoi(getenv("ORB_FAST_BANDS_PER_WG"))) : 0;
+  const int perWg = perWgEnv ? perWgEnv : (nimg <= 2 ? 1 : 2);
   if ((size_t)plan->maxBandBytes > (size_t)4 * FAST_LOADS * 256) return hipErrorInvalidValue;
   dim3 grid((nbands + perWg - 1) / perWg, nimg), block(256);
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
@@ -2260,14 +2305,21 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         hipStream_t s) {
   if (levelEnd <= levelBeg || nimg <= 0) return hipSuccess;
   const size_t lds = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, ldsKeyCap);
+  // register-resident keys for a few frames per call (one workgroup per level)
+  const bool reg = nimg <= 16;
+  const void* fn = reg ? (const void*)k_octree<true> : (const void*)k_octree<false>;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_octree,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   dim3 grid(nimg, levelEnd - levelBeg), block(512);
-  hipLaunchKernelGGL(k_octree, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys, gNid,
-                     ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, levelBeg);
+  if (reg)
+    hipLaunchKernelGGL(k_octree<true>, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys, gNid,
+                       ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, levelBeg);
+  else
+    hipLaunchKernelGGL(k_octree<false>, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,
+                       gNid, ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag,
+                       levelBeg);
   return hipGetLastError();
 }
 
@@ -2305,9 +2357,20 @@ hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0S
                              const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
                              int capacity, int32_t* counts, int nimg, hipStream_t s) {
   if (plan->slotsPerImage & 1) return hipErrorInvalidValue;
-  dim3 grid((plan->slotsPerImage + 8 * DESC_PPW - 1) / (8 * DESC_PPW), nimg), block(256);
-  hipLaunchKernelGGL(k_orient_desc, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts);
+  // DESC_PPW keypoint pairs per wave for batches (the next pair's loads overlap
+  // the current one); one pair per wave for a frame or two per call, where the
+  // grid is small and the per-wave chain is the latency (ORB_DESC_PPW overrides)
+  static const int kPpw = getenv("ORB_DESC_PPW") ? atoi(getenv("ORB_DESC_PPW")) : 0;
+  const int ppw = kPpw == 1 || kPpw == DESC_PPW ? kPpw : (nimg <= 2 ? 1 : DESC_PPW);
+  dim3 grid((plan->slotsPerImage + 8 * ppw - 1) / (8 * ppw), nimg), block(256);
+  if (ppw == DESC_PPW)
+    hipLaunchKernelGGL(k_orient_desc<DESC_PPW>, grid, block, 0, s, img0, img0Pitch, img0Stride,
+                       arena, arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity,
+                       counts, DESC_PPW);
+  else
+    hipLaunchKernelGGL(k_orient_desc<0>, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
+                       arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts,
+                       ppw);
   return hipGetLastError();
 }
 

@@ -290,3 +290,9 @@ def test_noise_720p_dense_levels(gpu, oracle):
     cand, _ = oracle.candidates(imgs[0], 2000, 1.2, 8, 20, 7)
     assert (cand["octave"] == 0).sum() > 65535 // 4, "noise frame not dense enough to matter"
     _batch_vs_oracle(gpu, oracle, imgs, 2000)
+
+
+def test_large_batch_vs_oracle(gpu, oracle):
+    """More than 16 frames per call: the octree keeps its keys in LDS / global
+    scratch instead of registers (the batch configuration of the bench)."""
+    _batch_vs_oracle(gpu, oracle, [gpu.synth_image(50, f, 640, 480) for f in range(20)])
