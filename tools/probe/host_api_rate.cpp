@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "../../include/orb_abi.h"
@@ -95,6 +96,21 @@ int main(int argc, char** argv) {
   }
   printf("stereo pair 1241x376 2000+2000 feat: two extractions %.3f ms + ComputeStereoMatches on the handles %.3f ms per pair\n",
          tx / NS, ts / NS);
+  // the same with the two extractions on two threads, as Frame's stereo
+  // constructor runs them (src/Frame.cc:81-84): the handles' streams overlap
+  double tc = 0;
+  for (int i = 0; i < NS + 10; ++i) {
+    const double t0 = now_ms();
+    std::thread left([&] {
+      CHECK(orb_extractor_extract(el, il.data(), W, H, W, kl.data(), dl.data(), cap2, &nl));
+    });
+    CHECK(orb_extractor_extract(er, ir.data(), W, H, W, kr.data(), dr.data(), cap2, &nr));
+    left.join();
+    CHECK(orb_stereo_match_extracted(m, el, er, 386.1448f, 718.856f, ur.data(), dp.data(), cap2, &nn));
+    if (i >= 10) tc += now_ms() - t0;
+  }
+  printf("stereo pair, the two extractions on two threads: %.3f ms per pair incl. ComputeStereoMatches\n",
+         tc / NS);
 
   // SearchByProjection(F, local map) on host buffers, 5000 map points
   std::vector<orb_mp_track_t> mps(5000);
