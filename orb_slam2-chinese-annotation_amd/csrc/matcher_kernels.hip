@@ -96,7 +96,9 @@ __global__ __launch_bounds__(64) void k_grid_build(const orb_keypoint_t* __restr
 // (the order GetFeaturesInArea visits them), so the scan is LDS-latency bound;
 // only the descriptors of window candidates come from global memory.  Frames
 // with more than PROJ_STAGE keypoints scan the global grid instead.
-#define PROJ_STAGE 2048
+#ifndef PROJ_STAGE
+#define PROJ_STAGE 4096  // frames with up to this many keypoints are staged (C5: 4000)
+#endif
 
 #ifndef PROJ_WG
 #define PROJ_WG 512  // map points per workgroup (grid staged once per workgroup; swept 256-1024)
@@ -389,6 +391,11 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
   if (mpMax <= 0 || nproblems <= 0) return hipSuccess;
   // dynamic LDS: the staged keypoints of a frame, sized to the key capacity
   const size_t lds = (size_t)std::min(kpStride, PROJ_STAGE) * sizeof(uint4);
+  if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {  // with the static grid table
+    hipError_t e = hipFuncSetAttribute((const void*)k_proj_candidates,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems),
                      dim3(PROJ_WG), lds, s,
                      keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
