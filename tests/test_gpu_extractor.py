@@ -194,6 +194,8 @@ def test_extractor_rejects_unsupported_scale(gpu):
     (640, 480, 644, 644 * 480 + 2, 5),      # aligned rows, images at alternating alignment
     (641, 479, 641, 641 * 479, 3),          # odd stride and odd image pitch
     (1241, 376, 1241, 1241 * 376, 9),       # 9 images: uneven images per workgroup
+    (1241, 376, 1241, 1241 * 376, 2),       # 2 images: the small-call launch shapes
+    (640, 480, 648, 648 * 480 + 4, 1),      # 1 image through the batch entry point
 ])
 def test_batch_layouts_vs_oracle(gpu, oracle, w, h, stride, pitch, B):
     """extract_batch over B images packed at (stride, pitch): the resize and blur
