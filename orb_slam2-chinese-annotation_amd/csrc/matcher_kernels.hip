@@ -7,6 +7,7 @@
 // first K candidates in (distance, scan order) order, and an ordered resolve
 // stage that replays the sequential semantics exactly.
 #include <algorithm>
+#include <cmath>
 
 #include "matcher_common.h"
 
@@ -446,12 +447,68 @@ struct StereoPairLevels {
   const uint8_t* R[ORB_MAX_LEVELS];
 };
 
+// vRowIndices (src/Frame.cc:531-550) as CSR per pair: row yi lists every right
+// keypoint whose band [floor(y - 2 s), ceil(y + 2 s)] contains it (s = the
+// keypoint's scale factor).  One workgroup per pair, LDS row counters.  The
+// order inside a row is free: the match is the lexicographic (distance, iR)
+// minimum, which is the reference's first minimum in ascending iR.
+__global__ __launch_bounds__(1024) void k_stereo_rows(const orb_keypoint_t* __restrict__ rkeys,
+                                                      const int32_t* __restrict__ nright,
+                                                      int kpStride, StereoParams P,
+                                                      int32_t* __restrict__ rowStart,
+                                                      int32_t* __restrict__ rowIdx, int rowCap) {
+  extern __shared__ int cnt[];  // rows + 1
+  __shared__ int tmp[17];
+  const int pair = blockIdx.x, t = threadIdx.x, T = blockDim.x;
+  const int H = P.h[0], NR = nright[pair];
+  const orb_keypoint_t* K = rkeys + (size_t)pair * kpStride;
+  for (int i = t; i <= H; i += T) cnt[i] = 0;
+  __syncthreads();
+  auto band = [&](const orb_keypoint_t& kp, int* lo, int* hi) {
+    const float r = 2.0f * P.scale[kp.octave];
+    *lo = max((int)floorf(kp.y - r), 0);
+    *hi = min((int)ceilf(kp.y + r), H - 1);
+  };
+  for (int iR = t; iR < NR; iR += T) {
+    int lo, hi;
+    band(K[iR], &lo, &hi);
+    for (int yi = lo; yi <= hi; ++yi) atomicAdd(&cnt[yi], 1);
+  }
+  __syncthreads();
+  {  // exclusive scan of the H + 1 counters, a chunk per thread
+    const int n = H + 1, per = (n + T - 1) / T, b = min(t * per, n), e = min(b + per, n);
+    int sum = 0;
+    for (int i = b; i < e; ++i) sum += cnt[i];
+    int total;
+    int ex = block_excl_scan(sum, tmp, &total);
+    for (int i = b; i < e; ++i) {
+      const int v = cnt[i];
+      cnt[i] = ex;
+      ex += v;
+    }
+    __syncthreads();
+  }
+  int32_t* rs = rowStart + (size_t)pair * (H + 1);
+  for (int i = t; i <= H; i += T) rs[i] = cnt[i];
+  __syncthreads();
+  int32_t* ri = rowIdx + (size_t)pair * rowCap;
+  for (int iR = t; iR < NR; iR += T) {
+    int lo, hi;
+    band(K[iR], &lo, &hi);
+    for (int yi = lo; yi <= hi; ++yi) {
+      const int pos = atomicAdd(&cnt[yi], 1);
+      if (pos < rowCap) ri[pos] = iR;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_stereo_match(
     const orb_keypoint_t* __restrict__ lkeys, const uint8_t* __restrict__ ldesc,
     const int32_t* __restrict__ nleft, const orb_keypoint_t* __restrict__ rkeys,
     const uint8_t* __restrict__ rdesc, const int32_t* __restrict__ nright, int kpStride,
     const StereoPairLevels* __restrict__ pyr, StereoParams P, float* __restrict__ uRight,
-    float* __restrict__ depth, int32_t* __restrict__ sad) {
+    float* __restrict__ depth, int32_t* __restrict__ sad, const int32_t* __restrict__ rowStart,
+    const int32_t* __restrict__ rowIdx, int rowCap) {
   const int pair = blockIdx.y, lane = threadIdx.x & 63;
   const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int NL = nleft[pair], NR = nright[pair];
@@ -467,13 +524,16 @@ __global__ __launch_bounds__(256) void k_stereo_match(
   const int row = (int)vL;  // vRowIndices[vL]: float -> size_t truncation
   const float minU = uL - maxD, maxU = uL - minD;
   int bestDist = 1 << 30, bestIdx = 1 << 30;
-  if (maxU >= 0) {
+  (void)NR;
+  if (maxU >= 0 && row >= 0 && row < P.h[0]) {
     const ulonglong4 dL = load_desc(ldesc + (base + iL) * 32);
-    for (int iR = lane; iR < NR; iR += 64) {
+    // vCandidates = vRowIndices[vL]: the right keypoints whose band holds the row
+    const int32_t* rs = rowStart + (size_t)pair * (P.h[0] + 1);
+    const int32_t* ri = rowIdx + (size_t)pair * rowCap;
+    const int jEnd = min(rs[row + 1], rowCap);
+    for (int j = rs[row] + lane; j < jEnd; j += 64) {
+      const int iR = ri[j];
       const orb_keypoint_t kpR = rkeys[base + iR];
-      const float r = 2.0f * P.scale[kpR.octave];
-      const int maxr = (int)ceilf(kpR.y + r), minr = (int)floorf(kpR.y - r);
-      if (row < minr || row > maxr) continue;
       if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
       const float uR = kpR.x;
       if (!(uR >= minU && uR <= maxU)) continue;
@@ -589,18 +649,38 @@ __global__ __launch_bounds__(256) void k_stereo_prune(const int32_t* __restrict_
 
 extern "C" size_t orb_k_stereo_params_size(void) { return sizeof(StereoParams); }
 
+// Row-index scratch of orb_k_stereo: ints per pair for the row starts and for
+// the row lists (every right keypoint listed in each row of its band).
+extern "C" void orb_k_stereo_scratch(const void* params, int kpStride, size_t* startInts,
+                                     size_t* idxInts) {
+  const StereoParams& P = *(const StereoParams*)params;
+  float smax = 1.f;
+  for (int l = 0; l < P.nLevels; ++l) smax = std::max(smax, P.scale[l]);
+  *startInts = (size_t)P.h[0] + 1;
+  *idxInts = (size_t)kpStride * (size_t)(std::ceil(4.0 * smax) + 3.0);
+}
+
 extern "C" hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc,
                                    const int32_t* nleft, const orb_keypoint_t* rkeys,
                                    const uint8_t* rdesc, const int32_t* nright, int kpStride,
                                    int maxLeft, const void* pyr, const void* params,
                                    float* uRight, float* depth, int32_t* sad, int npairs,
-                                   hipStream_t s) {
+                                   int32_t* rowStart, int32_t* rowIdx, hipStream_t s) {
   if (npairs <= 0 || maxLeft <= 0) return hipSuccess;
   const StereoParams P = *(const StereoParams*)params;
+  size_t startInts, idxInts;
+  orb_k_stereo_scratch(params, kpStride, &startInts, &idxInts);
+  const size_t rowsLds = ((size_t)P.h[0] + 1) * sizeof(int);
+  if (rowsLds > 64 * 1024) return hipErrorInvalidValue;  // images up to 16k rows
+  hipLaunchKernelGGL(k_stereo_rows, dim3(npairs), dim3(1024), rowsLds, s, rkeys, nright,
+                     kpStride, P, rowStart, rowIdx, (int)idxInts);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_stereo_match, dim3((maxLeft + 3) / 4, npairs), dim3(256), 0, s, lkeys,
                      ldesc, nleft, rkeys, rdesc, nright, kpStride,
-                     (const StereoPairLevels*)pyr, P, uRight, depth, sad);
-  hipError_t e = hipGetLastError();
+                     (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
+                     (int)idxInts);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_stereo_prune, dim3(npairs), dim3(256), 0, s, nleft, kpStride, uRight,
                      depth, sad);

@@ -83,7 +83,9 @@ size_t orb_k_stereo_params_size(void);
 hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc, const int32_t* nleft,
                         const orb_keypoint_t* rkeys, const uint8_t* rdesc, const int32_t* nright,
                         int kpStride, int maxLeft, const void* pyr, const void* params,
-                        float* uRight, float* depth, int32_t* sad, int npairs, hipStream_t s);
+                        float* uRight, float* depth, int32_t* sad, int npairs,
+                        int32_t* rowStart, int32_t* rowIdx, hipStream_t s);
+void orb_k_stereo_scratch(const void* params, int kpStride, size_t* startInts, size_t* idxInts);
 size_t orb_k_frame_params_size(void);
 size_t orb_k_frustum_params_size(void);
 hipError_t orb_k_frustum(const orb_map_point_t* mps, const int32_t* nmps, int mpStride,
@@ -1198,6 +1200,7 @@ struct orb_matcher {
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
   // stereo / frame / BoW scratch
+  DevBuf dStRowStart, dStRowIdx;  // stereo vRowIndices (CSR per pair)
   DevBuf dRKeys, dRDesc, dNR, dPyr, dPairLv, dDepth, dSad, dBowA, dBowB, dBowC, dBowD, dBowE,
       dBowF, dBowG, dBowH, dBowI, dBowJ, dBowK;
   HostBuf hPyr;  // pinned staging of the host stereo pyramids (one DMA)
@@ -1262,7 +1265,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
                     &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut,
                     &m->dRKeys, &m->dRDesc, &m->dNR, &m->dPyr, &m->dPairLv, &m->dDepth,
-                    &m->dSad, &m->dBowA, &m->dBowB, &m->dBowC, &m->dBowD, &m->dBowE,
+                    &m->dSad, &m->dStRowStart, &m->dStRowIdx, &m->dBowA, &m->dBowB, &m->dBowC, &m->dBowD, &m->dBowE,
                     &m->dBowF, &m->dBowG, &m->dBowH, &m->dBowI, &m->dBowJ, &m->dBowK,
                     &m->dMapPts, &m->dPose, &m->dTracks, &m->dNInView, &m->dK1, &m->dD1,
                     &m->dK2, &m->dD2, &m->dN1, &m->dN2, &m->dPrev, &m->dList, &m->dM12,
@@ -1507,6 +1510,15 @@ static orb_status_t upload(DevBuf& b, const void* src, size_t n, hipStream_t s) 
   return ORB_OK;
 }
 
+// the row-index scratch of orb_k_stereo for n_pairs pairs
+static orb_status_t stereo_scratch(orb_matcher* m, const void* params, int kpStride, int npairs) {
+  size_t a = 0, b = 0;
+  orb_k_stereo_scratch(params, kpStride, &a, &b);
+  orb_status_t st = m->dStRowStart.ensure(std::max<size_t>(a * npairs, 1) * 4);
+  if (st) return st;
+  return m->dStRowIdx.ensure(std::max<size_t>(b * npairs, 1) * 4);
+}
+
 orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in, float* u_right,
                               float* depth) {
   if (!m || !in || !in->left || !u_right || !depth) return ORB_EINVAL;
@@ -1578,10 +1590,12 @@ orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in, fl
   if ((st = m->dUr.ensure((size_t)stride * 4))) return st;
   if ((st = m->dDepth.ensure((size_t)stride * 4))) return st;
   if ((st = m->dSad.ensure((size_t)stride * 4))) return st;
+  if ((st = stereo_scratch(m, &P, stride, 1))) return st;
   HIP_TRY(orb_k_stereo(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(),
                        m->dNKeys.as<int32_t>(), m->dRKeys.as<orb_keypoint_t>(),
                        m->dRDesc.as<uint8_t>(), m->dNR.as<int32_t>(), stride, NL, m->dPairLv.p, &P,
-                       m->dUr.as<float>(), m->dDepth.as<float>(), m->dSad.as<int32_t>(), 1, s));
+                       m->dUr.as<float>(), m->dDepth.as<float>(), m->dSad.as<int32_t>(), 1,
+                       m->dStRowStart.as<int32_t>(), m->dStRowIdx.as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(u_right, m->dUr.p, (size_t)NL * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(depth, m->dDepth.p, (size_t)NL * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -1632,9 +1646,10 @@ orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor
   if (st) return st;
   HIP_TRY(hipMemcpyAsync(m->dPairLv.p, lv.data(), lv.size() * sizeof(StereoPairLevelsHost),
                          hipMemcpyHostToDevice, s));
+  if ((st = stereo_scratch(m, &P, kp_stride, n_pairs))) return st;
   HIP_TRY(orb_k_stereo(d_left_keys, d_left_desc, d_left_n, d_right_keys, d_right_desc, d_right_n,
                        kp_stride, kp_stride, m->dPairLv.p, &P, d_u_right, d_depth, d_sad,
-                       n_pairs, s));
+                       n_pairs, m->dStRowStart.as<int32_t>(), m->dStRowIdx.as<int32_t>(), s));
   // the pair-level pointer table must outlive the asynchronous launch
   HIP_TRY(hipStreamSynchronize(s));
   return ORB_OK;
@@ -1713,13 +1728,15 @@ orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_
   const int stride = std::max(left_ext->oneCap, right_ext->oneCap);
   // the two records blocks have their own capacities: pair 0 only, so the
   // shared kpStride of the kernel is never applied
+  if ((st = stereo_scratch(m, &P, stride, 1))) return st;
   HIP_TRY(orb_k_stereo(reinterpret_cast<const orb_keypoint_t*>(l1 + 16),
                        l1 + 16 + (size_t)left_ext->oneCap * sizeof(orb_keypoint_t),
                        reinterpret_cast<const int32_t*>(l1),
                        reinterpret_cast<const orb_keypoint_t*>(r1 + 16),
                        r1 + 16 + (size_t)right_ext->oneCap * sizeof(orb_keypoint_t),
                        reinterpret_cast<const int32_t*>(r1), stride, nL, m->dPairLv.p, &P,
-                       m->dUr.as<float>(), m->dDepth.as<float>(), m->dSad.as<int32_t>(), 1, s));
+                       m->dUr.as<float>(), m->dDepth.as<float>(), m->dSad.as<int32_t>(), 1,
+                       m->dStRowStart.as<int32_t>(), m->dStRowIdx.as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(m->hPyr.p, m->dUr.p, (size_t)nL * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(m->hPyr.as<uint8_t>() + (size_t)nL * 4, m->dDepth.p, (size_t)nL * 4,
                          hipMemcpyDeviceToHost, s));
