@@ -562,19 +562,46 @@ __global__ __launch_bounds__(256) void k_stereo_match(
       const int sL = P.strideL[levelL], sR = P.strideR[levelL];
       const int y0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
       const int cL = IL[(long long)(y0 + w) * sL + xl0 + w];
-      int dists[11];
+      // lane p < 121 (two rounds) owns patch pixel (yy, xx): its left value
+      // once, and the 11 right values it meets over the 11 shifts, which are
+      // consecutive bytes of one right row (four dword loads, realigned); the
+      // shifts' right centres come from lanes 0..10.  Per-shift SADs are
+      // < 121 * 255 < 2^16, so two share a word through the wave reduction.
+      const int xrb = (int)scaleduR0 - L - w;  // right patch column of shift -L
+      const int cRv = lane < 2 * L + 1 ? (int)IR[(long long)(y0 + w) * sR + xrb + w + lane] : 0;
+      int acc[11];
 #pragma unroll
-      for (int inc = -L; inc <= L; ++inc) {
-        const int xr0 = (int)scaleduR0 + inc - w;
-        const int cR = IR[(long long)(y0 + w) * sR + xr0 + w];
-        int acc = 0;
-        for (int p = lane; p < 121; p += 64) {
+      for (int k = 0; k < 11; ++k) acc[k] = 0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int p = lane + 64 * q;
+        if (p < 121) {
           const int yy = p / 11, xx = p - yy * 11;
           const int a = (int)IL[(long long)(y0 + yy) * sL + xl0 + xx] - cL;
-          const int b = (int)IR[(long long)(y0 + yy) * sR + xr0 + xx] - cR;
-          acc += abs(a - b);
+          const uint8_t* rrow = IR + (long long)(y0 + yy) * sR + xrb + xx;
+          const uintptr_t ra = (uintptr_t)rrow;
+          const uint32_t* rw = reinterpret_cast<const uint32_t*>(ra & ~(uintptr_t)3);
+          const uint32_t shb = (uint32_t)(ra & 3);
+          uint32_t wv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) wv[k] = rw[k];
+          uint32_t bw[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) bw[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], shb);
+#pragma unroll
+          for (int k = 0; k < 11; ++k) {
+            const int b = (int)((bw[k >> 2] >> (8 * (k & 3))) & 0xFFu) - __builtin_amdgcn_readlane(cRv, k);
+            acc[k] += abs(a - b);
+          }
         }
-        dists[inc + L] = wave_sum(acc);
+      }
+      int dists[11];
+#pragma unroll
+      for (int k = 0; k < 11; k += 2) {
+        const int packed = acc[k] | (k + 1 < 11 ? acc[k + 1] << 16 : 0);
+        const int sum = wave_sum(packed);
+        dists[k] = sum & 0xFFFF;
+        if (k + 1 < 11) dists[k + 1] = (int)((uint32_t)sum >> 16);
       }
       int bestSad = 2147483647, bestinc = 0;
 #pragma unroll
