@@ -50,16 +50,18 @@ def test_search_by_projection_local(gpu, oracle, w, h, nf, M, th, seed):
     assert n_ref > 0
 
 
-def test_search_by_projection_conflicts_and_flags(gpu, oracle):
+@pytest.mark.parametrize("M,nsrc", [(4000, 40), (24000, 120)])
+def test_search_by_projection_conflicts_and_flags(gpu, oracle, M, nsrc):
     """Many map points on few keypoints (deep first-come chains, top-K overflow),
     points without observations (claims that do not lock), bad / out-of-view
-    points, stereo gating through mvuRight."""
+    points, stereo gating through mvuRight.  24,000 points take the resolve's
+    512-point windows (local maps of 20,000 points and more), 4,000 its
+    256-point ones."""
     w, h = 640, 480
     k, d, scale = _frame(gpu, oracle, w, h, 1000, 3)
     rng = np.random.default_rng(7)
-    M = 4000
     mps = np.zeros(M, oracle.MP_TRACK_DTYPE)
-    src = rng.integers(0, 40, M)  # 4000 points onto 40 keypoints
+    src = rng.integers(0, nsrc, M)  # M points onto nsrc keypoints
     mps["proj_x"] = k["x"][src] + rng.uniform(-2, 2, M).astype(np.float32)
     mps["proj_y"] = k["y"][src] + rng.uniform(-2, 2, M).astype(np.float32)
     mps["proj_xr"] = mps["proj_x"] - rng.uniform(5, 40, M).astype(np.float32)
