@@ -25,8 +25,78 @@ __global__ __launch_bounds__(256) void k_hamming_batch(const uint8_t* __restrict
 // cell = (round((x-minX)*invW), round((y-minY)*invH)), out-of-grid keys dropped,
 // per-cell lists in ascending keypoint index.  Stored as CSR with cell index
 // ix*48+iy, the order GetFeaturesInArea scans (ix outer, iy inner, :391-400).
-// One wave per frame.
-__global__ __launch_bounds__(64) void k_grid_build(const orb_keypoint_t* __restrict__ keys,
+// One workgroup per frame: LDS counts, a block scan over the 3072 cells, an
+// unordered scatter by LDS cursors, then every cell's short list is put back
+// in keypoint order by one thread (insertion sort; cells hold ~1-10 keys).
+// Frames with kpStride up to GB_LDS_KEYS keypoints build their lists in LDS;
+// larger frames use k_grid_build_wave (one wave, stable ballot scatter).
+#define GB_T 256
+#define GB_LDS_KEYS 8192
+__global__ __launch_bounds__(GB_T) void k_grid_build(const orb_keypoint_t* __restrict__ keys,
+                                                     const int32_t* __restrict__ nkeys, int kpStride,
+                                                     float minX, float minY, float invW, float invH,
+                                                     int32_t* __restrict__ cellStart,
+                                                     int32_t* __restrict__ cellIdx) {
+  __shared__ int cnt[GRID_CELLS + 1];
+  __shared__ int cursor[GRID_CELLS];
+  __shared__ int sList[GB_LDS_KEYS];
+  __shared__ int tmp[20];
+  const int p = blockIdx.x, t = threadIdx.x;
+  const int n = nkeys[p];
+  const orb_keypoint_t* K = keys + (size_t)p * kpStride;
+  int32_t* ci = cellIdx + (size_t)p * kpStride;
+  for (int i = t; i <= GRID_CELLS; i += GB_T) cnt[i] = 0;
+  __syncthreads();
+  for (int k = t; k < n; k += GB_T) {
+    const int c = grid_cell(K[k], minX, minY, invW, invH);
+    if (c >= 0) atomicAdd(&cnt[c], 1);
+  }
+  __syncthreads();
+  {
+    constexpr int per = GRID_CELLS / GB_T;
+    static_assert(per * GB_T == GRID_CELLS, "cells split evenly over the threads");
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < per; ++i) s += cnt[t * per + i];
+    int tot;
+    int ex = block_excl_scan(s, tmp, &tot);
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+      const int v = cnt[t * per + i];
+      cnt[t * per + i] = ex;
+      cursor[t * per + i] = ex;
+      ex += v;
+    }
+    if (t == 0) cnt[GRID_CELLS] = tot;
+  }
+  __syncthreads();
+  int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
+  for (int i = t; i <= GRID_CELLS; i += GB_T) cs[i] = cnt[i];
+  for (int k = t; k < n; k += GB_T) {
+    const int c = grid_cell(K[k], minX, minY, invW, invH);
+    if (c >= 0) sList[atomicAdd(&cursor[c], 1)] = k;
+  }
+  __syncthreads();
+  for (int c = t; c < GRID_CELLS; c += GB_T) {
+    const int b = cnt[c], e = cnt[c + 1];
+    for (int i = b + 1; i < e; ++i) {
+      const int v = sList[i];
+      int j = i;
+      while (j > b) {
+        const int u = sList[j - 1];
+        if (u < v) break;
+        sList[j] = u;
+        --j;
+      }
+      sList[j] = v;
+    }
+  }
+  __syncthreads();
+  const int tot = cnt[GRID_CELLS];
+  for (int i = t; i < tot; i += GB_T) ci[i] = sList[i];
+}
+
+__global__ __launch_bounds__(64) void k_grid_build_wave(const orb_keypoint_t* __restrict__ keys,
                                                    const int32_t* __restrict__ nkeys, int kpStride,
                                                    float minX, float minY, float invW, float invH,
                                                    int32_t* __restrict__ cellStart,
@@ -375,6 +445,174 @@ __global__ __launch_bounds__(64 * NW) void k_proj_resolve(
   }
 }
 
+
+// Barrier ordering LDS only: global stores and atomics still in flight (the
+// fire-and-forget kpMatch updates, the next window's prefetch) are not waited
+// for, unlike __syncthreads().
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// One point's SearchByProjection decision (src/ORBmatcher.cc:83-132) with
+// "keypoint k taken before point m" = cur[k] < m (committed locks are -1,
+// claims of the current window hold the claiming point): the keypoint it
+// takes, or -1.
+__device__ __forceinline__ int fp_choose(const uint32_t (&e)[TOPK], int nc, int m, const int* cur,
+                                         const orb_mp_track_t* mpp, const uint8_t* mpd,
+                                         const orb_keypoint_t* K, const uint8_t* D,
+                                         const uint8_t* LK, const float* UR, const int32_t* cs,
+                                         const int32_t* ci, const ProjParams& P) {
+  int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+  int found = 0;
+  const int avail = nc < TOPK ? nc : TOPK;
+  bool taken[TOPK];
+#pragma unroll
+  for (int j = 0; j < TOPK; ++j) taken[j] = j < avail ? cur[cand_idx(e[j])] < m : true;
+#pragma unroll
+  for (int j = 0; j < TOPK; ++j) {
+    const bool use = found < 2 && !taken[j];
+    if (use && found == 0) {
+      bestDist = cand_dist(e[j]); bestLevel = cand_oct(e[j]); bestIdx = cand_idx(e[j]);
+    } else if (use) {
+      bestDist2 = cand_dist(e[j]); bestLevel2 = cand_oct(e[j]);
+    }
+    found += use ? 1 : 0;
+  }
+  if (nc > TOPK && found < 2) {
+    // top-K ran dry: exact scan of the point's area under the same locks
+    const orb_mp_track_t mp = *mpp;
+    const int lvl = mp.level;
+    float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;
+    if (P.th != 1.0f) r *= P.th;
+    const float rs = r * P.scale[lvl];
+    const ulonglong4 qd = load_desc(mpd);
+    bestDist = 256; bestLevel = -1; bestDist2 = 256; bestLevel2 = -1; bestIdx = -1;
+    for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
+                         [&](int idx, const orb_keypoint_t& kp) {
+                           if ((LK && LK[idx]) || cur[idx] < m) return;
+                           if (UR && UR[idx] > 0) {
+                             const float er = fabsf(mp.proj_xr - UR[idx]);
+                             if (er > rs) return;
+                           }
+                           const int dist = hamming256(qd, load_desc(D + (size_t)idx * 32));
+                           if (dist < bestDist) {
+                             bestDist2 = bestDist; bestDist = dist;
+                             bestLevel2 = bestLevel; bestLevel = kp.octave; bestIdx = idx;
+                           } else if (dist < bestDist2) {
+                             bestLevel2 = kp.octave; bestDist2 = dist;
+                           }
+                         });
+  }
+  const bool accept = bestIdx >= 0 && bestDist <= 100 &&
+                      !(bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2);
+  return accept ? bestIdx : -1;
+}
+
+// Fixed-point resolve for large local maps: a window of 1024 points (one per
+// thread) is iterated to the sequential result instead of being committed
+// prefix by prefix.  Each round every point re-decides with "taken" = a
+// committed lock or a claim by an earlier point of the window in the previous
+// round's choices, and claims (atomicMin of its index) the keypoint it locks.
+// The sequential result is the unique fixed point (the smallest point whose
+// choice differs from it sees a correct claim set and becomes correct next
+// round), so the loop ends after at most one round per point; C5 windows
+// settle in 2.2 rounds on average.  Claims are double-buffered (round r reads
+// buffer (r-1)&1, writes r&1); a committed lock is -1 in both buffers.  The
+// next window's inputs are loaded while the current one iterates, and rounds
+// synchronise on LDS only.
+__global__ __launch_bounds__(1024) void k_proj_resolve_fp(
+    const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
+    const float* __restrict__ uright, const uint8_t* __restrict__ locked,
+    const int32_t* __restrict__ nkeys, int kpStride, const orb_mp_track_t* __restrict__ mps,
+    const uint8_t* __restrict__ mpDesc, const int32_t* __restrict__ nmps, int mpStride,
+    const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
+    const uint32_t* __restrict__ topk, const int32_t* __restrict__ ncand,
+    int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches) {
+  constexpr int T = 1024;
+  constexpr int NOCLAIM = 0x7FFFFFFF;
+  extern __shared__ __attribute__((aligned(16))) int claims[];  // 2 x kpStride
+  __shared__ int sCount[T / 64];
+  __shared__ int sChanged[2];
+  const int p = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int n = nkeys[p], M = nmps[p];
+  if (t < 2) sChanged[t] = 0;
+  for (int i = t; i < 2 * kpStride; i += T) claims[i] = NOCLAIM;
+  int32_t* km = kpMatch + (size_t)p * kpStride;
+  for (int i = t; i < n; i += T) km[i] = -1;
+  __syncthreads();  // kpMatch reset before any window's atomicMax
+  const size_t pbase = (size_t)p * mpStride;
+  const orb_keypoint_t* K = keys + (size_t)p * kpStride;
+  const uint8_t* D = desc + (size_t)p * kpStride * 32;
+  const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
+  const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
+  const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
+  const int32_t* ci = cellIdx + (size_t)p * kpStride;
+  int matches = 0;
+  // inputs of the window starting at `start`, loaded one window ahead
+  uint4 nE = make_uint4(0, 0, 0, 0);
+  int nNc = -1, nObs = 0;
+  auto load = [&](int m) {
+    nNc = -1;
+    if (m < M) {
+      nE = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
+      nNc = ncand[pbase + m];
+      nObs = mps[pbase + m].has_obs;
+    }
+  };
+  load(t);
+  int round = 0;  // global round counter: buffer parity and change flags
+  for (int start = 0; start < M; start += T) {
+    const int m = start + t;
+    const uint32_t e[TOPK] = {nE.x, nE.y, nE.z, nE.w};
+    const int nc = nNc;
+    const bool obs = nObs != 0;
+    load(start + T + t);
+    int prev = -1;  // this point's claim in the previous round
+    int acc = -1;
+    while (true) {
+      const int* cur = claims + ((round + 1) & 1) * kpStride;
+      int* nxt = claims + (round & 1) * kpStride;
+      acc = nc > 0 ? fp_choose(e, nc, m, cur, mps + pbase + m, mpDesc + (pbase + m) * 32, K, D,
+                               LK, UR, cs, ci, P)
+                   : -1;
+      const int claim = obs ? acc : -1;
+      if (claim >= 0) atomicMin(&nxt[claim], m);
+      if (__ballot(claim != prev) != 0ull && lane == 0) sChanged[round & 1] = 1;
+      lds_barrier();
+      const bool any = sChanged[round & 1] != 0;
+      if (t == 0) sChanged[(round + 1) & 1] = 0;  // next written after the barrier below
+      // cur is not read any more: drop this point's claim of the previous
+      // round from it, it collects the next round's claims
+      if (prev >= 0) claims[((round + 1) & 1) * kpStride + prev] = NOCLAIM;
+      ++round;
+      if (!any) break;  // (uniform) claims stable: the window is at its fixed point
+      prev = claim;
+      lds_barrier();
+    }
+    // commit: the final claims become committed locks in both buffers
+    if (acc >= 0) {
+      atomicMax(&km[acc], m);
+      if (obs) {
+        claims[acc] = -1;
+        claims[kpStride + acc] = -1;
+      }
+      ++matches;
+    }
+    lds_barrier();
+  }
+  matches = wave_sum(matches);
+  if (lane == 0) sCount[wv] = matches;
+  __syncthreads();
+  if (t == 0) {
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < T / 64; ++i) tot += sCount[i];
+    nmatches[p] = tot;
+  }
+}
+
 // ------------------------------------------------------------ host launchers
 extern "C" {
 
@@ -387,8 +625,12 @@ hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
                             int32_t* cellIdx, int nproblems, hipStream_t s) {
-  hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride, minX,
-                     minY, invW, invH, cellStart, cellIdx);
+  if (kpStride <= GB_LDS_KEYS)
+    hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(GB_T), 0, s, keys, nkeys, kpStride,
+                       minX, minY, invW, invH, cellStart, cellIdx);
+  else
+    hipLaunchKernelGGL(k_grid_build_wave, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride,
+                       minX, minY, invW, invH, cellStart, cellIdx);
   return hipGetLastError();
 }
 
@@ -427,10 +669,19 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   if (nproblems <= 0) return hipSuccess;
   const size_t words = (size_t)((kpStride + 31) / 32);
   const size_t lds = ((words + 3) & ~(size_t)3) * 4 + (size_t)kpStride * 4;
-  // 256-point windows for local maps of a few thousand points (C4: 1 to 8
-  // waves measured equal within 2 %), 512-point windows for large ones (C5,
-  // 50,000 points: 12.3k -> 26.3k problems/s against one wave per problem)
-  if (mpStride >= 20000)
+  // 256-point prefix windows for local maps of a few thousand points (C4: 1 to
+  // 8 waves measured equal within 2 %; the fixed-point kernel 2 % slower on
+  // the headline bench).  Large maps (C5, 50,000 points): the fixed-point
+  // kernel, 1024-point windows (SearchByProjection alone 33.9k -> 40.3k
+  // problems/s over 512-point prefix windows; 2/4/8 points per thread measured
+  // 39.8k/37.1k/28.7k).  ORB_RESOLVE_FP=0 selects the prefix kernel.
+  static const int fpMode = getenv("ORB_RESOLVE_FP") ? atoi(getenv("ORB_RESOLVE_FP")) : 1;
+  const size_t ldsFp = (size_t)kpStride * 8;
+  if (mpStride >= 20000 && fpMode > 0 && ldsFp <= 64 * 1024) {
+    hipLaunchKernelGGL(k_proj_resolve_fp, dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
+                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
+                       cellIdx, P, topk, ncand, kpMatch, nmatches);
+  } else if (mpStride >= 20000)
     hipLaunchKernelGGL(k_proj_resolve<8>, dim3(nproblems), dim3(512), lds, s, keys, desc, uright,
                        locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
                        P, topk, ncand, kpMatch, nmatches);
