@@ -522,7 +522,8 @@ __device__ __forceinline__ int fp_choose(const uint32_t (&e)[TOPK], int nc, int 
 // buffer (r-1)&1, writes r&1); a committed lock is -1 in both buffers.  The
 // next window's inputs are loaded while the current one iterates, and rounds
 // synchronise on LDS only.
-__global__ __launch_bounds__(1024) void k_proj_resolve_fp(
+template <int T>
+__global__ __launch_bounds__(T) void k_proj_resolve_fp(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked,
     const int32_t* __restrict__ nkeys, int kpStride, const orb_mp_track_t* __restrict__ mps,
@@ -530,7 +531,6 @@ __global__ __launch_bounds__(1024) void k_proj_resolve_fp(
     const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
     const uint32_t* __restrict__ topk, const int32_t* __restrict__ ncand,
     int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches) {
-  constexpr int T = 1024;
   constexpr int NOCLAIM = 0x7FFFFFFF;
   extern __shared__ __attribute__((aligned(16))) int claims[];  // 2 x kpStride
   __shared__ int sCount[T / 64];
@@ -676,9 +676,18 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   // problems/s over 512-point prefix windows; 2/4/8 points per thread measured
   // 39.8k/37.1k/28.7k).  ORB_RESOLVE_FP=0 selects the prefix kernel.
   static const int fpMode = getenv("ORB_RESOLVE_FP") ? atoi(getenv("ORB_RESOLVE_FP")) : 1;
+  static const int fpMin = getenv("ORB_RESOLVE_FP_MIN") ? atoi(getenv("ORB_RESOLVE_FP_MIN")) : 20000;
   const size_t ldsFp = (size_t)kpStride * 8;
-  if (mpStride >= 20000 && fpMode > 0 && ldsFp <= 64 * 1024) {
-    hipLaunchKernelGGL(k_proj_resolve_fp, dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
+  if (mpStride >= fpMin && fpMode == 256 && ldsFp <= 64 * 1024) {
+    hipLaunchKernelGGL(k_proj_resolve_fp<256>, dim3(nproblems), dim3(256), ldsFp, s, keys, desc,
+                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
+                       cellIdx, P, topk, ncand, kpMatch, nmatches);
+  } else if (mpStride >= fpMin && fpMode == 512 && ldsFp <= 64 * 1024) {
+    hipLaunchKernelGGL(k_proj_resolve_fp<512>, dim3(nproblems), dim3(512), ldsFp, s, keys, desc,
+                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
+                       cellIdx, P, topk, ncand, kpMatch, nmatches);
+  } else if (mpStride >= fpMin && fpMode > 0 && ldsFp <= 64 * 1024) {
+    hipLaunchKernelGGL(k_proj_resolve_fp<1024>, dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
                        cellIdx, P, topk, ncand, kpMatch, nmatches);
   } else if (mpStride >= 20000)
