@@ -30,13 +30,20 @@ __global__ __launch_bounds__(256) void k_hamming_batch(const uint8_t* __restrict
 // in keypoint order by one thread (insertion sort; cells hold ~1-10 keys).
 // Frames with kpStride up to GB_LDS_KEYS keypoints build their lists in LDS;
 // larger frames use k_grid_build_wave (one wave, stable ballot scatter).
+// `staged` (optional): the keypoints in cell order as k_proj_candidates stages
+// them in LDS, {x, y, idx | octave << 24 | locked << 31, uR}, so that each of
+// its workgroups copies the frame's grid with coalesced loads instead of
+// gathering it through cellIdx.
 #define GB_T 256
 #define GB_LDS_KEYS 8192
 __global__ __launch_bounds__(GB_T) void k_grid_build(const orb_keypoint_t* __restrict__ keys,
                                                      const int32_t* __restrict__ nkeys, int kpStride,
                                                      float minX, float minY, float invW, float invH,
                                                      int32_t* __restrict__ cellStart,
-                                                     int32_t* __restrict__ cellIdx) {
+                                                     int32_t* __restrict__ cellIdx,
+                                                     const uint8_t* __restrict__ locked,
+                                                     const float* __restrict__ uright,
+                                                     uint4* __restrict__ staged) {
   __shared__ int cnt[GRID_CELLS + 1];
   __shared__ int cursor[GRID_CELLS];
   __shared__ int sList[GB_LDS_KEYS];
@@ -94,6 +101,21 @@ __global__ __launch_bounds__(GB_T) void k_grid_build(const orb_keypoint_t* __res
   __syncthreads();
   const int tot = cnt[GRID_CELLS];
   for (int i = t; i < tot; i += GB_T) ci[i] = sList[i];
+  if (staged) {
+    const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
+    const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
+    uint4* sg = staged + (size_t)p * kpStride;
+    for (int i = t; i < tot; i += GB_T) {
+      const int idx = sList[i];
+      const orb_keypoint_t kp = K[idx];
+      uint4 e;
+      e.x = __float_as_uint(kp.x);
+      e.y = __float_as_uint(kp.y);
+      e.z = (uint32_t)idx | ((uint32_t)kp.octave << 24) | ((LK && LK[idx]) ? 0x80000000u : 0u);
+      e.w = __float_as_uint(UR ? UR[idx] : -1.0f);
+      sg[i] = e;
+    }
+  }
 }
 
 __global__ __launch_bounds__(64) void k_grid_build_wave(const orb_keypoint_t* __restrict__ keys,
@@ -171,6 +193,9 @@ __global__ __launch_bounds__(64) void k_grid_build_wave(const orb_keypoint_t* __
 #define PROJ_STAGE 4096  // frames with up to this many keypoints are staged (C5: 4000)
 #endif
 
+#ifndef PROJ_QB
+#define PROJ_QB 4  // window candidates scored per batch of descriptor loads
+#endif
 #ifndef PROJ_WG
 #define PROJ_WG 512  // map points per workgroup (grid staged once per workgroup; swept 256-1024)
 #endif
@@ -179,7 +204,8 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
     const float* __restrict__ uright, const uint8_t* __restrict__ locked, int kpStride,
     const int32_t* __restrict__ nkeys, const orb_mp_track_t* __restrict__ mps,
     const uint8_t* __restrict__ mpDesc, const int32_t* __restrict__ nmps, int mpStride,
-    const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
+    const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx,
+    const uint4* __restrict__ stagedGrid, int stageCap, ProjParams P,
     uint32_t* __restrict__ topk, int32_t* __restrict__ ncand) {
   __shared__ int sCS[GRID_CELLS + 1];
   extern __shared__ __attribute__((aligned(16))) uint4 sKp[];  // min(kpStride, PROJ_STAGE)
@@ -195,13 +221,17 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
   const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
   const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
   const int32_t* ci = cellIdx + (size_t)p * kpStride;
-  const bool staged = N <= min(kpStride, PROJ_STAGE);
+  const bool staged = N <= stageCap;
 #pragma unroll
   for (int i = 0; i < ORB_MAX_LEVELS; ++i)
     if (tid == i) sScale[i] = P.scale[i];
   if (staged) {
     for (int i = tid; i <= GRID_CELLS; i += PROJ_WG) sCS[i] = cs[i];
     const int nInGrid = cs[GRID_CELLS];
+    if (stagedGrid) {
+      const uint4* sg = stagedGrid + (size_t)p * kpStride;
+      for (int j = tid; j < nInGrid; j += PROJ_WG) sKp[j] = sg[j];
+    } else {
     for (int j = tid; j < nInGrid; j += PROJ_WG) {
       const int idx = ci[j];
       const orb_keypoint_t kp = K[idx];
@@ -211,6 +241,7 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
       e.z = (uint32_t)idx | ((uint32_t)kp.octave << 24) | ((LK && LK[idx]) ? 0x80000000u : 0u);
       e.w = __float_as_uint(UR ? UR[idx] : -1.0f);
       sKp[j] = e;
+    }
     }
   }
   __syncthreads();
@@ -240,7 +271,29 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
     top.insert(pack_cand(idx, dist, oct), dist);
   };
   if (staged) {
-    // GetFeaturesInArea (src/Frame.cc:368-424) over the staged grid
+    // GetFeaturesInArea (src/Frame.cc:368-424) over the staged grid.  Window
+    // candidates that pass the lock and stereo tests queue up (scan order) and
+    // are scored PROJ_QB at a time, so their descriptor loads overlap.
+    // the queue lives in registers (qe[k] written through selects, no LDS:
+    // C5's staged frame already takes 76 KB of LDS per workgroup)
+    int nq = 0;
+    uint32_t qe[PROJ_QB];
+#pragma unroll
+    for (int k = 0; k < PROJ_QB; ++k) qe[k] = 0;
+    auto flush = [&](int cnt) {
+      ulonglong4 dd[PROJ_QB];
+#pragma unroll
+      for (int k = 0; k < PROJ_QB; ++k)
+        dd[k] = load_desc(D + (size_t)((k < cnt ? qe[k] : qe[0]) & 0xFFFFFFu) * 32);
+#pragma unroll
+      for (int k = 0; k < PROJ_QB; ++k) {
+        if (k >= cnt) break;
+        const int dist = hamming256(q, dd[k]);
+        if (dist >= 256) continue;  // can never become best or second
+        ++count;
+        top.insert(pack_cand((int)(qe[k] & 0xFFFFFFu), dist, (int)(qe[k] >> 24)), dist);
+      }
+    };
     const float x = mp.proj_x, y = mp.proj_y;
     const int nMinCellX = max(0, (int)floorf((x - P.minX - rs) * P.invW));
     const int nMaxCellX = min(ORB_GRID_COLS - 1, (int)ceilf((x - P.minX + rs) * P.invW));
@@ -258,12 +311,21 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
             const int oct = (int)((E.z >> 24) & 0x7Fu);
             if (oct < minL || oct > maxL) continue;
             const float dx = __uint_as_float(E.x) - x, dy = __uint_as_float(E.y) - y;
-            if (fabsf(dx) < rs && fabsf(dy) < rs)
-              visit((int)(E.z & 0xFFFFFFu), oct, (E.z >> 31) != 0, __uint_as_float(E.w));
+            if (!(fabsf(dx) < rs && fabsf(dy) < rs) || (E.z >> 31) != 0) continue;
+            const float ur = __uint_as_float(E.w);
+            if (ur > 0 && fabsf(mp.proj_xr - ur) > rs) continue;
+            const uint32_t qv = (E.z & 0xFFFFFFu) | ((uint32_t)oct << 24);
+#pragma unroll
+            for (int k = 0; k < PROJ_QB; ++k) qe[k] = nq == k ? qv : qe[k];
+            if (++nq == PROJ_QB) {
+              flush(PROJ_QB);
+              nq = 0;
+            }
           }
         }
       }
     }
+    if (nq) flush(nq);
   } else {
     for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
                          [&](int idx, const orb_keypoint_t& kp) {
@@ -627,12 +689,27 @@ hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, in
                             int32_t* cellIdx, int nproblems, hipStream_t s) {
   if (kpStride <= GB_LDS_KEYS)
     hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(GB_T), 0, s, keys, nkeys, kpStride,
-                       minX, minY, invW, invH, cellStart, cellIdx);
+                       minX, minY, invW, invH, cellStart, cellIdx, nullptr, nullptr, nullptr);
   else
     hipLaunchKernelGGL(k_grid_build_wave, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride,
                        minX, minY, invW, invH, cellStart, cellIdx);
   return hipGetLastError();
 }
+
+// grid + the cell-ordered staging copy for k_proj_candidates (16 B per
+// keypoint slot); returns hipErrorNotSupported beyond GB_LDS_KEYS keypoint slots
+hipError_t orb_k_grid_build_staged(const orb_keypoint_t* keys, const int32_t* nkeys,
+                                   const uint8_t* locked, const float* uright, int kpStride,
+                                   float minX, float minY, float invW, float invH,
+                                   int32_t* cellStart, int32_t* cellIdx, void* staged,
+                                   int nproblems, hipStream_t s) {
+  if (kpStride > GB_LDS_KEYS) return hipErrorNotSupported;
+  hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(GB_T), 0, s, keys, nkeys, kpStride, minX,
+                     minY, invW, invH, cellStart, cellIdx, locked, uright, (uint4*)staged);
+  return hipGetLastError();
+}
+
+int orb_k_grid_stage_max(void) { return GB_LDS_KEYS; }
 
 hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc,
                                  const float* uright, const uint8_t* locked, int kpStride,
@@ -640,12 +717,13 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
                                  const uint8_t* mpDesc,
                                  const int32_t* nmps, int mpStride, int mpMax,
                                  const int32_t* cellStart, const int32_t* cellIdx,
-                                 const void* params, uint32_t* topk, int32_t* ncand,
-                                 int nproblems, hipStream_t s) {
+                                 const void* stagedGrid, const void* params, uint32_t* topk,
+                                 int32_t* ncand, int nproblems, hipStream_t s) {
   const ProjParams P = *(const ProjParams*)params;
   if (mpMax <= 0 || nproblems <= 0) return hipSuccess;
   // dynamic LDS: the staged keypoints of a frame, sized to the key capacity
-  const size_t lds = (size_t)std::min(kpStride, PROJ_STAGE) * sizeof(uint4);
+  const int stageCap = std::min(kpStride, PROJ_STAGE);
+  const size_t lds = (size_t)stageCap * sizeof(uint4);
   if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {  // with the static grid table
     hipError_t e = hipFuncSetAttribute((const void*)k_proj_candidates,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -654,7 +732,7 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
   hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems),
                      dim3(PROJ_WG), lds, s,
                      keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
-                     cellStart, cellIdx, P, topk, ncand);
+                     cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P, topk, ncand);
   return hipGetLastError();
 }
 

@@ -69,8 +69,14 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
                                  const uint8_t* mpDesc,
                                  const int32_t* nmps, int mpStride, int mpMax,
                                  const int32_t* cellStart, const int32_t* cellIdx,
-                                 const void* params, uint32_t* topk, int32_t* ncand,
-                                 int nproblems, hipStream_t s);
+                                 const void* stagedGrid, const void* params, uint32_t* topk,
+                                 int32_t* ncand, int nproblems, hipStream_t s);
+hipError_t orb_k_grid_build_staged(const orb_keypoint_t* keys, const int32_t* nkeys,
+                                   const uint8_t* locked, const float* uright, int kpStride,
+                                   float minX, float minY, float invW, float invH,
+                                   int32_t* cellStart, int32_t* cellIdx, void* staged,
+                                   int nproblems, hipStream_t s);
+int orb_k_grid_stage_max(void);
 hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
                               const float* uright, const uint8_t* locked, const int32_t* nkeys,
                               int kpStride, const orb_mp_track_t* mps, const uint8_t* mpDesc,
@@ -1201,6 +1207,7 @@ struct orb_matcher {
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
   // stereo / frame / BoW scratch
   DevBuf dStRowStart, dStRowIdx;  // stereo vRowIndices (CSR per pair)
+  DevBuf dProjStage;              // cell-ordered keypoints for k_proj_candidates (16 B per slot)
   DevBuf dRKeys, dRDesc, dNR, dPyr, dPairLv, dDepth, dSad, dBowA, dBowB, dBowC, dBowD, dBowE,
       dBowF, dBowG, dBowH, dBowI, dBowJ, dBowK;
   HostBuf hPyr;  // pinned staging of the host stereo pyramids (one DMA)
@@ -1265,7 +1272,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
                     &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut,
                     &m->dRKeys, &m->dRDesc, &m->dNR, &m->dPyr, &m->dPairLv, &m->dDepth,
-                    &m->dSad, &m->dStRowStart, &m->dStRowIdx, &m->dBowA, &m->dBowB, &m->dBowC, &m->dBowD, &m->dBowE,
+                    &m->dSad, &m->dStRowStart, &m->dStRowIdx, &m->dProjStage, &m->dBowA, &m->dBowB, &m->dBowC, &m->dBowD, &m->dBowE,
                     &m->dBowF, &m->dBowG, &m->dBowH, &m->dBowI, &m->dBowJ, &m->dBowK,
                     &m->dMapPts, &m->dPose, &m->dTracks, &m->dNInView, &m->dK1, &m->dD1,
                     &m->dK2, &m->dD2, &m->dN1, &m->dN2, &m->dPrev, &m->dList, &m->dM12,
@@ -1328,17 +1335,26 @@ orb_status_t orb_match_projection_local_batch(
   if ((st = m->dCellIdx.ensure((size_t)n_problems * kp_stride * 4))) return st;
   if ((st = m->dTopk.ensure((size_t)n_problems * std::max(mp_stride, 1) * 16))) return st;
   if ((st = m->dNcand.ensure((size_t)n_problems * std::max(mp_stride, 1) * 4))) return st;
+  const bool stage = kp_stride <= orb_k_grid_stage_max();
+  if (stage && (st = m->dProjStage.ensure((size_t)n_problems * kp_stride * 16))) return st;
   StageProfiler& pf = m->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
   PROF_REC(ev, pf.b(ev, 0), s);
-  HIP_TRY(orb_k_grid_build(d_keys, d_nkeys, kp_stride, P.minX, P.minY, P.invW, P.invH,
-                           m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), n_problems, s));
+  if (stage)
+    HIP_TRY(orb_k_grid_build_staged(d_keys, d_nkeys, d_locked, nullptr, kp_stride, P.minX, P.minY,
+                                    P.invW, P.invH, m->dCellStart.as<int32_t>(),
+                                    m->dCellIdx.as<int32_t>(), m->dProjStage.p, n_problems, s));
+  else
+    HIP_TRY(orb_k_grid_build(d_keys, d_nkeys, kp_stride, P.minX, P.minY, P.invW, P.invH,
+                             m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), n_problems,
+                             s));
   PROF_REC(ev, pf.e(ev, 0), s);
   PROF_REC(ev, pf.b(ev, 1), s);
   HIP_TRY(orb_k_proj_candidates(d_keys, d_desc, nullptr, d_locked, kp_stride, d_nkeys, d_mps, d_mp_desc,
                                 d_nmps, mp_stride, mp_stride, m->dCellStart.as<int32_t>(),
-                                m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
+                                m->dCellIdx.as<int32_t>(), stage ? m->dProjStage.p : nullptr,
+                                &P, m->dTopk.as<uint32_t>(),
                                 m->dNcand.as<int32_t>(), n_problems, s));
   PROF_REC(ev, pf.e(ev, 1), s);
   PROF_REC(ev, pf.b(ev, 2), s);
@@ -1421,16 +1437,25 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   }
   const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
                                        F->scale_factors, th, nnratio);
-  HIP_TRY(orb_k_grid_build(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), N, P.minX,
-                           P.minY, P.invW, P.invH, m->dCellStart.as<int32_t>(),
-                           m->dCellIdx.as<int32_t>(), 1, s));
   const float* ur = F->u_right ? m->dUr.as<float>() : nullptr;
   const uint8_t* lk = kp_locked ? m->dLocked.as<uint8_t>() : nullptr;
+  const bool stage = N <= orb_k_grid_stage_max();
+  if (stage && (st = m->dProjStage.ensure((size_t)N * 16))) return st;
+  if (stage)
+    HIP_TRY(orb_k_grid_build_staged(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), lk, ur,
+                                    N, P.minX, P.minY, P.invW, P.invH,
+                                    m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
+                                    m->dProjStage.p, 1, s));
+  else
+    HIP_TRY(orb_k_grid_build(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), N, P.minX,
+                             P.minY, P.invW, P.invH, m->dCellStart.as<int32_t>(),
+                             m->dCellIdx.as<int32_t>(), 1, s));
   HIP_TRY(orb_k_proj_candidates(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(), ur, lk, N,
                                 m->dNKeys.as<int32_t>(),
                                 m->dMps.as<orb_mp_track_t>(), m->dMpDesc.as<uint8_t>(),
                                 m->dNMps.as<int32_t>(), std::max(M, 1), M,
-                                m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
+                                m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
+                                stage ? m->dProjStage.p : nullptr, &P,
                                 m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(), 1, s));
   HIP_TRY(orb_k_proj_resolve(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(), ur, lk,
                              m->dNKeys.as<int32_t>(), N, m->dMps.as<orb_mp_track_t>(),

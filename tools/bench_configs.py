@@ -13,6 +13,8 @@ results table:
   C5  1920x1080, 4000 features, SearchByProjection against a 50,000-point
       local map (th 1, nnratio 0.8), 16 problems per launch (problems/s for
       extract+match, and the matcher alone with its HBM roofline)
+  C4M the headline's matcher alone: 1241x376, 1000 features, 5,000-point local
+      maps, 512 problems per launch (same keys as C5)
   F1  SURVEY §8(f): SearchForInitialization, 640x480 frames from the 2000-feature
       initial extractor, window 100, ORBmatcher(0.9, true), 64 pairs per launch
       (pairs/s) + CPU oracle rate + exact check
@@ -174,11 +176,19 @@ def c3(args, orb, oracle, torch):
 
 
 def c5(args, orb, oracle, torch):
-    W, H, NF, M, B = 1920, 1080, 4000, 50000, 16
+    return proj_config(args, orb, oracle, torch, "C5", 1920, 1080, 4000, 50000, 16, 5)
+
+
+def c4m(args, orb, oracle, torch):
+    """the headline's matcher by itself: 512 KITTI-shaped frames, 5,000-point maps"""
+    return proj_config(args, orb, oracle, torch, "C4M", 1241, 376, 1000, 5000, 512, 7)
+
+
+def proj_config(args, orb, oracle, torch, name, W, H, NF, M, B, seed):
     ext = orb.ORBextractor(NF, 1.2, 8, 20, 7)
     scale = np.float32(ext.GetScaleFactors())
     cap = ext.capacity(W, H)
-    imgs = np.stack([orb.synth_image(5, f, W, H) for f in range(B)])
+    imgs = np.stack([orb.synth_image(seed, f, W, H) for f in range(B)])
     d = torch.from_numpy(imgs).cuda()
     k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
     de = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
@@ -193,7 +203,7 @@ def c5(args, orb, oracle, torch):
     mpd = np.zeros((B, M, 32), np.uint8)
     lk = np.zeros((B, cap), np.uint8)
     for i in range(B):
-        a, b_, c_ = orb.synth_local_map(5 + i, kh[i, :nh[i]], dh[i, :nh[i]], M, W, H)
+        a, b_, c_ = orb.synth_local_map(seed + i, kh[i, :nh[i]], dh[i, :nh[i]], M, W, H)
         mps[i], mpd[i], lk[i, :nh[i]] = a, b_, c_
     d_mps = torch.from_numpy(mps.view(np.uint8).reshape(B, -1)).cuda()
     d_mpd = torch.from_numpy(mpd).cuda()
@@ -221,7 +231,7 @@ def c5(args, orb, oracle, torch):
     nr, kmr = oracle.match_projection_local(kh[0, :n0], dh[0, :n0], scale, W, H, mps[0], mpd[0],
                                             1.0, 0.8, lk[0, :n0])
     exact = int(d_nmatch[0].item()) == nr and np.array_equal(d_km[0, :n0].cpu().numpy(), kmr)
-    return {"config": "C5", "workload": "1920x1080, 4000 feat, SearchByProjection vs 50,000 "
+    return {"config": name, "workload": f"{W}x{H}, {NF} feat, SearchByProjection vs {M:,} "
             f"map points, {B} problems per launch", "unit": "problems/s", "value": B / sec,
             "ms_per_step": sec * 1e3, "match_only_problems_per_s": B / msec,
             "match_only_alg_GBps": b_lm * B / msec / 1e9,
@@ -396,6 +406,8 @@ def main():
             r = c3(args, orb, oracle, torch)
         elif c == "C5":
             r = c5(args, orb, oracle, torch)
+        elif c == "C4M":
+            r = c4m(args, orb, oracle, torch)
         elif c == "F1":
             r = f1(args, orb, oracle, torch)
         elif c == "F2":
