@@ -54,9 +54,9 @@ def test_search_by_projection_local(gpu, oracle, w, h, nf, M, th, seed):
 def test_search_by_projection_conflicts_and_flags(gpu, oracle, M, nsrc):
     """Many map points on few keypoints (deep first-come chains, top-K overflow),
     points without observations (claims that do not lock), bad / out-of-view
-    points, stereo gating through mvuRight.  24,000 points take the resolve's
-    512-point windows (local maps of 20,000 points and more), 4,000 its
-    256-point ones."""
+    points, stereo gating through mvuRight.  24,000 points take the
+    fixed-point resolve (local maps of 20,000 points and more), 4,000 the
+    256-point prefix windows."""
     w, h = 640, 480
     k, d, scale = _frame(gpu, oracle, w, h, 1000, 3)
     rng = np.random.default_rng(7)
@@ -81,6 +81,26 @@ def test_search_by_projection_conflicts_and_flags(gpu, oracle, M, nsrc):
         n_gpu, km_gpu = gpu.ORBmatcher(0.8).SearchByProjection(F, mps, mpd, th, locked)
         assert n_gpu == n_ref
         assert np.array_equal(km_gpu, km_ref)
+
+
+def test_search_by_projection_large_frame(gpu, oracle):
+    """More than 8,192 keypoints: the one-wave grid build, the candidate scan
+    over the global grid (no LDS staging past 4,096 keypoints) and, with
+    20,000+ map points, the 512-point prefix resolve (the fixed-point kernel's
+    claim buffers would exceed 64 KiB of LDS)."""
+    w, h = 1920, 1080
+    rng = np.random.default_rng(1080)
+    img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    k, d, _ = oracle.extract(img, 12000, 1.2, 8, 20, 7)
+    assert len(k) > 8192
+    scale = oracle.params(12000)["scale"]
+    mps, mpd, locked = oracle.synth_local_map(11, k, d, 20000, w, h)
+    n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, mps, mpd, 1.0, 0.8, locked)
+    F = gpu.Frame(k, d, scale, w, h)
+    n_gpu, km_gpu = gpu.ORBmatcher(0.8).SearchByProjection(F, mps, mpd, 1.0, locked)
+    assert n_ref > 0
+    assert n_gpu == n_ref
+    assert np.array_equal(km_gpu, km_ref)
 
 
 def test_search_by_projection_empty(gpu, oracle):
