@@ -767,9 +767,17 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef FC_CCAP
 #define FC_CCAP 512     // corner list per wave; beyond it the NMS runs densely
 #endif
+#ifndef FC_PAD
+#define FC_PAD 0        // extra LDS row pitch (elements, multiple of 8)
+#endif
+#ifndef FC_PERM
+#define FC_PERM 1       // pretest lane -> pixel-group permutation (LDS banking)
+#endif
 
+// LDS row pitch (elements) of a cell ROI C pixels wide
+__host__ __device__ inline int fc_pitch(int C) { return ((C + 20) & ~7) + FC_PAD; }
 __host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
-  return maxRows * ((maxCols + 20) & ~7);
+  return maxRows * fc_pitch(maxCols);
 }
 __host__ __device__ inline int fc_wave_bytes(int tileElems) {
   // f16 tile + strengths + queue + corners + 64 rows x 64-bit bitmap
@@ -839,9 +847,9 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   const int R = cd.y1 - cd.y0, C = cd.x1 - cd.x0;
   const long long slot = (long long)img * plan.ncells + ci;
   const bool tiny = R < 7 || C < 7;
-  const int P = (C + 20) & ~7, PD = P >> 1;
+  const int P = fc_pitch(C), PD = P >> 1;
   if (!tiny && lane < R) {
-    const int nS = P >> 2;  // source dwords per row (<= 14, host-checked)
+    const int nS = ((C + 20) & ~7) >> 2;  // source dwords per row (<= 14, host-checked)
     uint4* dst = reinterpret_cast<uint4*>(tile32 + lane * PD);
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
@@ -916,7 +924,16 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     T.x = T.y = (_Float16)(float)(t + 1);
     const int nG = ih * nK;
     for (int g0 = 0; g0 < nG; g0 += 64) {
+#if FC_PERM
+      // The queue is a set (scores, corners and the NMS bitmap do not depend on
+      // its order), so lanes may take the round's 64 pixel groups in any order.
+      // With 4 groups per row (level-0 cells), give each ds_read_b128 lane
+      // group {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... the rows r, r+4, r+8,
+      // r+12, whose 16-dword runs fall in distinct banks at a 28-dword pitch.
+      const int gi = g0 + 4 * (int)((0xFEAB6732DC894510ull >> (4 * (lane >> 2))) & 15u) + (lane & 3);
+#else
       const int gi = g0 + lane;
+#endif
       uint32_t rp[4] = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
       int off = 0;
       if (gi < nG) {
