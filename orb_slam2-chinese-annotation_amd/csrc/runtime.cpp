@@ -953,34 +953,13 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   if ((st = h->dOne.ensure(outBytes))) return st;
   if ((st = h->hImg.ensure(pitch))) return st;
   if ((st = h->hOut.ensure(outBytes))) return st;
-  // image -> pinned staging at the device row pitch.  ORB_H2D_CHUNKS > 1: the
-  // rows go over in that many chunks, each DMA issued as soon as its rows are
-  // staged so it overlaps the host copy of the next (the graph then holds no
-  // H2D node); default one DMA inside the graph
-  static const int h2dChunks = [] {
-    const char* e = getenv("ORB_H2D_CHUNKS");
-    return e ? std::max(1, std::min(16, atoi(e))) : 1;
-  }();
-  const bool chunked = h2dChunks > 1 && !h->prof.enabled;
-  if (!chunked) {
-    for (int y = 0; y < height; ++y)
-      memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
-  } else {
-    const int rowsPer = (height + h2dChunks - 1) / h2dChunks;
-    for (int y0 = 0; y0 < height; y0 += rowsPer) {
-      const int y1 = std::min(height, y0 + rowsPer);
-      for (int y = y0; y < y1; ++y)
-        memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
-      HIP_TRY(hipMemcpyAsync(h->dImg.as<uint8_t>() + (size_t)y0 * dstride,
-                             h->hImg.as<uint8_t>() + (size_t)y0 * dstride,
-                             (size_t)(y1 - y0) * dstride, hipMemcpyHostToDevice, h->stream));
-    }
-  }
+  // image -> pinned staging at the device row pitch
+  for (int y = 0; y < height; ++y)
+    memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
   uint8_t* d1 = h->dOne.as<uint8_t>();
   // one DMA in, the extraction, one DMA out of the count and every record slot
   auto enqueue = [&](bool capturing) -> orb_status_t {
-    if (!chunked)
-      HIP_TRY(hipMemcpyAsync(h->dImg.p, h->hImg.p, pitch, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->dImg.p, h->hImg.p, pitch, hipMemcpyHostToDevice, h->stream));
     orb_status_t r = run_batch(h, h->dImg.as<uint8_t>(), 1, dstride, pitch,
                                reinterpret_cast<orb_keypoint_t*>(d1 + kOff), d1 + dOff, cap,
                                reinterpret_cast<int32_t*>(d1), h->stream, capturing);
@@ -996,7 +975,7 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
         h->dImg.p, h->dOne.p, h->hImg.p, h->hOut.p, h->dArena.p, h->dCellKeys.p, h->dGKeys.p,
         h->dGNid.p, h->dCellCount.p, h->dOutKeys.p, h->dOutCount.p, h->dErr.p, h->dRtab.p,
         h->dBands.p, h->dCells.p, (const void*)(intptr_t)width, (const void*)(intptr_t)height,
-        (const void*)(intptr_t)cap, (const void*)(intptr_t)chunked};
+        (const void*)(intptr_t)cap};
     if (!h->oneExec || key != h->oneKey) {
       if (h->oneExec) hipGraphExecDestroy(h->oneExec);
       h->oneExec = nullptr;
