@@ -327,7 +327,8 @@ orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor
  * (-1 = no match) are copied back.  *n_left = the left keypoint count; the
  * outputs need n_left entries (ORB_ECAPACITY if capacity is smaller; both
  * outputs NULL = size query).
- * ORB_EINVAL if either handle's last call was not orb_extractor_extract.
+ * ORB_EINVAL if either handle's last call was not orb_extractor_extract, or
+ * if the matcher and the two extractors were not created on one device.
  * Synchronous. */
 orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_ext,
                                         orb_extractor_t* right_ext, float bf, float fx,

@@ -9,6 +9,7 @@
 // not algorithm, and is not reproduced.
 #include "Frame.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -25,7 +26,10 @@ void Frame::ComputeStereoMatches() {
     ~Handle() { orb_matcher_destroy(h); }
   };
   thread_local Handle m;
-  orb_status_t st = m.h ? ORB_OK : orb_matcher_create(0, &m.h);
+  // same device as the extractors (integration/ORBextractor.cc): the match
+  // runs where both extractions left their pyramids
+  const char* dev = std::getenv("ORB_AMD_DEVICE");
+  orb_status_t st = m.h ? ORB_OK : orb_matcher_create(dev ? std::atoi(dev) : 0, &m.h);
   int n = 0;
   if (st == ORB_OK)
     st = orb_stereo_match_extracted(m.h, mpORBextractorLeft->gpu(), mpORBextractorRight->gpu(), mbf,

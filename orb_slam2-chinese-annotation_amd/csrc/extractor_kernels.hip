@@ -1899,18 +1899,27 @@ struct DescWaveLds {
 };
 
 #define DESC_PPW 4  // slot pairs per wave (software-pipelined: the next pair's window loads overlap this one)
+#ifndef DESC_MIN_WAVES
+#define DESC_MIN_WAVES 0  // __launch_bounds__ minimum waves per SIMD (A/B knob: 5 -> <= 96 VGPRs)
+#endif
+#if DESC_MIN_WAVES > 0
+#define DESC_LAUNCH_BOUNDS __launch_bounds__(256, DESC_MIN_WAVES)
+#else
+#define DESC_LAUNCH_BOUNDS __launch_bounds__(256)
+#endif
+#ifndef DESC_SMALL_CT
+#define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
+#endif
 
 template <int PPW>
-__global__ __launch_bounds__(256) void k_orient_desc(
+__global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const uint32_t* __restrict__ outKeys, const int32_t* __restrict__ outCount,
     const int32_t* __restrict__ errFlag, orb_keypoint_t* __restrict__ kps,
     uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts, int ppwRt) {
-  // PPW > 0: compile-time pairs per wave (batches); PPW == 0: ppwRt (small calls;
-  // an instantiation with a compile-time single pair, k_orient_desc<1>, wrote
-  // keypoints to the wrong slots under ROCm 7.2 hipcc while the same source with
-  // the count at run time is bit-exact)
+  // PPW > 0: compile-time pairs per wave (<4> batches, <1> one-pair calls);
+  // PPW == 0: ppwRt
   const int ppw = PPW ? PPW : ppwRt;
   __shared__ __attribute__((aligned(16))) DescWaveLds sm[4];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -2069,6 +2078,13 @@ __global__ __launch_bounds__(256) void k_orient_desc(
     }
     if (!P.valid) continue;  // wave-uniform
     const OrbLevelDesc& L = plan.lv[P.l];
+    // The level's output offset is read here, with every lane active.  Read
+    // inside the epilogue's `P.active && hl == 0` branch, hipcc sank the
+    // v_sub that forms cntx into that branch, so the v_readlane of lane P.l
+    // saw a lane the sub had not run in: a stale register (wrong slots in
+    // k_orient_desc<1>, an out-of-range store and a device fault under
+    // __launch_bounds__(256, 5)).
+    const int base = __builtin_amdgcn_readlane(cntx, P.l);
     const int cx = P.cx, cy = P.cy, colA = cx - 21;
     if (colA < 0 || cx + 21 >= L.w) {
       // window overhangs a level column edge: the lane's two rows go through
@@ -2157,7 +2173,6 @@ __global__ __launch_bounds__(256) void k_orient_desc(
       words[kq] = __ballot(v0 < v1);
     }
     if (P.active && hl == 0) {
-      const int base = __builtin_amdgcn_readlane(cntx, P.l);
       const long long o = (long long)img * capacity + base + P.i;
       uint32_t d[8];
 #pragma unroll
@@ -2384,6 +2399,10 @@ hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0S
     hipLaunchKernelGGL(k_orient_desc<DESC_PPW>, grid, block, 0, s, img0, img0Pitch, img0Stride,
                        arena, arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity,
                        counts, DESC_PPW);
+  else if (ppw == 1 && DESC_SMALL_CT)
+    hipLaunchKernelGGL(k_orient_desc<1>, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
+                       arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts,
+                       1);
   else
     hipLaunchKernelGGL(k_orient_desc<0>, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
                        arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts,

@@ -974,8 +974,8 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     const std::vector<const void*> key = {
         h->dImg.p, h->dOne.p, h->hImg.p, h->hOut.p, h->dArena.p, h->dCellKeys.p, h->dGKeys.p,
         h->dGNid.p, h->dCellCount.p, h->dOutKeys.p, h->dOutCount.p, h->dErr.p, h->dRtab.p,
-        h->dBands.p, h->dCells.p, (const void*)(intptr_t)width, (const void*)(intptr_t)height,
-        (const void*)(intptr_t)cap};
+        h->dBands.p, h->dCells.p, h->dBlur.p, h->dTiles.p, (const void*)(intptr_t)width,
+        (const void*)(intptr_t)height, (const void*)(intptr_t)cap};
     if (!h->oneExec || key != h->oneKey) {
       if (h->oneExec) hipGraphExecDestroy(h->oneExec);
       h->oneExec = nullptr;
@@ -998,6 +998,11 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     }
     HIP_TRY(hipGraphLaunch(h->oneExec, h->stream));
     HIP_TRY(hipEventRecord(h->evBatch, h->stream));
+    // a replayed graph skips run_batch's bookkeeping: level 0 of this call is
+    // the staged image again, not whatever an intervening batch call pointed at
+    h->lastImg0 = h->dImg.as<uint8_t>();
+    h->lastImg0Pitch = pitch;
+    h->lastImg0Stride = (int)dstride;
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->oneCap = cap;
@@ -1695,6 +1700,8 @@ orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_
   orb_extractor* b = left_ext < right_ext ? right_ext : left_ext;
   std::lock_guard<std::mutex> ga(a->mu), gb(b->mu);
   if (!left_ext->lastSingle || !right_ext->lastSingle) return ORB_EINVAL;
+  // the kernels read both handles' device buffers on the matcher's device
+  if (m->device != left_ext->device || m->device != right_ext->device) return ORB_EINVAL;
   const int L = left_ext->nlevels;
   if (L != right_ext->nlevels || left_ext->planW != right_ext->planW ||
       left_ext->planH != right_ext->planH)

@@ -298,3 +298,35 @@ def test_large_batch_vs_oracle(gpu, oracle):
     """More than 16 frames per call: the octree keeps its keys in LDS / global
     scratch instead of registers (the batch configuration of the bench)."""
     _batch_vs_oracle(gpu, oracle, [gpu.synth_image(50, f, 640, 480) for f in range(20)])
+
+
+def test_single_batch_single_keeps_level0(gpu, oracle):
+    """A replayed single-image graph must re-point level 0 at its own staged
+    image: single extract, a batch on the same handle, single extract again,
+    then mvImagePyramid[0] (read by Frame::ComputeStereoMatches,
+    src/Frame.cc:619,633) equals the last single image, and every level equals
+    the oracle's pyramid of it."""
+    torch = pytest.importorskip("torch")
+    w, h = 640, 480
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    a = gpu.synth_image(11, 0, w, h)
+    b = gpu.synth_image(12, 0, w, h)
+    ext(a)
+    cap = ext.capacity(w, h)
+    imgs = torch.from_numpy(np.stack([b, b])).cuda()
+    k = torch.zeros((2, cap, 7), dtype=torch.int32, device="cuda")
+    d = torch.zeros((2, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ext.extract_batch(imgs.data_ptr(), 2, w, h, w, w * h, k.data_ptr(), d.data_ptr(), cap,
+                      n.data_ptr())
+    torch.cuda.synchronize()
+    k1, d1 = ext(a)  # replays the captured graph
+    del imgs  # the batch's input is gone: nothing may still point at it
+    torch.cuda.empty_cache()
+    pyr = ext.mvImagePyramid
+    assert np.array_equal(pyr[0], a)
+    ref = oracle.pyramid(a, 1.2, 8)
+    for l in range(8):
+        assert np.array_equal(pyr[l], ref[l]), f"level {l}"
+    kr, dr, _ = oracle.extract(a, 1000, 1.2, 8, 20, 7)
+    assert k1.tobytes() == kr.tobytes() and d1.tobytes() == dr.tobytes()

@@ -118,15 +118,17 @@ def test_stereo_from_extracted_handles(gpu, oracle, seed):
     ur, dp = gpu.ORBmatcher().ComputeStereoMatchesExtracted(L, R, scenarios.BF, scenarios.FX)
     assert (ur_ref > 0).sum() > 50
     assert ur.tobytes() == ur_ref.tobytes() and dp.tobytes() == dp_ref.tobytes()
-    # a batch call on a handle invalidates its single-image state
+    # a batch call on a handle invalidates its single-image state (the batch
+    # itself must succeed: only the stereo call may raise)
+    torch = pytest.importorskip("torch")
+    img = torch.from_numpy(oracle.synth_image(seed, 1, sp["w"], sp["h"])).cuda()
+    cap = L.capacity(sp["w"], sp["h"])
+    k = torch.zeros((1, cap, 7), dtype=torch.int32, device="cuda")
+    d = torch.zeros((1, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(1, dtype=torch.int32, device="cuda")
+    L.extract_batch(img.data_ptr(), 1, sp["w"], sp["h"], sp["w"], sp["w"] * sp["h"],
+                    k.data_ptr(), d.data_ptr(), cap, n.data_ptr())
+    torch.cuda.synchronize()
+    assert int(n[0]) > 0
     with pytest.raises(gpu.OrbError):
-        torch = pytest.importorskip("torch")
-        img = torch.from_numpy(oracle.synth_image(seed, 1, sp["w"], sp["h"])).cuda()
-        cap = L.capacity(sp["w"], sp["h"])
-        k = torch.zeros((1, cap, 7), dtype=torch.int32, device="cuda")
-        d = torch.zeros((1, cap, 32), dtype=torch.uint8, device="cuda")
-        n = torch.zeros(1, dtype=torch.int32, device="cuda")
-        L.extract_batch(img.data_ptr(), 1, sp["w"], sp["h"], sp["w"], sp["w"] * sp["h"],
-                        k.data_ptr(), d.data_ptr(), cap, n.data_ptr())
-        torch.cuda.synchronize()
         gpu.ORBmatcher().ComputeStereoMatchesExtracted(L, R, scenarios.BF, scenarios.FX)
