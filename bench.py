@@ -6,14 +6,17 @@ Each GPU holds a resident sequence of D distinct synthetic KITTI-shaped
 path over all D frames, in launches of B = 512: ORBextractor (1000 features,
 8 levels, FAST 20/7) + SearchByProjection(F, local map) against each frame's
 own 5,000-point synthetic local map (the headline
-workload).  Frames shard per rank (weak scaling); the only collective is an
-RCCL all-gather of the per-frame keypoint counts per launch and of the per-rank
-times at the end.  Launches are pipelined over two HIP streams and two buffer
-sets: launch g's matcher overlaps launch g+1's extraction (every launch does
-all of its work; the timed region ends with a device synchronize).
+workload).  Frames shard per rank (weak scaling); the only collectives are one
+RCCL all-gather of the step's per-frame keypoint counts per step and a MAX of
+the per-rank times at the end.  Launches are pipelined over two HIP streams and
+two buffer sets: launch g's matcher overlaps launch g+1's extraction (every
+launch does all of its work; the timed region ends with a device synchronize).
 
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant
-kernel, HIP-event timed over the timed region) and `cpu_baseline` (the C++ CPU
+kernel, HIP-event timed over the timed region; HBM bytes per SURVEY §8(d) as
+the primary fraction, VALU issue beside it), `host_input` (the same pipeline
+fed from pinned host memory: H2D of every frame and D2H of every result, the
+drop-in's PCIe-inclusive rate, never `value`) and `cpu_baseline` (the C++ CPU
 oracle, single thread, on a bounded sample of the same workload).
 """
 from __future__ import annotations
@@ -80,8 +83,9 @@ def shard_frames(rank, frames):
 
 
 def gather_counts(dist, counts, out):
-    """RCCL all-gather of every frame's keypoint count (int32 per frame).  With
-    the gloo backend (the multi-process test on one GPU) through host copies."""
+    """RCCL all-gather of the step's per-frame keypoint counts (int32 per frame,
+    one collective per step).  With the gloo backend (the multi-process test on
+    one GPU) through host copies."""
     if dist.get_backend() == "gloo":
         parts = [c.cpu() for c in out.chunk(dist.get_world_size())]
         dist.all_gather(parts, counts.cpu())
@@ -113,10 +117,14 @@ def measured_traffic(kernel, batch):
     return k["traffic_bytes"] * batch / t["batch"], files[-1].name
 
 
-# VALU issue time per wave-instruction per SIMD on gfx950, measured by
-# tools/probe/valu_rates.hip (profiles/r01_valu_rates.txt): plain 32-bit
-# integer / f32 ops ~1.0 ns, packed, 3-input and 24/32-bit multiply ops ~1.8 ns.
-VALU_NS_FAST, VALU_NS_SLOW, N_SIMD = 1.0, 1.8, 1024
+# VALU issue peak (MI355X_MICROARCH.md "Wave scheduling"): 1,024 SIMDs, one
+# wave64 VALU instruction per 2 cycles each, at the 2.4 GHz maximum clock =
+# 1,229 G wave-instructions/s.  tools/probe/valu_rates.hip measured ~1.0 ns per
+# plain and ~1.8 ns per packed / 3-input / multiply wave-instruction per SIMD
+# under load (profiles/r01_valu_rates.txt): the range of the issue-time bound.
+N_SIMD, CLOCK_GHZ, VALU_CYCLES = 1024, 2.4, 2
+VALU_PEAK_G = N_SIMD * CLOCK_GHZ / VALU_CYCLES
+VALU_NS_FAST, VALU_NS_SLOW = 1.0, 1.8
 
 
 def valu_issue(kernel, batch, ms_per_launch):
@@ -298,6 +306,91 @@ def secondary_configs(orb, torch, args, dev, threads):
     return out
 
 
+def host_input_leg(orb, torch, ext, matcher, imgs, args, dev, sets, d_mps, d_mpd, d_lock,
+                   d_nmps, scale, cap, dist, rank):
+    """The same extract + match pipeline fed from pinned host memory, as a
+    drop-in caller pays it (src/Frame.cc:278-285 hands ORBextractor a host
+    cv::Mat): each launch's B frames go H2D on a copy stream into one of two
+    device slots, double-buffered against the extraction, and every result
+    (keypoints, descriptors, counts, match assignments) comes back D2H on a
+    second copy stream.  The local maps stay resident.  Frames cycle through
+    --host-frames pinned host frames.  Returns rates; never the headline."""
+    W, H, B, M = args.width, args.height, args.batch, args.mappoints
+    NB = args.frames // B
+    nh = min(args.host_frames, len(imgs)) // B * B
+    if nh < B:
+        return None
+    h_img = torch.from_numpy(imgs[:nh]).pin_memory()
+    slots = [torch.empty((B, H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+    outs = [dict(kps=torch.empty((B, cap, 7), dtype=torch.int32).pin_memory(),
+                 desc=torch.empty((B, cap, 32), dtype=torch.uint8).pin_memory(),
+                 cnt=torch.empty(B, dtype=torch.int32).pin_memory(),
+                 match=torch.empty((B, cap), dtype=torch.int32).pin_memory()) for _ in range(2)]
+    cnts = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in range(2)]
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    es, ms = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev = {k: [torch.cuda.Event() for _ in range(2)] for k in ("in", "ext", "match", "out")}
+    fb = W * H
+
+    def launch(g):
+        j, b, hb = g % 2, g % NB, g % (nh // B)
+        st, o = sets[j], outs[j]
+        if g >= 2:
+            h2d.wait_event(ev["ext"][j])  # slot j's previous frames are extracted
+        with torch.cuda.stream(h2d):
+            slots[j].copy_(h_img[hb * B:(hb + 1) * B], non_blocking=True)
+        ev["in"][j].record(h2d)
+        es.wait_event(ev["in"][j])
+        if g >= 2:
+            es.wait_event(ev["out"][j])  # result set j has been copied out
+        ext.extract_batch(slots[j].data_ptr(), B, W, H, W, fb, st["kps"].data_ptr(),
+                          st["desc"].data_ptr(), cap, cnts[j].data_ptr(), es.cuda_stream)
+        ev["ext"][j].record(es)
+        ms.wait_event(ev["ext"][j])
+        matcher.search_by_projection_batch(B, st["kps"].data_ptr(), st["desc"].data_ptr(),
+                                           cnts[j].data_ptr(), d_lock[b * B].data_ptr(), cap,
+                                           d_mps[b * B].data_ptr(), d_mpd[b * B].data_ptr(),
+                                           d_nmps.data_ptr(), M, W, H, scale, 1.0,
+                                           st["match"].data_ptr(), st["nmatch"].data_ptr(),
+                                           ms.cuda_stream)
+        ev["match"][j].record(ms)
+        d2h.wait_event(ev["match"][j])
+        with torch.cuda.stream(d2h):
+            o["kps"].copy_(st["kps"], non_blocking=True)
+            o["desc"].copy_(st["desc"], non_blocking=True)
+            o["cnt"].copy_(cnts[j], non_blocking=True)
+            o["match"].copy_(st["match"], non_blocking=True)
+        ev["out"][j].record(d2h)
+
+    g = 0
+    for _ in range(4):
+        launch(g)
+        g += 1
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    n = args.host_passes * NB
+    t0 = time.perf_counter()
+    for _ in range(n):
+        launch(g)
+        g += 1
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+        el = max_over_ranks(dist, el, dev if args.dist_backend == "nccl" else "cpu")
+    if min(int(o["cnt"].min().item()) for o in outs) < 0:
+        raise RuntimeError("host-input leg: an extraction reported a failed frame")
+    frames = n * B * (dist.get_world_size() if dist is not None else 1)
+    out_b = cap * (28 + 32 + 4) + 4
+    return {"frames_per_s": frames / el, "unit": "frames/s", "frames": frames, "seconds": el,
+            "h2d_GBps": frames * fb / el / 1e9, "d2h_GBps": frames * out_b / el / 1e9,
+            "bytes_per_frame": {"h2d": fb, "d2h": out_b},
+            "note": "pinned host frames -> H2D (copy stream, two device slots) -> extract -> "
+                    "SearchByProjection -> D2H of keypoints, descriptors, counts and matches "
+                    "(second copy stream); local maps resident; PCIe-inclusive drop-in rate"}
+
+
 def timed_loop(fn, steps, warmup, torch):
     for _ in range(warmup):
         fn()
@@ -331,6 +424,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the measured path); gloo only for the multi-rank test "
                          "on one GPU (ORB_BENCH_DEVICE pins every rank to one device)")
+    ap.add_argument("--host-frames", type=int, default=2048,
+                    help="pinned host frames the host-input leg cycles through (0: skip the leg)")
+    ap.add_argument("--host-passes", type=int, default=4,
+                    help="timed passes of the host-input leg over --frames frames")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -342,7 +439,9 @@ def main():
         local = int(os.environ["ORB_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    # a torchrun launch initialises the process group even at world size 1, so
+    # the RCCL gather runs (and is verified) on a single GPU too
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or "MASTER_ADDR" in os.environ:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -374,9 +473,12 @@ def main():
                  desc=torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev),
                  cnt=torch.zeros(B, dtype=torch.int32, device=dev),
                  match=torch.zeros((B, cap), dtype=torch.int32, device=dev),
-                 nmatch=torch.zeros(B, dtype=torch.int32, device=dev),
-                 gathered=torch.zeros(world * B, dtype=torch.int32, device=dev) if world > 1 else None)
+                 nmatch=torch.zeros(B, dtype=torch.int32, device=dev))
             for _ in range(2)]
+    # every frame's keypoint count of a step, double-buffered over steps (the
+    # step's one all-gather reads buffer k % 2 while step k + 1 writes the other)
+    step_counts = [torch.zeros(D, dtype=torch.int32, device=dev) for _ in range(2)]
+    gathered = [torch.zeros(world * D, dtype=torch.int32, device=dev) for _ in range(2)]
     extracted = [torch.cuda.Event(), torch.cuda.Event()]
     matched = [torch.cuda.Event(), torch.cuda.Event()]
     frame_bytes = W * H
@@ -417,20 +519,25 @@ def main():
     def launch(g):
         j, b = g % 2, g % NB
         st = sets[j]
+        cnt = step_counts[(g // NB) % 2][b * B:(b + 1) * B]
+        st["cnt"] = cnt
         if g >= 2:
             ext_stream.wait_event(matched[j])
-        extract(st, b, ext_stream)
+        ext.extract_batch(d_img.data_ptr() + b * B * frame_bytes, B, W, H, W, frame_bytes,
+                          st["kps"].data_ptr(), st["desc"].data_ptr(), cap, cnt.data_ptr(),
+                          ext_stream.cuda_stream)
         extracted[j].record(ext_stream)
         match_stream.wait_event(extracted[j])
         matcher.search_by_projection_batch(B, st["kps"].data_ptr(), st["desc"].data_ptr(),
-                                           st["cnt"].data_ptr(), d_lock[b * B].data_ptr(), cap,
+                                           cnt.data_ptr(), d_lock[b * B].data_ptr(), cap,
                                            d_mps[b * B].data_ptr(), d_mpd[b * B].data_ptr(),
                                            d_nmps.data_ptr(), M, W, H, scale, 1.0,
                                            st["match"].data_ptr(), st["nmatch"].data_ptr(),
                                            match_stream.cuda_stream)
-        if dist is not None:  # RCCL: gather every frame's keypoint count
+        if dist is not None and b == NB - 1:  # one RCCL all-gather of the step's counts
+            k = (g // NB) % 2
             with torch.cuda.stream(match_stream):
-                gather_counts(dist, st["cnt"], st["gathered"])
+                gather_counts(dist, step_counts[k], gathered[k])
         matched[j].record(match_stream)
 
     g = 0
@@ -455,14 +562,14 @@ def main():
     elapsed = t1 - t0
     if dist is not None:
         elapsed = max_over_ranks(dist, elapsed, dev if args.dist_backend == "nccl" else "cpu")
-    for st in sets:
-        if int(st["cnt"].min().item()) < 0:
-            raise RuntimeError("extraction reported a failed frame (negative count)")
+    if min(int(c.min().item()) for c in step_counts) < 0:
+        raise RuntimeError("extraction reported a failed frame (negative count)")
     gather_ok = None
-    if dist is not None:  # the gathered counts of this rank's last launch are its own
-        j = (g - 1) % 2
-        mine = sets[j]["gathered"][rank * B:(rank + 1) * B]
-        gather_ok = bool(torch.equal(mine, sets[j]["cnt"]))
+    if dist is not None:  # the gathered counts of the last step hold this rank's own
+        k = ((g - 1) // NB) % 2
+        mine = gathered[k][rank * D:(rank + 1) * D]
+        gather_ok = bool(torch.equal(mine, step_counts[k])) and bool(
+            torch.equal(step_counts[k].cpu(), torch.from_numpy(cnt_h)))
         ok = torch.tensor([1 if gather_ok else 0], dtype=torch.int32)
         if args.dist_backend == "nccl":
             ok = ok.to(dev)
@@ -510,29 +617,40 @@ def main():
     traffic, traffic_src = measured_traffic(dom, B)
     valu = valu_issue(dom, B, dom_ms_per_launch)
     total_frames = D * args.steps * world
+    # the HBM roofline of the dominant kernel is the primary
+    # fraction (algorithmic bytes per launch / its launch time); its VALU issue
+    # rate against the guide's peak sits beside it (the integer kernels of this
+    # path are instruction-bound, not bandwidth-bound: DESIGN.md §4)
+    roof = {"kernel": dom, "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_launch": dom_bytes,
+            "bytes_note": f"SURVEY §8(d) algorithmic bytes of {dom}: every pyramid pixel read "
+                          f"once ({alg[dom]:.0f} B/frame) x {B} frames per launch"}
     if valu is not None:
-        # VALU issue: the roofline that binds this integer kernel (its HBM
-        # fraction is reported beside it)
         rate = valu["valu_instr_per_launch"] / (dom_ms_per_launch * 1e-3) / 1e9
-        peak = N_SIMD / VALU_NS_FAST
-        roof = {"kernel": dom, "bound": "valu", "achieved": rate, "peak": peak,
-                "unit": "G VALU wave-instructions/s", "frac": rate / peak,
-                "note": "peak = 1024 SIMDs x one plain 32-bit VALU wave-instruction per ns "
-                        "(profiles/r01_valu_rates.txt); SQ_INSTS_VALU per launch from "
-                        + valu["source"].split(" ")[0],
-                "valu_issue": valu}
-    else:
-        roof = {"kernel": dom, "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS}
+        roof["valu"] = {"achieved": rate, "peak": VALU_PEAK_G, "unit": "G wave-instructions/s",
+                        "frac": rate / VALU_PEAK_G,
+                        "note": f"peak = {N_SIMD} SIMDs x {CLOCK_GHZ} GHz / {VALU_CYCLES} cycles per "
+                                "wave64 VALU instruction (MI355X_MICROARCH.md); SQ_INSTS_VALU per "
+                                "launch from " + valu["source"].split(" ")[0],
+                        "issue_bound": valu}
     roof.update({
         "traffic": traffic,
         "traffic_source": f"profiles/{traffic_src} (rocprofv3 FETCH_SIZE x 2 (gfx950 "
                           "calibration, profiles/r02_fetch_calib.txt) + WRITE_SIZE, separate "
                           "passes)" if traffic_src else None,
-        "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_launch": dom_bytes},
         "ms_per_launch": dom_ms_per_launch,
     })
+    host = None
+    if args.host_frames > 0:
+        del d_img
+        host = host_input_leg(orb, torch, ext, matcher, imgs, args, dev, sets, d_mps, d_mpd,
+                              d_lock, d_nmps, scale, cap, dist, rank)
+    if dist is None:
+        par = "single rank; no collective (one process, one GPU)"
+    else:
+        par = (f"frames sharded over {world} rank(s); one "
+               f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-gather of the step's "
+               f"per-frame keypoint counts per step")
     result = {
         "metric": METRIC,
         "value": total_frames / elapsed,
@@ -553,8 +671,9 @@ def main():
             "distinct_frames_per_gpu": D,
             "frames_per_launch": B,
             "timed_region_s": elapsed,
-            "parallelism": f"frames sharded over {world} rank(s), "
-                           f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-gather of counts",
+            "inputs": "frames resident in HBM before the timed region (device-resident rate; "
+                      "the PCIe-inclusive drop-in rate is `host_input`)",
+            "parallelism": par,
             "count_gather_verified": gather_ok,
             "mean_keypoints_per_frame": n_kp,
             "mean_matches_per_frame": nmatch,
@@ -564,9 +683,11 @@ def main():
         "extraction_kernels_ms_per_launch": sum(kern[k][0] for k in ext_kern) / (args.steps * NB),
         "extraction_call_ms_per_launch": call_ms / max(call_n, 1),
         "level0_side_stream_ms_per_launch": side_ms,
+        "host_input": host,
     }
     if rank == 0 and world == 1 and not args.no_secondary:
-        del d_img
+        if args.host_frames <= 0:
+            del d_img
         result.update(secondary_configs(orb, torch, args, dev, args.threads))
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(imgs[:64], maps[:64], args, scale)

@@ -738,6 +738,15 @@ __global__ __launch_bounds__(256) void k_fast_band(
   }  // band loop
 }
 
+// v_cndmask with a wave-uniform 64-bit lane mask as the condition: lanes whose
+// bit is set take ifSet.  (A select on a per-lane bool derived from a ballot
+// makes hipcc rebuild the mask through VGPR 0/1 values and compares.)
+__device__ __forceinline__ int lane_select(unsigned long long mask, int ifSet, int ifClear) {
+  int r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(ifClear), "v"(ifSet), "s"(mask));
+  return r;
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -747,14 +756,24 @@ __device__ __forceinline__ void wave_lds_sync() {
 // ============================================================ k_fast_cells
 // FAST per cell, one wave per cell (src/ORBextractor.cc:816-865), no
 // workgroup barriers: a wave stages its cell's ROI (cell + the 3-px FAST
-// border) as biased f16 in its own LDS slice, pretests 8 pixels per lane
-// (compass test, as k_fast_band), queues the candidates with wave ballots,
-// scores them (arc strengths), lists the corners (m > t), runs the cell-local
-// 3x3 NMS into a row bitmap and compacts it row by row (lane = window row).
-// A cell without a keypoint at iniThFAST reruns the same at minThFAST over
-// its window, keeping the strengths already computed (:846-850).  Output per
-// cell: keys in row-major window order (cv::FAST's order), packed
-// x | y << 12 | score << 24 in level coordinates, and their count.
+// border) as bytes in its own LDS slice, pretests 8 pixels per lane (compass
+// test), queues the candidates with wave ballots, scores them (arc strengths),
+// lists the corners (m > t), runs the cell-local 3x3 NMS into a row bitmap and
+// compacts it row by row (lane = window row).  A cell without a keypoint at
+// iniThFAST reruns the same at minThFAST over its window, keeping the
+// strengths already computed (:846-850).  Output per cell: keys in row-major
+// window order (cv::FAST's order), packed x | y << 12 | score << 24 in level
+// coordinates, and their count.
+//
+// Arithmetic: a pixel byte I is read as the f16 whose bit pattern is I, i.e.
+// the subnormal I * 2^-24 (f16 subnormals are kept: the kernel runs with
+// .amdhsa_float_denorm_mode_16_64 3).  Differences and sums of such values
+// (|.| < 1024 * 2^-24) are exact, so the packed f16 three-input min / max of
+// gfx950 do exact integer arithmetic on pixels with no conversion: a byte
+// loaded by ds_read_u8 is already its f16, and a pair of bytes becomes an f16
+// pair with one v_perm.  The tile is one byte per pixel, which keeps a wave's
+// LDS slice at ~7 KB (22-24 waves per CU; occupancy is what this
+// latency-bound kernel's time follows).
 #ifndef FC_WAVES
 #define FC_WAVES 1      // waves per workgroup (LDS slices; swept 1-4)
 #endif
@@ -762,26 +781,71 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define FC_CPW 4        // cells per wave (software-pipelined ROI loads)
 #endif
 #ifndef FC_QCAP
-#define FC_QCAP 1024    // candidate queue per wave (one pretest round adds <= 512)
+#define FC_QCAP 768     // candidate queue per wave (one pretest round adds <= 512)
 #endif
 #ifndef FC_CCAP
-#define FC_CCAP 512     // corner list per wave; beyond it the NMS runs densely
+#define FC_CCAP 256     // corner list per wave; beyond it the NMS runs densely
 #endif
 #ifndef FC_PAD
-#define FC_PAD 0        // extra LDS row pitch (elements, multiple of 8)
+#define FC_PAD 0        // extra LDS row pitch (bytes, multiple of 8)
 #endif
 #ifndef FC_PERM
 #define FC_PERM 1       // pretest lane -> pixel-group permutation (LDS banking)
 #endif
 
-// LDS row pitch (elements) of a cell ROI C pixels wide
+// LDS row pitch (bytes) of a cell ROI C pixels wide: byte 8 is interior column
+// 0 (ROI column 3), groups of 8 interior pixels read [8k, 8k + 24)
 __host__ __device__ inline int fc_pitch(int C) { return ((C + 20) & ~7) + FC_PAD; }
 __host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
   return maxRows * fc_pitch(maxCols);
 }
 __host__ __device__ inline int fc_wave_bytes(int tileElems) {
-  // f16 tile + strengths + queue + corners + 64 rows x 64-bit bitmap
-  return ((3 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + 512) + 15) & ~15;
+  // byte tile + strengths + queue + corners + 64 rows x 64-bit bitmap
+  return ((2 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + 512) + 15) & ~15;
+}
+
+// f16 pair {byte i0, byte i1} of the 8 bytes {hi:lo} (i in 0..7, lo first)
+__device__ __forceinline__ uint32_t byte_pair(uint32_t hi, uint32_t lo, int i0, int i1) {
+  return __builtin_amdgcn_perm(hi, lo, (uint32_t)i0 | 0x0C00u | ((uint32_t)i1 << 16) | 0x0C000000u);
+}
+
+// FAST arc strength of the byte pixel at `c` (row pitch p bytes), as
+// fast_score on the subnormal encoding above
+__device__ __forceinline__ int fast_score_u8(const uint8_t* c, int p) {
+  const int off[16] = {3 * p,      3 * p + 1,  2 * p + 2,  p + 3,       3,  -p + 3,
+                       -2 * p + 2, -3 * p + 1, -3 * p,     -3 * p - 1, -2 * p - 2, -p - 3,
+                       -3,         p - 3,      2 * p - 2,  3 * p - 1};
+  const _Float16 v = __builtin_bit_cast(_Float16, (uint16_t)c[0]);
+  const h16x2 vv = {v, -v}, sg = {(_Float16)-1.0f, (_Float16)1.0f};
+  h16x2 q[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const _Float16 ck = __builtin_bit_cast(_Float16, (uint16_t)c[off[k]]);
+    const h16x2 cc = {ck, ck};
+    q[k] = __builtin_elementwise_fma(cc, sg, vv);  // (v - ck, ck - v), exact
+  }
+  h16x2 w3[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    w3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(q[k], q[(k + 1) & 15]),
+                                          q[(k + 2) & 15]);
+  h16x2 w9[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    w9[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(w3[k], w3[(k + 3) & 15]),
+                                          w3[(k + 6) & 15]);
+  h16x2 m5[6];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    m5[k] = __builtin_elementwise_maximum(__builtin_elementwise_maximum(w9[3 * k], w9[3 * k + 1]),
+                                          w9[3 * k + 2]);
+  m5[5] = w9[15];
+  const h16x2 ma = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m5[0], m5[1]), m5[2]);
+  const h16x2 mb = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m5[3], m5[4]), m5[5]);
+  const h16x2 best = __builtin_elementwise_maximum(ma, mb);
+  // the subnormal's bit pattern is the integer strength; negative -> 0
+  const int s = (int)(short)__builtin_bit_cast(uint16_t, __builtin_fmaxf16(best.x, best.y));
+  return min(max(s, 0), 255);
 }
 
 __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
@@ -797,10 +861,8 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   xcd_swizzle(bx, img);
   // the image's status starts clean (k_octree may flag it, k_orient_desc reads it)
   if (bx == 0 && threadIdx.x == 0) errFlag[img] = 0;
-  unsigned char* wbase = smem + wave * fc_wave_bytes(tileElems);
-  uint32_t* tile32 = (uint32_t*)wbase;
-  const _Float16* tileh = (const _Float16*)wbase;
-  uint8_t* sc = wbase + 2 * tileElems;
+  uint8_t* tile = smem + wave * fc_wave_bytes(tileElems);
+  uint8_t* sc = tile + tileElems;  // strengths, same byte layout as the tile
   uint16_t* queue = (uint16_t*)(sc + tileElems);
   uint16_t* corners = queue + FC_QCAP;
   uint32_t* bits = (uint32_t*)(corners + FC_CCAP);  // row y: words 2y, 2y+1
@@ -809,9 +871,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   auto cell_of = [&](int j) { return cellBeg + (bx * FC_CPW + j) * FC_WAVES + wave; };
   // ---- staging: lane r loads ROI row r, bytes [x0 - LPAD, x0 - LPAD + P)
   // of level row y0 + r, as four 16-byte loads from the 4-aligned byte at or
-  // below its start (any caller stride), realigned in registers; every byte
-  // becomes a biased f16 (one v_perm per f16 pair: the bias byte comes from
-  // the constant operand)
+  // below its start (any caller stride), realigned in registers
   uint32_t raw[16], rsh = 0;
   auto issue = [&](const OrbCellDesc& q) {
     const int ql = q.level, qR = q.y1 - q.y0;
@@ -847,22 +907,15 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   const int R = cd.y1 - cd.y0, C = cd.x1 - cd.x0;
   const long long slot = (long long)img * plan.ncells + ci;
   const bool tiny = R < 7 || C < 7;
-  const int P = fc_pitch(C), PD = P >> 1;
+  const int P = fc_pitch(C);
   if (!tiny && lane < R) {
-    const int nS = ((C + 20) & ~7) >> 2;  // source dwords per row (<= 14, host-checked)
-    uint4* dst = reinterpret_cast<uint4*>(tile32 + lane * PD);
+    const int nS = ((C + 20) & ~7) >> 2;  // dwords per row (<= 14, host-checked)
+    uint2* dst = reinterpret_cast<uint2*>(tile + lane * P);
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      if (2 * k < nS) {
-        const uint32_t w0 = __builtin_amdgcn_alignbyte(raw[2 * k + 1], raw[2 * k], rsh);
-        const uint32_t w1 = __builtin_amdgcn_alignbyte(raw[2 * k + 2], raw[2 * k + 1], rsh);
-        uint4 h;
-        h.x = __builtin_amdgcn_perm(0x64646464u, w0, 0x04010400u);
-        h.y = __builtin_amdgcn_perm(0x64646464u, w0, 0x04030402u);
-        h.z = __builtin_amdgcn_perm(0x64646464u, w1, 0x04010400u);
-        h.w = __builtin_amdgcn_perm(0x64646464u, w1, 0x04030402u);
-        dst[k] = h;
-      }
+      if (2 * k < nS)
+        dst[k] = make_uint2(__builtin_amdgcn_alignbyte(raw[2 * k + 1], raw[2 * k], rsh),
+                            __builtin_amdgcn_alignbyte(raw[2 * k + 2], raw[2 * k + 1], rsh));
     }
   }
   const int ciNext = jc + 1 < FC_CPW ? cell_of(jc + 1) : cellEnd;
@@ -894,17 +947,15 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       if (j < nq) {
         off = queue[j];
         int m;
-        if (fresh) {  // the 16 ring reads go out with the strength read
-          const int s = min(max(fast_score(tileh + off, P), 0), 255);
-          m = sc[off];
-          if (m == 0) {
-            m = s;
-            sc[off] = (uint8_t)m;
-          }
+        if (fresh) {
+          // phase A queues interior pixels only (fast_pass masks the columns
+          // past the window), and none has a strength yet: no strength read
+          m = fast_score_u8(tile + off, P);
+          sc[off] = (uint8_t)m;
         } else {
           m = sc[off];  // 0: not scored yet; phase B keeps phase-A strengths
           if (m == 0) {
-            m = min(max(fast_score(tileh + off, P), 0), 255);
+            m = fast_score_u8(tile + off, P);
             sc[off] = (uint8_t)m;
           }
         }
@@ -918,56 +969,78 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     }
     nq = 0;
   };
-  // one FAST pass at threshold t over the window: pretest, queue, strengths, corners
+  // One FAST pass at threshold t over the window: pretest, queue, strengths,
+  // corners.  Lane state: its pixel group (group k of an interior row) and the
+  // group's tile byte `off`, advanced by 64 groups per round with adds.
+  // Invalid lanes (past the window) and the pixels past the interior in a
+  // row's last group are masked out of the queue by SGPR lane masks; the
+  // queue writes of lanes that do not pass go to a per-lane trash word (the
+  // NMS bitmap, unused while a pass runs) instead of branching on EXEC.
   auto fast_pass = [&](int t, bool fresh) {
     h16x2 T;
-    T.x = T.y = (_Float16)(float)(t + 1);
+    T.x = T.y = __builtin_bit_cast(_Float16, (uint16_t)(t + 1));
     const int nG = ih * nK;
-    for (int g0 = 0; g0 < nG; g0 += 64) {
 #if FC_PERM
-      // The queue is a set (scores, corners and the NMS bitmap do not depend on
-      // its order), so lanes may take the round's 64 pixel groups in any order.
-      // With 4 groups per row (level-0 cells), give each ds_read_b128 lane
-      // group {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... the rows r, r+4, r+8,
-      // r+12, whose 16-dword runs fall in distinct banks at a 28-dword pitch.
-      const int gi = g0 + 4 * (int)((0xFEAB6732DC894510ull >> (4 * (lane >> 2))) & 15u) + (lane & 3);
+    // The queue is a set (scores, corners and the NMS bitmap do not depend on
+    // its order), so lanes may take the round's 64 pixel groups in any order:
+    // spread each LDS lane group's rows over the banks.
+    const int pl = 4 * (int)((0xFEAB6732DC894510ull >> (4 * (lane >> 2))) & 15u) + (lane & 3);
 #else
-      const int gi = g0 + lane;
+    const int pl = lane;
 #endif
-      uint32_t rp[4] = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
-      int off = 0;
-      if (gi < nG) {
-        const int rr = (int)(((float)gi + 0.5f) * invK), k = gi - rr * nK;
-        const int r = rr + 3;
-        off = r * P + 8 + 8 * k;  // element of interior column 8k
-        const uint32_t* row = tile32 + r * PD + 4 + 4 * k;
-        const uint2 a = *reinterpret_cast<const uint2*>(row - 2);
-        const uint4 b = *reinterpret_cast<const uint4*>(row);
-        const uint2 c = *reinterpret_cast<const uint2*>(row + 4);
-        const uint4 u = *reinterpret_cast<const uint4*>(row + 3 * PD);  // circle 0 (y + 3)
-        const uint4 d = *reinterpret_cast<const uint4*>(row - 3 * PD);  // circle 8 (y - 3)
-        const uint32_t D[8] = {a.x, a.y, b.x, b.y, b.z, b.w, c.x, c.y};
-        const uint32_t U[4] = {u.x, u.y, u.z, u.w}, Dn[4] = {d.x, d.y, d.z, d.w};
+    const int rr0 = (int)(((float)pl + 0.5f) * invK);
+    int k = pl - rr0 * nK;
+    int off = (rr0 + 3) * P + 8 + 8 * k;  // byte of interior column 8k
+    const int rInc = 64 / nK, kInc = 64 - rInc * nK;  // wave-uniform
+    const int dOff = rInc * P + 8 * kInc, wrapOff = P - 8 * nK;
+    // trash slots in the NMS bitmap, as indices into the queue (u16) and the
+    // strength map (u64 words): 4- and 8-byte lane strides
+    const int trashQ = (int)(reinterpret_cast<uint16_t*>(bits) - queue) + 2 * lane;
+    unsigned long long* const sc64 = reinterpret_cast<unsigned long long*>(sc);
+    const int trashS = (int)(reinterpret_cast<unsigned long long*>(bits) - sc64) + lane;
+    for (int g0 = 0; g0 < nG; g0 += 64) {
+      const bool valid = g0 + pl < nG;
+      const bool last = k == nK - 1;
+      const int o = valid ? off : 3 * P + 8;  // invalid lanes read group 0 (masked below)
+      // bytes o-8 .. o+15 of the row, and o .. o+7 three rows down / up
+      const uint2* rw = reinterpret_cast<const uint2*>(tile + o);
+      const uint2 A = rw[-1], B = rw[0], Cc = rw[1];
+      const uint2 Uu = *reinterpret_cast<const uint2*>(tile + o + 3 * P);  // circle 0 (y + 3)
+      const uint2 Dd = *reinterpret_cast<const uint2*>(tile + o - 3 * P);  // circle 8 (y - 3)
+      // f16 pairs of pixels (2i, 2i+1): v, x + 3, y + 3, y - 3, x - 3
+      const uint32_t q4_0 = byte_pair(B.y, B.x, 3, 4);
+      const uint32_t V[4] = {byte_pair(B.y, B.x, 0, 1), byte_pair(B.y, B.x, 2, 3),
+                             byte_pair(Cc.x, B.y, 0, 1), byte_pair(Cc.x, B.y, 2, 3)};
+      const uint32_t Q4[4] = {q4_0, byte_pair(Cc.x, B.y, 1, 2), byte_pair(Cc.x, B.y, 3, 4),
+                              byte_pair(Cc.y, Cc.x, 1, 2)};
+      const uint32_t Q0[4] = {byte_pair(Uu.y, Uu.x, 0, 1), byte_pair(Uu.y, Uu.x, 2, 3),
+                              byte_pair(Uu.y, Uu.x, 4, 5), byte_pair(Uu.y, Uu.x, 6, 7)};
+      const uint32_t Q8[4] = {byte_pair(Dd.y, Dd.x, 0, 1), byte_pair(Dd.y, Dd.x, 2, 3),
+                              byte_pair(Dd.y, Dd.x, 4, 5), byte_pair(Dd.y, Dd.x, 6, 7)};
+      const uint32_t Q12[4] = {byte_pair(A.y, A.x, 5, 6), byte_pair(B.x, A.y, 3, 4),
+                               byte_pair(B.x, A.y, 5, 6), q4_0};
+      uint32_t rp[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t q4 = __builtin_amdgcn_alignbyte(D[i + 4], D[i + 3], 2);   // x + 3
-          const uint32_t q12 = __builtin_amdgcn_alignbyte(D[i + 1], D[i], 2);      // x - 3
-          rp[i] = pretest_pair(D[i + 2], U[i], q4, Dn[i], q12, T);
-        }
-        if (fresh) {  // strengths start at 0, FAST_OUTSIDE past the interior
-          const unsigned long long z = k == nK - 1 ? outsideLast : 0ull;
-          *reinterpret_cast<unsigned long long*>(sc + off) = z;
-        }
-      }
+      for (int i = 0; i < 4; ++i) rp[i] = pretest_pair(V[i], Q0[i], Q4[i], Q8[i], Q12[i], T);
+      if (fresh)  // strengths start at 0, FAST_OUTSIDE past the interior (o is a multiple of 8)
+        sc64[valid ? (o >> 3) : trashS] = last ? outsideLast : 0ull;
+      // pixel j of a valid lane is interior when j < nvLast or the group is not a row's last
+      const unsigned long long vm = __ballot(valid), vIn = __ballot(valid && !last);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t w = rp[j >> 1];
-        const bool pass = (j & 1) ? ((int)w >= 0) : ((short)(w & 0xFFFFu) >= 0);
-        const unsigned long long bj = __ballot(pass);
-        const int pos = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bj, 0u));
-        if (pass) queue[pos] = (uint16_t)(off + j);
+        const bool sgn = (j & 1) ? ((int)w >= 0) : ((short)(w & 0xFFFFu) >= 0);
+        const unsigned long long bj = __ballot(sgn) & (j < nvLast ? vm : vIn);
+        const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bj, (uint32_t)nq));
+        queue[lane_select(bj, pos, trashQ)] = (uint16_t)(off + j);
         nq += __popcll(bj);
+      }
+      k += kInc;
+      off += dOff;
+      if (k >= nK) {
+        k -= nK;
+        off += wrapOff;
       }
       if (nq > FC_QCAP - 512 || g0 + 64 >= nG) {
         wave_lds_sync();
@@ -2301,9 +2374,17 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
                             int32_t* errFlag, int cellBeg, int cellEnd, int nimg, hipStream_t s) {
   if (cellEnd <= cellBeg) return hipSuccess;
-  const int tileElems = fc_tile_elems(plan->maxCellRows, plan->maxCellCols);
-  const size_t lds = orb_k_fast_cells_lds(plan->maxCellRows, plan->maxCellCols);
   if (!orb_k_fast_cells_fits(plan)) return hipErrorInvalidValue;
+  // LDS sized for the largest cell of the levels this launch covers (level 0's
+  // side launch gets the smaller slices of its 38-row cells)
+  int mr = 7, mc = 7;
+  for (int l = 0; l < plan->nlevels; ++l)
+    if (plan->lv[l].cellBeg < cellEnd && plan->lv[l].cellEnd > cellBeg) {
+      mr = std::max(mr, plan->lv[l].cellMaxRows);
+      mc = std::max(mc, plan->lv[l].cellMaxCols);
+    }
+  const int tileElems = fc_tile_elems(mr, mc);
+  const size_t lds = orb_k_fast_cells_lds(mr, mc);
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k_fast_cells,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

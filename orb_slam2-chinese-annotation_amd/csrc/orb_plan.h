@@ -31,6 +31,7 @@ struct OrbLevelDesc {
   int rtabX, rtabY;  // offsets of this level's resize tables (x: xofs/alpha, y: yofs/beta)
   int xmax;          // first dx whose source tap sx+1 falls outside (resize)
   int tileBeg;       // first blur tile of this level
+  int cellMaxRows, cellMaxCols;  // largest cell ROI of this level (k_fast_cells LDS per launch)
 };
 
 struct OrbPlanDesc {

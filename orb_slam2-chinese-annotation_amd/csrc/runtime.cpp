@@ -484,6 +484,8 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
         const int rows = c.y1 - c.y0, cols = c.x1 - c.x0;
         maxRows = std::max(maxRows, rows);
         maxCols = std::max(maxCols, cols);
+        d.cellMaxRows = std::max(d.cellMaxRows, rows);
+        d.cellMaxCols = std::max(d.cellMaxCols, cols);
         if (rows >= 7 && cols >= 7)
           keyCap = std::max(keyCap, ((rows - 6 + 1) / 2) * ((cols - 6 + 1) / 2));
       }
