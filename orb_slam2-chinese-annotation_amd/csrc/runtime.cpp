@@ -234,20 +234,29 @@ struct HostBuf {
 // the launch path); read() drains every recorded set and accumulates per-stage
 // milliseconds, so a timed region of K calls is measured without perturbing it.
 struct StageProfiler {
-  // Per call: a (begin, end) event pair per stage, recorded on whichever stream
-  // runs that stage (stages may overlap), plus a (begin, end) pair for the
-  // whole call on the caller's stream.
-  static const int kMaxStages = 8;
+  // Per call: (begin, end) event pairs per stage -- up to maxSeg[stage]
+  // segments, e.g. one per level for a stage launched level by level, whose
+  // durations are summed -- recorded on whichever stream runs that stage
+  // (stages may overlap), plus a (begin, end) pair for the whole call on the
+  // caller's stream.
+  static constexpr int kMaxStages = 8;
   bool enabled = false;
   int nStages = 0;
   const char* names[kMaxStages] = {};
-  std::vector<std::vector<hipEvent_t>> pool;  // each: 2 * nStages + 2 events
-  std::vector<unsigned> ran;                   // per call: stages whose events were recorded
+  int maxSeg[kMaxStages] = {1, 1, 1, 1, 1, 1, 1, 1};
+  std::vector<std::vector<hipEvent_t>> pool;  // each: 2 * sum(maxSeg) + 2 events
+  std::vector<std::vector<uint8_t>> segs;     // per call: segments recorded per stage
   size_t used = 0;
   double ms[kMaxStages + 1] = {};
   long launches[kMaxStages + 1] = {};
   int launchesPerCall[kMaxStages] = {};
 
+  int base(int stage) const {
+    int o = 0;
+    for (int i = 0; i < stage; ++i) o += maxSeg[i];
+    return o;
+  }
+  int total() const { return base(nStages); }
   void reset() {
     used = 0;
     for (int i = 0; i <= kMaxStages; ++i) { ms[i] = 0; launches[i] = 0; }
@@ -255,34 +264,46 @@ struct StageProfiler {
   std::vector<hipEvent_t>* begin_call() {
     if (!enabled) return nullptr;
     if (used == pool.size()) {
-      pool.emplace_back(2 * nStages + 2);
+      pool.emplace_back(2 * total() + 2);
       for (hipEvent_t& e : pool.back()) hipEventCreate(&e);
-      ran.push_back(0);
+      segs.emplace_back(kMaxStages, 0);
     }
-    ran[used] = ~0u;
+    std::fill(segs[used].begin(), segs[used].end(), (uint8_t)1);
     return &pool[used++];
   }
-  void not_run(int stage) { ran[used - 1] &= ~(1u << stage); }  // of the current call
-  hipEvent_t b(std::vector<hipEvent_t>* ev, int stage) const { return (*ev)[2 * stage]; }
-  hipEvent_t e(std::vector<hipEvent_t>* ev, int stage) const { return (*ev)[2 * stage + 1]; }
-  hipEvent_t t0(std::vector<hipEvent_t>* ev) const { return (*ev)[2 * nStages]; }
-  hipEvent_t t1(std::vector<hipEvent_t>* ev) const { return (*ev)[2 * nStages + 1]; }
+  // of the current call: stage not run / run as n segments
+  void not_run(int stage) { segs[used - 1][stage] = 0; }
+  void segments(int stage, int n) { segs[used - 1][stage] = (uint8_t)n; }
+  hipEvent_t b(std::vector<hipEvent_t>* ev, int stage, int seg = 0) const {
+    return (*ev)[2 * (base(stage) + seg)];
+  }
+  hipEvent_t e(std::vector<hipEvent_t>* ev, int stage, int seg = 0) const {
+    return (*ev)[2 * (base(stage) + seg) + 1];
+  }
+  hipEvent_t t0(std::vector<hipEvent_t>* ev) const { return (*ev)[2 * total()]; }
+  hipEvent_t t1(std::vector<hipEvent_t>* ev) const { return (*ev)[2 * total() + 1]; }
   void drain() {
     for (size_t c = 0; c < used; ++c) {
       std::vector<hipEvent_t>& ev = pool[c];
-      if (hipEventSynchronize(ev[2 * nStages + 1]) != hipSuccess) continue;
+      if (hipEventSynchronize(t1(&ev)) != hipSuccess) continue;
       for (int i = 0; i < nStages; ++i) {
-        float t = 0.f;
-        if (launchesPerCall[i] == 0 || !(ran[c] >> i & 1)) continue;  // stage not run
-        if (hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]) == hipSuccess) {
-          ms[i] += t;
+        if (launchesPerCall[i] == 0 || segs[c][i] == 0) continue;  // stage not run
+        bool ok = true;
+        double sum = 0;
+        for (int g = 0; g < segs[c][i] && ok; ++g) {
+          float t = 0.f;
+          ok = hipEventElapsedTime(&t, b(&ev, i, g), e(&ev, i, g)) == hipSuccess;
+          sum += t;
+        }
+        if (ok) {
+          ms[i] += sum;
           launches[i] += launchesPerCall[i];
         } else {
           (void)hipGetLastError();  // clear it: torch checks the last error after its launches
         }
       }
       float t = 0.f;
-      if (hipEventElapsedTime(&t, ev[2 * nStages], ev[2 * nStages + 1]) == hipSuccess) {
+      if (hipEventElapsedTime(&t, t0(&ev), t1(&ev)) == hipSuccess) {
         ms[nStages] += t;
         launches[nStages] += 1;
       }
@@ -293,7 +314,7 @@ struct StageProfiler {
     for (auto& v : pool)
       for (hipEvent_t ev : v) hipEventDestroy(ev);
     pool.clear();
-    ran.clear();
+    segs.clear();
     used = 0;
   }
 };
@@ -328,9 +349,11 @@ struct orb_extractor {
   std::vector<int> quota;
   int umax[16];
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // side stream: blur runs beside FAST + octree
+  hipStream_t stream2 = nullptr;  // side stream: FAST beside the resize chain (blur in split mode)
+  hipStream_t stream3 = nullptr;  // resize chain, high priority (ORB_CHAIN_STREAM=1)
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   hipEvent_t evL0Fork = nullptr, evL0Join = nullptr;  // level-0 FAST beside the resize chain
+  hipEvent_t evLvl[ORB_MAX_LEVELS] = {};  // level l written by the resize chain (per-level FAST)
   hipEvent_t evBatch = nullptr;  // recorded at the end of every run_batch on its stream
   bool ownStream = false;
   std::mutex mu;
@@ -699,6 +722,13 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   // events, graph-capturable); levels >= 1 follow the chain on the main stream.
   const int l0End = P.lv[0].cellEnd;
   const bool l0Side = !useBands && !noL0Overlap && l0End > 0 && P.nlevels > 1;
+  // ORB_FAST_PER_LEVEL=1 (A/B knob, off): levels >= 1 on the side stream too,
+  // each launched as soon as the chain has written its level.  Measured slower
+  // (255k vs 260k frames/s; the chain, 0.52 -> 0.81 ms, loses its CUs to FAST),
+  // with or without stream priorities (profiles/r03_fast_schedule.txt)
+  static const bool fastPerLevelEnv =
+      getenv("ORB_FAST_PER_LEVEL") && atoi(getenv("ORB_FAST_PER_LEVEL")) > 0;
+  const bool perLevel = l0Side && fastPerLevelEnv;
   if (l0Side) {
     HIP_TRY(hipEventRecord(h->evL0Fork, s));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->evL0Fork, 0));
@@ -708,11 +738,19 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                              h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, l0End, B,
                              h->stream2));
     PROF_REC(ev, pf.e(ev, 5), h->stream2);
-    HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
+    if (!perLevel) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
   } else if (ev) {
     pf.not_run(5);
   }
-  PROF_REC(ev, pf.b(ev, 0), s);
+  // the resize chain: on the caller's stream, or (per-level mode,
+  // ORB_CHAIN_STREAM=1) on a high-priority third stream forked from it
+  hipStream_t cs = s;
+  if (perLevel && h->stream3) {
+    cs = h->stream3;
+    HIP_TRY(hipStreamWaitEvent(cs, h->evL0Fork, 0));
+  }
+  PROF_REC(ev, pf.b(ev, 0), cs);
+  int fastSeg = 0;
   for (int l = 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
     const OrbLevelDesc& sd = P.lv[l - 1];
@@ -721,9 +759,32 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     const int srcStride = l == 1 ? (int)stride : sd.pitch;
     HIP_TRY(orb_k_pyr_resize(src, srcPitch, srcStride, sd.w, sd.h, arena + d.arenaOff, ap, d.pitch, d.w,
                              d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
-                             rt + d.rtabY + d.h, d.xmax, B, s));
+                             rt + d.rtabY + d.h, d.xmax, B, cs));
+    if (perLevel && d.cellEnd > d.cellBeg) {
+      // level l's cells on the side stream as soon as the chain has produced it
+      HIP_TRY(hipEventRecord(h->evLvl[l], cs));
+      HIP_TRY(hipStreamWaitEvent(h->stream2, h->evLvl[l], 0));
+      PROF_REC(ev, pf.b(ev, 2, fastSeg), h->stream2);
+      HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                               h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
+                               h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), d.cellBeg,
+                               d.cellEnd, B, h->stream2));
+      PROF_REC(ev, pf.e(ev, 2, fastSeg), h->stream2);
+      ++fastSeg;
+    }
   }
-  PROF_REC(ev, pf.e(ev, 0), s);
+  PROF_REC(ev, pf.e(ev, 0), cs);
+  if (cs != s) {  // the caller's stream also follows the whole chain (levels without cells)
+    HIP_TRY(hipEventRecord(h->evLvl[0], cs));
+    HIP_TRY(hipStreamWaitEvent(s, h->evLvl[0], 0));
+  }
+  if (perLevel) {
+    HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
+    if (ev) {
+      if (fastSeg) pf.segments(2, fastSeg);
+      else pf.not_run(2);
+    }
+  } else {
   PROF_REC(ev, pf.b(ev, 2), s);
   if (useBands)
     HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
@@ -736,6 +797,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                              h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(),
                              l0Side ? l0End : 0, P.ncells, B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
+  }
   // (level 0's octree on the side stream as well measured no gain: the octree's
   // time is its per-workgroup pass latency, not level 0's size)
   if (l0Side) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));
@@ -802,6 +864,40 @@ orb_status_t orb_device_count(int* n) {
   return c > 0 ? ORB_OK : ORB_ENODEV;
 }
 
+// Side-stream priorities (A/B knobs): ORB_STREAM2_PRIO = least | normal |
+// greatest for the FAST side stream; ORB_CHAIN_STREAM=1 runs the resize chain
+// on a third stream at the greatest priority.
+static int stream_prio(const char* var, const char* dflt) {
+  int least = 0, greatest = 0;
+  hipDeviceGetStreamPriorityRange(&least, &greatest);
+  const char* v = getenv(var);
+  const std::string m = v ? v : dflt;
+  if (getenv("ORB_AMD_DEBUG"))
+    fprintf(stderr, "[orb_amd] stream priorities least %d greatest %d, %s=%s\n", least, greatest,
+            var, m.c_str());
+  return m == "least" ? least : m == "greatest" ? greatest : 0;
+}
+static bool chain_stream() {
+  static const bool v = getenv("ORB_CHAIN_STREAM") && atoi(getenv("ORB_CHAIN_STREAM")) > 0;
+  return v;
+}
+static bool create_side_streams(orb_extractor* h) {
+  if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking,
+                                  stream_prio("ORB_STREAM2_PRIO", "normal")) != hipSuccess)
+    return false;
+  if (chain_stream() &&
+      hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking,
+                                  stream_prio("ORB_CHAIN_PRIO", "greatest")) != hipSuccess)
+    return false;
+  return true;
+}
+
+static bool create_level_events(orb_extractor* h) {
+  for (hipEvent_t& e : h->evLvl)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+  return true;
+}
+
 orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int ini_th_fast,
                                   int min_th_fast, int device, orb_extractor_t** out) {
   if (!out) return ORB_EINVAL;
@@ -824,24 +920,29 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   compute_tables(h);
   hipSetDevice(device);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+      !create_side_streams(h) ||
       hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evL0Fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evL0Join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->evBatch, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&h->evBatch, hipEventDisableTiming) != hipSuccess ||
+      !create_level_events(h)) {
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->stream2) hipStreamDestroy(h->stream2);
+    if (h->stream3) hipStreamDestroy(h->stream3);
     if (h->evFork) hipEventDestroy(h->evFork);
     if (h->evJoin) hipEventDestroy(h->evJoin);
     if (h->evL0Fork) hipEventDestroy(h->evL0Fork);
     if (h->evL0Join) hipEventDestroy(h->evL0Join);
     if (h->evBatch) hipEventDestroy(h->evBatch);
+    for (hipEvent_t e : h->evLvl)
+      if (e) hipEventDestroy(e);
     delete h;
     return ORB_EDEVICE;
   }
   h->ownStream = true;
   h->prof.nStages = 6;
+  h->prof.maxSeg[2] = ORB_MAX_LEVELS;  // FAST of levels >= 1: one launch per level
   const char* names[6] = {"k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree",
                           "k_orient_desc", "k_fast_cells_l0"};
   for (int i = 0; i < 6; ++i) {
@@ -875,11 +976,14 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
+  if (h->stream3) hipStreamDestroy(h->stream3);
   if (h->evFork) hipEventDestroy(h->evFork);
   if (h->evJoin) hipEventDestroy(h->evJoin);
   if (h->evL0Fork) hipEventDestroy(h->evL0Fork);
   if (h->evL0Join) hipEventDestroy(h->evL0Join);
   if (h->evBatch) hipEventDestroy(h->evBatch);
+  for (hipEvent_t e : h->evLvl)
+    if (e) hipEventDestroy(e);
   delete h;
 }
 
