@@ -10,12 +10,19 @@
 // ORBextractor's public/protected methods are exactly the reference's, so the
 // drop-ins compile against the unchanged reference headers plus the two
 // documented additions (marked INTEGRATION CHANGE).
+//
+// With ORB_RUN_HARNESS defined (tests/integration_run/harness.cc only) the
+// classes also carry the storage and test constructors of the runnable
+// harness; those #ifdef blocks are not part of the checked declarations.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
 
 #include <list>
 #include <map>
+#ifdef ORB_RUN_HARNESS
+#include <memory>
+#endif
 #include <mutex>
 #include <set>
 #include <utility>
@@ -60,6 +67,10 @@ class Mat {
   bool empty() const;
   int type() const;
   double dot(const Mat& m) const;
+#ifdef ORB_RUN_HARNESS
+  std::shared_ptr<unsigned char> mem;  // owner of data
+  int typ = 0;                         // CV_8U or CV_32F
+#endif
 };
 Mat operator*(const Mat& a, const Mat& b);
 Mat operator+(const Mat& a, const Mat& b);
@@ -70,11 +81,17 @@ class _InputArray {
   _InputArray(const Mat& m);
   Mat getMat() const;
   bool empty() const;
+#ifdef ORB_RUN_HARNESS
+  const Mat* m = nullptr;
+#endif
 };
 class _OutputArray {
  public:
   _OutputArray(Mat& m);
   void release() const;
+#ifdef ORB_RUN_HARNESS
+  Mat* m = nullptr;
+#endif
 };
 typedef const _InputArray& InputArray;
 }  // namespace cv
@@ -174,6 +191,14 @@ class KeyFrame {
   const int mnMinY;
   const int mnMaxX;
   const int mnMaxY;
+#ifdef ORB_RUN_HARNESS
+  KeyFrame(const Frame& F, const cv::Mat& Rcw, const cv::Mat& tcw, const cv::Mat& Ow,
+           const std::vector<float>& levelSigma2, const std::vector<float>& invLevelSigma2);
+  cv::Mat Rcw_, tcw_, Ow_;
+  std::vector<MapPoint*> mvpMapPoints_;
+  void ReplaceMapPointMatch(size_t idx, MapPoint* pMP);
+  void EraseMapPointMatch(size_t idx);
+#endif
 };
 
 class MapPoint {
@@ -199,6 +224,16 @@ class MapPoint {
   float mfMinDistance;
   float mfMaxDistance;
   std::mutex mMutexPos;
+#ifdef ORB_RUN_HARNESS
+ public:
+  MapPoint(const float* pos, const float* normal, float minDist, float maxDist,
+           const unsigned char* desc, int extraObservations, bool bad);
+  cv::Mat pos_, normal_, desc_;
+  std::map<KeyFrame*, size_t> obs_;
+  int extraObs_ = 0;  // observations by keyframes outside the scenario
+  bool bad_ = false;
+  int id_ = -1;       // scenario id (harness output)
+#endif
 };
 
 class ORBmatcher {
