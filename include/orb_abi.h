@@ -100,6 +100,22 @@ typedef struct orb_matcher orb_matcher_t;
 
 /* ---------------------------------------------------------------- extractor */
 
+/* Limits (the reference has none; these are where this build stops, each a
+ * status, never a silent change of results):
+ *   create: 0 <= nfeatures <= 60000, 1 <= nlevels <= 16, 1 < scale_factor <= 1.9
+ *     (ORB_EINVAL otherwise; every ORB-SLAM2 configuration uses 1.2).
+ *   extract: every pyramid level between 40 and 4095 px in each dimension
+ *     (keys pack x and y in 12 bits), FAST cells at most 64 x 64 interior
+ *     pixels: ORB_EINVAL from the call (and orb_extractor_capacity < 0).
+ *   DistributeOctTree (src/ORBextractor.cc:558-782): node tables hold
+ *     quota + 4 nodes per level (the reference's list never exceeds quota + 3,
+ *     or 4 x its root count after the first pass), at most 512 passes (distinct
+ *     keys separate in about 12; the final phase adds a few) and 2^24 created
+ *     nodes.  Exceeding any of them is not reachable with keys the FAST stage
+ *     emits; if it happened the image fails as a whole: orb_extractor_extract
+ *     returns ORB_EDEVICE and the batch form writes d_counts[i] = ORB_EDEVICE
+ *     (negative).  ORB_OCTREE_MAX_PASSES (environment, test hook) lowers the
+ *     pass bound to drive that path (tests/test_gpu_extractor.py). */
 orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels,
                                   int ini_th_fast, int min_th_fast, int device,
                                   orb_extractor_t** out);

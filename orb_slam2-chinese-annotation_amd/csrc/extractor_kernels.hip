@@ -1270,7 +1270,8 @@ __global__ __launch_bounds__(512) void k_octree(
     OrbPlanDesc plan, const int32_t* __restrict__ cellCount, const uint32_t* __restrict__ cellKeys,
     uint32_t* __restrict__ gKeys, uint16_t* __restrict__ gNid, int ldsKeyCap, int nodeCapMax,
     int maxCellsPerLevel, uint32_t* __restrict__ outKeys, int32_t* __restrict__ outCount,
-    int32_t* __restrict__ errFlag, int levelBeg) {
+    int32_t* __restrict__ errFlag, int levelBeg, int maxPasses, unsigned char* __restrict__ gNodes,
+    long long nodeStride) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int tmp[52];
   __shared__ int sh[8];
@@ -1282,8 +1283,11 @@ __global__ __launch_bounds__(512) void k_octree(
   const int NC = nodeCapMax;
   int n2 = 1;
   while (n2 < NC) n2 <<= 1;
-  // ---- LDS carve (all offsets multiples of 16)
-  unsigned char* p = smem;
+  // ---- node tables: LDS carve (all offsets multiples of 16), or, for
+  // feature counts whose tables outgrow a CU's LDS, the same carve in a global
+  // scratch slice per (image, level) (one workgroup's barriers order it; only
+  // the keys stay in LDS then)
+  unsigned char* p = gNodes ? gNodes + ((long long)img * gridDim.y + blockIdx.y) * nodeStride : smem;
   unsigned long long* sortBuf = (unsigned long long*)p; p += (size_t)n2 * 8;
   OctNode* A = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
   OctNode* B = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
@@ -1293,6 +1297,7 @@ __global__ __launch_bounds__(512) void k_octree(
   int* g2 = (int*)p; p += (size_t)NC * 4;
   int* rk = (int*)p; p += (size_t)NC * 4;
   int* cellBase = (int*)p; p += (size_t)((maxCellsPerLevel + 3) & ~3) * 4;
+  if (gNodes) p = smem;
   uint32_t* Klds = (uint32_t*)p; p += (size_t)ldsKeyCap * 4;
   uint16_t* Nlds = (uint16_t*)p;
 
@@ -1390,7 +1395,7 @@ __global__ __launch_bounds__(512) void k_octree(
   bool finalPhase = false;
   int pass = 0;
   __syncthreads();
-  for (; pass < OCT_MAX_PASSES; ++pass) {
+  for (; pass < maxPasses; ++pass) {
     const int prev = alive;
     if (!finalPhase) {
       // ================= regular pass: divide every node with > 1 key (:625-684)
@@ -1567,7 +1572,7 @@ __global__ __launch_bounds__(512) void k_octree(
       if (alive >= N || alive == prev) break;  // :753-754
     }
   }
-  if (pass >= OCT_MAX_PASSES && t == 0) atomicOr(errFlag, 4);
+  if (pass >= maxPasses && t == 0) atomicOr(errFlag, 4);
   // ---- retain the best key of each node (:760-779)
   uint32_t* best = (uint32_t*)g0;
   for (int a = t; a < alive; a += T) best[a] = 0u;
@@ -2415,9 +2420,11 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
                         int nodeCapMax, int maxCellsPerLevel, uint32_t* outKeys,
                         int32_t* outCount, int32_t* errFlag, int levelBeg, int levelEnd, int nimg,
-                        hipStream_t s) {
+                        uint8_t* gNodes, long long nodeStride, hipStream_t s) {
   if (levelEnd <= levelBeg || nimg <= 0) return hipSuccess;
-  const size_t lds = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, ldsKeyCap);
+  // global node tables (gNodes): the LDS holds the keys only
+  const size_t lds = gNodes ? (size_t)ldsKeyCap * 6
+                            : orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, ldsKeyCap);
   // register-resident keys for a few frames per call (one workgroup per level)
   const bool reg = nimg <= 16;
   const void* fn = reg ? (const void*)k_octree<true> : (const void*)k_octree<false>;
@@ -2425,14 +2432,22 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
+  // The pass bound is never reached with the reference's own bounds (a pass
+  // halves every divided node; distinct keys separate in ~12 passes, the
+  // final phase adds a few).  ORB_OCTREE_MAX_PASSES lowers it: a test hook
+  // that drives the failed-image path (negative count, ORB_EDEVICE).
+  static const int maxPasses = getenv("ORB_OCTREE_MAX_PASSES")
+                                   ? std::max(1, std::min(OCT_MAX_PASSES, atoi(getenv("ORB_OCTREE_MAX_PASSES"))))
+                                   : OCT_MAX_PASSES;
   dim3 grid(nimg, levelEnd - levelBeg), block(512);
   if (reg)
     hipLaunchKernelGGL(k_octree<true>, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys, gNid,
-                       ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, levelBeg);
+                       ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, levelBeg,
+                       maxPasses, gNodes, nodeStride);
   else
     hipLaunchKernelGGL(k_octree<false>, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,
                        gNid, ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag,
-                       levelBeg);
+                       levelBeg, maxPasses, gNodes, nodeStride);
   return hipGetLastError();
 }
 

@@ -43,7 +43,8 @@ size_t orb_k_octree_lds(int nodeCapMax, int maxCellsPerLevel, int ldsKeyCap);
 hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                         const uint32_t* cellKeys, uint32_t* gKeys, uint16_t* gNid, int ldsKeyCap,
                         int nodeCapMax, int maxCellsPerLevel, uint32_t* outKeys,
-                        int32_t* outCount, int32_t* errFlag, int levelBeg, int levelEnd, int nimg, hipStream_t s);
+                        int32_t* outCount, int32_t* errFlag, int levelBeg, int levelEnd, int nimg,
+                        uint8_t* gNodes, long long nodeStride, hipStream_t s);
 hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0Stride,
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
@@ -369,6 +370,8 @@ struct orb_extractor {
   // batch scratch
   int batchCap = 0;
   DevBuf dArena, dBlur, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
+  DevBuf dOctNodes;            // octree node tables in global memory (large nfeatures)
+  long long octNodeBytes = 0;  // per (image, level) slice; 0: node tables in LDS
   // single-image API scratch
   // single-image API: dImg (the image at a 64-B row pitch) and dOne = [count,
   // pad x3 | cap keypoints | cap x 32 descriptors], mirrored by the pinned
@@ -622,9 +625,13 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   const size_t nodeBytes = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, 0);
   const char* lk = getenv("ORB_OCTREE_LDS_KB");
   const size_t budget = (size_t)(lk ? std::max(16, std::min(150, atoi(lk))) : 52) * 1024;
-  int ldsKeyCap = nodeBytes < budget ? (int)((budget - nodeBytes) / 6) : 0;
+  // node tables beyond 128 KiB (nfeatures above ~7,500 at 1.2 / 8 levels) go
+  // to a global scratch slice per (image, level); the LDS then holds keys only
+  const bool octGlobal = nodeBytes > 128 * 1024;
+  const size_t ldsNodes = octGlobal ? 0 : nodeBytes;
+  int ldsKeyCap = ldsNodes < budget ? (int)((budget - ldsNodes) / 6) : 0;
   ldsKeyCap &= ~7;
-  if (nodeBytes + (size_t)ldsKeyCap * 6 > 160 * 1024) return ORB_EINVAL;
+  if (ldsNodes + (size_t)ldsKeyCap * 6 > 160 * 1024) return ORB_EINVAL;
 
   hipSetDevice(h->device);
   orb_status_t st = h->dCells.ensure(cells.size() * sizeof(OrbCellDesc));
@@ -652,6 +659,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   h->maxCellsPerLevel = maxCellsPerLevel;
   h->nodeCapMax = nodeCapMax;
   h->ldsKeyCap = ldsKeyCap;
+  h->octNodeBytes = octGlobal ? (long long)((nodeBytes + 255) & ~(size_t)255) : 0;
   h->planW = W;
   h->planH = H;
   h->batchCap = 0;  // scratch layout depends on the plan
@@ -682,6 +690,9 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
   if ((st = h->dOutKeys.ensure((size_t)B * P.slotsPerImage * 4))) return st;
   if ((st = h->dOutCount.ensure((size_t)B * P.nlevels * 4))) return st;
   if ((st = h->dErr.ensure((size_t)B * 4))) return st;
+  if (h->octNodeBytes &&
+      (st = h->dOctNodes.ensure((size_t)B * P.nlevels * (size_t)h->octNodeBytes)))
+    return st;
   h->batchCap = B;
   return ORB_OK;
 }
@@ -818,7 +829,8 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                        h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
-                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, P.nlevels, B, s));
+                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, P.nlevels, B,
+                       h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr, h->octNodeBytes, s));
   PROF_REC(ev, pf.e(ev, 3), s);
   if (split && s2 != s) HIP_TRY(hipStreamWaitEvent(s, h->evJoin, 0));
   PROF_REC(ev, pf.b(ev, 4), s);
@@ -965,7 +977,7 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   if (!h) return;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  DevBuf* bufs[] = {&h->dCells, &h->dRtab, &h->dTiles, &h->dBlur, &h->dArena, &h->dCellKeys, &h->dCellCount,
+  DevBuf* bufs[] = {&h->dCells, &h->dRtab, &h->dTiles, &h->dBlur, &h->dArena, &h->dCellKeys, &h->dCellCount, &h->dOctNodes,
                     &h->dGKeys, &h->dGNid, &h->dOutKeys, &h->dOutCount, &h->dErr,
                     &h->dImg, &h->dOne};
   for (DevBuf* b : bufs) b->release();
@@ -1080,7 +1092,7 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     const std::vector<const void*> key = {
         h->dImg.p, h->dOne.p, h->hImg.p, h->hOut.p, h->dArena.p, h->dCellKeys.p, h->dGKeys.p,
         h->dGNid.p, h->dCellCount.p, h->dOutKeys.p, h->dOutCount.p, h->dErr.p, h->dRtab.p,
-        h->dBands.p, h->dCells.p, h->dBlur.p, h->dTiles.p, (const void*)(intptr_t)width,
+        h->dBands.p, h->dCells.p, h->dBlur.p, h->dTiles.p, h->dOctNodes.p, (const void*)(intptr_t)width,
         (const void*)(intptr_t)height, (const void*)(intptr_t)cap};
     if (!h->oneExec || key != h->oneKey) {
       if (h->oneExec) hipGraphExecDestroy(h->oneExec);

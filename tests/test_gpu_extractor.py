@@ -330,3 +330,71 @@ def test_single_batch_single_keeps_level0(gpu, oracle):
         assert np.array_equal(pyr[l], ref[l]), f"level {l}"
     kr, dr, _ = oracle.extract(a, 1000, 1.2, 8, 20, 7)
     assert k1.tobytes() == kr.tobytes() and d1.tobytes() == dr.tobytes()
+
+
+def test_octree_12k_features_1080p_noise(gpu, oracle):
+    """The largest DistributeOctTree the configurations reach and then some:
+    1920x1080 uniform noise (FAST candidates everywhere) with 12,000 features,
+    on the GPU (single frame and a batch of two), bit-exact against the oracle."""
+    import torch
+    rng = np.random.default_rng(12)
+    w, h, nf = 1920, 1080, 12000
+    img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    kr, dr, per = oracle.extract(img, nf)
+    assert len(kr) >= nf - 8
+    ext = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    k, d = ext(img)
+    assert k.tobytes() == kr.tobytes() and d.tobytes() == dr.tobytes()
+    cap = ext.capacity(w, h)
+    imgs = torch.from_numpy(np.stack([img, img])).cuda()
+    kb = torch.zeros((2, cap, 7), dtype=torch.int32, device="cuda")
+    db = torch.zeros((2, cap, 32), dtype=torch.uint8, device="cuda")
+    nb = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ext.extract_batch(imgs.data_ptr(), 2, w, h, w, w * h, kb.data_ptr(), db.data_ptr(), cap,
+                      nb.data_ptr())
+    torch.cuda.synchronize()
+    for i in range(2):
+        n = int(nb[i])
+        assert n == len(kr)
+        assert kb[i, :n].cpu().numpy().tobytes() == kr.tobytes()
+        assert db[i, :n].cpu().numpy().tobytes() == dr.tobytes()
+
+
+def test_octree_pass_bound_fails_cleanly(gpu):
+    """An octree that hits its pass bound fails the image as a whole: the
+    single-frame call raises ORB_EDEVICE, the batch form reports a negative
+    count, and the handle keeps working afterwards (the bound lowered through
+    the ORB_OCTREE_MAX_PASSES test hook, in a child process)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    code = f"""
+import sys, numpy as np, torch
+sys.path.insert(0, {str(root)!r}); sys.path.insert(0, {str(root / 'tests')!r})
+from conftest import load_pkg
+orb = load_pkg()
+img = orb.synth_image(1, 0, 640, 480)
+ext = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+try:
+    ext(img)
+    print('single: no error')
+except orb.OrbError as e:
+    print('single:', e.status)
+cap = ext.capacity(640, 480)
+imgs = torch.from_numpy(np.stack([img] * 4)).cuda()
+k = torch.zeros((4, cap, 7), dtype=torch.int32, device='cuda')
+d = torch.zeros((4, cap, 32), dtype=torch.uint8, device='cuda')
+n = torch.zeros(4, dtype=torch.int32, device='cuda')
+ext.extract_batch(imgs.data_ptr(), 4, 640, 480, 640, 640 * 480, k.data_ptr(), d.data_ptr(), cap, n.data_ptr())
+torch.cuda.synchronize()
+print('batch:', n.tolist())
+"""
+    import os
+    env = dict(os.environ, ORB_OCTREE_MAX_PASSES="2")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = dict(l.split(": ", 1) for l in r.stdout.strip().splitlines())
+    assert out["single"] == str(gpu.ORB_EDEVICE)
+    assert out["batch"] == str([gpu.ORB_EDEVICE] * 4)
