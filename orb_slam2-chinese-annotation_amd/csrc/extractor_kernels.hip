@@ -1265,7 +1265,7 @@ __device__ void block_bitonic_desc(unsigned long long* v, int n2) {
 #define OCT_RANK_MAX 512
 #define OCT_REG_KEYS 8  // keys per thread held in registers (n <= 8 x 512), small batches  // final-phase candidates ranked by counting (multiple of the 512 threads)
 
-template <bool REG>
+template <bool REG, bool GNODES>
 __global__ __launch_bounds__(512) void k_octree(
     OrbPlanDesc plan, const int32_t* __restrict__ cellCount, const uint32_t* __restrict__ cellKeys,
     uint32_t* __restrict__ gKeys, uint16_t* __restrict__ gNid, int ldsKeyCap, int nodeCapMax,
@@ -1287,7 +1287,9 @@ __global__ __launch_bounds__(512) void k_octree(
   // feature counts whose tables outgrow a CU's LDS, the same carve in a global
   // scratch slice per (image, level) (one workgroup's barriers order it; only
   // the keys stay in LDS then)
-  unsigned char* p = gNodes ? gNodes + ((long long)img * gridDim.y + blockIdx.y) * nodeStride : smem;
+  // (GNODES is a template parameter so that the LDS build keeps ds_*
+  // instructions: a pointer that may be either would compile to flat ones)
+  unsigned char* p = GNODES ? gNodes + ((long long)img * gridDim.y + blockIdx.y) * nodeStride : smem;
   unsigned long long* sortBuf = (unsigned long long*)p; p += (size_t)n2 * 8;
   OctNode* A = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
   OctNode* B = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
@@ -1297,7 +1299,7 @@ __global__ __launch_bounds__(512) void k_octree(
   int* g2 = (int*)p; p += (size_t)NC * 4;
   int* rk = (int*)p; p += (size_t)NC * 4;
   int* cellBase = (int*)p; p += (size_t)((maxCellsPerLevel + 3) & ~3) * 4;
-  if (gNodes) p = smem;
+  if (GNODES) p = smem;
   uint32_t* Klds = (uint32_t*)p; p += (size_t)ldsKeyCap * 4;
   uint16_t* Nlds = (uint16_t*)p;
 
@@ -2427,7 +2429,9 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                             : orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, ldsKeyCap);
   // register-resident keys for a few frames per call (one workgroup per level)
   const bool reg = nimg <= 16;
-  const void* fn = reg ? (const void*)k_octree<true> : (const void*)k_octree<false>;
+  const bool gn = gNodes != nullptr;
+  const void* fn = reg ? (gn ? (const void*)k_octree<true, true> : (const void*)k_octree<true, false>)
+                       : (gn ? (const void*)k_octree<false, true> : (const void*)k_octree<false, false>);
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -2440,14 +2444,15 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
                                    ? std::max(1, std::min(OCT_MAX_PASSES, atoi(getenv("ORB_OCTREE_MAX_PASSES"))))
                                    : OCT_MAX_PASSES;
   dim3 grid(nimg, levelEnd - levelBeg), block(512);
-  if (reg)
-    hipLaunchKernelGGL(k_octree<true>, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys, gNid,
-                       ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, levelBeg,
-                       maxPasses, gNodes, nodeStride);
-  else
-    hipLaunchKernelGGL(k_octree<false>, grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,
-                       gNid, ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag,
-                       levelBeg, maxPasses, gNodes, nodeStride);
+#define ORB_OCTREE_LAUNCH(R, G)                                                                 \
+  hipLaunchKernelGGL((k_octree<R, G>), grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,  \
+                     gNid, ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, \
+                     levelBeg, maxPasses, gNodes, nodeStride)
+  if (reg && gn) ORB_OCTREE_LAUNCH(true, true);
+  else if (reg) ORB_OCTREE_LAUNCH(true, false);
+  else if (gn) ORB_OCTREE_LAUNCH(false, true);
+  else ORB_OCTREE_LAUNCH(false, false);
+#undef ORB_OCTREE_LAUNCH
   return hipGetLastError();
 }
 

@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--no-cpu --steps 2 --warmup 1 $*"
+ARGS="--no-cpu --steps 2 --warmup 1 --host-frames 0 $*"
 ORB_FAST_L0_INLINE=1 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH GRBM_GUI_ACTIVE \
   -d "$O/pmcA_$TAG" -o run --output-format csv -- python3 "$R/bench.py" $ARGS > "$O/pmcA_$TAG.log" 2>&1
 ORB_FAST_L0_INLINE=1 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU \

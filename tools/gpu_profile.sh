@@ -7,20 +7,20 @@
 #   per dispatch and the level-0 split changes no instruction or byte counts).
 # Usage: tools/gpu_profile.sh <tag>
 set -eo pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd "$R"
 timeout -k 10 400 python bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err"
 cd /tmp && export TMPDIR=/tmp
-SMALL="--no-cpu --no-secondary --frames 1024 --steps 10 --warmup 1"
+SMALL="--no-cpu --no-secondary --frames 1024 --steps 10 --warmup 1 --host-frames 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$TAG" -o run --output-format csv \
   -- python3 "$R/bench.py" $SMALL > "$O/prof_$TAG.json" 2> "$O/prof_$TAG.err"
 ORB_FAST_L0_INLINE=1 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$O/pmcf_$TAG" -o run --output-format csv \
-  -- python3 "$R/bench.py" --no-cpu --no-secondary --frames 512 --steps 2 --warmup 1 > "$O/pmcf_$TAG.json" 2> "$O/pmcf_$TAG.err"
+  -- python3 "$R/bench.py" --no-cpu --no-secondary --frames 512 --steps 2 --warmup 1 --host-frames 0 > "$O/pmcf_$TAG.json" 2> "$O/pmcf_$TAG.err"
 ORB_FAST_L0_INLINE=1 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$O/pmcw_$TAG" -o run --output-format csv \
-  -- python3 "$R/bench.py" --no-cpu --no-secondary --frames 512 --steps 2 --warmup 1 > "$O/pmcw_$TAG.json" 2> "$O/pmcw_$TAG.err"
+  -- python3 "$R/bench.py" --no-cpu --no-secondary --frames 512 --steps 2 --warmup 1 --host-frames 0 > "$O/pmcw_$TAG.json" 2> "$O/pmcw_$TAG.err"
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib_$TAG" -o run --output-format csv \
   -- "$R/tools/probe/fetch_calib" > "$O/calib_$TAG.log" 2>&1
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d "$O/calibw_$TAG" -o run --output-format csv \

@@ -27,16 +27,21 @@ with open(P / f"{tag}_pmc_table.txt", "w") as f:
                     str(P / f"{tag}_pmc.json"), str(O / f"pmcA_{tag}"), str(O / f"pmcB_{tag}")],
                    check=True, stdout=f)
 shutil.copy(O / f"prof_{tag}" / "run_kernel_stats.csv", P / f"{tag}_kernel_stats.csv")
-shutil.copy(O / f"tests_{tag}.log", P / f"{tag}_gpu_tests.log")
+if (O / f"tests_{tag}.log").exists():
+    shutil.copy(O / f"tests_{tag}.log", P / f"{tag}_gpu_tests.log")
 
 b = json.loads((O / f"bench_{tag}.json").read_text())
 r = b["roofline"]
 r["traffic"], _ = bench.measured_traffic(r["kernel"], 512)
-r["valu_issue"] = bench.valu_issue(r["kernel"], 512, r["ms_per_launch"])
+vi = bench.valu_issue(r["kernel"], 512, r["ms_per_launch"])
+if vi is not None:  # re-derived from the new PMC files
+    rate = vi["valu_instr_per_launch"] / (r["ms_per_launch"] * 1e-3) / 1e9
+    r["valu"] = dict(r.get("valu", {}), achieved=rate, frac=rate / bench.VALU_PEAK_G,
+                     issue_bound=vi)
 (P / f"{tag}_bench.json").write_text(json.dumps(b))
 print(f"value {b['value']:.0f} frames/s, {b['ms_per_step']:.3f} ms/step, cpu {b['cpu_baseline']['value']:.1f}")
 print(f"roofline {r['kernel']} {r['achieved']:.0f} GB/s frac {r['frac']:.4f} "
-      f"{r['ms_per_launch']:.3f} ms/launch valu {r['valu_issue']['frac_range']}")
+      f"{r['ms_per_launch']:.3f} ms/launch valu frac {r.get('valu', {}).get('frac')}")
 
 agg = {}
 for x in csv.DictReader(open(P / f"{tag}_kernel_stats.csv")):
