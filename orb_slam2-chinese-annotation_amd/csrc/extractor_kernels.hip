@@ -2026,6 +2026,9 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // exclusive prefix (output offsets): loaded once, read by v_readlane
   const int cntv = lane < plan.nlevels ? cnts[lane] : 0;
   const int cntx = wave_incl_scan(cntv) - cntv;
+  // each level's first output slot, lane l = level l (ascending): a pair's
+  // level is a ballot count instead of a loop of dependent scalar loads
+  const int offv = lane < plan.nlevels ? plan.lv[lane].outOff : INT_MAX;
   uint32_t (*rsp)[DESC_RS_DW] = sm[w].rsp[half];
   // lane hl < 22 holds rows 2 hl and 2 hl + 1 (row 43 only feeds a zero weight)
   const bool second = hl < DESC_RS_PAIRS;
@@ -2041,9 +2044,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     P.valid = false;
     const int slot0 = 2 * (pairBase + 4 * j);
     if (slot0 >= plan.slotsPerImage) return P;
-    int l = 0;
-    while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot0) ++l;
-    const int i0 = slot0 - plan.lv[l].outOff, nl = __builtin_amdgcn_readlane(cntv, l);
+    const int l = __builtin_amdgcn_readfirstlane(__popcll(__ballot(offv <= slot0)) - 1);
+    const int i0 = slot0 - __builtin_amdgcn_readlane(offv, l), nl = __builtin_amdgcn_readlane(cntv, l);
     if (i0 >= nl) return P;
     P.valid = true;
     P.l = l;

@@ -101,7 +101,8 @@ def c2(args, orb, oracle, torch):
     k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
     de = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
     n = torch.zeros(B, dtype=torch.int32, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
+    # an explicit stream: a NULL stream would mean the handle's own stream
+    s = torch.cuda.Stream().cuda_stream
 
     def step():
         ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
@@ -122,46 +123,24 @@ def c2(args, orb, oracle, torch):
 
 
 def c3(args, orb, oracle, torch):
+    """bench.c3_workload (the driver line's C3 key, same inputs and schedule)
+    plus the oracle check of pair 0 and the oracle's CPU rate."""
     import scenarios
 
-    W, H, P, NF = 1241, 376, args.batch // 2, 2000
-    L = orb.ORBextractor(NF, 1.2, 8, 20, 7)
-    R = orb.ORBextractor(NF, 1.2, 8, 20, 7)
-    cap = L.capacity(W, H)
-    il = np.stack([orb.synth_image(SEED + p, 0, W, H, 0) for p in range(P)])
-    ir = np.stack([orb.synth_image(SEED + p, 0, W, H, 1) for p in range(P)])
-    dl, dr = torch.from_numpy(il).cuda(), torch.from_numpy(ir).cuda()
-    out = {}
-    for name in ("l", "r"):
-        out[name] = (torch.zeros((P, cap, 7), dtype=torch.int32, device="cuda"),
-                     torch.zeros((P, cap, 32), dtype=torch.uint8, device="cuda"),
-                     torch.zeros(P, dtype=torch.int32, device="cuda"))
-    ur = torch.zeros((P, cap), dtype=torch.float32, device="cuda")
-    dp = torch.zeros((P, cap), dtype=torch.float32, device="cuda")
-    sad = torch.zeros((P, cap), dtype=torch.int32, device="cuda")
-    m = orb.ORBmatcher()
-    s = torch.cuda.current_stream().cuda_stream
-    (kl, dsl, nl), (kr, dsr, nr) = out["l"], out["r"]
-
-    def step():
-        L.extract_batch(dl.data_ptr(), P, W, H, W, W * H, kl.data_ptr(), dsl.data_ptr(), cap,
-                        nl.data_ptr(), s)
-        R.extract_batch(dr.data_ptr(), P, W, H, W, W * H, kr.data_ptr(), dsr.data_ptr(), cap,
-                        nr.data_ptr(), s)
-        m.stereo_match_batch(P, L, R, kl.data_ptr(), dsl.data_ptr(), nl.data_ptr(), kr.data_ptr(),
-                             dsr.data_ptr(), nr.data_ptr(), cap, scenarios.BF, scenarios.FX,
-                             ur.data_ptr(), dp.data_ptr(), sad.data_ptr(), s)
-
-    sec = timed(step, args.steps, 2, torch)
+    dev = torch.device("cuda:0")
+    r, st = bench.c3_workload(orb, torch, dev, 16, steps=max(args.steps, 40), warmup=5,
+                              pairs=args.batch // 2)
+    il, ir, s0 = st["il"], st["ir"], st["set0"]
+    W, H, NF = 1241, 376, 2000
     p = oracle.params(NF)
     klh, dlh, _ = oracle.extract(il[0], NF)
     krh, drh, _ = oracle.extract(ir[0], NF)
     ur_ref, dp_ref = oracle.stereo_match(klh, dlh, p["scale"], krh, drh, oracle.pyramid(il[0]),
                                          oracle.pyramid(ir[0]), p["inv_scale"], scenarios.BF,
                                          scenarios.FX, W, H)
-    n0 = int(nl[0].item())
-    exact = n0 == len(klh) and ur[0, :n0].cpu().numpy().tobytes() == ur_ref.tobytes() and \
-        dp[0, :n0].cpu().numpy().tobytes() == dp_ref.tobytes()
+    n0 = int(s0["nl"][0].item())
+    exact = n0 == len(klh) and s0["ur"][0, :n0].cpu().numpy().tobytes() == ur_ref.tobytes() and \
+        s0["dp"][0, :n0].cpu().numpy().tobytes() == dp_ref.tobytes()
 
     def cpu_pair(i):
         a, da, _ = oracle.extract(il[i], NF)
@@ -169,14 +148,12 @@ def c3(args, orb, oracle, torch):
         oracle.stereo_match(a, da, p["scale"], b, db, oracle.pyramid(il[i]), oracle.pyramid(ir[i]),
                             p["inv_scale"], scenarios.BF, scenarios.FX, W, H)
 
-    cpu = cpu_rate(cpu_pair, min(P, 4), args.cpu_seconds, 1)
-    return {"config": "C3", "workload": f"1241x376 stereo pairs, 2000 feat/img, extraction x2 + "
-            f"ComputeStereoMatches, {P} pairs per step", "unit": "pairs/s", "value": P / sec,
-            "ms_per_step": sec * 1e3, "bit_exact_pair_0": bool(exact), "cpu_1_thread": cpu}
+    cpu = cpu_rate(cpu_pair, 4, args.cpu_seconds, 1)
+    return dict(config="C3", bit_exact_pair_0=bool(exact), cpu_1_thread=cpu, **r)
 
 
 def c5(args, orb, oracle, torch):
-    return proj_config(args, orb, oracle, torch, "C5", 1920, 1080, 4000, 50000, 16, 5)
+    return proj_config(args, orb, oracle, torch, "C5", 1920, 1080, 4000, 50000, 16, bench.C5_SEED)
 
 
 def c4m(args, orb, oracle, torch):
@@ -185,58 +162,18 @@ def c4m(args, orb, oracle, torch):
 
 
 def proj_config(args, orb, oracle, torch, name, W, H, NF, M, B, seed):
-    ext = orb.ORBextractor(NF, 1.2, 8, 20, 7)
-    scale = np.float32(ext.GetScaleFactors())
-    cap = ext.capacity(W, H)
-    imgs = np.stack([orb.synth_image(seed, f, W, H) for f in range(B)])
-    d = torch.from_numpy(imgs).cuda()
-    k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
-    de = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
-    n = torch.zeros(B, dtype=torch.int32, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
-    ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
-                      n.data_ptr(), s)
-    torch.cuda.synchronize()
-    kh = k.cpu().numpy().view(orb.KEYPOINT_DTYPE).reshape(B, cap)
-    dh, nh = de.cpu().numpy(), n.cpu().numpy()
-    mps = np.zeros((B, M), orb.MP_TRACK_DTYPE)
-    mpd = np.zeros((B, M, 32), np.uint8)
-    lk = np.zeros((B, cap), np.uint8)
-    for i in range(B):
-        a, b_, c_ = orb.synth_local_map(seed + i, kh[i, :nh[i]], dh[i, :nh[i]], M, W, H)
-        mps[i], mpd[i], lk[i, :nh[i]] = a, b_, c_
-    d_mps = torch.from_numpy(mps.view(np.uint8).reshape(B, -1)).cuda()
-    d_mpd = torch.from_numpy(mpd).cuda()
-    d_lk = torch.from_numpy(lk).cuda()
-    d_nm = torch.full((B,), M, dtype=torch.int32, device="cuda")
-    d_km = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
-    d_nmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
-    mt = orb.ORBmatcher(0.8)
-
-    def match():
-        mt.search_by_projection_batch(B, k.data_ptr(), de.data_ptr(), n.data_ptr(), d_lk.data_ptr(),
-                                      cap, d_mps.data_ptr(), d_mpd.data_ptr(), d_nm.data_ptr(), M,
-                                      W, H, scale, 1.0, d_km.data_ptr(), d_nmatch.data_ptr(), s)
-
-    def step():
-        ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
-                          n.data_ptr(), s)
-        match()
-
-    sec = timed(step, args.steps, 2, torch)
-    msec = timed(match, args.steps, 2, torch)
-    n_kp = float(n.float().mean().item())
-    b_lm = 60 * M + 48 * n_kp + 24576  # SURVEY §8(d) B_lm
-    n0 = int(nh[0])
-    nr, kmr = oracle.match_projection_local(kh[0, :n0], dh[0, :n0], scale, W, H, mps[0], mpd[0],
-                                            1.0, 0.8, lk[0, :n0])
-    exact = int(d_nmatch[0].item()) == nr and np.array_equal(d_km[0, :n0].cpu().numpy(), kmr)
-    return {"config": name, "workload": f"{W}x{H}, {NF} feat, SearchByProjection vs {M:,} "
-            f"map points, {B} problems per launch", "unit": "problems/s", "value": B / sec,
-            "ms_per_step": sec * 1e3, "match_only_problems_per_s": B / msec,
-            "match_only_alg_GBps": b_lm * B / msec / 1e9,
-            "match_only_frac_of_8TBps": b_lm * B / msec / 8e12,
-            "mean_keypoints": n_kp, "bit_exact_problem_0": bool(exact)}
+    """bench.proj_workload (the driver line's C5 key for C5) plus the oracle
+    check of problem 0."""
+    dev = torch.device("cuda:0")
+    # ~0.1 s timed regions (bench.secondary_configs): short ones are noisy
+    steps = max(args.steps, 200 if B <= 64 else 40)
+    r, st = bench.proj_workload(orb, torch, dev, 16, W, H, NF, M, B, seed, steps=steps, warmup=10)
+    n0 = int(st["nh"][0])
+    s0 = st["set0"]
+    nr, kmr = oracle.match_projection_local(st["kh"][0, :n0], st["dh"][0, :n0], st["scale"], W, H,
+                                            st["mps"][0], st["mpd"][0], 1.0, 0.8, st["lk"][0, :n0])
+    exact = int(s0["nm"][0].item()) == nr and np.array_equal(s0["km"][0, :n0].cpu().numpy(), kmr)
+    return dict(config=name, bit_exact_problem_0=bool(exact), **r)
 
 
 def f1(args, orb, oracle, torch):
