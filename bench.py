@@ -658,14 +658,15 @@ def main():
             continue  # stage not run (k_blur_levels: split A/B mode only)
         kern[name] = (ms, n)
         ext_kern.append(name)
-    # level 0's FAST runs as its own launch on the side stream (beside the
-    # resize chain): one pass of a kernel = both launches (summed durations, counted once per call)
+    # FAST of level 0 and levels 1-2 runs as launches of its own on the side
+    # stream (beside the resize chain): one pass of the kernel = all its launches
+    # (summed durations, counted once per call)
     side_ms = {}
-    for name in [k for k in ext_kern if k.endswith("_l0")]:
+    for name in [k for k in ext_kern if k.endswith("_side")]:
         ms0, _ = kern.pop(name)
         ext_kern.remove(name)
         side_ms[name] = ms0 / (args.steps * NB)
-        base = name[:-3]
+        base = name[:-5]
         if base in kern:
             ms1, n1 = kern[base]
             kern[base] = (ms0 + ms1, n1)
@@ -753,7 +754,7 @@ def main():
         "kernels_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kern.items()},
         "extraction_kernels_ms_per_launch": sum(kern[k][0] for k in ext_kern) / (args.steps * NB),
         "extraction_call_ms_per_launch": call_ms / max(call_n, 1),
-        "level0_side_stream_ms_per_launch": side_ms,
+        "fast_side_stream_ms_per_launch": side_ms,
         "host_input": host,
     }
     if rank == 0 and world == 1 and not args.no_secondary:

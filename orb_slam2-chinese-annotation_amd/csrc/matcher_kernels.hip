@@ -196,6 +196,9 @@ __global__ __launch_bounds__(64) void k_grid_build_wave(const orb_keypoint_t* __
 #ifndef PROJ_QB
 #define PROJ_QB 4  // window candidates scored per batch of descriptor loads
 #endif
+#ifndef PROJ_XCD
+#define PROJ_XCD 1  // XCD-contiguous workgroup order (A/B knob)
+#endif
 #ifndef PROJ_WG
 #define PROJ_WG 512  // map points per workgroup (grid staged once per workgroup; swept 256-1024)
 #endif
@@ -210,11 +213,19 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
   __shared__ int sCS[GRID_CELLS + 1];
   extern __shared__ __attribute__((aligned(16))) uint4 sKp[];  // min(kpStride, PROJ_STAGE)
   __shared__ float sScale[ORB_MAX_LEVELS];
-  const int p = blockIdx.y;
+  // XCD-contiguous order: a problem's workgroups share one L2, which then
+  // serves the staged grid and the frame's descriptors to all of them
+  int bx, p;
+#if PROJ_XCD
+  xcd_swizzle(bx, p);
+#else
+  bx = blockIdx.x;
+  p = blockIdx.y;
+#endif
   const int tid = threadIdx.x;
-  const int m = blockIdx.x * blockDim.x + tid;
+  const int m = bx * blockDim.x + tid;
   const int M = nmps[p], N = nkeys[p];
-  if ((int)(blockIdx.x * blockDim.x) >= M) return;  // whole workgroup idle (uniform)
+  if ((int)(bx * blockDim.x) >= M) return;  // whole workgroup idle (uniform)
   const orb_keypoint_t* K = keys + (size_t)p * kpStride;
   const uint8_t* D = desc + (size_t)p * kpStride * 32;
   const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;

@@ -237,3 +237,27 @@ __device__ __forceinline__ uint32_t pack_key(int x, int y, int s) {
 __device__ __forceinline__ int key_x(uint32_t k) { return (int)(k & 0xFFFu); }
 __device__ __forceinline__ int key_y(uint32_t k) { return (int)((k >> 12) & 0xFFFu); }
 __device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 24); }
+
+// Workgroups are dispatched round-robin over the 8 XCDs (linear id L runs on
+// XCD L % 8), and each XCD has its own L2.  With a (work item, image) grid that
+// spreads one image's neighbouring cells / keypoint runs over all eight L2s, so
+// every XCD fetches every image.  xcd_swizzle remaps the linear id so that XCD
+// k runs one contiguous range of (blockIdx.x, blockIdx.y): the workgroups in
+// flight on an XCD cover a couple of images, whose rows its L2 then serves.
+#ifndef ORB_XCD_SWIZZLE
+#define ORB_XCD_SWIZZLE 1
+#endif
+__device__ __forceinline__ void xcd_swizzle(int& bx, int& by) {
+  const int gx = gridDim.x, n = gx * gridDim.y;
+  const int L = blockIdx.x + gx * blockIdx.y;
+  if (!ORB_XCD_SWIZZLE) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    return;
+  }
+  const int xcd = L & 7, pos = L >> 3, q = n >> 3, r = n & 7;
+  const int logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  by = logical / gx;
+  bx = logical - by * gx;
+}
+

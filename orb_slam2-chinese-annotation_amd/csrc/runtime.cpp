@@ -730,7 +730,9 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   pf.names[2] = useBands ? "k_fast_band" : "k_fast_cells";
   // Level 0 is the caller's image: its FAST cells need no pyramid, so they run
   // on the side stream beside the latency-bound resize chain (fork / join by
-  // events, graph-capturable); levels >= 1 follow the chain on the main stream.
+  // events, graph-capturable).  Levels 1..sideLevels follow on the side stream
+  // in one launch once the chain has written level sideLevels; the rest follow
+  // the chain on the main stream.
   const int l0End = P.lv[0].cellEnd;
   const bool l0Side = !useBands && !noL0Overlap && l0End > 0 && P.nlevels > 1;
   // ORB_FAST_PER_LEVEL=1 (A/B knob, off): levels >= 1 on the side stream too,
@@ -740,6 +742,13 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   static const bool fastPerLevelEnv =
       getenv("ORB_FAST_PER_LEVEL") && atoi(getenv("ORB_FAST_PER_LEVEL")) > 0;
   const bool perLevel = l0Side && fastPerLevelEnv;
+  // ORB_FAST_SIDE_LEVELS=n (default 2): extraction alone 1.770 / 1.723 /
+  // 1.708 / 1.709 ms per 512 frames for n = 0 / 1 / 2 / 3, bench 259.7k /
+  // 262.3k / 263.6k / 263.4k frames/s (profiles/r03_schedule_xcd.txt)
+  static const int sideLevelsEnv =
+      getenv("ORB_FAST_SIDE_LEVELS") ? atoi(getenv("ORB_FAST_SIDE_LEVELS")) : 2;
+  const int sideLevels = (l0Side && !perLevel) ? std::min(sideLevelsEnv, P.nlevels - 1) : 0;
+  const int sideEnd = sideLevels > 0 ? P.lv[sideLevels].cellEnd : l0End;
   if (l0Side) {
     HIP_TRY(hipEventRecord(h->evL0Fork, s));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->evL0Fork, 0));
@@ -749,7 +758,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                              h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, l0End, B,
                              h->stream2));
     PROF_REC(ev, pf.e(ev, 5), h->stream2);
-    if (!perLevel) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
+    if (!perLevel && sideLevels == 0) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
   } else if (ev) {
     pf.not_run(5);
   }
@@ -783,6 +792,18 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
       PROF_REC(ev, pf.e(ev, 2, fastSeg), h->stream2);
       ++fastSeg;
     }
+    if (l == sideLevels && sideEnd > l0End) {
+      HIP_TRY(hipEventRecord(h->evLvl[l], cs));
+      HIP_TRY(hipStreamWaitEvent(h->stream2, h->evLvl[l], 0));
+      PROF_REC(ev, pf.b(ev, 5, 1), h->stream2);
+      HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                               h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
+                               h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), l0End,
+                               sideEnd, B, h->stream2));
+      PROF_REC(ev, pf.e(ev, 5, 1), h->stream2);
+      if (ev) pf.segments(5, 2);
+    }
+    if (l == sideLevels && sideLevels > 0) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
   }
   PROF_REC(ev, pf.e(ev, 0), cs);
   if (cs != s) {  // the caller's stream also follows the whole chain (levels without cells)
@@ -806,7 +827,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
                              h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(),
-                             l0Side ? l0End : 0, P.ncells, B, s));
+                             l0Side ? sideEnd : 0, P.ncells, B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
   }
   // (level 0's octree on the side stream as well measured no gain: the octree's
@@ -955,8 +976,9 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   h->ownStream = true;
   h->prof.nStages = 6;
   h->prof.maxSeg[2] = ORB_MAX_LEVELS;  // FAST of levels >= 1: one launch per level
+  h->prof.maxSeg[5] = 2;  // side-stream FAST: level 0, then levels 1..sideLevels
   const char* names[6] = {"k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree",
-                          "k_orient_desc", "k_fast_cells_l0"};
+                          "k_orient_desc", "k_fast_cells_side"};
   for (int i = 0; i < 6; ++i) {
     h->prof.names[i] = names[i];
     h->prof.launchesPerCall[i] = 1;
