@@ -224,12 +224,53 @@ def cpu_baseline(imgs_host, maps, args, scale):
             "host_cpu": model, "host_nproc": ncpu}
 
 
+_HIP = None
+_STREAMS = {}
+# HIP backs streams by a few HSA queues per priority level (GPU_MAX_HW_QUEUES,
+# 4 here), and two streams on one queue run in submission order.  The
+# extractor's side stream is high priority (its own pool); the extraction
+# stream is normal priority and the match stream low priority, so no two of
+# the three can share a queue (tools/probe/c5_swap.py, profiles/r03_streams.txt)
+_STREAM_PRIO = {"extract": "normal", "match": "least", "h2d": "greatest", "d2h": "least"}
+
+
+def _hip(torch):
+    global _HIP
+    import ctypes
+    if _HIP is None:  # torch's own HIP runtime (one runtime per process)
+        _HIP = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    return _HIP
+
+
+def new_stream(torch, dev, key):
+    """The bench's stream for `key` (created once per process): a HIP stream of
+    the priority _STREAM_PRIO names, or (ORB_BENCH_STREAMS=torch) a torch pool
+    stream."""
+    import ctypes
+    mode = os.environ.get("ORB_BENCH_STREAMS", "prio")
+    if mode == "torch":
+        return torch.cuda.Stream(dev)
+    if key in _STREAMS:
+        return _STREAMS[key]
+    hip = _hip(torch)
+    h = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        least, greatest = ctypes.c_int(), ctypes.c_int()
+        hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest))
+        prio = {"normal": 0, "least": least.value, "greatest": greatest.value}[_STREAM_PRIO[key]]
+        rc = hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(1), ctypes.c_int(prio))
+    if rc != 0:
+        raise RuntimeError(f"HIP stream creation failed ({rc})")
+    _STREAMS[key] = torch.cuda.ExternalStream(h.value, device=dev)  # kept for the process's lifetime
+    return _STREAMS[key]
+
+
 def pipelined(torch, dev, extract, match, n_sets, steps, warmup):
     """Seconds per step of `extract(j, stream)` then `match(j, stream)` over
     buffer set j = step % n_sets, pipelined on two streams: step k's match
     overlaps step k+1's extraction; a set is rewritten only after its previous
     match has finished (events).  Every step does all of its work."""
-    es, ms = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    es, ms = new_stream(torch, dev, "extract"), new_stream(torch, dev, "match")
     ext_done = [torch.cuda.Event() for _ in range(n_sets)]
     match_done = [torch.cuda.Event() for _ in range(n_sets)]
 
@@ -398,8 +439,8 @@ def host_input_leg(orb, torch, ext, matcher, imgs, args, dev, sets, d_mps, d_mpd
                  cnt=torch.empty(B, dtype=torch.int32).pin_memory(),
                  match=torch.empty((B, cap), dtype=torch.int32).pin_memory()) for _ in range(2)]
     cnts = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in range(2)]
-    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    es, ms = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    h2d, d2h = new_stream(torch, dev, "h2d"), new_stream(torch, dev, "d2h")
+    es, ms = new_stream(torch, dev, "extract"), new_stream(torch, dev, "match")
     ev = {k: [torch.cuda.Event() for _ in range(2)] for k in ("in", "ext", "match", "out")}
     fb = W * H
 
@@ -536,8 +577,8 @@ def main():
     # stream) overlaps launch g+1's extraction (extract stream).  Launch g
     # writes buffer set g % 2 once the matcher of launch g - 2 (the set's
     # previous reader) has finished; its matcher starts once it is done.
-    ext_stream = torch.cuda.Stream(dev)
-    match_stream = torch.cuda.Stream(dev)
+    ext_stream = new_stream(torch, dev, "extract")
+    match_stream = new_stream(torch, dev, "match")
     torch.cuda.set_stream(ext_stream)
     d_img = torch.from_numpy(imgs).to(dev)
     sets = [dict(kps=torch.zeros((B, cap, 7), dtype=torch.int32, device=dev),

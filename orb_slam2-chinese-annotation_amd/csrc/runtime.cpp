@@ -915,8 +915,12 @@ static bool chain_stream() {
   return v;
 }
 static bool create_side_streams(orb_extractor* h) {
+  // The side stream is high priority: HIP backs streams by a few HSA queues
+  // per priority level, and a side stream sharing the caller's (normal
+  // priority) queue runs in submission order with it, which serialises level
+  // 0's FAST with the resize chain (profiles/r03_streams.txt)
   if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking,
-                                  stream_prio("ORB_STREAM2_PRIO", "normal")) != hipSuccess)
+                                  stream_prio("ORB_STREAM2_PRIO", "greatest")) != hipSuccess)
     return false;
   if (chain_stream() &&
       hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking,

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 3: full bench line (C4 + host input + C3 + C5) vs the extractor side stream's priority
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out; mkdir -p "$O"
+OUT=$O/prio3.txt; : > "$OUT"
+for set in "ORB_STREAM2_PRIO=normal" "ORB_STREAM2_PRIO=greatest" "ORB_STREAM2_PRIO=least" "ORB_STREAM2_PRIO=normal" "ORB_STREAM2_PRIO=greatest" "ORB_STREAM2_PRIO=least"; do
+  env $set timeout -k 10 200 python "$R/bench.py" --no-cpu > "$O/prio3_b.json" 2>/dev/null || exit 1
+  python3 -c "import json;b=json.load(open('$O/prio3_b.json'));print('$set', 'bench', round(b['value']), 'C3', round(b['C3_stereo_pairs_per_s']['value']), 'C5', round(b['C5_problems_per_s']['value']), 'host', round(b['host_input']['frames_per_s']))" >> "$OUT"
+done
+cat "$OUT"
