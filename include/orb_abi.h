@@ -179,10 +179,11 @@ void* orb_extractor_stream(orb_extractor_t* h);
  * enables; profile_read drains the recorded events and returns the summed
  * milliseconds, launch count and kernel name of `stage`:
  * 0 k_pyr_resize (nlevels-1 launches per call), 1 k_blur_levels (split mode
- * only), 2 FAST (k_fast_cells on levels >= 1, or k_fast_band on all levels),
- * 3 k_octree, 4 k_orient_desc, 5 k_fast_cells_l0 (level 0's cells on the side
- * stream, beside the resize chain; 0 launches when not split off), 6 = the
- * whole extraction call. */
+ * only), 2 FAST (k_fast_cells on the levels the main stream runs, or
+ * k_fast_band on all levels), 3 k_octree, 4 k_orient_desc,
+ * 5 k_fast_cells_side (the cells of level 0, then of levels 1-2, on the
+ * handle's side stream beside the resize chain; durations summed; 0 launches
+ * when not split off), 6 = the whole extraction call. */
 orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable);
 orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
                                         int* launches, const char** name);

@@ -3,9 +3,10 @@
 // Pipeline for a batch of B images (every launch covers all B images; HBM
 // layout in DESIGN.md §3):
 //   k_pyr_resize   x (nlevels-1)  bilinear level l from level l-1    src/ORBextractor.cc:1172-1207
-//   k_fast_cells   x 2            FAST-9/16 + cell-local NMS + iniTh  src/ORBextractor.cc:785-865
-//                                 -> minTh fallback, one wave per cell; level 0's cells
-//                                 on a side stream beside the resize chain, then levels >= 1
+//   k_fast_cells   x 3            FAST-9/16 + cell-local NMS + iniTh  src/ORBextractor.cc:785-865
+//                                 -> minTh fallback, one wave per cell; level 0's cells,
+//                                 then levels 1-2, on a side stream beside the resize
+//                                 chain; levels >= 3 after it
 //   (k_fast_band   x 1            the same per band of cells; single frames, oversized cells)
 //   k_octree       x 1            DistributeOctTree, one workgroup    src/ORBextractor.cc:558-782
 //                                 per (image, level), list order emulated exactly
