@@ -228,10 +228,11 @@ _HIP = None
 _STREAMS = {}
 # HIP backs streams by a few HSA queues per priority level (GPU_MAX_HW_QUEUES,
 # 4 here), and two streams on one queue run in submission order.  The
-# extractor's side stream is high priority (its own pool); the extraction
-# stream is normal priority and the match stream low priority, so no two of
-# the three can share a queue (tools/probe/c5_swap.py, profiles/r03_streams.txt)
-_STREAM_PRIO = {"extract": "normal", "match": "least", "h2d": "greatest", "d2h": "least"}
+# extractor's side stream is low priority (its own pool); the extraction
+# stream is normal priority and the match and copy streams high priority, so
+# no two of the concurrently busy streams can share a queue
+# (tools/probe/c5_swap.py, profiles/r03_streams.txt)
+_STREAM_PRIO = {"extract": "normal", "match": "greatest", "h2d": "greatest", "d2h": "greatest"}
 
 
 def _hip(torch):
@@ -257,7 +258,8 @@ def new_stream(torch, dev, key):
     with torch.cuda.device(dev):
         least, greatest = ctypes.c_int(), ctypes.c_int()
         hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest))
-        prio = {"normal": 0, "least": least.value, "greatest": greatest.value}[_STREAM_PRIO[key]]
+        name = os.environ.get("ORB_BENCH_PRIO_" + key.upper(), _STREAM_PRIO[key])
+        prio = {"normal": 0, "least": least.value, "greatest": greatest.value}[name]
         rc = hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(1), ctypes.c_int(prio))
     if rc != 0:
         raise RuntimeError(f"HIP stream creation failed ({rc})")

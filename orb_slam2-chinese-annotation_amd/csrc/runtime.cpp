@@ -765,7 +765,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   // the resize chain: on the caller's stream, or (per-level mode,
   // ORB_CHAIN_STREAM=1) on a high-priority third stream forked from it
   hipStream_t cs = s;
-  if (perLevel && h->stream3) {
+  if (l0Side && h->stream3) {
     cs = h->stream3;
     HIP_TRY(hipStreamWaitEvent(cs, h->evL0Fork, 0));
   }
@@ -915,12 +915,14 @@ static bool chain_stream() {
   return v;
 }
 static bool create_side_streams(orb_extractor* h) {
-  // The side stream is high priority: HIP backs streams by a few HSA queues
+  // The side stream is low priority: HIP backs streams by a few HSA queues
   // per priority level, and a side stream sharing the caller's (normal
   // priority) queue runs in submission order with it, which serialises level
-  // 0's FAST with the resize chain (profiles/r03_streams.txt)
+  // 0's FAST with the resize chain.  Low rather than high: the chain on the
+  // caller's stream then wins the CUs the side FAST also wants (extraction
+  // 1.703 vs 1.727 ms per 512 frames; profiles/r03_streams.txt)
   if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking,
-                                  stream_prio("ORB_STREAM2_PRIO", "greatest")) != hipSuccess)
+                                  stream_prio("ORB_STREAM2_PRIO", "least")) != hipSuccess)
     return false;
   if (chain_stream() &&
       hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking,
