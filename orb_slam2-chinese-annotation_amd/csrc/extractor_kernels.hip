@@ -838,7 +838,8 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   int bx, img;
   xcd_swizzle(bx, img);
   // the image's status starts clean (k_octree may flag it, k_orient_desc reads it)
-  if (bx == 0 && threadIdx.x == 0) errFlag[img] = 0;
+  // (errFlag null: the caller cleared the flags before any octree could run)
+  if (errFlag && bx == 0 && threadIdx.x == 0) errFlag[img] = 0;
   uint8_t* tile = smem + wave * fc_wave_bytes(tileElems);
   uint8_t* sc = tile + tileElems;  // strengths, same byte layout as the tile
   uint16_t* queue = (uint16_t*)(sc + tileElems);
@@ -1975,7 +1976,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const uint32_t* __restrict__ outKeys, const int32_t* __restrict__ outCount,
     const int32_t* __restrict__ errFlag, orb_keypoint_t* __restrict__ kps,
-    uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts, int ppwRt) {
+    uint8_t* __restrict__ desc, int capacity, int32_t* __restrict__ counts, int ppwRt,
+    int slotBeg, int slotEnd) {
   // PPW > 0: compile-time pairs per wave (<4> batches, <1> one-pair calls);
   // PPW == 0: ppwRt
   const int ppw = PPW ? PPW : ppwRt;
@@ -1985,20 +1987,23 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   int bx, img;
   xcd_swizzle(bx, img);
   const int32_t* cnts = outCount + img * plan.nlevels;
-  if (bx == 0 && threadIdx.x == 0) {
+  // the launch whose slot range ends the image writes its count (a launch over
+  // the first levels runs beside the rest; its caller orders the last after it)
+  if (bx == 0 && threadIdx.x == 0 && slotEnd == plan.slotsPerImage) {
     int tot = 0;
     for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
     counts[img] = errFlag[img] ? (int32_t)ORB_EDEVICE : tot;  // failed image: negative count
   }
   // this wave's slot pairs: pairBase + 4 j, j < ppw <= DESC_PPW (the workgroup's
   // four waves interleave); lane 2 j + h holds the packed key of slot 2 (pairBase + 4 j) + h
-  const int pairBase = bx * 4 * ppw + w;
-  if (2 * pairBase >= plan.slotsPerImage) return;
+  // slots [slotBeg, slotEnd): whole levels (level slot ranges are even)
+  const int pairBase = (slotBeg >> 1) + bx * 4 * ppw + w;
+  if (2 * pairBase >= slotEnd) return;
   const uint32_t* imgKeys = outKeys + (long long)img * plan.slotsPerImage;
   uint32_t keyv = 0;
   if (lane < 2 * ppw) {
     const int slot = 2 * (pairBase + 4 * (lane >> 1)) + (lane & 1);
-    if (slot < plan.slotsPerImage) keyv = imgKeys[slot];
+    if (slot < slotEnd) keyv = imgKeys[slot];
   }
   // the image's per-level keypoint counts, lane l = level l, and their
   // exclusive prefix (output offsets): loaded once, read by v_readlane
@@ -2021,7 +2026,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     Pair P;
     P.valid = false;
     const int slot0 = 2 * (pairBase + 4 * j);
-    if (slot0 >= plan.slotsPerImage) return P;
+    if (slot0 >= slotEnd) return P;
     const int l = __builtin_amdgcn_readfirstlane(__popcll(__ballot(offv <= slot0)) - 1);
     const int i0 = slot0 - __builtin_amdgcn_readlane(offv, l), nl = __builtin_amdgcn_readlane(cntv, l);
     if (i0 >= nl) return P;
@@ -2468,26 +2473,31 @@ hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const uint32_t* outKeys, const int32_t* outCount,
                              const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
-                             int capacity, int32_t* counts, int nimg, hipStream_t s) {
+                             int capacity, int32_t* counts, int nimg, int levelBeg,
+                             int levelEnd, hipStream_t s) {
   if (plan->slotsPerImage & 1) return hipErrorInvalidValue;
+  if (levelBeg < 0 || levelEnd > plan->nlevels || levelBeg >= levelEnd) return hipErrorInvalidValue;
+  const int slotBeg = plan->lv[levelBeg].outOff;
+  const int slotEnd = levelEnd == plan->nlevels ? plan->slotsPerImage : plan->lv[levelEnd].outOff;
+  if ((slotBeg | slotEnd) & 1) return hipErrorInvalidValue;
   // DESC_PPW keypoint pairs per wave for batches (the next pair's loads overlap
   // the current one); one pair per wave for a frame or two per call, where the
   // grid is small and the per-wave chain is the latency (ORB_DESC_PPW overrides)
   static const int kPpw = getenv("ORB_DESC_PPW") ? atoi(getenv("ORB_DESC_PPW")) : 0;
   const int ppw = kPpw == 1 || kPpw == DESC_PPW ? kPpw : (nimg <= 2 ? 1 : DESC_PPW);
-  dim3 grid((plan->slotsPerImage + 8 * ppw - 1) / (8 * ppw), nimg), block(256);
+  dim3 grid((slotEnd - slotBeg + 8 * ppw - 1) / (8 * ppw), nimg), block(256);
   if (ppw == DESC_PPW)
     hipLaunchKernelGGL(k_orient_desc<DESC_PPW>, grid, block, 0, s, img0, img0Pitch, img0Stride,
                        arena, arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity,
-                       counts, DESC_PPW);
+                       counts, DESC_PPW, slotBeg, slotEnd);
   else if (ppw == 1 && DESC_SMALL_CT)
     hipLaunchKernelGGL(k_orient_desc<1>, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
                        arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts,
-                       1);
+                       1, slotBeg, slotEnd);
   else
     hipLaunchKernelGGL(k_orient_desc<0>, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
                        arenaPitch, *plan, outKeys, outCount, errFlag, kps, desc, capacity, counts,
-                       ppw);
+                       ppw, slotBeg, slotEnd);
   return hipGetLastError();
 }
 

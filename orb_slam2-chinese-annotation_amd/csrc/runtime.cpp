@@ -59,7 +59,8 @@ hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const uint32_t* outKeys, const int32_t* outCount,
                              const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
-                             int capacity, int32_t* counts, int nimg, hipStream_t s);
+                             int capacity, int32_t* counts, int nimg, int levelBeg,
+                             int levelEnd, hipStream_t s);
 hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out, hipStream_t s);
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
@@ -749,13 +750,28 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
       getenv("ORB_FAST_SIDE_LEVELS") ? atoi(getenv("ORB_FAST_SIDE_LEVELS")) : 2;
   const int sideLevels = (l0Side && !perLevel) ? std::min(sideLevelsEnv, P.nlevels - 1) : 0;
   const int sideEnd = sideLevels > 0 ? P.lv[sideLevels].cellEnd : l0End;
+  // ORB_SIDE_TAIL=1 (A/B knob): the side stream also runs the octree and
+  // k_orient_desc of its levels 0..sideLevels, beside the main stream's FAST /
+  // octree of the rest; the main stream's k_orient_desc (which writes the
+  // counts) waits for the side octree, and the call ends on both streams
+  static const bool sideTailEnv = getenv("ORB_SIDE_TAIL") && atoi(getenv("ORB_SIDE_TAIL")) > 0;
+  const bool sideTail = sideTailEnv && l0Side && !perLevel && !split_blur() && sideLevels > 0 &&
+                        sideLevels + 1 < P.nlevels;
+  const int tailSplit = sideLevels + 1;  // first level of the main stream's tail
+  // with a split tail, octrees run on both streams: the status flags are cleared
+  // before the fork, not by the FAST launches (which would race a side octree)
+  int32_t* fastErr = h->dErr.as<int32_t>();
+  if (sideTail) {
+    HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
+    fastErr = nullptr;
+  }
   if (l0Side) {
     HIP_TRY(hipEventRecord(h->evL0Fork, s));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->evL0Fork, 0));
     PROF_REC(ev, pf.b(ev, 5), h->stream2);
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, l0End, B,
+                             h->dCellCount.as<int32_t>(), fastErr, 0, l0End, B,
                              h->stream2));
     PROF_REC(ev, pf.e(ev, 5), h->stream2);
     if (!perLevel && sideLevels == 0) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
@@ -798,10 +814,33 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
       PROF_REC(ev, pf.b(ev, 5, 1), h->stream2);
       HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                                h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                               h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), l0End,
+                               h->dCellCount.as<int32_t>(), fastErr, l0End,
                                sideEnd, B, h->stream2));
       PROF_REC(ev, pf.e(ev, 5, 1), h->stream2);
       if (ev) pf.segments(5, 2);
+    }
+    if (l == sideLevels && sideTail) {
+      // the side stream's tail: octree of levels 0..sideLevels, then their
+      // descriptors (the main stream's octree of the rest runs beside it)
+      PROF_REC(ev, pf.b(ev, 3, 1), h->stream2);
+      HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
+                           h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
+                           h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
+                           h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, tailSplit, B,
+                           h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr,
+                           h->octNodeBytes, h->stream2));
+      PROF_REC(ev, pf.e(ev, 3, 1), h->stream2);
+      HIP_TRY(hipEventRecord(h->evFork, h->stream2));  // side octree done
+      PROF_REC(ev, pf.b(ev, 4, 1), h->stream2);
+      HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                                h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
+                                h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, 0,
+                                tailSplit, h->stream2));
+      PROF_REC(ev, pf.e(ev, 4, 1), h->stream2);
+      if (ev) {
+        pf.segments(3, 2);
+        pf.segments(4, 2);
+      }
     }
     if (l == sideLevels && sideLevels > 0) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
   }
@@ -826,13 +865,13 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   else
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(),
+                             h->dCellCount.as<int32_t>(), fastErr,
                              l0Side ? sideEnd : 0, P.ncells, B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
   }
   // (level 0's octree on the side stream as well measured no gain: the octree's
   // time is its per-workgroup pass latency, not level 0's size)
-  if (l0Side) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));
+  if (l0Side && !sideTail) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));
   const bool split = split_blur();
   if (split) {
     if (s2 != s) {
@@ -850,9 +889,12 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                        h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
-                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, P.nlevels, B,
-                       h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr, h->octNodeBytes, s));
+                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), sideTail ? tailSplit : 0,
+                       P.nlevels, B, h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr,
+                       h->octNodeBytes, s));
   PROF_REC(ev, pf.e(ev, 3), s);
+  // the main k_orient_desc writes every image's count: it needs the side octree
+  if (sideTail) HIP_TRY(hipStreamWaitEvent(s, h->evFork, 0));
   if (split && s2 != s) HIP_TRY(hipStreamWaitEvent(s, h->evJoin, 0));
   PROF_REC(ev, pf.b(ev, 4), s);
   if (split)
@@ -863,8 +905,10 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   else
     HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                               h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
-                              h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
+                              h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B,
+                              sideTail ? tailSplit : 0, P.nlevels, s));
   PROF_REC(ev, pf.e(ev, 4), s);
+  if (sideTail) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));  // the side tail is done
   PROF_REC(ev, pf.t1(ev), s);
   if (!capturing) HIP_TRY(hipEventRecord(h->evBatch, s));  // readbacks on the handle stream wait for it
   h->lastImg0 = d_images;
@@ -983,6 +1027,8 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   h->prof.nStages = 6;
   h->prof.maxSeg[2] = ORB_MAX_LEVELS;  // FAST of levels >= 1: one launch per level
   h->prof.maxSeg[5] = 2;  // side-stream FAST: level 0, then levels 1..sideLevels
+  h->prof.maxSeg[3] = 2;  // octree / orient: main stream, then (split tail) side stream
+  h->prof.maxSeg[4] = 2;
   const char* names[6] = {"k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree",
                           "k_orient_desc", "k_fast_cells_side"};
   for (int i = 0; i < 6; ++i) {
