@@ -271,6 +271,8 @@ def test_batch_hard_cases_vs_oracle(gpu, oracle):
     (1920, 1080, 2000, 1.5, 6),
     (1241, 376, 1000, 1.9, 4),
     (640, 480, 1000, 1.2, 1),
+    (640, 480, 1000, 1.2, 2),      # the side stream's FAST covers every level >= 1,
+    (1241, 376, 1000, 1.2, 3),     # the main stream's FAST launch is empty
 ])
 def test_batch_parameters_vs_oracle(gpu, oracle, w, h, nf, sf, nl):
     _batch_vs_oracle(gpu, oracle, [gpu.synth_image(40, f, w, h) for f in range(4)], nf, sf, nl)
