@@ -352,6 +352,7 @@ struct orb_extractor {
   int umax[16];
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // side stream: FAST beside the resize chain (blur in split mode)
+  bool sharedSide = false;        // stream2 is the device's shared side stream (not destroyed)
   hipStream_t stream3 = nullptr;  // resize chain, high priority (ORB_CHAIN_STREAM=1)
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   hipEvent_t evL0Fork = nullptr, evL0Join = nullptr;  // level-0 FAST beside the resize chain
@@ -958,6 +959,22 @@ static bool chain_stream() {
   static const bool v = getenv("ORB_CHAIN_STREAM") && atoi(getenv("ORB_CHAIN_STREAM")) > 0;
   return v;
 }
+// One side stream per device, shared by every extractor handle of the process
+// (ORB_SIDE_SHARED=0: one per handle).  Each stream holds an HSA queue, and a
+// process with more queues than the hardware maps at once (the bench with its
+// C3 / C5 handles: 11) saw the side stream's cross-queue fork / join slow its
+// extraction by 30-50 % whenever a matcher ran beside it (profiles/r03_streams.txt).
+// Handles on one device share it safely: fork / join are per-handle events.
+static hipStream_t shared_side_stream(int device, int prio) {
+  static std::mutex mu;
+  static hipStream_t s[64] = {};
+  if (device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!s[device] && hipStreamCreateWithPriority(&s[device], hipStreamNonBlocking, prio) != hipSuccess)
+    s[device] = nullptr;
+  return s[device];  // process lifetime
+}
+
 static bool create_side_streams(orb_extractor* h) {
   // The side stream is low priority: HIP backs streams by a few HSA queues
   // per priority level, and a side stream sharing the caller's (normal
@@ -965,9 +982,15 @@ static bool create_side_streams(orb_extractor* h) {
   // 0's FAST with the resize chain.  Low rather than high: the chain on the
   // caller's stream then wins the CUs the side FAST also wants (extraction
   // 1.703 vs 1.727 ms per 512 frames; profiles/r03_streams.txt)
-  if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking,
-                                  stream_prio("ORB_STREAM2_PRIO", "least")) != hipSuccess)
+  static const bool shared = !getenv("ORB_SIDE_SHARED") || atoi(getenv("ORB_SIDE_SHARED")) > 0;
+  const int prio = stream_prio("ORB_STREAM2_PRIO", "least");
+  if (shared) {
+    h->stream2 = shared_side_stream(h->device, prio);
+    h->sharedSide = true;
+    if (!h->stream2) return false;
+  } else if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, prio) != hipSuccess) {
     return false;
+  }
   if (chain_stream() &&
       hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking,
                                   stream_prio("ORB_CHAIN_PRIO", "greatest")) != hipSuccess)
@@ -1011,7 +1034,7 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
       hipEventCreateWithFlags(&h->evBatch, hipEventDisableTiming) != hipSuccess ||
       !create_level_events(h)) {
     if (h->stream) hipStreamDestroy(h->stream);
-    if (h->stream2) hipStreamDestroy(h->stream2);
+    if (h->stream2 && !h->sharedSide) hipStreamDestroy(h->stream2);
     if (h->stream3) hipStreamDestroy(h->stream3);
     if (h->evFork) hipEventDestroy(h->evFork);
     if (h->evJoin) hipEventDestroy(h->evJoin);
@@ -1061,7 +1084,7 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   if (h->oneExec) hipGraphExecDestroy(h->oneExec);
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
-  if (h->stream2) hipStreamDestroy(h->stream2);
+  if (h->stream2 && !h->sharedSide) hipStreamDestroy(h->stream2);
   if (h->stream3) hipStreamDestroy(h->stream3);
   if (h->evFork) hipEventDestroy(h->evFork);
   if (h->evJoin) hipEventDestroy(h->evJoin);
