@@ -3,7 +3,7 @@
 
 Each GPU holds a resident sequence of D distinct synthetic KITTI-shaped
 1241x376 frames (default 8192) in HBM; one step = one pass of the whole hot
-path over all D frames, in launches of B = 512: ORBextractor (1000 features,
+path over all D frames, in launches of B = 1024: ORBextractor (1000 features,
 8 levels, FAST 20/7) + SearchByProjection(F, local map) against each frame's
 own 5,000-point synthetic local map (the headline
 workload).  Frames shard per rank (weak scaling); the only collectives are one
@@ -524,7 +524,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=8192,
                     help="distinct resident frames per GPU (a step processes each once)")
-    ap.add_argument("--batch", type=int, default=512, help="frames per extraction launch")
+    ap.add_argument("--batch", type=int, default=1024,
+                    help="frames per extraction launch (capped at --frames)")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--features", type=int, default=1000)
@@ -562,8 +563,9 @@ def main():
         else:
             dist.init_process_group("gloo")
     orb = load_package()
-    W, H, B, NF, M = args.width, args.height, args.batch, args.features, args.mappoints
     D = args.frames
+    args.batch = min(args.batch, D)
+    W, H, B, NF, M = args.width, args.height, args.batch, args.features, args.mappoints
     if D % B:
         raise SystemExit("--frames must be a multiple of --batch")
     NB = D // B

@@ -32,8 +32,9 @@ if (O / f"tests_{tag}.log").exists():
 
 b = json.loads((O / f"bench_{tag}.json").read_text())
 r = b["roofline"]
-r["traffic"], _ = bench.measured_traffic(r["kernel"], 512)
-vi = bench.valu_issue(r["kernel"], 512, r["ms_per_launch"])
+bl = b["config"]["frames_per_launch"]  # the PMC files are per 512-frame launch, scaled
+r["traffic"], _ = bench.measured_traffic(r["kernel"], bl)
+vi = bench.valu_issue(r["kernel"], bl, r["ms_per_launch"])
 if vi is not None:  # re-derived from the new PMC files
     rate = vi["valu_instr_per_launch"] / (r["ms_per_launch"] * 1e-3) / 1e9
     r["valu"] = dict(r.get("valu", {}), achieved=rate, frac=rate / bench.VALU_PEAK_G,
@@ -60,12 +61,13 @@ pm = json.loads((P / f"{tag}_pmc.json").read_text())["kernels"]
 # >= 1); the PMC passes run FAST inline (one dispatch), so their per-dispatch
 # counters are already per call
 calls = {k: agg[k][0] / agg["k_orient_desc"][0] for k in agg}
+tb = json.loads((O / f"prof_{tag}.json").read_text())["config"]["frames_per_launch"]
 for k in [k for k in ["k_pyr_resize", "k_blur_levels", "k_fast_band", "k_fast_cells", "k_octree",
                       "k_orient_desc"] if k in agg and k in pm]:
     n_launch = round(calls[k])
     ms = agg[k][1] / agg[k][0] / 1e6 * n_launch
-    a = alg[k] * 512
-    t = h[k]["traffic_bytes"] * (7 if k == "k_pyr_resize" else 1)
+    a = alg[k] * tb  # the trace run's frames per launch
+    t = h[k]["traffic_bytes"] * (7 if k == "k_pyr_resize" else 1) * tb / 512
     d = pm[k]
     w = d["SQ_WAVE_CYCLES"]
     print(f"{k:16s} {ms:.3f} ms/call ({n_launch} dispatches)  {a / ms / 1e6:6.0f} GB/s  "
