@@ -767,8 +767,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef FC_PAD
 #define FC_PAD 0        // extra LDS row pitch (bytes, multiple of 8)
 #endif
+#ifndef FC_ROWMAJOR
+#define FC_ROWMAJOR 1   // candidates queued in row-major order, keys written by NMS in order
+#endif
 #ifndef FC_PERM
-#define FC_PERM 1       // pretest lane -> pixel-group permutation (LDS banking)
+#define FC_PERM (!FC_ROWMAJOR)  // pretest lane -> pixel-group permutation (LDS banking)
 #endif
 
 // LDS row pitch (bytes) of a cell ROI C pixels wide: byte 8 is interior column
@@ -974,7 +977,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     const int dOff = rInc * P + 8 * kInc, wrapOff = P - 8 * nK;
     // trash slots in the NMS bitmap, as indices into the queue (u16) and the
     // strength map (u64 words): 4- and 8-byte lane strides
-    const int trashQ = (int)(reinterpret_cast<uint16_t*>(bits) - queue) + 2 * lane;
+    [[maybe_unused]] const int trashQ = (int)(reinterpret_cast<uint16_t*>(bits) - queue) + 2 * lane;
     unsigned long long* const sc64 = reinterpret_cast<unsigned long long*>(sc);
     const int trashS = (int)(reinterpret_cast<unsigned long long*>(bits) - sc64) + lane;
     for (int g0 = 0; g0 < nG; g0 += 64) {
@@ -1003,6 +1006,30 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       for (int i = 0; i < 4; ++i) rp[i] = pretest_pair(V[i], Q0[i], Q4[i], Q8[i], Q12[i], T);
       if (fresh)  // strengths start at 0, FAST_OUTSIDE past the interior (o is a multiple of 8)
         sc64[valid ? (o >> 3) : trashS] = last ? outsideLast : 0ull;
+#if FC_ROWMAJOR
+      // lane-major append: lane = pixel group in row-major order, so the queue
+      // (and the corner list built from it) is in cv::FAST's row-major order
+      // and NMS can write the keys in place.  Pass mask: the sign bits of the
+      // eight f16 results (bit 15 / 31 of rp[i] = pixels 2i / 2i+1), masked to
+      // the lane's interior pixels.
+      uint32_t mk = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t ns = ~rp[i];
+        mk |= ((ns >> 15) & 1u) << (2 * i);
+        mk |= (ns >> 31) << (2 * i + 1);
+      }
+      mk &= valid ? (last ? (1u << nvLast) - 1u : 0xFFu) : 0u;
+      const int cnt = __builtin_popcount(mk);
+      const int incl = wave_incl_scan(cnt);
+      int pos = nq + incl - cnt;
+      while (mk) {
+        const int j = __builtin_ctz(mk);
+        mk &= mk - 1u;
+        queue[pos++] = (uint16_t)(off + j);
+      }
+      nq += __builtin_amdgcn_readlane(incl, 63);
+#else
       // pixel j of a valid lane is interior when j < nvLast or the group is not a row's last
       const unsigned long long vm = __ballot(valid), vIn = __ballot(valid && !last);
 #pragma unroll
@@ -1015,6 +1042,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
         queue[lane_select(bj, pos, trashQ)] = (uint16_t)(off + j);
         nq += __popcll(bj);
       }
+#endif
       k += kInc;
       off += dOff;
       if (k >= nK) {
@@ -1064,6 +1092,48 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   };
   // keys of the window in row-major order (lane = window row, ih <= 64)
   uint32_t* out = cellKeys + slot * plan.keyCap;
+  // FC_ROWMAJOR: the corner list (or, dense, the window) is in row-major
+  // order, so each survivor's key goes straight to its output position
+  auto nms_emit = [&](int t) -> int {
+    const bool dense = nc > FC_CCAP;
+    const int nItems = dense ? ih * iw : nc;
+    const uint32_t kx0 = (uint32_t)(cd.x0 + 3), ky0 = (uint32_t)(cd.y0 + 3);
+    int nOut = 0;
+    for (int j0 = 0; j0 < nItems; j0 += 64) {
+      const int j = j0 + lane;
+      bool ok = false;
+      int x = 0, y = 0, m = 0;
+      if (j < nItems) {
+        int off;
+        if (dense) {
+          y = (int)(((float)j + 0.5f) * invW);
+          x = j - y * iw;
+          off = (y + 3) * P + (x + 8);
+        } else {
+          off = corners[j];
+          const int ry = (int)(((float)off + 0.5f) * invP);
+          y = ry - 3;
+          x = off - ry * P - 8;
+        }
+        const uint8_t* cp = sc + off;
+        m = cp[0];
+        const int r0 = cp[-P - 1], r1 = cp[-P], r2 = cp[-P + 1], r3 = cp[-1], r4 = cp[1],
+                  r5 = cp[P - 1], r6 = cp[P], r7 = cp[P + 1];
+        const bool L = x > 0, Rt = x < iw - 1, U = y > 0, D = y < ih - 1;
+        const int nb[8] = {(U && L) ? r0 : 0, U ? r1 : 0, (U && Rt) ? r2 : 0, L ? r3 : 0,
+                           Rt ? r4 : 0, (D && L) ? r5 : 0, D ? r6 : 0, (D && Rt) ? r7 : 0};
+        ok = m > t && m >= 2;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ok = ok && !(nb[k] > t && nb[k] >= m);
+      }
+      const unsigned long long bal = __ballot(ok);
+      const int pos = nOut + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      if (ok) out[pos] = pack_key(kx0 + x, ky0 + y, m - 1);
+      nOut += __popcll(bal);
+    }
+    return nOut;
+  };
   auto compact = [&]() -> int {
     unsigned long long row = 0ull;
     if (lane < ih) {
@@ -1090,15 +1160,27 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     return total;
   };
   // ---- phase A at iniThFAST
+#if FC_ROWMAJOR
+  (void)nms;
+  (void)compact;
+#endif
   fast_pass(ti, true);
+#if FC_ROWMAJOR
+  int n = nms_emit(ti);
+#else
   nms(ti);
   int n = compact();
+#endif
   if (n == 0 && tm != ti) {
     // ---- phase B: no keypoint at iniThFAST -> minThFAST (:846-850)
     nc = 0;
     fast_pass(tm, false);
+#if FC_ROWMAJOR
+    n = nms_emit(tm);
+#else
     nms(tm);
     n = compact();
+#endif
   }
   if (lane == 0) cellCount[slot] = n;
   ci = ciNext;
