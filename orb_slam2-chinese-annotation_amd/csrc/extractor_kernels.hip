@@ -1012,16 +1012,20 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       // and NMS can write the keys in place.  Pass mask: the sign bits of the
       // eight f16 results (bit 15 / 31 of rp[i] = pixels 2i / 2i+1), masked to
       // the lane's interior pixels.
-      uint32_t mk = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t ns = ~rp[i];
-        mk |= ((ns >> 15) & 1u) << (2 * i);
-        mk |= (ns >> 31) << (2 * i + 1);
-      }
-      mk &= valid ? (last ? (1u << nvLast) - 1u : 0xFFu) : 0u;
+      // gather the sign bytes (bytes 1, 3 of each rp[i]: pixels 0..7), move the
+      // sign bits to bit 0 (pixels 0-3) / bit 4 (pixels 4-7) of each byte, and
+      // collect them into bits 24..31 with one multiply (no carries: every
+      // partial product lands on its own bit); a set sign bit = no pass
+      const uint32_t X = __builtin_amdgcn_perm(rp[1], rp[0], 0x07050301u);
+      const uint32_t Y = __builtin_amdgcn_perm(rp[3], rp[2], 0x07050301u);
+      const uint32_t fails = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
+      uint32_t mk = ~((fails * 0x01020408u) >> 24) &
+                    (valid ? (last ? (1u << nvLast) - 1u : 0xFFu) : 0u);
       const int cnt = __builtin_popcount(mk);
-      const int incl = wave_incl_scan(cnt);
+      int incl = wave_incl_scan(cnt);
+      // opaque: otherwise hipcc forms incl - cnt from the scan's partial DPP
+      // terms and keeps each as a separate v_mov_b32_dpp + v_add
+      __asm__ volatile("" : "+v"(incl));
       int pos = nq + incl - cnt;
       while (mk) {
         const int j = __builtin_ctz(mk);

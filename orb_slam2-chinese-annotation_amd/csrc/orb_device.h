@@ -196,10 +196,12 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 // each 16-lane row, then row_bcast 15 and 31 across rows): six VALU ops, no
 // LDS round trips.  All 64 lanes must be active.
 __device__ __forceinline__ int wave_incl_scan(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  // row_shr steps with bound_ctrl (lanes shifted in read 0): hipcc folds each
+  // into one v_add_u32_dpp instead of a v_mov_b32_dpp + v_add pair
+  v += __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_mov_dpp(v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_mov_dpp(v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_mov_dpp(v, 0x118, 0xf, 0xf, true);  // row_shr:8
   v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
   return v;
