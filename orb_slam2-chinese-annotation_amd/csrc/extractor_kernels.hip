@@ -916,7 +916,12 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   const unsigned long long outsideLast =
       nvLast >= 8 ? 0ull : (0x0101010101010101ull << (8 * nvLast));
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
-  const float invK = 1.0f / (float)nK, invP = 1.0f / (float)P, invW = 1.0f / (float)iw;
+  // quotients q = (int)((x + 0.5) * (1 / d)) for x < 2^13, d <= 88 are exact
+  // with the hardware reciprocal (<= 1 ulp): (x + 0.5) / d sits >= 0.5 / d
+  // (>= 0.0057) from an integer, the reciprocal and product err < 2e-5.  An
+  // IEEE division (this library's default for 1.0f / x) costs ~11 VALU each
+  const float invK = __builtin_amdgcn_rcpf((float)nK), invP = __builtin_amdgcn_rcpf((float)P),
+              invW = __builtin_amdgcn_rcpf((float)iw);
   wave_lds_sync();
 
   int nq = 0, nc = 0;  // wave-uniform queue / corner counts
@@ -973,7 +978,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     const int rr0 = (int)(((float)pl + 0.5f) * invK);
     int k = pl - rr0 * nK;
     int off = (rr0 + 3) * P + 8 + 8 * k;  // byte of interior column 8k
-    const int rInc = 64 / nK, kInc = 64 - rInc * nK;  // wave-uniform
+    const int rInc = (int)(64.5f * invK), kInc = 64 - rInc * nK;  // wave-uniform, = 64 / nK
     const int dOff = rInc * P + 8 * kInc, wrapOff = P - 8 * nK;
     // trash slots in the NMS bitmap, as indices into the queue (u16) and the
     // strength map (u64 words): 4- and 8-byte lane strides
