@@ -791,11 +791,43 @@ __device__ __forceinline__ uint32_t byte_pair(uint32_t hi, uint32_t lo, int i0, 
 }
 
 // FAST arc strength of the byte pixel at `c` (row pitch p bytes), as
-// fast_score on the subnormal encoding above
-__device__ __forceinline__ int fast_score_u8(const uint8_t* c, int p) {
+// fast_score on the subnormal encoding above.  Dark and bright strengths ride
+// in one f16 pair (lo, hi) = (-max c, min c) over the ring: the first min3
+// layer reads each ring byte from the low half for both lanes (op_sel_hi 0)
+// and negates the low lane (neg_lo), so the raw ds_read_u8 values need no
+// conversion; the pixel value enters once at the end:
+//   dark = max_k min_arc (v - c) = v + max_k (-max_arc c),
+//   bright = max_k min_arc (c - v) = max_k min_arc c - v.
+#ifndef FC_SCORE_RAW
+#define FC_SCORE_RAW 1
+#endif
+__device__ __forceinline__ uint32_t pk_min3_negpair(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_pk_minimum3_f16 %0, %1, %2, %3 op_sel_hi:[0,0,0] neg_lo:[1,1,1]"
+      : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+template <bool CONST_P>
+__device__ __forceinline__ int fast_score_u8(const uint8_t* tile, int coff, int p) {
+  const uint8_t* c = tile + coff;
   const int off[16] = {3 * p,      3 * p + 1,  2 * p + 2,  p + 3,       3,  -p + 3,
                        -2 * p + 2, -3 * p + 1, -3 * p,     -3 * p - 1, -2 * p - 2, -p - 3,
                        -3,         p - 3,      2 * p - 2,  3 * p - 1};
+#if FC_SCORE_RAW
+  // one base at the ring's top-left corner: every read is a non-negative
+  // immediate offset when p is a compile-time constant
+  // (the base offset is made opaque: hipcc would otherwise fold it back into
+  // c + off[k] and add the negative offsets one by one)
+  int o0 = coff - (3 * p + 3);
+  if (CONST_P) __asm__ volatile("" : "+v"(o0));
+  uint32_t r[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) r[k] = tile[o0 + off[k] + 3 * p + 3];
+  h16x2 w3[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    w3[k] = __builtin_bit_cast(h16x2, pk_min3_negpair(r[k], r[(k + 1) & 15], r[(k + 2) & 15]));
+#else
   const _Float16 v = __builtin_bit_cast(_Float16, (uint16_t)c[0]);
   const h16x2 vv = {v, -v}, sg = {(_Float16)-1.0f, (_Float16)1.0f};
   h16x2 q[16];
@@ -810,6 +842,7 @@ __device__ __forceinline__ int fast_score_u8(const uint8_t* c, int p) {
   for (int k = 0; k < 16; ++k)
     w3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(q[k], q[(k + 1) & 15]),
                                           q[(k + 2) & 15]);
+#endif
   h16x2 w9[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k)
@@ -823,12 +856,23 @@ __device__ __forceinline__ int fast_score_u8(const uint8_t* c, int p) {
   m5[5] = w9[15];
   const h16x2 ma = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m5[0], m5[1]), m5[2]);
   const h16x2 mb = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m5[3], m5[4]), m5[5]);
-  const h16x2 best = __builtin_elementwise_maximum(ma, mb);
+  h16x2 best = __builtin_elementwise_maximum(ma, mb);
+#if FC_SCORE_RAW
+  {
+    const _Float16 v = __builtin_bit_cast(_Float16, (uint16_t)c[0]);
+    const h16x2 vv = {v, -v};
+    best = best + vv;  // (dark, bright): exact sums of subnormals
+  }
+#endif
   // the subnormal's bit pattern is the integer strength; negative -> 0
   const int s = (int)(short)__builtin_bit_cast(uint16_t, __builtin_fmaxf16(best.x, best.y));
   return min(max(s, 0), 255);
 }
 
+// PT > 0: the launch's LDS row pitch as a compile-time constant (every cell's
+// rows at pitch PT >= fc_pitch(C)), so every ring / neighbour / row read is an
+// immediate offset from one address; PT = 0: per-cell fc_pitch(C)
+template <int PT>
 __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
@@ -889,7 +933,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   const int R = cd.y1 - cd.y0, C = cd.x1 - cd.x0;
   const long long slot = (long long)img * plan.ncells + ci;
   const bool tiny = R < 7 || C < 7;
-  const int P = fc_pitch(C);
+  const int P = PT ? PT : fc_pitch(C);
   if (!tiny && lane < R) {
     const int nS = ((C + 20) & ~7) >> 2;  // dwords per row (<= 14, host-checked)
     uint2* dst = reinterpret_cast<uint2*>(tile + lane * P);
@@ -937,12 +981,12 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
         if (fresh) {
           // phase A queues interior pixels only (fast_pass masks the columns
           // past the window), and none has a strength yet: no strength read
-          m = fast_score_u8(tile + off, P);
+          m = fast_score_u8<(PT != 0)>(tile, off, P);
           sc[off] = (uint8_t)m;
         } else {
           m = sc[off];  // 0: not scored yet; phase B keeps phase-A strengths
           if (m == 0) {
-            m = fast_score_u8(tile + off, P);
+            m = fast_score_u8<(PT != 0)>(tile, off, P);
             sc[off] = (uint8_t)m;
           }
         }
@@ -1124,10 +1168,12 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
           y = ry - 3;
           x = off - ry * P - 8;
         }
-        const uint8_t* cp = sc + off;
-        m = cp[0];
-        const int r0 = cp[-P - 1], r1 = cp[-P], r2 = cp[-P + 1], r3 = cp[-1], r4 = cp[1],
-                  r5 = cp[P - 1], r6 = cp[P], r7 = cp[P + 1];
+        int oq = off - P - 1;  // 3x3 window from its top-left byte (opaque: see fast_score_u8)
+        if (PT) __asm__ volatile("" : "+v"(oq));
+        const uint8_t* cq = sc + oq;
+        m = cq[P + 1];
+        const int r0 = cq[0], r1 = cq[1], r2 = cq[2], r3 = cq[P], r4 = cq[P + 2],
+                  r5 = cq[2 * P], r6 = cq[2 * P + 1], r7 = cq[2 * P + 2];
         const bool L = x > 0, Rt = x < iw - 1, U = y > 0, D = y < ih - 1;
         const int nb[8] = {(U && L) ? r0 : 0, U ? r1 : 0, (U && Rt) ? r2 : 0, L ? r3 : 0,
                            Rt ? r4 : 0, (D && L) ? r5 : 0, D ? r6 : 0, (D && Rt) ? r7 : 0};
@@ -2468,16 +2514,25 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
     }
   const int tileElems = fc_tile_elems(mr, mc);
   const size_t lds = orb_k_fast_cells_lds(mr, mc);
+  // every W = 30 cell grid of the ORB-SLAM2 configurations has ROI widths of
+  // 36-43 pixels: pitch 56, the compile-time instance
+  static const bool noConstPitch = getenv("ORB_FAST_RT_PITCH") && atoi(getenv("ORB_FAST_RT_PITCH")) > 0;
+  const bool p56 = fc_pitch(mc) == 56 && !noConstPitch;
+  const void* fn = p56 ? (const void*)k_fast_cells<56> : (const void*)k_fast_cells<0>;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_fast_cells,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   const int n = cellEnd - cellBeg;
   dim3 grid((n + FC_WAVES * FC_CPW - 1) / (FC_WAVES * FC_CPW), nimg), block(64 * FC_WAVES);
-  hipLaunchKernelGGL(k_fast_cells, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, *plan, cells, cellKeys, cellCount, tileElems, cellBeg, cellEnd,
-                     errFlag);
+  if (p56)
+    hipLaunchKernelGGL(k_fast_cells<56>, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
+                       arenaPitch, *plan, cells, cellKeys, cellCount, tileElems, cellBeg, cellEnd,
+                       errFlag);
+  else
+    hipLaunchKernelGGL(k_fast_cells<0>, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
+                       arenaPitch, *plan, cells, cellKeys, cellCount, tileElems, cellBeg, cellEnd,
+                       errFlag);
   return hipGetLastError();
 }
 
