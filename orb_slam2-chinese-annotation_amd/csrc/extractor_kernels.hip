@@ -778,7 +778,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // 0 (ROI column 3), groups of 8 interior pixels read [8k, 8k + 24)
 __host__ __device__ inline int fc_pitch(int C) { return ((C + 20) & ~7) + FC_PAD; }
 __host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
-  return maxRows * fc_pitch(maxCols);
+  return (maxRows * fc_pitch(maxCols) + 15) & ~15;  // 16-byte aligned strength map
 }
 __host__ __device__ inline int fc_wave_bytes(int tileElems) {
   // byte tile + strengths + queue + corners + 64 rows x 64-bit bitmap
@@ -944,6 +944,14 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
                             __builtin_amdgcn_alignbyte(raw[2 * k + 2], raw[2 * k + 1], rsh));
     }
   }
+#if FC_ROWMAJOR
+  // strengths start at 0 over the whole map: the halo and the columns past the
+  // interior are never scored, so NMS reads 0 there without bounds tests
+  {
+    uint4* sc16 = reinterpret_cast<uint4*>(tile + tileElems);
+    for (int i = lane; i < (tileElems >> 4); i += 64) sc16[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+#endif
   const int ciNext = jc + 1 < FC_CPW ? cell_of(jc + 1) : cellEnd;
   if (ciNext < cellEnd) {
     ncd = cells[ciNext];
@@ -957,7 +965,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   const int iw = C - 6, ih = R - 6;
   const int nK = (iw + 7) >> 3;  // 8-pixel groups per interior row
   const int nvLast = iw - 8 * (nK - 1);
-  const unsigned long long outsideLast =
+  [[maybe_unused]] const unsigned long long outsideLast =
       nvLast >= 8 ? 0ull : (0x0101010101010101ull << (8 * nvLast));
   const int ti = min(max(plan.iniTh, 0), 255), tm = min(max(plan.minTh, 0), 255);
   // quotients q = (int)((x + 0.5) * (1 / d)) for x < 2^13, d <= 88 are exact
@@ -1028,7 +1036,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     // strength map (u64 words): 4- and 8-byte lane strides
     [[maybe_unused]] const int trashQ = (int)(reinterpret_cast<uint16_t*>(bits) - queue) + 2 * lane;
     unsigned long long* const sc64 = reinterpret_cast<unsigned long long*>(sc);
-    const int trashS = (int)(reinterpret_cast<unsigned long long*>(bits) - sc64) + lane;
+    [[maybe_unused]] const int trashS = (int)(reinterpret_cast<unsigned long long*>(bits) - sc64) + lane;
     for (int g0 = 0; g0 < nG; g0 += 64) {
       const bool valid = g0 + pl < nG;
       const bool last = k == nK - 1;
@@ -1053,8 +1061,10 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       uint32_t rp[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) rp[i] = pretest_pair(V[i], Q0[i], Q4[i], Q8[i], Q12[i], T);
+#if !FC_ROWMAJOR
       if (fresh)  // strengths start at 0, FAST_OUTSIDE past the interior (o is a multiple of 8)
         sc64[valid ? (o >> 3) : trashS] = last ? outsideLast : 0ull;
+#endif
 #if FC_ROWMAJOR
       // lane-major append: lane = pixel group in row-major order, so the queue
       // (and the corner list built from it) is in cv::FAST's row-major order
@@ -1172,11 +1182,9 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
         if (PT) __asm__ volatile("" : "+v"(oq));
         const uint8_t* cq = sc + oq;
         m = cq[P + 1];
-        const int r0 = cq[0], r1 = cq[1], r2 = cq[2], r3 = cq[P], r4 = cq[P + 2],
-                  r5 = cq[2 * P], r6 = cq[2 * P + 1], r7 = cq[2 * P + 2];
-        const bool L = x > 0, Rt = x < iw - 1, U = y > 0, D = y < ih - 1;
-        const int nb[8] = {(U && L) ? r0 : 0, U ? r1 : 0, (U && Rt) ? r2 : 0, L ? r3 : 0,
-                           Rt ? r4 : 0, (D && L) ? r5 : 0, D ? r6 : 0, (D && Rt) ? r7 : 0};
+        // neighbours outside the interior read 0 (the map is cleared per cell)
+        const int nb[8] = {cq[0], cq[1], cq[2], cq[P], cq[P + 2], cq[2 * P], cq[2 * P + 1],
+                           cq[2 * P + 2]};
         ok = m > t && m >= 2;
 #pragma unroll
         for (int k = 0; k < 8; ++k) ok = ok && !(nb[k] > t && nb[k] >= m);
