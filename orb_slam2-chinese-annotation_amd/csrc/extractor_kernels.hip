@@ -2111,6 +2111,9 @@ struct DescWaveLds {
 #else
 #define DESC_LAUNCH_BOUNDS __launch_bounds__(256)
 #endif
+#ifndef DESC_LDS_TABLES
+#define DESC_LDS_TABLES 1  // rBRIEF pattern floats and column weights in LDS (k_orient_desc)
+#endif
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
@@ -2127,6 +2130,23 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // PPW == 0: ppwRt
   const int ppw = PPW ? PPW : ppwRt;
   __shared__ __attribute__((aligned(16))) DescWaveLds sm[4];
+#if DESC_LDS_TABLES
+  // per workgroup: the rBRIEF pattern as floats (one ds_read_b128 per test
+  // pair of points instead of a constant-memory load and four conversions),
+  // and the column-pass weights of both row parities (one ds_read_b128 per
+  // sample instead of four selects)
+  __shared__ __attribute__((aligned(16))) float4 sPat[ORB_PATTERN_POINTS / 2];
+  __shared__ __attribute__((aligned(16))) uint4 sW[2];
+  {
+    const int t = threadIdx.x;  // 256 threads, 256 tests
+    sPat[t] = make_float4((float)c_pattern[4 * t], (float)c_pattern[4 * t + 1],
+                          (float)c_pattern[4 * t + 2], (float)c_pattern[4 * t + 3]);
+    if (t < 2)  // even rows: (18,34) (49,55) (49,34) (18,0); odd: (0,18) (34,49) (55,49) (34,18)
+      sW[t] = t == 0 ? make_uint4(18u | 34u << 16, 49u | 55u << 16, 49u | 34u << 16, 18u)
+                     : make_uint4(18u << 16, 34u | 49u << 16, 55u | 49u << 16, 34u | 18u << 16);
+    __syncthreads();  // before any wave can leave early
+  }
+#endif
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31;
   int bx, img;
@@ -2361,6 +2381,24 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
                             __builtin_bit_cast(uint32_t, E2), __builtin_bit_cast(uint32_t, E3)};
     const uint32_t wO[4] = {__builtin_bit_cast(uint32_t, O0), __builtin_bit_cast(uint32_t, O1),
                             __builtin_bit_cast(uint32_t, O2), __builtin_bit_cast(uint32_t, O3)};
+#if DESC_LDS_TABLES
+    (void)wE;
+    (void)wO;
+    auto blurred = [&](int ry, int rx) -> int {
+      const int y = ry + 18;  // 0..36
+      // pair row y >> 1, column rx + 18: (y & ~1) * (DESC_RS_DW / 2) + rx is
+      // one 24-bit multiply-add
+      const uint32_t* p = &rsp[0][0] + ((y & ~1) * (DESC_RS_DW / 2) + rx + 18);
+      const uint4 wv = sW[y & 1];
+      const uint32_t wk[4] = {wv.x, wv.y, wv.z, wv.w};
+      uint32_t s = 1u << 15;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        s = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p[k * DESC_RS_DW]),
+                                   __builtin_bit_cast(u16x2, wk[k]), s, false);
+      return min((int)(s >> 16), 255);
+    };
+#else
     auto blurred = [&](int ry, int rx) -> int {
       const int y = ry + 18;
       const uint32_t* p = &rsp[y >> 1][rx + 18];
@@ -2372,12 +2410,18 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
                                    __builtin_bit_cast(u16x2, odd ? wO[k] : wE[k]), s, false);
       return min((int)(s >> 16), 255);
     };
+#endif
     unsigned long long words[8];
 #pragma unroll
     for (int kq = 0; kq < 8; ++kq) {
       const int test = hl + 32 * kq;
+#if DESC_LDS_TABLES
+      const float4 pt = sPat[test];
+      const float px0 = pt.x, py0 = pt.y, px1 = pt.z, py1 = pt.w;
+#else
       const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
       const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
+#endif
       const int v0 = blurred(cv_round(px0 * b + py0 * a), cv_round(px0 * a - py0 * b));
       const int v1 = blurred(cv_round(px1 * b + py1 * a), cv_round(px1 * a - py1 * b));
       words[kq] = __ballot(v0 < v1);
