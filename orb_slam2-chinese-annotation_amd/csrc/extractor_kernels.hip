@@ -2353,9 +2353,11 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
           o[h][3] = __builtin_amdgcn_udot4(w0, T3a, __builtin_amdgcn_udot4(w1, T3b,
                                            __builtin_amdgcn_udot4(w2, T3c, 0u, false), false), false);
         }
+        // (row sums are < 2^16: one v_perm packs the pair)
+        auto pk = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); };
         *reinterpret_cast<uint4*>(&rsp[hl][4 * g]) =
-            make_uint4(o[0][0] | (o[1][0] << 16), o[0][1] | (o[1][1] << 16),
-                       o[0][2] | (o[1][2] << 16), o[0][3] | (o[1][3] << 16));
+            make_uint4(pk(o[0][0], o[1][0]), pk(o[0][1], o[1][1]), pk(o[0][2], o[1][2]),
+                       pk(o[0][3], o[1][3]));
       }
     }
     if (j + 1 < ppw) {
