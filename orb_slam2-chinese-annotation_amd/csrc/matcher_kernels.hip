@@ -783,10 +783,28 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
     hipLaunchKernelGGL(k_proj_resolve<8>, dim3(nproblems), dim3(512), lds, s, keys, desc, uright,
                        locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
                        P, topk, ncand, kpMatch, nmatches);
-  else
-    hipLaunchKernelGGL(k_proj_resolve<4>, dim3(nproblems), dim3(256), lds, s, keys, desc, uright,
-                       locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
-                       P, topk, ncand, kpMatch, nmatches);
+  else {
+    // waves per problem for small maps: each problem's workgroup holds its
+    // waves for the whole sequential resolve.  Batches (>= 128 problems, run
+    // beside the next launch's extraction) take one wave per problem: the
+    // longer per-problem chain is hidden and the extraction keeps the CU slots
+    // (bench 306.5k vs 304.9k frames/s with four, profiles/r03_resolve_nw.txt);
+    // a few problems per call keep four waves for latency.  ORB_RESOLVE_NW overrides.
+    static const int nwEnv = getenv("ORB_RESOLVE_NW") ? atoi(getenv("ORB_RESOLVE_NW")) : 0;
+    const int nw = nwEnv > 0 ? nwEnv : (nproblems >= 128 ? 1 : 4);
+    if (nw == 1)
+      hipLaunchKernelGGL(k_proj_resolve<1>, dim3(nproblems), dim3(64), lds, s, keys, desc, uright,
+                         locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
+                         P, topk, ncand, kpMatch, nmatches);
+    else if (nw == 2)
+      hipLaunchKernelGGL(k_proj_resolve<2>, dim3(nproblems), dim3(128), lds, s, keys, desc, uright,
+                         locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
+                         P, topk, ncand, kpMatch, nmatches);
+    else
+      hipLaunchKernelGGL(k_proj_resolve<4>, dim3(nproblems), dim3(256), lds, s, keys, desc, uright,
+                         locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
+                         P, topk, ncand, kpMatch, nmatches);
+  }
   return hipGetLastError();
 }
 

@@ -24,16 +24,14 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
   const float p5 = 0.1555786518463281f * r2d, p7 = -0.04432655554792128f * r2d;
   const float eps = (float)2.2204460492503131e-16;
   const float ax = fabsf(x), ay = fabsf(y);
-  float a;
-  if (ax >= ay) {
-    const float c = __fdiv_rn(ay, ax + eps);
-    const float c2 = c * c;
-    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-  } else {
-    const float c = __fdiv_rn(ax, ay + eps);
-    const float c2 = c * c;
-    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-  }
+  // both branches of the reference's if / else as selects (the same float
+  // operations in the same order; no divergent branch between the two
+  // keypoints a wave orients)
+  const bool xm = ax >= ay;
+  const float c = __fdiv_rn(xm ? ay : ax, (xm ? ax : ay) + eps);
+  const float c2 = c * c;
+  const float pa = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  float a = xm ? pa : 90.f - pa;
   if (x < 0) a = 180.f - a;
   if (y < 0) a = 360.f - a;
   return a;
