@@ -2111,6 +2111,12 @@ struct DescWaveLds {
 #else
 #define DESC_LAUNCH_BOUNDS __launch_bounds__(256)
 #endif
+#ifndef DESC_MFMA_ROWS
+// 1: row pass on the matrix cores (v_mfma_i32_16x16x64_i8). Bit-exact but
+// slower: orient 0.495 vs 0.422 ms per 512 frames (124 vs 97 VGPRs, 35 KB LDS
+// per workgroup; profiles/r03_orient_mfma.txt), so the VALU dot4 pass stays.
+#define DESC_MFMA_ROWS 0
+#endif
 #ifndef DESC_LDS_TABLES
 #define DESC_LDS_TABLES 1  // rBRIEF pattern floats and column weights in LDS (k_orient_desc)
 #endif
@@ -2137,8 +2143,26 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // sample instead of four selects)
   __shared__ __attribute__((aligned(16))) float4 sPat[ORB_PATTERN_POINTS / 2];
   __shared__ __attribute__((aligned(16))) uint4 sW[2];
+#if DESC_MFMA_ROWS
+  // row pass as a product on the matrix cores: rows x bytes (signed, x - 128)
+  // times the 64 x 48 Toeplitz matrix of the 7 taps (column c takes bytes
+  // c..c+6); sB[n][lane] = lane's B fragment of column tile n
+  __shared__ __attribute__((aligned(16))) uint4 sB[3][64];
+#endif
   {
     const int t = threadIdx.x;  // 256 threads, 256 tests
+#if DESC_MFMA_ROWS
+    if (t < 192) {
+      const int n = t >> 6, l = t & 63, c = 16 * n + (l & 15);
+      const uint32_t taps[7] = {18, 34, 49, 55, 49, 34, 18};
+      uint32_t wd[4] = {0u, 0u, 0u, 0u};
+      for (int j = 0; j < 16; ++j) {
+        const int d = 16 * (l >> 4) + j - c;  // byte b = 16 (l >> 4) + j of column c
+        if (d >= 0 && d <= 6) wd[j >> 2] |= taps[d] << (8 * (j & 3));
+      }
+      sB[n][l] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    }
+#endif
     sPat[t] = make_float4((float)c_pattern[4 * t], (float)c_pattern[4 * t + 1],
                           (float)c_pattern[4 * t + 2], (float)c_pattern[4 * t + 3]);
     if (t < 2)  // even rows: (18,34) (49,55) (49,34) (18,0); odd: (0,18) (34,49) (55,49) (34,18)
@@ -2253,10 +2277,10 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     dst[2] = make_uint4(d[8], d[9], d[10], d[11]);
   };
   constexpr uint32_t k0 = 18, k1 = 34, k2 = 49, k3 = 55, k4 = 49, k5 = 34, k6 = 18;
-  constexpr uint32_t T0a = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), T0b = k4 | (k5 << 8) | (k6 << 16);
-  constexpr uint32_t T1a = (k0 << 8) | (k1 << 16) | (k2 << 24), T1b = k3 | (k4 << 8) | (k5 << 16) | (k6 << 24);
-  constexpr uint32_t T2a = (k0 << 16) | (k1 << 24), T2b = k2 | (k3 << 8) | (k4 << 16) | (k5 << 24), T2c = k6;
-  constexpr uint32_t T3a = k0 << 24, T3b = k1 | (k2 << 8) | (k3 << 16) | (k4 << 24), T3c = k5 | (k6 << 8);
+  [[maybe_unused]] constexpr uint32_t T0a = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), T0b = k4 | (k5 << 8) | (k6 << 16);
+ [[maybe_unused]] constexpr uint32_t T1a = (k0 << 8) | (k1 << 16) | (k2 << 24), T1b = k3 | (k4 << 8) | (k5 << 16) | (k6 << 24);
+ [[maybe_unused]] constexpr uint32_t T2a = (k0 << 16) | (k1 << 24), T2b = k2 | (k3 << 8) | (k4 << 16) | (k5 << 24), T2c = k6;
+ [[maybe_unused]] constexpr uint32_t T3a = k0 << 24, T3b = k1 | (k2 << 8) | (k3 << 16) | (k4 << 24), T3c = k5 | (k6 << 8);
   typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
   const u16x2 E0 = {18, 34}, E1 = {49, 55}, E2 = {49, 34}, E3 = {18, 0};
   const u16x2 O0 = {0, 18}, O1 = {34, 49}, O2 = {55, 49}, O3 = {34, 18};
@@ -2338,6 +2362,58 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       wave_lds_sync();
     }
     // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
+#if DESC_MFMA_ROWS
+    // On the matrix cores: each half-wave stages its keypoint's 44 rows as
+    // signed bytes (x - 128) at a 64-byte pitch in that keypoint's row-sum
+    // area; per keypoint, the 3 row tiles (A fragments) are read, then 3 x 3
+    // v_mfma_i32_16x16x64_i8 against the Toeplitz column tiles, each result
+    // biased by 128 * 257 (the taps' sum) and packed into the row-sum pairs,
+    // overwriting the staging (every fragment is in registers by then).
+    // Bytes 48..63 and rows 44..47 of the staging are never written: they only
+    // reach the padding columns 40..47 and rows 44..47, which are not stored.
+    if (second) {
+      uint4* st0 = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(&rsp[0][0]) + 128 * hl);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        st0[q] = make_uint4(ra[4 * q] ^ 0x80808080u, ra[4 * q + 1] ^ 0x80808080u,
+                            ra[4 * q + 2] ^ 0x80808080u, ra[4 * q + 3] ^ 0x80808080u);
+        st0[4 + q] = make_uint4(rb[4 * q] ^ 0x80808080u, rb[4 * q + 1] ^ 0x80808080u,
+                                rb[4 * q + 2] ^ 0x80808080u, rb[4 * q + 3] ^ 0x80808080u);
+      }
+    }
+    wave_lds_sync();
+    {
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+      for (int kp = 0; kp < 2; ++kp) {
+        uint32_t* area = &sm[w].rsp[kp][0][0];
+        const uint8_t* stg = reinterpret_cast<const uint8_t*>(area);
+        v4i a[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+          a[m] = *reinterpret_cast<const v4i*>(stg + (16 * m + lr) * 64 + 16 * lq);
+#pragma unroll
+        for (int n = 0; n < 3; ++n) {
+          const v4i bf = __builtin_bit_cast(v4i, sB[n][lane]);
+#pragma unroll
+          for (int m = 0; m < 3; ++m) {
+            // C = the bias 128 * (18 + 34 + 49 + 55 + 49 + 34 + 18) = 32896
+            const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[m], bf, (v4i){32896, 32896, 32896, 32896},
+                                                                  0, 0, 0);
+            const int c = 16 * n + lr, r0 = 16 * m + 4 * lq;  // D: column lr, rows r0 .. r0 + 3
+            if ((n < 2 || c < 40) && (m < 2 || r0 < 44)) {
+              area[(r0 >> 1) * DESC_RS_DW + c] =
+                  __builtin_amdgcn_perm((uint32_t)acc[1], (uint32_t)acc[0], 0x05040100u);
+              area[((r0 >> 1) + 1) * DESC_RS_DW + c] =
+                  __builtin_amdgcn_perm((uint32_t)acc[3], (uint32_t)acc[2], 0x05040100u);
+            }
+          }
+        }
+      }
+    }
+#else
+    // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
     if (second) {  // the lane's row pair from registers, group by group
 #pragma unroll
       for (int g = 0; g < 10; ++g) {
@@ -2360,6 +2436,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
                        pk(o[0][3], o[1][3]));
       }
     }
+#endif
     if (j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
