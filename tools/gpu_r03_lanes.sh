@@ -1,0 +1,38 @@
+#!/bin/bash
+# A/B: extraction lanes (two extractor handles on streams of their own) against
+# the one-lane pipeline; each variant one bench run without the extra legs.
+set -eo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p "$O"
+cd "$R"
+Q="--no-cpu --no-secondary --host-frames 0"
+run() {  # tag, env...
+  local tag=$1; shift
+  env "$@" timeout -k 10 240 python bench.py $Q > "$O/lanes_$tag.json" 2> "$O/lanes_$tag.err"
+  python - "$O/lanes_$tag.json" "$tag" <<'P'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], round(d["value"]), round(d["ms_per_step"], 3), flush=True)
+P
+}
+if [ "$1" = "sweep2" ]; then
+  run base ORB_BENCH_LANES=1
+  run l2s ORB_BENCH_LANES=2
+  run l3s ORB_BENCH_LANES=3
+  run l4s ORB_BENCH_LANES=4
+  Q="$Q --batch 512"
+  run l2s_b512 ORB_BENCH_LANES=2
+  run l3s_b512 ORB_BENCH_LANES=3
+  run l4s_b512 ORB_BENCH_LANES=4
+  Q="${Q% --batch 512}"
+  run l2s_r ORB_BENCH_LANES=2
+  run base_r ORB_BENCH_LANES=1
+  exit 0
+fi
+run base ORB_BENCH_LANES=1
+run l2s ORB_BENCH_LANES=2 ORB_BENCH_LANE_MATCH=stream
+run l2i ORB_BENCH_LANES=2 ORB_BENCH_LANE_MATCH=inlane
+run l2i_ss0 ORB_BENCH_LANES=2 ORB_BENCH_LANE_MATCH=inlane ORB_SIDE_SHARED=0
+run l2s_ss0 ORB_BENCH_LANES=2 ORB_BENCH_LANE_MATCH=stream ORB_SIDE_SHARED=0
+run base2 ORB_BENCH_LANES=1
