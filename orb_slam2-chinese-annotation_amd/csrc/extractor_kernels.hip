@@ -2463,12 +2463,18 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
 #if DESC_LDS_TABLES
     (void)wE;
     (void)wO;
+    // the patch centre's row-sum pair (an opaque base: hipcc would split the
+    // constant between the address and the 8-bit ds_read2 offsets)
+    const uint32_t* rs0 = &sm[0].rsp[0][0][0];
+    int rsc = (int)(&rsp[0][0] - rs0) + (18 * (DESC_RS_DW / 2) + 18);
+    __asm__ volatile("" : "+v"(rsc));
     auto blurred = [&](int ry, int rx) -> int {
-      const int y = ry + 18;  // 0..36
-      // pair row y >> 1, column rx + 18: (y & ~1) * (DESC_RS_DW / 2) + rx is
-      // one 24-bit multiply-add
-      const uint32_t* p = &rsp[0][0] + ((y & ~1) * (DESC_RS_DW / 2) + rx + 18);
-      const uint4 wv = sW[y & 1];
+      // pair row (ry + 18) >> 1, column rx + 18: the constant part folds into
+      // the LDS offset, (ry & ~1) * (DESC_RS_DW / 2) is a signed 24-bit
+      // multiply (ry is -18..18; hipcc cannot bound a plain int product and
+      // emits the quarter-rate v_mul_lo_u32), the parity row is ry & 1
+      const uint32_t* p = rs0 + (rsc + __mul24(ry & ~1, DESC_RS_DW / 2) + rx);
+      const uint4 wv = sW[ry & 1];
       const uint32_t wk[4] = {wv.x, wv.y, wv.z, wv.w};
       uint32_t s = 1u << 15;
 #pragma unroll

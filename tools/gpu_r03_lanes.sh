@@ -16,6 +16,17 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(sys.argv[2], round(d["value"]), round(d["ms_per_step"], 3), flush=True)
 P
 }
+if [ "$1" = "sweep3" ]; then  # schedule knobs under two lanes
+  run l2 ORB_BENCH_LANES=2
+  run l2_side1 ORB_BENCH_LANES=2 ORB_FAST_SIDE_LEVELS=1
+  run l2_side3 ORB_BENCH_LANES=2 ORB_FAST_SIDE_LEVELS=3
+  run l2_side0 ORB_BENCH_LANES=2 ORB_FAST_SIDE_LEVELS=0
+  run l2_s2norm ORB_BENCH_LANES=2 ORB_STREAM2_PRIO=normal
+  run l2_q8 ORB_BENCH_LANES=2 GPU_MAX_HW_QUEUES=8
+  run l3_q8 ORB_BENCH_LANES=3 GPU_MAX_HW_QUEUES=8
+  run l2_r ORB_BENCH_LANES=2
+  exit 0
+fi
 if [ "$1" = "sweep2" ]; then
   run base ORB_BENCH_LANES=1
   run l2s ORB_BENCH_LANES=2
