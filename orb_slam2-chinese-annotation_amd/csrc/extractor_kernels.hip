@@ -2120,6 +2120,9 @@ struct DescWaveLds {
 #ifndef DESC_LDS_TABLES
 #define DESC_LDS_TABLES 1  // rBRIEF pattern floats and column weights in LDS (k_orient_desc)
 #endif
+#ifndef DESC_MAGIC_ROUND
+#define DESC_MAGIC_ROUND 1  // rBRIEF sample coordinates rounded by the 1.5 * 2^23 adder
+#endif
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
@@ -2468,13 +2471,29 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     const uint32_t* rs0 = &sm[0].rsp[0][0][0];
     int rsc = (int)(&rsp[0][0] - rs0) + (18 * (DESC_RS_DW / 2) + 18);
     __asm__ volatile("" : "+v"(rsc));
-    auto blurred = [&](int ry, int rx) -> int {
+#if DESC_MAGIC_ROUND
+    // cvRound by the adder: for |v| < 2^22, the bits of v + 1.5 * 2^23 are
+    // 0x4B400000 + rint(v) (round half to even, as rintf), so a coordinate
+    // costs one v_add_f32 instead of v_rndne + v_cvt; the biases of both
+    // coordinates go into the base (0x4B400000 is even: parity and ry & ~1
+    // read the same bits; its low 24 bits 0x400000 keep the signed 24-bit
+    // multiply's operand positive)
+    rsc -= 0x400000 * (DESC_RS_DW / 2) + 0x4B400000;
+    auto blurred = [&](float fy, float fx) -> int {
+      const int by = __builtin_bit_cast(int, fy + 12582912.0f);
+      const int bx = __builtin_bit_cast(int, fx + 12582912.0f);
+      const uint32_t* p = rs0 + (rsc + __mul24(by & ~1, DESC_RS_DW / 2) + bx);
+      const uint4 wv = sW[by & 1];
+#else
+    auto blurred = [&](float fy, float fx) -> int {
+      const int ry = cv_round(fy), rx = cv_round(fx);
       // pair row (ry + 18) >> 1, column rx + 18: the constant part folds into
       // the LDS offset, (ry & ~1) * (DESC_RS_DW / 2) is a signed 24-bit
       // multiply (ry is -18..18; hipcc cannot bound a plain int product and
       // emits the quarter-rate v_mul_lo_u32), the parity row is ry & 1
       const uint32_t* p = rs0 + (rsc + __mul24(ry & ~1, DESC_RS_DW / 2) + rx);
       const uint4 wv = sW[ry & 1];
+#endif
       const uint32_t wk[4] = {wv.x, wv.y, wv.z, wv.w};
       uint32_t s = 1u << 15;
 #pragma unroll
@@ -2484,7 +2503,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       return min((int)(s >> 16), 255);
     };
 #else
-    auto blurred = [&](int ry, int rx) -> int {
+    auto blurred = [&](float fy, float fx) -> int {
+      const int ry = cv_round(fy), rx = cv_round(fx);
       const int y = ry + 18;
       const uint32_t* p = &rsp[y >> 1][rx + 18];
       uint32_t s = 1u << 15;
@@ -2507,8 +2527,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
       const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
 #endif
-      const int v0 = blurred(cv_round(px0 * b + py0 * a), cv_round(px0 * a - py0 * b));
-      const int v1 = blurred(cv_round(px1 * b + py1 * a), cv_round(px1 * a - py1 * b));
+      const int v0 = blurred(px0 * b + py0 * a, px0 * a - py0 * b);
+      const int v1 = blurred(px1 * b + py1 * a, px1 * a - py1 * b);
       words[kq] = __ballot(v0 < v1);
     }
     if (P.active && hl == 0) {
