@@ -693,6 +693,7 @@ def main():
     ext.profile(True)
     matcher.profile(True)
     t0 = time.perf_counter()
+    g_first = g
     for k in range(args.steps):
         for _ in range(NB):
             launch(g)
@@ -727,6 +728,8 @@ def main():
     # The extract stream is the critical path (the matcher stream runs in its
     # shadow, so matcher kernel times include time-sharing with the next
     # launch's extraction): the roofline kernel is the longest extraction kernel.
+    # the profiled handle is lane 0's: it ran every L-th launch of the region
+    n_prof = sum(1 for gg in range(g_first, g) if gg % L == 0)
     kern, ext_kern = {}, []
     for st in range(6):
         name, ms, n = ext.profile_read(st)
@@ -741,7 +744,7 @@ def main():
     for name in [k for k in ext_kern if k.endswith("_side")]:
         ms0, _ = kern.pop(name)
         ext_kern.remove(name)
-        side_ms[name] = ms0 / (args.steps * NB)
+        side_ms[name] = ms0 / n_prof
         base = name[:-5]
         if base in kern:
             ms1, n1 = kern[base]
@@ -762,7 +765,7 @@ def main():
     dom_ms_per_launch = kern[dom][0] / max(kern[dom][1], 1)
     # bytes one launch of the dominant kernel processes (B frames; the resize
     # runs nlevels-1 launches per extraction)
-    launches_per_extract = kern[dom][1] / (args.steps * NB)
+    launches_per_extract = kern[dom][1] / n_prof
     dom_bytes = alg[dom] * B / launches_per_extract
     hbm_gbs = dom_bytes / (dom_ms_per_launch * 1e-3) / 1e9
     traffic, traffic_src = measured_traffic(dom, B)
@@ -833,7 +836,7 @@ def main():
         },
         "roofline": roof,
         "kernels_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kern.items()},
-        "extraction_kernels_ms_per_launch": sum(kern[k][0] for k in ext_kern) / (args.steps * NB),
+        "extraction_kernels_ms_per_launch": sum(kern[k][0] for k in ext_kern) / n_prof,
         "extraction_call_ms_per_launch": call_ms / max(call_n, 1),
         "fast_side_stream_ms_per_launch": side_ms,
         "host_input": host,

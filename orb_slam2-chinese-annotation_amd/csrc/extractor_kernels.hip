@@ -2123,6 +2123,9 @@ struct DescWaveLds {
 #ifndef DESC_MAGIC_ROUND
 #define DESC_MAGIC_ROUND 1  // rBRIEF sample coordinates rounded by the 1.5 * 2^23 adder
 #endif
+#ifndef DESC_ROW37
+#define DESC_ROW37 1     // row pass stops at column 36, the last one a sample reaches
+#endif
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
@@ -2309,7 +2312,9 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     }
     // ---- IC_Angle from the rows in registers: row v = ri - 15 is staged row
     // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
-    // by one byte).  m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
+    // by one byte; reading dwords 1..9 as loaded under byte-shifted masks
+    // measured slower: 0.464 vs 0.414 ms per 512 frames, profiles/r03_orient_row37.txt).
+    // m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
     int m01 = 0, m10 = 0;
     auto ic_row = [&](const uint32_t* d, const uint32_t* mk, int ri) {  // staged row ri + 6, ri in [0, 31)
       uint32_t rs = 0, rm = 0;
@@ -2418,8 +2423,16 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
 #else
     // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
     if (second) {  // the lane's row pair from registers, group by group
+      // (samples reach columns 0..36 only: |rotated pattern point| <= 18.4,
+      // so the last group computes column 36 alone)
 #pragma unroll
       for (int g = 0; g < 10; ++g) {
+        if (DESC_ROW37 && g == 9) {
+          const uint32_t c0 = __builtin_amdgcn_udot4(ra[9], T0a, __builtin_amdgcn_udot4(ra[10], T0b, 0u, false), false);
+          const uint32_t c1 = __builtin_amdgcn_udot4(rb[9], T0a, __builtin_amdgcn_udot4(rb[10], T0b, 0u, false), false);
+          rsp[hl][36] = __builtin_amdgcn_perm(c1, c0, 0x05040100u);
+          break;
+        }
         uint32_t o[2][4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {

@@ -59,13 +59,15 @@ __device__ __forceinline__ void pinned_sincos(float angle, float* s_out, float* 
   const double hz = 0.5 * z, w = 1.0 - hz;
   const double cs = w + (((1.0 - w) - hz) + z * pc);
   const int q = ((int)k) & 3;
-  double s, c;
-  if (q == 0) { s = sn; c = cs; }
-  else if (q == 1) { s = cs; c = -sn; }
-  else if (q == 2) { s = -sn; c = -cs; }
-  else { s = -cs; c = sn; }
-  *s_out = (float)s;
-  *c_out = (float)c;
+  // quadrant q: (s, c) = (sn, cs), (cs, -sn), (-sn, -cs), (-cs, sn).  Rounding
+  // to float commutes with negation, so both are rounded first and the
+  // quadrant is applied as selects and sign flips (no divergent branch
+  // between the two keypoints a wave orients)
+  const float fs = (float)sn, fc = (float)cs;
+  const bool odd = q & 1;
+  const uint32_t sgnS = (uint32_t)(q & 2) << 30, sgnC = (uint32_t)((q + 1) & 2) << 30;
+  *s_out = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, odd ? fc : fs) ^ sgnS);
+  *c_out = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, odd ? fs : fc) ^ sgnC);
 }
 
 // ------------------------------------------------ A.7 pinned log (double)
