@@ -308,6 +308,9 @@ __device__ __forceinline__ unsigned long long bit_run(const uint32_t* bits, int 
   return n >= 64 ? v : (v & ((1ull << n) - 1ull));
 }
 
+#ifndef FC_PRETEST4
+#define FC_PRETEST4 0
+#endif
 // Compass pretest of a pixel pair (f16 halves): a pixel can be a FAST(t)
 // corner only if two circularly adjacent compass pixels (circle positions
 // 0,4,8,12) are both darker than v - t or both brighter than v + t.  Each
@@ -324,9 +327,17 @@ __device__ __forceinline__ uint32_t pretest_pair(uint32_t v, uint32_t q0, uint32
                                                 __builtin_elementwise_minimum(Q4, Q12));
   const h16x2 B = __builtin_elementwise_minimum(__builtin_elementwise_maximum(Q0, Q8),
                                                 __builtin_elementwise_maximum(Q4, Q12));
+#if FC_PRETEST4
+  // dark <=> V - A >= T, bright <=> B - V >= T: one max and one subtraction
+  // of T instead of V -+ T, two differences and an AND (exact: every operand
+  // is a small integer in f16)
+  const h16x2 r = __builtin_elementwise_maximum(V - A, B - V) - T;
+  return __builtin_bit_cast(uint32_t, r);
+#else
   const h16x2 x = (V - T) - A;  // >= +0: dark
   const h16x2 y = B - (V + T);  // >= +0: bright
   return __builtin_bit_cast(uint32_t, x) & __builtin_bit_cast(uint32_t, y);
+#endif
 }
 
 #ifdef ORB_FAST_STAMPS  // phase timing probe (tools/probe/fast_stamps.py), off by default
@@ -1385,8 +1396,32 @@ __device__ void block_bitonic_desc(unsigned long long* v, int n2) {
   }
 }
 
-#define OCT_MAX_PASSES 512
 #define OCT_RANK_MAX 512
+// Rank up to OCT_RANK_MAX distinct keys by counting (every thread scans the keys
+// as LDS broadcasts; RQ keys per thread), then scatter them sorted descending.
+template <int RQ>
+__device__ __forceinline__ void oct_rank_by_count(unsigned long long* sortBuf, int ncand, int t, int T) {
+  unsigned long long mine[RQ];
+  int rank[RQ];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int j = t + q * T;
+    mine[q] = j < ncand ? sortBuf[j] : 0ull;
+    rank[q] = 0;
+  }
+  for (int i = 0; i < ncand; ++i) {
+    const unsigned long long k = sortBuf[i];
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) rank[q] += k > mine[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < RQ; ++q)
+    if (t + q * T < ncand) sortBuf[rank[q]] = mine[q];
+  __syncthreads();
+}
+
+#define OCT_MAX_PASSES 512
 #define OCT_REG_KEYS 8  // keys per thread held in registers (n <= 8 x 512), small batches  // final-phase candidates ranked by counting (multiple of the 512 threads)
 
 template <bool REG, bool GNODES>
@@ -1611,24 +1646,11 @@ __global__ __launch_bounds__(512) void k_octree(
       // by counting (every thread scans the keys as LDS broadcasts: two
       // barriers) instead of the bitonic network's log^2 barrier steps.
       if (ncand <= OCT_RANK_MAX) {
-        unsigned long long mine[OCT_RANK_MAX / 512];
-        int rank[OCT_RANK_MAX / 512];
-#pragma unroll
-        for (int q = 0; q < OCT_RANK_MAX / 512; ++q) {
-          const int j = t + q * T;
-          mine[q] = j < ncand ? sortBuf[j] : 0ull;
-          rank[q] = 0;
-        }
-        for (int i = 0; i < ncand; ++i) {
-          const unsigned long long k = sortBuf[i];
-#pragma unroll
-          for (int q = 0; q < OCT_RANK_MAX / 512; ++q) rank[q] += k > mine[q];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < OCT_RANK_MAX / 512; ++q)
-          if (t + q * T < ncand) sortBuf[rank[q]] = mine[q];
-        __syncthreads();
+        // (OCT_RANK_MAX / T candidates per thread: workgroups of 256 or 512)
+        if (T >= OCT_RANK_MAX)
+          oct_rank_by_count<1>(sortBuf, ncand, t, T);
+        else
+          oct_rank_by_count<OCT_RANK_MAX / 256>(sortBuf, ncand, t, T);
       } else {
         block_bitonic_desc(sortBuf, m2);
       }
@@ -2744,7 +2766,14 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
   static const int maxPasses = getenv("ORB_OCTREE_MAX_PASSES")
                                    ? std::max(1, std::min(OCT_MAX_PASSES, atoi(getenv("ORB_OCTREE_MAX_PASSES"))))
                                    : OCT_MAX_PASSES;
-  dim3 grid(nimg, levelEnd - levelBeg), block(512);
+  // Batches take 256-thread workgroups: the octree alone is slower (0.150 vs
+  // 0.132 ms per 512 frames) but the smaller workgroups fit better beside the
+  // other lane's kernels (bench 317.0k / 316.6k vs 315.5k / 315.2k frames/s,
+  // two interleaved pairs, profiles/r03_octree256.txt); ORB_OCTREE_THREADS=512
+  // restores the old shape
+  static const int bthreads =
+      getenv("ORB_OCTREE_THREADS") && atoi(getenv("ORB_OCTREE_THREADS")) == 512 ? 512 : 256;
+  dim3 grid(nimg, levelEnd - levelBeg), block(reg ? 512 : bthreads);
 #define ORB_OCTREE_LAUNCH(R, G)                                                                 \
   hipLaunchKernelGGL((k_octree<R, G>), grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,  \
                      gNid, ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, \
