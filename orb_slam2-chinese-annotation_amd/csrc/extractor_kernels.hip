@@ -309,7 +309,7 @@ __device__ __forceinline__ unsigned long long bit_run(const uint32_t* bits, int 
 }
 
 #ifndef FC_PRETEST4
-#define FC_PRETEST4 0
+#define FC_PRETEST4 1
 #endif
 // Compass pretest of a pixel pair (f16 halves): a pixel can be a FAST(t)
 // corner only if two circularly adjacent compass pixels (circle positions
