@@ -14,7 +14,10 @@ mkdir -p "$O"
 cd "$R"
 timeout -k 10 400 python bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err"
 cd /tmp && export TMPDIR=/tmp
-SMALL="--no-cpu --no-secondary --frames 1024 --steps 10 --warmup 1 --host-frames 0"
+# the kernel-trace pass runs the bench's own timed workload (8192 resident
+# frames, two lanes, 60 steps) without the side legs, so its per-kernel averages
+# compare with the line's HIP-event times
+SMALL="--no-cpu --no-secondary --host-frames 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$TAG" -o run --output-format csv \
   -- python3 "$R/bench.py" $SMALL > "$O/prof_$TAG.json" 2> "$O/prof_$TAG.err"
 ORB_FAST_L0_INLINE=1 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$O/pmcf_$TAG" -o run --output-format csv \
