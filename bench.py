@@ -271,17 +271,23 @@ def new_stream(torch, dev, key):
     return _STREAMS[key]
 
 
-def pipelined(torch, dev, extract, match, n_sets, steps, warmup):
+def pipelined(torch, dev, extract, match, n_sets, steps, warmup, lanes=None):
     """Seconds per step of `extract(j, stream)` then `match(j, stream)` over
-    buffer set j = step % n_sets, pipelined on two streams: step k's match
-    overlaps step k+1's extraction; a set is rewritten only after its previous
-    match has finished (events).  Every step does all of its work."""
-    es, ms = new_stream(torch, dev, "extract"), new_stream(torch, dev, "match")
+    buffer set j = step % n_sets, pipelined: set j's extraction runs on lane
+    j % lanes (a stream of its own; each set has its own extractor handles),
+    every match on one match stream, so step k's match overlaps the next steps'
+    extraction; a set is rewritten only after its previous match has finished
+    (events).  Every step does all of its work."""
+    if lanes is None:
+        lanes = min(n_sets, max(1, int(os.environ.get("ORB_BENCH_LANES", "2"))))
+    ess = [new_stream(torch, dev, "extract" if i == 0 else f"extract{i}") for i in range(lanes)]
+    ms = new_stream(torch, dev, "match")
     ext_done = [torch.cuda.Event() for _ in range(n_sets)]
     match_done = [torch.cuda.Event() for _ in range(n_sets)]
 
     def one(g):
         j = g % n_sets
+        es = ess[j % lanes]
         if g >= n_sets:
             es.wait_event(match_done[j])
         extract(j, es.cuda_stream)
@@ -347,7 +353,7 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
     res = {"value": P / sec, "unit": "pairs/s", "pairs_per_step": P, "ms_per_step": sec * 1e3,
            "workload": f"1241x376 stereo pairs (frames 0..{P - 1} of seed {C3_SEED:#x}, left and "
                        "right views), 2000 feat/img, extraction x2 + ComputeStereoMatches, "
-                       "pipelined over two streams"}
+                       "pipelined over two extraction lanes and a match stream"}
     return res, dict(il=il, ir=ir, set0=sets[0], bf=bf, fx=fx)
 
 
@@ -357,6 +363,7 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
     per launch, pipelined as `pipelined`; also the matcher alone, serial on
     one stream.  Returns (result, state) with set 0's outputs for parity."""
     ext = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
+    exts = [ext, orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)]  # one per set (lane)
     scale = np.float32(ext.GetScaleFactors())
     cap = ext.capacity(W, H)
     d = torch.from_numpy(synth_images(orb, seed, list(range(B)), W, H, threads)).to(dev)
@@ -384,8 +391,8 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
 
     def extract(j, s):
         st = sets[j]
-        ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, st["k"].data_ptr(), st["de"].data_ptr(),
-                          cap, st["n"].data_ptr(), s)
+        exts[j].extract_batch(d.data_ptr(), B, W, H, W, W * H, st["k"].data_ptr(),
+                              st["de"].data_ptr(), cap, st["n"].data_ptr(), s)
 
     def match(j, s):
         st = sets[j]
@@ -407,7 +414,7 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
            "mean_matches": float(sets[0]["nm"].float().mean().item()),
            "workload": f"{W}x{H}, {NF} feat, extraction + SearchByProjection vs {M:,} map points "
                        f"(frames 0..{B - 1} of seed {seed}), {B} problems per launch, pipelined "
-                       "over two streams"}
+                       "over two extraction lanes and a match stream"}
     return res, dict(scale=scale, kh=kh, dh=dh, nh=nh, mps=mps, mpd=mpd, lk=lk, set0=sets[0])
 
 
