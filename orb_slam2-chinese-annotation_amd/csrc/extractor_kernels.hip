@@ -1422,7 +1422,7 @@ __device__ __forceinline__ void oct_rank_by_count(unsigned long long* sortBuf, i
 }
 
 #define OCT_MAX_PASSES 512
-#define OCT_REG_KEYS 8  // keys per thread held in registers (n <= 8 x 512), small batches  // final-phase candidates ranked by counting (multiple of the 512 threads)
+#define OCT_REG_KEYS 8  // keys per thread held in registers (n <= 8 x 512), small batches
 
 template <bool REG, bool GNODES>
 __global__ __launch_bounds__(512) void k_octree(
@@ -2628,9 +2628,11 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   (void)xmax;  // folded into the alpha table: (2048, 0) past xmax
   // tile bounds: narrow variant for a per-level downscale <= 1.25, wide <= 1.9
   const bool wide = (double)sw / dw > 1.25 || (double)sh / dh > 1.25;
-  // each workgroup resizes one tile of ORB_RESIZE_IMAGES_PER_WG images (default 8; swept 2-16)
+  // each workgroup resizes one tile of ORB_RESIZE_IMAGES_PER_WG images (default
+  // 16: with two extraction lanes 12 / 16 / 24 measured 323.8k / 322.3-324.4k /
+  // 324.7k against 321.3-321.8k frames/s for 8, profiles/r03_lanes.txt)
   static const int perWg =
-      getenv("ORB_RESIZE_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_RESIZE_IMAGES_PER_WG"))) : 8;
+      getenv("ORB_RESIZE_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_RESIZE_IMAGES_PER_WG"))) : 16;
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, (nimg + perWg - 1) / perWg),
       block(256);
   // every image base and row start 4-aligned: one load per staged dword
