@@ -2118,7 +2118,9 @@ __global__ __launch_bounds__(256) void k_orient_desc_split(
 //     the row's parity), (sum + 2^15) >> 16 saturated -- instead of a column
 //     pass over the whole 37 x 37 patch (about a third of its pixels are
 //     sampled); ballots.
+#ifndef DESC_RS_DW
 #define DESC_RS_DW 40    // row-sum pair row pitch (dwords): 10 groups of 4 columns
+#endif
 #define DESC_RS_PAIRS 22 // 43 rows + the unused odd row of the last pair
 struct DescWaveLds {
   uint32_t rsp[2][DESC_RS_PAIRS][DESC_RS_DW];

@@ -10,6 +10,12 @@ cd "$R"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_extractor.py tests/test_golden.py -x -q \
   --timeout 120 --timeout-method thread > "$O/t_$TAG.log" 2>&1
 tail -1 "$O/t_$TAG.log"
+for v in "$@"; do  # each variant's extractor + golden parity too
+  ORB_AMD_LIB=$R/orb_slam2-chinese-annotation_amd/lib/variants/$v.so timeout -k 10 300 \
+    python -u -m pytest tests/test_gpu_extractor.py tests/test_golden.py -x -q \
+    --timeout 120 --timeout-method thread > "$O/t_${TAG}_$v.log" 2>&1
+  echo "$v: $(tail -1 "$O/t_${TAG}_$v.log")"
+done
 timeout -k 10 120 python tools/probe/stage_times.py --batch 512 > "$O/st_${TAG}_base.txt" 2>&1
 for v in "$@"; do
   ORB_AMD_LIB=$R/orb_slam2-chinese-annotation_amd/lib/variants/$v.so timeout -k 10 120 \
