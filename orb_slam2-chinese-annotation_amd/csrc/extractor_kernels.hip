@@ -2126,7 +2126,9 @@ struct DescWaveLds {
   uint32_t rsp[2][DESC_RS_PAIRS][DESC_RS_DW];
 };
 
+#ifndef DESC_PPW
 #define DESC_PPW 4  // slot pairs per wave (software-pipelined: the next pair's window loads overlap this one)
+#endif
 #ifndef DESC_MIN_WAVES
 #define DESC_MIN_WAVES 0  // __launch_bounds__ minimum waves per SIMD (A/B knob: 5 -> <= 96 VGPRs)
 #endif
