@@ -217,7 +217,9 @@ def cpu_baseline(imgs_host, maps, args, scale):
             os.sched_setaffinity(0, aff)
     med = float(np.median(times))
     model, ncpu = host_cpu()
+    allc = cpu_all_cores(imgs_host, maps, args, scale, oracle) if args.cpu_all_seconds > 0 else None
     return {"value": 1.0 / med, "unit": "frames/s", "cores": 1, "kind": "port",
+            "all_cores": allc,
             "sample": f"{len(times)} timed frames (after 3 warm-up) of the same {args.width}x"
                       f"{args.height} stream: oracle ORBextractor ({args.features} feat) + "
                       f"SearchByProjection vs {args.mappoints} map points, C++ -O3 "
@@ -225,6 +227,51 @@ def cpu_baseline(imgs_host, maps, args, scale):
                       f"{core}; median {med * 1e3:.2f} ms/frame (mean "
                       f"{np.mean(times) * 1e3:.2f}), {el:.1f} s",
             "host_cpu": model, "host_nproc": ncpu}
+
+
+def cpu_threads():
+    """Host threads this process may use: its CPU affinity, capped by
+    OMP_NUM_THREADS where the box sets it (the GPU box grants 16 cores and
+    sets it to 16; nproc there counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, omp) if omp > 0 else n)
+
+
+def cpu_all_cores(imgs_host, maps, args, scale, oracle):
+    """The same oracle extract + match on every host thread this process may
+    use (one frame per thread at a time, as a CPU deployment would shard the
+    sequence), frames/s over a bounded wall-clock sample."""
+    import threading
+
+    nthr = cpu_threads()
+    done = [0] * nthr
+    stop = [False]
+
+    def worker(t):
+        i = t
+        while not stop[0]:
+            f = i % len(imgs_host)
+            k, d, _ = oracle.extract(imgs_host[f], args.features, 1.2, 8, 20, 7)
+            mps, mpd, locked = maps[f]
+            oracle.match_projection_local(k, d, scale, args.width, args.height, mps, mpd, 1.0, 0.8,
+                                          locked[: len(k)])
+            done[t] += 1
+            i += nthr
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(nthr)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    time.sleep(args.cpu_all_seconds)
+    n0, t1 = sum(done), time.perf_counter()
+    stop[0] = True
+    for th in ths:
+        th.join()
+    return {"value": n0 / (t1 - t0), "unit": "frames/s", "cores": nthr,
+            "sample": f"{n0} frames completed in {t1 - t0:.1f} s on {nthr} threads (oracle "
+                      "extract + SearchByProjection, one frame per thread at a time; the "
+                      "ctypes calls release the GIL)"}
 
 
 _HIP = None
@@ -516,6 +563,47 @@ def host_input_leg(orb, torch, ext, matcher, imgs, args, dev, sets, d_mps, d_mpd
                     "(second copy stream); local maps resident; PCIe-inclusive drop-in rate"}
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` from a plain shell: start one rank per GPU as a child
+    `torch.distributed.run` (never exec: this process has made no GPU call and
+    makes none), relay its output and return its exit code.  The ranks shard
+    the frame sequence as the driver loop of Examples/Monocular/mono_kitti.cc:73-119
+    would if each GPU took every N-th block of frames."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(Path(__file__).resolve()), *sys.argv[1:]]
+    env = dict(os.environ, ORB_BENCH_LAUNCHED_BY="bench.py --gpus")
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=env).returncode
+
+
+def resolve_world(gpus, environ):
+    """(world size, launch-children?) for `--gpus` against the launcher's env.
+    WORLD_SIZE set: the ranks already exist and must match --gpus (a mismatch is
+    an error, not a silent single-GPU run).  Unset and --gpus > 1: start them."""
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; launch one "
+                             "rank per GPU (or drop --gpus / WORLD_SIZE)")
+        return world, False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return n, n > 1
+
+
 def timed_loop(fn, steps, warmup, torch):
     for _ in range(warmup):
         fn()
@@ -529,7 +617,9 @@ def timed_loop(fn, steps, warmup, torch):
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks, one per GPU); > 1 without WORLD_SIZE starts the ranks "
+                         "with torch.distributed.run (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=60,
                     help="timed steps; one step = one pass over the --frames resident frames")
     ap.add_argument("--warmup", type=int, default=2)
@@ -543,6 +633,8 @@ def main():
     ap.add_argument("--mappoints", type=int, default=5000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-max-frames", type=int, default=400)
+    ap.add_argument("--cpu-all-seconds", type=float, default=8.0,
+                    help="wall-clock sample of the all-cores oracle rate (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3 / C5 extra keys")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input synthesis")
@@ -564,7 +656,9 @@ def main():
                          "its extraction")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, spawn = resolve_world(args.gpus, os.environ)
+    if spawn:  # before any torch / HIP call in this process
+        raise SystemExit(launch_ranks(world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch

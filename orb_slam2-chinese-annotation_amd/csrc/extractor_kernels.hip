@@ -1448,7 +1448,9 @@ __global__ __launch_bounds__(512) void k_octree(
   // the keys stay in LDS then)
   // (GNODES is a template parameter so that the LDS build keeps ds_*
   // instructions: a pointer that may be either would compile to flat ones)
-  unsigned char* p = GNODES ? gNodes + ((long long)img * gridDim.y + blockIdx.y) * nodeStride : smem;
+  // (the slice is indexed by the absolute level: two launches over disjoint
+  // level ranges of one batch -- ORB_SIDE_TAIL -- run concurrently on two streams)
+  unsigned char* p = GNODES ? gNodes + ((long long)img * plan.nlevels + l) * nodeStride : smem;
   unsigned long long* sortBuf = (unsigned long long*)p; p += (size_t)n2 * 8;
   OctNode* A = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
   OctNode* B = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);

@@ -353,6 +353,7 @@ struct orb_extractor {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // side stream: FAST beside the resize chain (blur in split mode)
   bool sharedSide = false;        // stream2 is the device's shared side stream (not destroyed)
+  hipStream_t privSide = nullptr; // this handle's side stream while its caller's stream is captured
   hipStream_t stream3 = nullptr;  // resize chain, high priority (ORB_CHAIN_STREAM=1)
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   hipEvent_t evL0Fork = nullptr, evL0Join = nullptr;  // level-0 FAST beside the resize chain
@@ -699,6 +700,8 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
   return ORB_OK;
 }
 
+static int stream_prio(const char* var, const char* dflt);
+
 static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, size_t stride,
                               size_t imgPitch, orb_keypoint_t* d_kps, uint8_t* d_desc,
                               int capacity, int32_t* d_counts, hipStream_t s,
@@ -713,7 +716,22 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   const long long ap = h->arenaBytes;
   static const bool sideStream =
       getenv("ORB_EXTRACT_STREAMS") && atoi(getenv("ORB_EXTRACT_STREAMS")) > 1;
-  hipStream_t s2 = sideStream ? h->stream2 : s;
+  // the side stream: the device's shared one, or -- while the caller's stream
+  // is being captured into a graph -- a stream of this handle's own, so a
+  // capture never pulls another handle's side work into its graph
+  hipStream_t side = h->stream2;
+  if (h->sharedSide) {
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone) {
+      if (!h->privSide && hipStreamCreateWithPriority(&h->privSide, hipStreamNonBlocking,
+                                                      stream_prio("ORB_STREAM2_PRIO", "least")) != hipSuccess) {
+        h->privSide = nullptr;
+        return ORB_EDEVICE;
+      }
+      side = h->privSide;
+    }
+  }
+  hipStream_t s2 = sideStream ? side : s;
   StageProfiler& pf = h->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
@@ -748,7 +766,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   // 1.708 / 1.709 ms per 512 frames for n = 0 / 1 / 2 / 3, bench 259.7k /
   // 262.3k / 263.6k / 263.4k frames/s (profiles/r03_schedule_xcd.txt)
   static const int sideLevelsEnv =
-      getenv("ORB_FAST_SIDE_LEVELS") ? atoi(getenv("ORB_FAST_SIDE_LEVELS")) : 2;
+      getenv("ORB_FAST_SIDE_LEVELS") ? std::max(0, atoi(getenv("ORB_FAST_SIDE_LEVELS"))) : 2;
   const int sideLevels = (l0Side && !perLevel) ? std::min(sideLevelsEnv, P.nlevels - 1) : 0;
   const int sideEnd = sideLevels > 0 ? P.lv[sideLevels].cellEnd : l0End;
   // ORB_SIDE_TAIL=1 (A/B knob): the side stream also runs the octree and
@@ -768,14 +786,14 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   }
   if (l0Side) {
     HIP_TRY(hipEventRecord(h->evL0Fork, s));
-    HIP_TRY(hipStreamWaitEvent(h->stream2, h->evL0Fork, 0));
-    PROF_REC(ev, pf.b(ev, 5), h->stream2);
+    HIP_TRY(hipStreamWaitEvent(side, h->evL0Fork, 0));
+    PROF_REC(ev, pf.b(ev, 5), side);
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
                              h->dCellCount.as<int32_t>(), fastErr, 0, l0End, B,
-                             h->stream2));
-    PROF_REC(ev, pf.e(ev, 5), h->stream2);
-    if (!perLevel && sideLevels == 0) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
+                             side));
+    PROF_REC(ev, pf.e(ev, 5), side);
+    if (!perLevel && sideLevels == 0) HIP_TRY(hipEventRecord(h->evL0Join, side));
   } else if (ev) {
     pf.not_run(5);
   }
@@ -800,50 +818,50 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     if (perLevel && d.cellEnd > d.cellBeg) {
       // level l's cells on the side stream as soon as the chain has produced it
       HIP_TRY(hipEventRecord(h->evLvl[l], cs));
-      HIP_TRY(hipStreamWaitEvent(h->stream2, h->evLvl[l], 0));
-      PROF_REC(ev, pf.b(ev, 2, fastSeg), h->stream2);
+      HIP_TRY(hipStreamWaitEvent(side, h->evLvl[l], 0));
+      PROF_REC(ev, pf.b(ev, 2, fastSeg), side);
       HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                                h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
                                h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), d.cellBeg,
-                               d.cellEnd, B, h->stream2));
-      PROF_REC(ev, pf.e(ev, 2, fastSeg), h->stream2);
+                               d.cellEnd, B, side));
+      PROF_REC(ev, pf.e(ev, 2, fastSeg), side);
       ++fastSeg;
     }
     if (l == sideLevels && sideEnd > l0End) {
       HIP_TRY(hipEventRecord(h->evLvl[l], cs));
-      HIP_TRY(hipStreamWaitEvent(h->stream2, h->evLvl[l], 0));
-      PROF_REC(ev, pf.b(ev, 5, 1), h->stream2);
+      HIP_TRY(hipStreamWaitEvent(side, h->evLvl[l], 0));
+      PROF_REC(ev, pf.b(ev, 5, 1), side);
       HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                                h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
                                h->dCellCount.as<int32_t>(), fastErr, l0End,
-                               sideEnd, B, h->stream2));
-      PROF_REC(ev, pf.e(ev, 5, 1), h->stream2);
+                               sideEnd, B, side));
+      PROF_REC(ev, pf.e(ev, 5, 1), side);
       if (ev) pf.segments(5, 2);
     }
     if (l == sideLevels && sideTail) {
       // the side stream's tail: octree of levels 0..sideLevels, then their
       // descriptors (the main stream's octree of the rest runs beside it)
-      PROF_REC(ev, pf.b(ev, 3, 1), h->stream2);
+      PROF_REC(ev, pf.b(ev, 3, 1), side);
       HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                            h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                            h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
                            h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, tailSplit, B,
                            h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr,
-                           h->octNodeBytes, h->stream2));
-      PROF_REC(ev, pf.e(ev, 3, 1), h->stream2);
-      HIP_TRY(hipEventRecord(h->evFork, h->stream2));  // side octree done
-      PROF_REC(ev, pf.b(ev, 4, 1), h->stream2);
+                           h->octNodeBytes, side));
+      PROF_REC(ev, pf.e(ev, 3, 1), side);
+      HIP_TRY(hipEventRecord(h->evFork, side));  // side octree done
+      PROF_REC(ev, pf.b(ev, 4, 1), side);
       HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                                 h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
                                 h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, 0,
-                                tailSplit, h->stream2));
-      PROF_REC(ev, pf.e(ev, 4, 1), h->stream2);
+                                tailSplit, side));
+      PROF_REC(ev, pf.e(ev, 4, 1), side);
       if (ev) {
         pf.segments(3, 2);
         pf.segments(4, 2);
       }
     }
-    if (l == sideLevels && sideLevels > 0) HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
+    if (l == sideLevels && sideLevels > 0) HIP_TRY(hipEventRecord(h->evL0Join, side));
   }
   PROF_REC(ev, pf.e(ev, 0), cs);
   if (cs != s) {  // the caller's stream also follows the whole chain (levels without cells)
@@ -851,7 +869,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     HIP_TRY(hipStreamWaitEvent(s, h->evLvl[0], 0));
   }
   if (perLevel) {
-    HIP_TRY(hipEventRecord(h->evL0Join, h->stream2));
+    HIP_TRY(hipEventRecord(h->evL0Join, side));
     if (ev) {
       if (fastSeg) pf.segments(2, fastSeg);
       else pf.not_run(2);
@@ -1085,6 +1103,7 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
   if (h->stream2 && !h->sharedSide) hipStreamDestroy(h->stream2);
+  if (h->privSide) hipStreamDestroy(h->privSide);
   if (h->stream3) hipStreamDestroy(h->stream3);
   if (h->evFork) hipEventDestroy(h->evFork);
   if (h->evJoin) hipEventDestroy(h->evJoin);

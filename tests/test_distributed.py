@@ -47,3 +47,33 @@ def test_bench_distributed_plumbing_gloo():
     for _, _, gathered, t in res:
         assert gathered == [1000 + f for f in range(8)]
         assert t == 2.0  # slowest rank's time
+
+
+def test_bench_gpus_flag_world_resolution():
+    """`--gpus` against the launcher's env: a mismatch with WORLD_SIZE fails
+    loudly; --gpus > 1 from a plain shell asks for child ranks."""
+    import bench
+
+    assert bench.resolve_world(None, {}) == (1, False)
+    assert bench.resolve_world(1, {}) == (1, False)
+    assert bench.resolve_world(8, {}) == (8, True)
+    assert bench.resolve_world(None, {"WORLD_SIZE": "4"}) == (4, False)
+    assert bench.resolve_world(4, {"WORLD_SIZE": "4"}) == (4, False)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(8, {"WORLD_SIZE": "1"})
+    with pytest.raises(SystemExit):
+        bench.resolve_world(0, {})
+
+
+def test_bench_gpus_mismatch_exits_nonzero():
+    """A rank whose WORLD_SIZE differs from --gpus exits non-zero before it
+    touches a device (it never measures one GPU under an N-GPU label)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

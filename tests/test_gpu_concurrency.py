@@ -93,3 +93,65 @@ def test_vocabulary_handle_from_many_threads(gpu, oracle):
     for g, r in zip(got, refs):
         assert np.array_equal(g[0], r[0]) and np.array_equal(g[1].view(np.uint64), r[1].view(np.uint64))
         assert all(np.array_equal(a, b) for a, b in zip(g[2], r[2:5]))
+
+
+def test_graph_capture_beside_another_handle(gpu):
+    """extract_batch is graph-capturable (include/orb_abi.h) while another
+    handle on the same device keeps running batches on another thread: the
+    captured handle forks its side work onto a stream of its own during the
+    capture, so the other handle's side-stream launches never join the graph,
+    and both give the same results as uncaptured calls."""
+    import torch
+    W, H, B = 1241, 376, 8
+    imgs = np.stack([gpu.synth_image(40, f, W, H) for f in range(B)])
+    d = torch.from_numpy(imgs).cuda()
+    ha, hb = gpu.ORBextractor(1000, 1.2, 8, 20, 7), gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    cap = ha.capacity(W, H)
+
+    def bufs():
+        return (torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda"),
+                torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda"),
+                torch.zeros(B, dtype=torch.int32, device="cuda"))
+
+    a, b = bufs(), bufs()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def call(h, o, s):
+        h.extract_batch(d.data_ptr(), B, W, H, W, W * H, o[0].data_ptr(), o[1].data_ptr(), cap,
+                        o[2].data_ptr(), s.cuda_stream)
+
+    call(ha, a, sa)
+    call(hb, b, sb)
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in a]
+    assert int(ref[2].min()) > 0
+    stop = threading.Event()
+    errors = []
+
+    def other():
+        try:
+            while not stop.is_set():
+                call(hb, b, sb)
+                sb.synchronize()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+
+    t = threading.Thread(target=other)
+    t.start()
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g, stream=sa, capture_error_mode="relaxed"):
+            call(ha, a, sa)
+    finally:
+        stop.set()
+        t.join(timeout=60)
+    assert not errors, errors
+    for x in a:
+        x.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    for x, r in zip(a, ref):
+        assert torch.equal(x, r)
+    for x, r in zip(b, ref):
+        assert torch.equal(x, r)

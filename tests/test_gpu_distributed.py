@@ -41,6 +41,23 @@ def test_two_ranks_shard_and_gather(gpu):
         < 1e-6 * res["value"]
 
 
+def test_bench_gpus_flag_launches_ranks(gpu):
+    """`bench.py --gpus 2` from a plain shell (no WORLD_SIZE) starts two ranks
+    itself (a torch.distributed.run child) and the job line reports both."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+                        "TORCHELASTIC_RUN_ID")}
+    env.update(ORB_BENCH_DEVICE="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--frames", "512", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-secondary",
+           "--threads", "4", "--host-frames", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["n_gpus"] == 2
+    assert res["config"]["count_gather_verified"] is True
+
+
 def test_rccl_gather_single_rank_torchrun(gpu):
     """The RCCL path itself: bench.py under torchrun with one rank initialises
     the nccl (= RCCL) process group, all-gathers each step's per-frame counts

@@ -400,3 +400,51 @@ print('batch:', n.tolist())
     out = dict(l.split(": ", 1) for l in r.stdout.strip().splitlines())
     assert out["single"] == str(gpu.ORB_EDEVICE)
     assert out["batch"] == str([gpu.ORB_EDEVICE] * 4)
+
+
+@pytest.mark.parametrize("side_tail", ["0", "1"])
+def test_octree_12k_batch4_global_nodes(gpu, oracle, tmp_path, side_tail):
+    """12,000 features put the octree's node tables in global memory (one slice
+    per (image, level)); a batch of 4 takes the cell FAST path and, with
+    ORB_SIDE_TAIL=1, runs the octree of levels 0..2 on the side stream beside
+    levels 3..7 on the main one: the two launches must not share slices
+    (run in a child: the schedule knobs are read once per process)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    rng = np.random.default_rng(12)
+    w, h, nf = 1920, 1080, 12000
+    img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    np.save(tmp_path / "img.npy", img)
+    code = f"""
+import sys, numpy as np, torch
+sys.path.insert(0, {str(root)!r}); sys.path.insert(0, {str(root / 'tests')!r})
+from conftest import load_pkg
+orb = load_pkg()
+img = np.load({str(tmp_path / 'img.npy')!r})
+ext = orb.ORBextractor({nf}, 1.2, 8, 20, 7)
+cap = ext.capacity({w}, {h})
+imgs = torch.from_numpy(np.stack([img] * 4)).cuda()
+k = torch.zeros((4, cap, 7), dtype=torch.int32, device='cuda')
+d = torch.zeros((4, cap, 32), dtype=torch.uint8, device='cuda')
+n = torch.zeros(4, dtype=torch.int32, device='cuda')
+s = torch.cuda.Stream()
+for _ in range(3):
+    ext.extract_batch(imgs.data_ptr(), 4, {w}, {h}, {w}, {w * h}, k.data_ptr(), d.data_ptr(), cap,
+                      n.data_ptr(), s.cuda_stream)
+torch.cuda.synchronize()
+np.savez({str(tmp_path / 'out.npz')!r}, k=k.cpu().numpy(), d=d.cpu().numpy(), n=n.cpu().numpy())
+"""
+    import os
+    env = dict(os.environ, ORB_SIDE_TAIL=side_tail)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = np.load(tmp_path / "out.npz")
+    kr, dr, _ = oracle.extract(img, nf)
+    for i in range(4):
+        n = int(out["n"][i])
+        assert n == len(kr), (i, n, len(kr))
+        assert out["k"][i, :n].tobytes() == kr.tobytes()
+        assert out["d"][i, :n].tobytes() == dr.tobytes()
