@@ -604,6 +604,102 @@ def resolve_world(gpus, environ):
     return n, n > 1
 
 
+def isolated_kernels(ext, matcher, launch, stream, nb, n, torch):
+    """Per-stage HIP-event times with every kernel alone: profile mode 2 runs
+    the extraction's stages one after another on the caller's stream (no side
+    stream), and the matcher follows on the same stream.  Returns
+    ({name: (total ms, launches)}, calls)."""
+    torch.cuda.synchronize()
+    ext.profile(2)
+    matcher.profile(True)
+    for i in range(n):
+        launch(i % nb, stream)
+    torch.cuda.synchronize()
+    out = {}
+    for st in range(6):
+        name, ms, cnt = ext.profile_read(st)
+        if cnt:
+            out[name] = (ms, cnt)
+    for st in range(3):
+        name, ms, cnt = matcher.profile_read(st)
+        if cnt:
+            out[name] = (ms, cnt)
+    ext.profile(False)
+    matcher.profile(False)
+    return out, n
+
+
+def kernel_table(iso, calls, pipelined_kern, n_prof, alg, batch):
+    """Every extraction and match kernel: SURVEY §8(d) algorithmic bytes per
+    launch, time per launch alone and pipelined, and the HBM fraction alone."""
+    table = {}
+    for name, (ms, n) in iso.items():
+        per_call = n / calls
+        ms_l = ms / n
+        b = alg.get(name, 0.0) * batch / per_call
+        row = {"launches_per_call": per_call, "ms_per_launch_isolated": ms_l,
+               "ms_per_call_isolated": ms / calls, "alg_bytes_per_launch": b,
+               "alg_GBps_isolated": b / (ms_l * 1e-3) / 1e9,
+               "frac_hbm_isolated": b / (ms_l * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        if name in pipelined_kern:
+            pm, pn = pipelined_kern[name]
+            row["ms_per_call_pipelined"] = pm / n_prof if name.startswith("k_fast") or \
+                name in ("k_pyr_resize", "k_octree", "k_orient_desc") else pm / max(pn, 1)
+            row["ms_per_launch_pipelined"] = row["ms_per_call_pipelined"] / per_call
+        table[name] = row
+    return table
+
+
+HARNESS_DIR = ROOT / "tests" / "integration_run"
+
+
+def dropin_leg(orb, imgs, maps, scale, args, threads, iters=500, nfr=16):
+    """The reference-typed drop-ins (integration/*.cc, linked to the library by
+    tests/integration_run) timed at ORB-SLAM2's own granularity, one frame per
+    call: mono = ORBextractor::operator() + SearchByProjection(F, vpMapPoints)
+    over 5,000 MapPoint objects (Frame::ExtractORB, Tracking::SearchLocalPoints);
+    stereo = both extractions on two threads + Frame::ComputeStereoMatches.
+    Both harness builds: ORB_AMD_GPU_STEREO (the recommended integration:
+    nothing reads mvImagePyramid on the host) and the default (mvImagePyramid
+    mirrored to the host every call).  Median wall ms per frame / pair."""
+    import subprocess
+    import tempfile
+
+    W, H, M = args.width, args.height, args.mappoints
+    nfr = min(nfr, len(imgs), len(maps))
+    right = synth_images(orb, args.seed, list(range(nfr)), W, H, threads, view=1)
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        d = Path(d)
+        np.ascontiguousarray(imgs[:nfr]).tofile(d / "imgs.bin")
+        np.ascontiguousarray(right).tofile(d / "imgsR.bin")
+        np.concatenate([np.ascontiguousarray(maps[i][0]).view(np.uint8).reshape(-1)
+                        for i in range(nfr)]).tofile(d / "tracks.bin")
+        np.concatenate([np.ascontiguousarray(maps[i][1]).reshape(-1)
+                        for i in range(nfr)]).tofile(d / "mpdesc.bin")
+        np.asarray(scale, np.float32).tofile(d / "scale.bin")
+        (d / "meta.txt").write_text(f"{W} {H} {args.features} {M} {nfr} {iters} 386.1448 718.856")
+        for key, exe in (("gpu_stereo_build", "dropin_harness_gpustereo"),
+                         ("host_pyramid_build", "dropin_harness")):
+            path = HARNESS_DIR / exe
+            if not path.exists():
+                out[key] = f"{path.name} not built (make -C tests/integration_run)"
+                continue
+            r = subprocess.run([str(path), "time", str(d)], capture_output=True, text=True,
+                               timeout=240)
+            if r.returncode != 0:
+                raise RuntimeError(f"{exe} time: {r.stderr[-1000:]}")
+            out[key] = json.loads((d / "time.json").read_text())
+    out["note"] = ("integration/ORBextractor.cc + ORBmatcher.cc (+ FrameStereo.cc) run by "
+                   "tests/integration_run/harness.cc with stand-in cv::Mat / Frame / MapPoint, "
+                   f"1241x376 frames 0..{nfr - 1} of the bench stream (right views for stereo), "
+                   f"{args.features} feat mono / {2 * args.features} per image stereo, "
+                   f"SearchByProjection vs {M} MapPoint objects per frame, th 1, nnratio 0.8; "
+                   f"median of {iters} calls after 3 warm-up; PCIe-inclusive (host images in, "
+                   "host keypoints / descriptors / matches out)")
+    return out
+
+
 def timed_loop(fn, steps, warmup, torch):
     for _ in range(warmup):
         fn()
@@ -633,10 +729,14 @@ def main():
     ap.add_argument("--mappoints", type=int, default=5000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-max-frames", type=int, default=400)
+    ap.add_argument("--iso-launches", type=int, default=8,
+                    help="extract + match calls timed with every kernel alone (kernel table)")
     ap.add_argument("--cpu-all-seconds", type=float, default=8.0,
                     help="wall-clock sample of the all-cores oracle rate (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3 / C5 extra keys")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the per-frame drop-in timing (tests/integration_run harness)")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input synthesis")
     ap.add_argument("--seed", type=int, default=0x4B495454)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -859,27 +959,45 @@ def main():
     n_kp = float(cnt_h.mean())
     nmatch = float(sets[0]["nmatch"].float().mean().item())
     alg = algorithmic_bytes(W, H, scale, 8, n_kp, M)
-    # the roofline kernel is SURVEY §8(d)'s k_fast_cells (the largest extraction
-    # kernel by itself; with two lanes every kernel's event time also holds the
-    # other lane's time-sharing, which stretches the latency-bound orient most)
-    dom = "k_fast_cells" if "k_fast_cells" in kern else max(ext_kern, key=lambda k: kern[k][0])
-    dom_ms_per_launch = kern[dom][0] / max(kern[dom][1], 1)
-    # bytes one launch of the dominant kernel processes (B frames; the resize
-    # runs nlevels-1 launches per extraction)
-    launches_per_extract = kern[dom][1] / n_prof
-    dom_bytes = alg[dom] * B / launches_per_extract
-    hbm_gbs = dom_bytes / (dom_ms_per_launch * 1e-3) / 1e9
+    # every kernel alone (one stream, every stage after the previous one, no
+    # side stream): kernel-only launch times for the roofline and the per-kernel
+    # table; the pipelined HIP-event times above stay beside them
+    def launch_iso(b, stream):
+        st = sets[0]
+        ext.extract_batch(d_img.data_ptr() + b * B * frame_bytes, B, W, H, W, frame_bytes,
+                          st["kps"].data_ptr(), st["desc"].data_ptr(), cap, st["cnt"].data_ptr(),
+                          stream.cuda_stream)
+        matcher.search_by_projection_batch(B, st["kps"].data_ptr(), st["desc"].data_ptr(),
+                                           st["cnt"].data_ptr(), d_lock[b * B].data_ptr(), cap,
+                                           d_mps[b * B].data_ptr(), d_mpd[b * B].data_ptr(),
+                                           d_nmps.data_ptr(), M, W, H, scale, 1.0,
+                                           st["match"].data_ptr(), st["nmatch"].data_ptr(),
+                                           stream.cuda_stream)
+
+    iso, iso_calls = isolated_kernels(ext, matcher, launch_iso, ext_stream, NB, args.iso_launches,
+                                      torch)
+    table = kernel_table(iso, iso_calls, kern, n_prof, alg, B)
+    # the roofline kernel: the longest kernel per call when each runs alone
+    dom = max(table, key=lambda k: table[k]["ms_per_call_isolated"])
+    t = table[dom]
+    dom_ms_per_launch = t["ms_per_launch_isolated"]
+    dom_bytes = t["alg_bytes_per_launch"]
+    hbm_gbs = t["alg_GBps_isolated"]
     traffic, traffic_src = measured_traffic(dom, B)
     valu = valu_issue(dom, B, dom_ms_per_launch)
     total_frames = D * args.steps * world
     # the HBM roofline of the dominant kernel is the primary
-    # fraction (algorithmic bytes per launch / its launch time); its VALU issue
-    # rate against the guide's peak sits beside it (the integer kernels of this
-    # path are instruction-bound, not bandwidth-bound: DESIGN.md §4)
+    # fraction (algorithmic bytes per launch / its launch time alone); its VALU
+    # issue rate against the guide's peak sits beside it (the integer kernels of
+    # this path are instruction-bound, not bandwidth-bound: DESIGN.md §4)
     roof = {"kernel": dom, "bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_launch": dom_bytes,
-            "bytes_note": f"SURVEY §8(d) algorithmic bytes of {dom}: every pyramid pixel read "
-                          f"once ({alg[dom]:.0f} B/frame) x {B} frames per launch"}
+            "bytes_note": f"SURVEY §8(d) algorithmic bytes of {dom} ({alg[dom]:.0f} B/frame) x "
+                          f"{B} frames / {t['launches_per_call']:g} launch(es) per call",
+            "timing": f"HIP events around each launch, kernels run one after another on one "
+                      f"stream ({iso_calls} calls after the timed region); "
+                      "`ms_per_launch_pipelined` is the same kernel inside the timed pipeline "
+                      "(time-shared with the other lane and the matcher)"}
     if valu is not None:
         rate = valu["valu_instr_per_launch"] / (dom_ms_per_launch * 1e-3) / 1e9
         roof["valu"] = {"achieved": rate, "peak": VALU_PEAK_G, "unit": "G wave-instructions/s",
@@ -894,6 +1012,7 @@ def main():
                           "calibration, profiles/r02_fetch_calib.txt) + WRITE_SIZE, separate "
                           "passes)" if traffic_src else None,
         "ms_per_launch": dom_ms_per_launch,
+        "ms_per_launch_pipelined": t.get("ms_per_launch_pipelined"),
     })
     host = None
     if args.host_frames > 0:
@@ -937,6 +1056,7 @@ def main():
         },
         "roofline": roof,
         "kernels_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kern.items()},
+        "kernels": table,
         "extraction_kernels_ms_per_launch": sum(kern[k][0] for k in ext_kern) / n_prof,
         "extraction_call_ms_per_launch": call_ms / max(call_n, 1),
         "fast_side_stream_ms_per_launch": side_ms,
@@ -946,8 +1066,12 @@ def main():
         if args.host_frames <= 0:
             del d_img
         result.update(secondary_configs(orb, torch, args, dev, args.threads))
+    if rank == 0 and world == 1 and not args.no_dropin:
+        result["dropin"] = dropin_leg(orb, imgs, maps, scale, args, args.threads)
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(imgs[:64], maps[:64], args, scale)
+        if isinstance(result.get("dropin"), dict):
+            result["dropin"]["cpu_oracle_frame_ms"] = 1e3 / result["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

@@ -146,6 +146,17 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
  * The copy waits for the last call's stream.  dst may be NULL to query the size. */
 orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t* dst,
                                          size_t dst_stride, int* width, int* height);
+/* mvImagePyramid[level] of the last orb_extractor_extract call without a copy
+ * out: a pointer into pinned host memory the library owns, valid until the
+ * next call on this handle (the reference rebuilds mvImagePyramid on every
+ * call too, src/ORBextractor.cc:1172-1207; its only reader is
+ * Frame::ComputeStereoMatches, src/Frame.cc:524,619,633,639, right after the
+ * extraction).  Level 0 is the call's pinned staging of the image; levels 1..
+ * come from one DMA of the device pyramid, which the first request makes
+ * synchronously and which from then on rides in every call's graph after the
+ * keypoint copy.  ORB_EINVAL after a batch call. */
+orb_status_t orb_extractor_host_pyramid(orb_extractor_t* h, int level, const uint8_t** data,
+                                        int* width, int* height, size_t* stride);
 /* The 7x7 Gaussian-blurred copy of level `level` of the first image of the
  * last call (the image computeDescriptors samples, src/ORBextractor.cc:1143-1145);
  * same conventions as orb_extractor_pyramid_level. */
@@ -183,7 +194,10 @@ void* orb_extractor_stream(orb_extractor_t* h);
  * k_fast_band on all levels), 3 k_octree, 4 k_orient_desc,
  * 5 k_fast_cells_side (the cells of level 0, then of levels 1-2, on the
  * handle's side stream beside the resize chain; durations summed; 0 launches
- * when not split off), 6 = the whole extraction call. */
+ * when not split off), 6 = the whole extraction call.
+ * enable = 2 times every stage alone: while it is set the batch form runs all
+ * stages one after another on the caller's stream (no side stream), so each
+ * stage's events bracket its own kernels only (bench.py's isolated table). */
 orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable);
 orb_status_t orb_extractor_profile_read(orb_extractor_t* h, int stage, double* total_ms,
                                         int* launches, const char** name);

@@ -11,7 +11,8 @@
 // Frame.cc and Tracking.cc compile unchanged.
 //
 // mvImagePyramid (public, read by Frame::ComputeStereoMatches,
-// src/Frame.cc:524,619,633,639) is refreshed from the device after each call.
+// src/Frame.cc:524,619,633,639) points at the library's pinned host mirror of
+// the call's levels after each call (orb_extractor_host_pyramid).
 // With ORB_AMD_GPU_STEREO defined (and integration/FrameStereo.cc replacing
 // Frame::ComputeStereoMatches) nothing reads it on the host, and the copy is
 // skipped: keypoints, descriptors and pyramids then stay in HBM for stereo.
@@ -87,13 +88,15 @@ void ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoi
   else
     desc.rowRange(0, n).copyTo(_descriptors);
 #ifndef ORB_AMD_GPU_STEREO
+  // mvImagePyramid aliases the library's pinned host mirror of this call's
+  // levels (one DMA in the call's graph, no copy here), valid until the next
+  // call, as the reference's own levels are rebuilt on every call
   for (int l = 0; l < nlevels; ++l) {
+    const uint8_t* p = nullptr;
     int w = 0, h = 0;
-    check(orb_extractor_pyramid_level(mpGpu, l, nullptr, 0, &w, &h), "mvImagePyramid");
-    mvImagePyramid[l].create(h, w, CV_8U);
-    check(orb_extractor_pyramid_level(mpGpu, l, mvImagePyramid[l].ptr<uint8_t>(),
-                                      mvImagePyramid[l].step, nullptr, nullptr),
-          "mvImagePyramid");
+    size_t step = 0;
+    check(orb_extractor_host_pyramid(mpGpu, l, &p, &w, &h, &step), "mvImagePyramid");
+    mvImagePyramid[l] = Mat(h, w, CV_8U, const_cast<uint8_t*>(p), step);
   }
 #endif
 }

@@ -106,6 +106,7 @@ def lib() -> ctypes.CDLL:
         "orb_extractor_extract": (i32, [vp, vp, i32, i32, sz, vp, vp, i32, vp]),
         "orb_extractor_pyramid_level": (i32, [vp, i32, vp, sz, vp, vp]),
         "orb_extractor_blurred_level": (i32, [vp, i32, vp, sz, vp, vp]),
+        "orb_extractor_host_pyramid": (i32, [vp, i32, vp, vp, vp, vp]),
         "orb_extractor_extract_batch": (i32, [vp, vp, i32, i32, i32, sz, sz, vp, vp, i32, vp, vp]),
         "orb_extractor_batch_level": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "orb_extractor_stream": (vp, [vp]),
@@ -292,6 +293,16 @@ class ORBextractor:
                                            _ptr(desc), cap, ctypes.byref(n)),
                "orb_extractor_extract")
         return kps[: n.value].copy(), desc[: n.value].copy()
+
+    def host_pyramid(self, level: int) -> np.ndarray:
+        """Level `level` of the last __call__ through the library's pinned host
+        mirror (orb_extractor_host_pyramid), copied into a new array."""
+        p, w, h, st = ctypes.c_void_p(), ctypes.c_int(0), ctypes.c_int(0), ctypes.c_size_t(0)
+        _check(lib().orb_extractor_host_pyramid(self._h, level, ctypes.byref(p), ctypes.byref(w),
+                                                ctypes.byref(h), ctypes.byref(st)), "host_pyramid")
+        buf = (ctypes.c_uint8 * (st.value * (h.value - 1) + w.value)).from_address(p.value)
+        a = np.frombuffer(buf, np.uint8)
+        return np.lib.stride_tricks.as_strided(a, (h.value, w.value), (st.value, 1)).copy()
 
     @property
     def mvImagePyramid(self) -> list:

@@ -25,140 +25,116 @@ __global__ __launch_bounds__(256) void k_hamming_batch(const uint8_t* __restrict
 // cell = (round((x-minX)*invW), round((y-minY)*invH)), out-of-grid keys dropped,
 // per-cell lists in ascending keypoint index.  Stored as CSR with cell index
 // ix*48+iy, the order GetFeaturesInArea scans (ix outer, iy inner, :391-400).
-// One workgroup per frame: LDS counts, a block scan over the 3072 cells, an
-// unordered scatter by LDS cursors, then every cell's short list is put back
-// in keypoint order by one thread (insertion sort; cells hold ~1-10 keys).
-// Frames with kpStride up to GB_LDS_KEYS keypoints build their lists in LDS;
-// larger frames use k_grid_build_wave (one wave, stable ballot scatter).
+//
+// One wave per frame and 12 KB of LDS (the 3,073 cell counters): LDS counts,
+// a wave scan over the cells (48 per lane, read and written as b128), then a
+// stable scatter in keypoint order, 64 keys a round: lanes holding the same
+// cell find each other with 12 ballots over the cell id bits, so a key's slot
+// is its cell's cursor plus the same-cell lanes below it, and the group's
+// highest lane advances the cursor.  The next round's keypoint fields are
+// loaded while the current one scatters.  (Round 3's 256-thread form held
+// 56.7 KB of LDS per frame and sorted each cell's list with one thread; beside
+// the extraction kernels it waited for LDS and ran 2.3 ms per 1,024 frames.)
 // `staged` (optional): the keypoints in cell order as k_proj_candidates stages
 // them in LDS, {x, y, idx | octave << 24 | locked << 31, uR}, so that each of
 // its workgroups copies the frame's grid with coalesced loads instead of
 // gathering it through cellIdx.
-#define GB_T 256
-#define GB_LDS_KEYS 8192
-__global__ __launch_bounds__(GB_T) void k_grid_build(const orb_keypoint_t* __restrict__ keys,
-                                                     const int32_t* __restrict__ nkeys, int kpStride,
-                                                     float minX, float minY, float invW, float invH,
-                                                     int32_t* __restrict__ cellStart,
-                                                     int32_t* __restrict__ cellIdx,
-                                                     const uint8_t* __restrict__ locked,
-                                                     const float* __restrict__ uright,
-                                                     uint4* __restrict__ staged) {
-  __shared__ int cnt[GRID_CELLS + 1];
-  __shared__ int cursor[GRID_CELLS];
-  __shared__ int sList[GB_LDS_KEYS];
-  __shared__ int tmp[20];
-  const int p = blockIdx.x, t = threadIdx.x;
-  const int n = nkeys[p];
-  const orb_keypoint_t* K = keys + (size_t)p * kpStride;
-  int32_t* ci = cellIdx + (size_t)p * kpStride;
-  for (int i = t; i <= GRID_CELLS; i += GB_T) cnt[i] = 0;
-  __syncthreads();
-  for (int k = t; k < n; k += GB_T) {
-    const int c = grid_cell(K[k], minX, minY, invW, invH);
-    if (c >= 0) atomicAdd(&cnt[c], 1);
-  }
-  __syncthreads();
-  {
-    constexpr int per = GRID_CELLS / GB_T;
-    static_assert(per * GB_T == GRID_CELLS, "cells split evenly over the threads");
-    int s = 0;
-#pragma unroll
-    for (int i = 0; i < per; ++i) s += cnt[t * per + i];
-    int tot;
-    int ex = block_excl_scan(s, tmp, &tot);
-#pragma unroll
-    for (int i = 0; i < per; ++i) {
-      const int v = cnt[t * per + i];
-      cnt[t * per + i] = ex;
-      cursor[t * per + i] = ex;
-      ex += v;
-    }
-    if (t == 0) cnt[GRID_CELLS] = tot;
-  }
-  __syncthreads();
-  int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
-  for (int i = t; i <= GRID_CELLS; i += GB_T) cs[i] = cnt[i];
-  for (int k = t; k < n; k += GB_T) {
-    const int c = grid_cell(K[k], minX, minY, invW, invH);
-    if (c >= 0) sList[atomicAdd(&cursor[c], 1)] = k;
-  }
-  __syncthreads();
-  for (int c = t; c < GRID_CELLS; c += GB_T) {
-    const int b = cnt[c], e = cnt[c + 1];
-    for (int i = b + 1; i < e; ++i) {
-      const int v = sList[i];
-      int j = i;
-      while (j > b) {
-        const int u = sList[j - 1];
-        if (u < v) break;
-        sList[j] = u;
-        --j;
-      }
-      sList[j] = v;
-    }
-  }
-  __syncthreads();
-  const int tot = cnt[GRID_CELLS];
-  for (int i = t; i < tot; i += GB_T) ci[i] = sList[i];
-  if (staged) {
-    const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
-    const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
-    uint4* sg = staged + (size_t)p * kpStride;
-    for (int i = t; i < tot; i += GB_T) {
-      const int idx = sList[i];
-      const orb_keypoint_t kp = K[idx];
-      uint4 e;
-      e.x = __float_as_uint(kp.x);
-      e.y = __float_as_uint(kp.y);
-      e.z = (uint32_t)idx | ((uint32_t)kp.octave << 24) | ((LK && LK[idx]) ? 0x80000000u : 0u);
-      e.w = __float_as_uint(UR ? UR[idx] : -1.0f);
-      sg[i] = e;
-    }
-  }
-}
-
-__global__ __launch_bounds__(64) void k_grid_build_wave(const orb_keypoint_t* __restrict__ keys,
+#define GB_LDS_KEYS 8192  // staged copies for frames of up to this many keypoint slots
+__global__ __launch_bounds__(64) void k_grid_build(const orb_keypoint_t* __restrict__ keys,
                                                    const int32_t* __restrict__ nkeys, int kpStride,
                                                    float minX, float minY, float invW, float invH,
                                                    int32_t* __restrict__ cellStart,
-                                                   int32_t* __restrict__ cellIdx) {
-  __shared__ int cnt[GRID_CELLS + 1];
+                                                   int32_t* __restrict__ cellIdx,
+                                                   const uint8_t* __restrict__ locked,
+                                                   const float* __restrict__ uright,
+                                                   uint4* __restrict__ staged) {
+  __shared__ __attribute__((aligned(16))) int cnt[GRID_CELLS + 4];
   const int p = blockIdx.x, lane = threadIdx.x;
-  const int n = nkeys[p];
+  const int n = max(nkeys[p], 0);
   const orb_keypoint_t* K = keys + (size_t)p * kpStride;
-  for (int i = lane; i <= GRID_CELLS; i += 64) cnt[i] = 0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  {
+    int4* c4 = reinterpret_cast<int4*>(cnt);
+    for (int i = lane; i < (GRID_CELLS + 4) / 4; i += 64) c4[i] = make_int4(0, 0, 0, 0);
+  }
   __syncthreads();
-  for (int k = lane; k < n; k += 64) {
-    const int c = grid_cell(K[k], minX, minY, invW, invH);
-    if (c >= 0) atomicAdd(&cnt[c], 1);
+  // counts: four keys per lane in flight
+  for (int base = 0; base < n; base += 256) {
+    int c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = base + 64 * j + lane;
+      c[j] = k < n ? grid_cell(K[k], minX, minY, invW, invH) : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (c[j] >= 0) atomicAdd(&cnt[c[j]], 1);
   }
   __syncthreads();
   // exclusive scan over 3072 cells: 48 consecutive cells per lane
   {
-    const int per = GRID_CELLS / 64;
+    constexpr int per = GRID_CELLS / 64;
+    static_assert(per * 64 == GRID_CELLS && per % 4 == 0, "cells split evenly over the lanes");
+    int4* c4 = reinterpret_cast<int4*>(cnt + lane * per);
+    int4 v[per / 4];
     int s = 0;
-    for (int i = 0; i < per; ++i) s += cnt[lane * per + i];
-    int ex = wave_incl_scan(s) - s;
-    for (int i = 0; i < per; ++i) {
-      const int v = cnt[lane * per + i];
-      cnt[lane * per + i] = ex;
-      ex += v;
+#pragma unroll
+    for (int i = 0; i < per / 4; ++i) {
+      v[i] = c4[i];
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
     }
-    if (lane == 63) cnt[GRID_CELLS] = ex;
+    int ex = wave_incl_scan(s) - s;
+    int4* cs4 = reinterpret_cast<int4*>(cellStart + (size_t)p * (GRID_CELLS + 1));
+    const bool al16 = ((uintptr_t)cs4 & 15) == 0;
+    int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1) + lane * per;
+#pragma unroll
+    for (int i = 0; i < per / 4; ++i) {
+      const int4 e = make_int4(ex, ex + v[i].x, ex + v[i].x + v[i].y, ex + v[i].x + v[i].y + v[i].z);
+      ex = e.w + v[i].w;
+      c4[i] = e;
+      if (al16) {
+        reinterpret_cast<int4*>(cs)[i] = e;
+      } else {
+        cs[4 * i] = e.x;
+        cs[4 * i + 1] = e.y;
+        cs[4 * i + 2] = e.z;
+        cs[4 * i + 3] = e.w;
+      }
+    }
+    if (lane == 63) cellStart[(size_t)p * (GRID_CELLS + 1) + GRID_CELLS] = ex;
   }
   __syncthreads();
-  int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
-  for (int i = lane; i <= GRID_CELLS; i += 64) cs[i] = cnt[i];
-  __syncthreads();
-  // stable scatter in keypoint order, 64 keys at a time; lanes holding the same
-  // cell find each other with 12 ballots over the cell id bits
   int32_t* ci = cellIdx + (size_t)p * kpStride;
+  const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
+  const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
+  uint4* sg = staged ? staged + (size_t)p * kpStride : nullptr;
   const unsigned long long ltMask = (1ull << lane) - 1ull;
+  // round r's fields, loaded one round ahead
+  float nx = 0.f, ny = 0.f, nu = -1.f;
+  int noct = 0, nlk = 0;
+  auto load = [&](int k) {
+    if (k < n) {
+      nx = K[k].x;
+      ny = K[k].y;
+      if (sg) {
+        noct = K[k].octave;
+        nlk = LK ? LK[k] : 0;
+        nu = UR ? UR[k] : -1.0f;
+      }
+    }
+  };
+  load(lane);
   for (int base = 0; base < n; base += 64) {
     const int k = base + lane;
-    int c = k < n ? grid_cell(K[k], minX, minY, invW, invH) : -1;
+    const float x = nx, y = ny, u = nu;
+    const int oct = noct, lk = nlk;
+    load(k + 64);
+    int c = -1;
+    if (k < n) {
+      orb_keypoint_t kp;
+      kp.x = x;
+      kp.y = y;
+      c = grid_cell(kp, minX, minY, invW, invH);
+    }
     const int id = c < 0 ? 4095 : c;
     unsigned long long peers = __ballot(1);
 #pragma unroll
@@ -171,6 +147,14 @@ __global__ __launch_bounds__(64) void k_grid_build_wave(const orb_keypoint_t* __
     __builtin_amdgcn_wave_barrier();
     if (c >= 0) {
       ci[pos] = k;
+      if (sg) {
+        uint4 e;
+        e.x = __float_as_uint(x);
+        e.y = __float_as_uint(y);
+        e.z = (uint32_t)k | ((uint32_t)oct << 24) | (lk ? 0x80000000u : 0u);
+        e.w = __float_as_uint(u);
+        sg[pos] = e;
+      }
       if ((peers >> lane) == 1ull) cnt[c] += __popcll(peers);  // highest lane of the group
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -698,12 +682,8 @@ hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
                             int32_t* cellIdx, int nproblems, hipStream_t s) {
-  if (kpStride <= GB_LDS_KEYS)
-    hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(GB_T), 0, s, keys, nkeys, kpStride,
-                       minX, minY, invW, invH, cellStart, cellIdx, nullptr, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL(k_grid_build_wave, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride,
-                       minX, minY, invW, invH, cellStart, cellIdx);
+  hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride, minX,
+                     minY, invW, invH, cellStart, cellIdx, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -715,7 +695,7 @@ hipError_t orb_k_grid_build_staged(const orb_keypoint_t* keys, const int32_t* nk
                                    int32_t* cellStart, int32_t* cellIdx, void* staged,
                                    int nproblems, hipStream_t s) {
   if (kpStride > GB_LDS_KEYS) return hipErrorNotSupported;
-  hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(GB_T), 0, s, keys, nkeys, kpStride, minX,
+  hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride, minX,
                      minY, invW, invH, cellStart, cellIdx, locked, uright, (uint4*)staged);
   return hipGetLastError();
 }

@@ -243,6 +243,7 @@ struct StageProfiler {
   // caller's stream.
   static constexpr int kMaxStages = 8;
   bool enabled = false;
+  bool serial = false;  // isolated timing: every stage on the caller's stream, one after another
   int nStages = 0;
   const char* names[kMaxStages] = {};
   int maxSeg[kMaxStages] = {1, 1, 1, 1, 1, 1, 1, 1};
@@ -381,6 +382,10 @@ struct orb_extractor {
   // hImg / hOut so each call is one DMA in and one DMA out
   DevBuf dImg, dOne;
   HostBuf hImg, hOut, hLvl;  // hLvl: staging of orb_extractor_pyramid_level / _blurred_level
+  // host mirror of the single-frame call's levels 1.. (orb_extractor_host_pyramid):
+  // once asked for, the arena's D2H joins every later call's graph
+  HostBuf hPyr;
+  bool pyrReadback = false, hPyrValid = false;
   int oneCap = 0;            // capacity of the dOne layout
   bool lastSingle = false;   // the last call was orb_extractor_extract (dOne is current)
   // the whole single-image call (H2D, every kernel, D2H) as one hipGraph per
@@ -754,7 +759,8 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   // in one launch once the chain has written level sideLevels; the rest follow
   // the chain on the main stream.
   const int l0End = P.lv[0].cellEnd;
-  const bool l0Side = !useBands && !noL0Overlap && l0End > 0 && P.nlevels > 1;
+  // (profile mode 2 times each stage alone: no side stream)
+  const bool l0Side = !useBands && !noL0Overlap && !(ev && pf.serial) && l0End > 0 && P.nlevels > 1;
   // ORB_FAST_PER_LEVEL=1 (A/B knob, off): levels >= 1 on the side stream too,
   // each launched as soon as the chain has written its level.  Measured slower
   // (255k vs 260k frames/s; the chain, 0.52 -> 0.81 ms, loses its CUs to FAST),
@@ -1099,6 +1105,7 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   h->hImg.release();
   h->hOut.release();
   h->hLvl.release();
+  h->hPyr.release();
   if (h->oneExec) hipGraphExecDestroy(h->oneExec);
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
@@ -1187,6 +1194,8 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   if ((st = h->dOne.ensure(outBytes))) return st;
   if ((st = h->hImg.ensure(pitch))) return st;
   if ((st = h->hOut.ensure(outBytes))) return st;
+  if (h->pyrReadback && (st = h->hPyr.ensure((size_t)std::max<long long>(h->arenaBytes, 1)))) return st;
+  h->hPyrValid = false;
   // image -> pinned staging at the device row pitch
   for (int y = 0; y < height; ++y)
     memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
@@ -1199,6 +1208,9 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
                                reinterpret_cast<int32_t*>(d1), h->stream, capturing);
     if (r) return r;
     HIP_TRY(hipMemcpyAsync(h->hOut.p, d1, outBytes, hipMemcpyDeviceToHost, h->stream));
+    if (h->pyrReadback && h->arenaBytes > 0)  // levels 1.. for the host mirror, one DMA
+      HIP_TRY(hipMemcpyAsync(h->hPyr.p, h->dArena.p, (size_t)h->arenaBytes, hipMemcpyDeviceToHost,
+                             h->stream));
     return ORB_OK;
   };
   static const bool noGraph = getenv("ORB_NO_GRAPH") && atoi(getenv("ORB_NO_GRAPH")) > 0;
@@ -1208,7 +1220,8 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     const std::vector<const void*> key = {
         h->dImg.p, h->dOne.p, h->hImg.p, h->hOut.p, h->dArena.p, h->dCellKeys.p, h->dGKeys.p,
         h->dGNid.p, h->dCellCount.p, h->dOutKeys.p, h->dOutCount.p, h->dErr.p, h->dRtab.p,
-        h->dBands.p, h->dCells.p, h->dBlur.p, h->dTiles.p, h->dOctNodes.p, (const void*)(intptr_t)width,
+        h->dBands.p, h->dCells.p, h->dBlur.p, h->dTiles.p, h->dOctNodes.p,
+        h->pyrReadback ? h->hPyr.p : nullptr, (const void*)(intptr_t)width,
         (const void*)(intptr_t)height, (const void*)(intptr_t)cap};
     if (!h->oneExec || key != h->oneKey) {
       if (h->oneExec) hipGraphExecDestroy(h->oneExec);
@@ -1241,6 +1254,7 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->oneCap = cap;
   h->lastSingle = true;
+  h->hPyrValid = h->pyrReadback;
   const uint8_t* ho = h->hOut.as<uint8_t>();
   int32_t n = 0;
   memcpy(&n, ho, 4);
@@ -1307,6 +1321,37 @@ orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t*
   return copy_level_to_host(h, dst, dst_stride, src, sstride, w, hh);
 }
 
+orb_status_t orb_extractor_host_pyramid(orb_extractor_t* h, int level, const uint8_t** data,
+                                        int* width, int* height, size_t* stride) {
+  if (!h || !data) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (!h->lastSingle || level < 0 || level >= h->nlevels || h->planW < 0) return ORB_EINVAL;
+  const OrbLevelDesc& d = h->plan.lv[level];
+  if (width) *width = d.w;
+  if (height) *height = d.h;
+  if (level == 0) {  // the call's own pinned staging of the image
+    *data = h->hImg.as<uint8_t>();
+    if (stride) *stride = ((size_t)d.w + 63) & ~(size_t)63;
+    return ORB_OK;
+  }
+  if (!h->hPyrValid) {
+    // first request: this call's levels now (one DMA), every later call's in
+    // its graph
+    hipSetDevice(h->device);
+    orb_status_t st = h->hPyr.ensure((size_t)std::max<long long>(h->arenaBytes, 1));
+    if (st) return st;
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));
+    HIP_TRY(hipMemcpyAsync(h->hPyr.p, h->dArena.p, (size_t)h->arenaBytes, hipMemcpyDeviceToHost,
+                           h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->pyrReadback = true;
+    h->hPyrValid = true;
+  }
+  *data = h->hPyr.as<uint8_t>() + d.arenaOff;
+  if (stride) *stride = (size_t)d.pitch;
+  return ORB_OK;
+}
+
 orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t* dst,
                                          size_t dst_stride, int* width, int* height) {
   if (!h) return ORB_EINVAL;
@@ -1342,6 +1387,7 @@ orb_status_t orb_extractor_profile(orb_extractor_t* h, int enable) {
   h->prof.drain();
   h->prof.reset();
   h->prof.enabled = enable != 0;
+  h->prof.serial = enable == 2;
   return ORB_OK;
 }
 

@@ -22,13 +22,17 @@
 //   harness fuse    DIR   Fuse(pKF, vpMapPoints, th) against a sequential loop
 //                         over the oracle's targets (Replace / AddObservation order)
 //   harness sim3    DIR   SearchBySim3(pKF1, pKF2, vpMatches12, ...)
+//   harness time    DIR   per-frame wall times of the drop-ins (bench.py `dropin`)
 #include <assert.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <chrono>
 #include <fstream>
+#include <thread>
 #include <functional>
 #include <sstream>
 #include <string>
@@ -45,6 +49,9 @@ namespace cv {
 static size_t elem(int t) { return t == CV_32F ? 4 : 1; }
 Mat::Mat() : rows(0), cols(0), step(0), data(nullptr) {}
 Mat::Mat(int r, int c, int t) : Mat() { create(r, c, t); }
+Mat::Mat(int r, int c, int t, void* d, size_t st) : rows(r), cols(c), step(st), data((unsigned char*)d) {
+  typ = t;
+}
 void Mat::create(int r, int c, int t) {
   if (data && rows == r && cols == c && typ == t) return;
   rows = r;
@@ -550,9 +557,118 @@ static int run_sim3() {
   return 0;
 }
 
+
+// ------------------------------------------------------------- timing
+// harness time DIR: the drop-ins at ORB-SLAM2's own call granularity, one
+// frame per call (bench.py's `dropin` key).  Mono: Frame::ExtractORB
+// (src/Frame.cc:278-285) through ORBextractor::operator(), then
+// Tracking::SearchLocalPoints' SearchByProjection(F, vpMapPoints, th)
+// (src/Tracking.cc:1381-1390) over MapPoint objects (the flatten of every point
+// -- mutexed getters, GetDescriptor -- included).  Stereo: the two extractions
+// on two threads as the stereo Frame constructor runs them (src/Frame.cc:81-84),
+// then Frame::ComputeStereoMatches.  Median wall times of ITERS frames.
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+static double median(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 0.0 : v[v.size() / 2];
+}
+static int run_time() {
+  const std::vector<double> m = meta();
+  const int W = (int)m[0], H = (int)m[1], NF = (int)m[2], NMP = (int)m[3], NFR = (int)m[4],
+            ITERS = (int)m[5];
+  const float bf = (float)m[6], fx = (float)m[7];
+  auto imgs = rdv<uint8_t>("imgs.bin"), imgsR = rdv<uint8_t>("imgsR.bin");
+  auto trk = rdv<orb_mp_track_t>("tracks.bin");
+  auto mpd = rdv<uint8_t>("mpdesc.bin");
+  auto scale = rdv<float>("scale.bin");
+  Frame::mnMinX = 0.f;
+  Frame::mnMaxX = (float)W;
+  Frame::mnMinY = 0.f;
+  Frame::mnMaxY = (float)H;
+  Frame::fx = fx;
+  std::vector<cv::Mat> fr(NFR), frR(NFR);
+  for (int f = 0; f < NFR; ++f) {
+    fr[f] = cv::Mat(H, W, CV_8U);
+    frR[f] = cv::Mat(H, W, CV_8U);
+    memcpy(fr[f].data, &imgs[(size_t)f * W * H], (size_t)W * H);
+    memcpy(frR[f].data, &imgsR[(size_t)f * W * H], (size_t)W * H);
+  }
+  // each frame's local map as MapPoint objects (built once: the map exists
+  // before tracking runs)
+  std::vector<std::vector<MapPoint*>> maps(NFR);
+  for (int f = 0; f < NFR; ++f)
+    for (int i = 0; i < NMP; ++i) {
+      const orb_mp_track_t& t = trk[(size_t)f * NMP + i];
+      MapPoint* p = new MapPoint(nullptr, nullptr, 0, 0, &mpd[((size_t)f * NMP + i) * 32], t.has_obs,
+                                 t.bad);
+      p->mTrackProjX = t.proj_x;
+      p->mTrackProjY = t.proj_y;
+      p->mTrackProjXR = t.proj_xr;
+      p->mTrackViewCos = t.view_cos;
+      p->mnTrackScaleLevel = t.level;
+      p->mbTrackInView = t.in_view != 0;
+      p->id_ = i;
+      maps[f].push_back(p);
+    }
+  ORBextractor ext(NF, 1.2f, 8, 20, 7);
+  ORBmatcher matcher(0.8f, true);
+  std::vector<double> tExt, tMatch, tTot;
+  long matches = 0;
+  for (int it = -3; it < ITERS; ++it) {
+    const int f = (it + 3) % NFR;
+    Frame F;
+    const double t0 = now_ms();
+    ext(fr[f], cv::Mat(), F.mvKeys, F.mDescriptors);
+    const double t1 = now_ms();
+    F.N = (int)F.mvKeys.size();
+    F.mvKeysUn = F.mvKeys;
+    F.mvScaleFactors = scale;
+    F.mnScaleLevels = (int)scale.size();
+    F.mvpMapPoints.assign(F.N, nullptr);
+    const int n = matcher.SearchByProjection(F, maps[f], 1.0f);
+    const double t2 = now_ms();
+    if (it >= 0) {
+      tExt.push_back(t1 - t0);
+      tMatch.push_back(t2 - t1);
+      tTot.push_back(t2 - t0);
+      matches += n;
+    }
+  }
+  ORBextractor L(2 * NF, 1.2f, 8, 20, 7), R(2 * NF, 1.2f, 8, 20, 7);
+  std::vector<double> tSt;
+  for (int it = -3; it < ITERS; ++it) {
+    const int f = (it + 3) % NFR;
+    Frame F;
+    F.mpORBextractorLeft = &L;
+    F.mpORBextractorRight = &R;
+    F.mbf = bf;
+    const double t0 = now_ms();
+    std::thread tl([&] { L(fr[f], cv::Mat(), F.mvKeys, F.mDescriptors); });
+    R(frR[f], cv::Mat(), F.mvKeysRight, F.mDescriptorsRight);
+    tl.join();
+    F.N = (int)F.mvKeys.size();
+    F.ComputeStereoMatches();
+    const double t1 = now_ms();
+    if (it >= 0) tSt.push_back(t1 - t0);
+  }
+  char buf[512];
+  snprintf(buf, sizeof buf,
+           "{\"mono_extract_ms\": %.5f, \"mono_search_by_projection_ms\": %.5f, "
+           "\"mono_frame_ms\": %.5f, \"stereo_pair_ms\": %.5f, \"frames\": %d, "
+           "\"mean_matches\": %.2f}\n",
+           median(tExt), median(tMatch), median(tTot), median(tSt), ITERS, (double)matches / ITERS);
+  wr("time.json", buf, strlen(buf));
+  for (auto& v : maps)
+    for (MapPoint* p : v) delete p;
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc != 3) {
-    fprintf(stderr, "usage: harness extract|stereo|local|fuse|sim3 DIR\n");
+    fprintf(stderr, "usage: harness extract|stereo|local|fuse|sim3|time DIR\n");
     return 2;
   }
   g_dir = argv[2];
@@ -563,6 +679,7 @@ int main(int argc, char** argv) {
     if (cmd == "local") return run_local();
     if (cmd == "fuse") return run_fuse();
     if (cmd == "sim3") return run_sim3();
+    if (cmd == "time") return run_time();
   } catch (const std::exception& e) {
     fprintf(stderr, "harness: %s\n", e.what());
     return 1;

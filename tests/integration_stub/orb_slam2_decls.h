@@ -47,6 +47,7 @@ class Mat {
  public:
   Mat();
   Mat(int rows, int cols, int type);
+  Mat(int rows, int cols, int type, void* data, size_t step);  // external data, not owned
   int rows, cols;
   size_t step;
   unsigned char* data;

@@ -28,7 +28,7 @@ def test_two_ranks_shard_and_gather(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
            "--dist-backend", "gloo", "--frames", "512", "--steps", "2", "--warmup", "1",
-           "--no-cpu", "--no-secondary", "--threads", "4"]
+           "--no-cpu", "--no-secondary", "--no-dropin", "--threads", "4"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -49,7 +49,7 @@ def test_bench_gpus_flag_launches_ranks(gpu):
                         "TORCHELASTIC_RUN_ID")}
     env.update(ORB_BENCH_DEVICE="0", OMP_NUM_THREADS="4")
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-           "--frames", "512", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-secondary",
+           "--frames", "512", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-secondary", "--no-dropin",
            "--threads", "4", "--host-frames", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -66,7 +66,7 @@ def test_rccl_gather_single_rank_torchrun(gpu):
     env = dict(os.environ, OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
-           "--frames", "1024", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-secondary",
+           "--frames", "1024", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-secondary", "--no-dropin",
            "--threads", "4", "--host-frames", "1024", "--host-passes", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -448,3 +448,18 @@ np.savez({str(tmp_path / 'out.npz')!r}, k=k.cpu().numpy(), d=d.cpu().numpy(), n=
         assert n == len(kr), (i, n, len(kr))
         assert out["k"][i, :n].tobytes() == kr.tobytes()
         assert out["d"][i, :n].tobytes() == dr.tobytes()
+
+
+def test_host_pyramid_mirror(gpu, oracle):
+    """orb_extractor_host_pyramid: the first request copies the call's levels
+    once, later calls carry the copy in their graph; every level equals the
+    oracle.s pyramid on consecutive frames."""
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    for f in range(3):
+        img = gpu.synth_image(21, f, 1241, 376)
+        ext(img)
+        ref = oracle.pyramid(img)
+        for l in range(8):
+            assert np.array_equal(ext.host_pyramid(l), ref[l]), (f, l)
+    with pytest.raises(gpu.OrbError):
+        ext.host_pyramid(8)
