@@ -784,6 +784,19 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef FC_PERM
 #define FC_PERM (!FC_ROWMAJOR)  // pretest lane -> pixel-group permutation (LDS banking)
 #endif
+// Attribution builds (tools/r04/fast_attr.sh; results WRONG, never shipped):
+// FC_STUB = k drops the last k phases of the cell pipeline, each build keeping
+// the work before it alive through a sink, so the differences between
+// successive builds give each phase's time and instruction counts:
+//   1 NMS + key emit, 2 + arc-strength scoring / corner list,
+//   3 + candidate queue append (scan, per-lane loop), 4 + compass pretest,
+//   5 + LDS staging stores (the global loads stay, XOR-ed into the sink).
+// Stubbed builds write a count of 0 (the octree and descriptors then idle).
+// Phase B (minThFAST) still runs where the real kernel would run it while the
+// corner count is known (FC_STUB 1); from FC_STUB 2 on it follows the queue.
+#ifndef FC_STUB
+#define FC_STUB 0
+#endif
 
 // LDS row pitch (bytes) of a cell ROI C pixels wide: byte 8 is interior column
 // 0 (ROI column 3), groups of 8 interior pixels read [8k, 8k + 24)
@@ -935,6 +948,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       raw[4 * k + 3] = (uint32_t)v[3];
     }
   };
+  [[maybe_unused]] uint32_t sink = 0;
   int ci = cell_of(0);
   if (ci >= cellEnd) return;
   OrbCellDesc ncd = cells[ci];
@@ -945,7 +959,12 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   const long long slot = (long long)img * plan.ncells + ci;
   const bool tiny = R < 7 || C < 7;
   const int P = PT ? PT : fc_pitch(C);
+#if FC_STUB >= 5
+  for (int k = 0; k < 16; ++k) sink ^= raw[k];
+  if (false) {
+#else
   if (!tiny && lane < R) {
+#endif
     const int nS = ((C + 20) & ~7) >> 2;  // dwords per row (<= 14, host-checked)
     uint2* dst = reinterpret_cast<uint2*>(tile + lane * P);
 #pragma unroll
@@ -990,6 +1009,11 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   int nq = 0, nc = 0;  // wave-uniform queue / corner counts
   // score the queued candidates, list the corners (m > t)
   auto flush = [&](int t, bool fresh) {
+#if FC_STUB >= 2
+    nc += nq;  // stand-in corner count: every queued candidate
+    nq = 0;
+    return;
+#endif
     for (int j0 = 0; j0 < nq; j0 += 64) {
       const int j = j0 + lane;
       bool corner = false;
@@ -1052,6 +1076,12 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       const bool valid = g0 + pl < nG;
       const bool last = k == nK - 1;
       const int o = valid ? off : 3 * P + 8;  // invalid lanes read group 0 (masked below)
+#if FC_STUB >= 4
+      sink ^= (uint32_t)o;
+      if (false) {
+#else
+      {
+#endif
       // bytes o-8 .. o+15 of the row, and o .. o+7 three rows down / up
       const uint2* rw = reinterpret_cast<const uint2*>(tile + o);
       const uint2 A = rw[-1], B = rw[0], Cc = rw[1];
@@ -1091,6 +1121,10 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
       const uint32_t fails = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
       uint32_t mk = ~((fails * 0x01020408u) >> 24) &
                     (valid ? (last ? (1u << nvLast) - 1u : 0xFFu) : 0u);
+#if FC_STUB >= 3
+      sink ^= mk;
+      nq += __builtin_amdgcn_readfirstlane(mk) & 1;  // (a wave-uniform stand-in count)
+#else
       const int cnt = __builtin_popcount(mk);
       int incl = wave_incl_scan(cnt);
       // opaque: otherwise hipcc forms incl - cnt from the scan's partial DPP
@@ -1103,6 +1137,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
         queue[pos++] = (uint16_t)(off + j);
       }
       nq += __builtin_amdgcn_readlane(incl, 63);
+#endif  // FC_STUB >= 3
 #else
       // pixel j of a valid lane is interior when j < nvLast or the group is not a row's last
       const unsigned long long vm = __ballot(valid), vIn = __ballot(valid && !last);
@@ -1117,6 +1152,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
         nq += __popcll(bj);
       }
 #endif
+      }  // pretest (FC_STUB < 4)
       k += kInc;
       off += dOff;
       if (k >= nK) {
@@ -1239,7 +1275,10 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
   (void)compact;
 #endif
   fast_pass(ti, true);
-#if FC_ROWMAJOR
+#if FC_STUB >= 1
+  int n = nc;
+  (void)nms_emit;
+#elif FC_ROWMAJOR
   int n = nms_emit(ti);
 #else
   nms(ti);
@@ -1249,14 +1288,21 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     // ---- phase B: no keypoint at iniThFAST -> minThFAST (:846-850)
     nc = 0;
     fast_pass(tm, false);
-#if FC_ROWMAJOR
+#if FC_STUB >= 1
+    n = nc;
+#elif FC_ROWMAJOR
     n = nms_emit(tm);
 #else
     nms(tm);
     n = compact();
 #endif
   }
+#if FC_STUB >= 1
+  sink ^= (uint32_t)n;
+  if (lane == 0) cellCount[slot] = sink == 0xFFFFFFFFu ? 1 : 0;
+#else
   if (lane == 0) cellCount[slot] = n;
+#endif
   ci = ciNext;
   wave_lds_sync();  // the next cell's staging overwrites the tile
   }  // cell loop

@@ -18,3 +18,5 @@ print("cpu", r["cpu_baseline"]["value"], r["cpu_baseline"]["all_cores"])
 print("dropin", r.get("dropin"))
 print("host", r["host_input"]["frames_per_s"])
 PY
+bash tools/r04/fast_attr.sh > "$O/s1_fattr.log" 2>&1 || { tail -20 "$O/s1_fattr.log"; exit 1; }
+tail -14 "$O/s1_fattr.log"
