@@ -587,12 +587,15 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
     const uint8_t* __restrict__ mpDesc, const int32_t* __restrict__ nmps, int mpStride,
     const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
     const uint32_t* __restrict__ topk, const int32_t* __restrict__ ncand,
-    int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches) {
+    int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches,
+    const int32_t* __restrict__ done, long long doneStride) {
   constexpr int NOCLAIM = 0x7FFFFFFF;
   extern __shared__ __attribute__((aligned(16))) int claims[];  // 2 x kpStride
   __shared__ int sCount[T / 64];
   __shared__ int sChanged[2];
   const int p = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // after the Jacobi rounds (k_proj_jacobi): only problems they left unsettled
+  if (done && done[(long long)p * doneStride] != 0) return;
   const int n = nkeys[p], M = nmps[p];
   if (t < 2) sChanged[t] = 0;
   for (int i = t; i < 2 * kpStride; i += T) claims[i] = NOCLAIM;
@@ -670,6 +673,109 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
   }
 }
 
+
+// Jacobi resolve for large local maps (C5: 16 problems x 50,000 points): the
+// fixed-point iteration of k_proj_resolve_fp taken over a whole problem at
+// once and spread over the chip, one launch per round.  Round r: every point
+// m re-decides with "keypoint k taken" = claims_{r-1}[k] < m (the smallest
+// point that claimed k with observations in round r-1), stores its decision,
+// and claims its locking choice in claims_r (atomicMin).  The sequential
+// result is the unique fixed point (point 0 decides alone; point m's decision
+// depends only on earlier points'), so once a round changes no claim its
+// decisions are final: the next launch commits them (kpMatch = the last
+// accepting point, atomicMax) and marks the problem done.  Three claim
+// buffers rotate (round r reads r-1, writes r, clears r+1, which round r-2
+// wrote and round r-1 read).  The launch sequence is fixed (rounds 0..R-1, a
+// commit-only launch R, then k_proj_resolve_fp for the problems not done), so
+// the result is exact however many rounds a problem needs.
+// Scratch per problem: flags[0..R) "round r changed a claim", flags[R] done,
+// three claim buffers of kpStride, the decisions (mpStride).
+__host__ __device__ inline long long jacobi_claims_off() { return 64; }
+__host__ __device__ inline long long jacobi_stride(int kpStride, int mpStride) {
+  return (jacobi_claims_off() + 3LL * kpStride + mpStride + 63) & ~63LL;
+}
+#define JAC_T 256
+__global__ __launch_bounds__(JAC_T) void k_proj_jacobi_init(int32_t* __restrict__ scr, long long stride,
+                                                         int kpStride, int R,
+                                                         const int32_t* __restrict__ nkeys,
+                                                         int32_t* __restrict__ kpMatch,
+                                                         int32_t* __restrict__ nmatches) {
+  const int p = blockIdx.y, i = blockIdx.x * JAC_T + threadIdx.x;
+  int32_t* S = scr + (long long)p * stride;
+  if (i <= R) S[i] = 0;
+  if (i < 3 * kpStride) S[jacobi_claims_off() + i] = 0x7FFFFFFF;
+  if (i < kpStride && i < nkeys[p]) kpMatch[(long long)p * kpStride + i] = -1;
+  if (i == 0) nmatches[p] = 0;
+}
+
+__global__ __launch_bounds__(JAC_T) void k_proj_jacobi(
+    const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
+    const float* __restrict__ uright, const uint8_t* __restrict__ locked,
+    int kpStride, const orb_mp_track_t* __restrict__ mps,
+    const uint8_t* __restrict__ mpDesc, const int32_t* __restrict__ nmps, int mpStride,
+    const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx, ProjParams P,
+    const uint32_t* __restrict__ topk, const int32_t* __restrict__ ncand,
+    int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches, int32_t* __restrict__ scr,
+    long long stride, int r, int R) {
+  __shared__ int sCnt[JAC_T / 64];
+  const int p = blockIdx.y, t = threadIdx.x, lane = t & 63;
+  const int m = blockIdx.x * JAC_T + t, M = nmps[p];
+  int32_t* S = scr + (long long)p * stride;
+  // S[R] = the launch that committed the problem, + 1: an earlier launch's
+  // commit ends the problem; a commit by another workgroup of this launch
+  // does not (this workgroup's points are still to be committed)
+  const int done = S[R];
+  if (done != 0 && done != r + 1) return;
+  int32_t* claims = S + jacobi_claims_off();
+  int32_t* dec = claims + 3LL * kpStride;
+  const size_t pbase = (size_t)p * mpStride;
+  if (r >= 1 && S[r - 1] == 0) {
+    // round r-1 changed no claim: its decisions are the sequential result
+    int acc = -1;
+    if (m < M) {
+      acc = dec[m];
+      if (acc >= 0) atomicMax(&kpMatch[(size_t)p * kpStride + acc], m);
+    }
+    const int c = __popcll(__ballot(acc >= 0));
+    if (lane == 0) sCnt[t >> 6] = c;
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+#pragma unroll
+      for (int i = 0; i < JAC_T / 64; ++i) tot += sCnt[i];
+      if (tot) atomicAdd(&nmatches[p], tot);
+      S[R] = r + 1;
+    }
+    return;
+  }
+  if (r >= R) return;  // commit-only launch, problem still changing: k_proj_resolve_fp
+  const int* cur = claims + (long long)((r + 2) % 3) * kpStride;
+  int* nxt = claims + (long long)(r % 3) * kpStride;
+  int* clr = claims + (long long)((r + 1) % 3) * kpStride;
+  for (int i = blockIdx.x * JAC_T + t; i < kpStride; i += gridDim.x * JAC_T) clr[i] = 0x7FFFFFFF;
+  bool changed = false;
+  if (m < M) {
+    const int nc = ncand[pbase + m];
+    int acc = -1;
+    if (nc > 0) {
+      const uint4 q = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
+      const uint32_t e[TOPK] = {q.x, q.y, q.z, q.w};
+      acc = fp_choose(e, nc, m, cur, mps + pbase + m, mpDesc + (pbase + m) * 32,
+                      keys + (size_t)p * kpStride, desc + (size_t)p * kpStride * 32,
+                      locked ? locked + (size_t)p * kpStride : nullptr,
+                      uright ? uright + (size_t)p * kpStride : nullptr,
+                      cellStart + (size_t)p * (GRID_CELLS + 1), cellIdx + (size_t)p * kpStride, P);
+    }
+    const int old = r > 0 ? dec[m] : -1;
+    dec[m] = acc;
+    const bool obs = acc >= 0 && mps[pbase + m].has_obs != 0;
+    if (obs) atomicMin(&nxt[acc], m);
+    const int oldClaim = (old >= 0 && mps[pbase + m].has_obs != 0) ? old : -1;
+    changed = (obs ? acc : -1) != oldClaim;
+  }
+  if (__ballot(changed) != 0ull && lane == 0) S[r] = 1;
+}
+
 // ------------------------------------------------------------ host launchers
 extern "C" {
 
@@ -733,7 +839,7 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
                               const int32_t* nmps, int mpStride, const int32_t* cellStart,
                               const int32_t* cellIdx, const void* params, const uint32_t* topk,
                               const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
-                              int nproblems, hipStream_t s) {
+                              int nproblems, int32_t* jacScratch, hipStream_t s) {
   const ProjParams P = *(const ProjParams*)params;
   if (nproblems <= 0) return hipSuccess;
   const size_t words = (size_t)((kpStride + 31) / 32);
@@ -747,18 +853,40 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   static const int fpMode = getenv("ORB_RESOLVE_FP") ? atoi(getenv("ORB_RESOLVE_FP")) : 1;
   static const int fpMin = getenv("ORB_RESOLVE_FP_MIN") ? atoi(getenv("ORB_RESOLVE_FP_MIN")) : 20000;
   const size_t ldsFp = (size_t)kpStride * 8;
-  if (mpStride >= fpMin && fpMode == 256 && ldsFp <= 64 * 1024) {
+  // Large maps: Jacobi rounds over the whole chip first (k_proj_jacobi), the
+  // windowed fixed-point kernel after them for any problem not yet settled
+  // (ORB_RESOLVE_JACOBI=0: the windowed kernel alone; ORB_JACOBI_ROUNDS = R)
+  static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 1;
+  static const int jacR =
+      getenv("ORB_JACOBI_ROUNDS") ? std::max(1, std::min(48, atoi(getenv("ORB_JACOBI_ROUNDS")))) : 4;
+  const bool fp = mpStride >= fpMin && fpMode > 0 && ldsFp <= 64 * 1024;
+  const int32_t* done = nullptr;
+  long long doneStride = 0;
+  if (fp && jacOn > 0 && jacScratch) {
+    const long long js = jacobi_stride(kpStride, mpStride);
+    const int initN = std::max(3 * kpStride, jacR + 1);
+    hipLaunchKernelGGL(k_proj_jacobi_init, dim3((initN + JAC_T - 1) / JAC_T, nproblems), dim3(JAC_T),
+                       0, s, jacScratch, js, kpStride, jacR, nkeys, kpMatch, nmatches);
+    const dim3 g((mpStride + JAC_T - 1) / JAC_T, nproblems);
+    for (int r = 0; r <= jacR; ++r)
+      hipLaunchKernelGGL(k_proj_jacobi, g, dim3(JAC_T), 0, s, keys, desc, uright, locked, kpStride,
+                         mps, mpDesc, nmps, mpStride, cellStart, cellIdx, P, topk, ncand, kpMatch,
+                         nmatches, jacScratch, js, r, jacR);
+    done = jacScratch + jacR;
+    doneStride = js;
+  }
+  if (fp && fpMode == 256) {
     hipLaunchKernelGGL(k_proj_resolve_fp<256>, dim3(nproblems), dim3(256), ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                       cellIdx, P, topk, ncand, kpMatch, nmatches);
-  } else if (mpStride >= fpMin && fpMode == 512 && ldsFp <= 64 * 1024) {
+                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
+  } else if (fp && fpMode == 512) {
     hipLaunchKernelGGL(k_proj_resolve_fp<512>, dim3(nproblems), dim3(512), ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                       cellIdx, P, topk, ncand, kpMatch, nmatches);
-  } else if (mpStride >= fpMin && fpMode > 0 && ldsFp <= 64 * 1024) {
+                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
+  } else if (fp) {
     hipLaunchKernelGGL(k_proj_resolve_fp<1024>, dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                       cellIdx, P, topk, ncand, kpMatch, nmatches);
+                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
   } else if (mpStride >= 20000)
     hipLaunchKernelGGL(k_proj_resolve<8>, dim3(nproblems), dim3(512), lds, s, keys, desc, uright,
                        locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
@@ -789,6 +917,13 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
 }
 
 size_t orb_k_proj_params_size(void) { return sizeof(ProjParams); }
+
+// bytes of Jacobi-resolve scratch for n problems (0: the windowed kernel only)
+size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems) {
+  static const int fpMin = getenv("ORB_RESOLVE_FP_MIN") ? atoi(getenv("ORB_RESOLVE_FP_MIN")) : 20000;
+  if (mpStride < fpMin) return 0;
+  return (size_t)jacobi_stride(kpStride, mpStride) * 4 * (size_t)nproblems;
+}
 
 }  // extern "C"
 

@@ -85,7 +85,8 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
                               const int32_t* nmps, int mpStride, const int32_t* cellStart,
                               const int32_t* cellIdx, const void* params, const uint32_t* topk,
                               const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
-                              int nproblems, hipStream_t s);
+                              int nproblems, int32_t* jacScratch, hipStream_t s);
+size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems);
 size_t orb_k_proj_params_size(void);
 size_t orb_k_stereo_params_size(void);
 hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc, const int32_t* nleft,
@@ -1490,6 +1491,7 @@ struct orb_matcher {
   StageProfiler prof;
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
+  DevBuf dJac;  // Jacobi-resolve scratch (large local maps)
   // stereo / frame / BoW scratch
   DevBuf dStRowStart, dStRowIdx;  // stereo vRowIndices (CSR per pair)
   DevBuf dProjStage;              // cell-ordered keypoints for k_proj_candidates (16 B per slot)
@@ -1555,7 +1557,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
   hipStreamSynchronize(m->stream);
   DevBuf* bufs[] = {&m->dKeys, &m->dDesc, &m->dUr, &m->dLocked, &m->dNKeys, &m->dMps,
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
-                    &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut,
+                    &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut, &m->dJac,
                     &m->dRKeys, &m->dRDesc, &m->dNR, &m->dPyr, &m->dPairLv, &m->dDepth,
                     &m->dSad, &m->dStRowStart, &m->dStRowIdx, &m->dProjStage, &m->dBowA, &m->dBowB, &m->dBowC, &m->dBowD, &m->dBowE,
                     &m->dBowF, &m->dBowG, &m->dBowH, &m->dBowI, &m->dBowJ, &m->dBowK,
@@ -1622,6 +1624,8 @@ orb_status_t orb_match_projection_local_batch(
   if ((st = m->dNcand.ensure((size_t)n_problems * std::max(mp_stride, 1) * 4))) return st;
   const bool stage = kp_stride <= orb_k_grid_stage_max();
   if (stage && (st = m->dProjStage.ensure((size_t)n_problems * kp_stride * 16))) return st;
+  const size_t jb = orb_k_proj_jacobi_bytes(kp_stride, mp_stride, n_problems);
+  if (jb && (st = m->dJac.ensure(jb))) return st;
   StageProfiler& pf = m->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
@@ -1646,7 +1650,8 @@ orb_status_t orb_match_projection_local_batch(
   HIP_TRY(orb_k_proj_resolve(d_keys, d_desc, nullptr, d_locked, d_nkeys, kp_stride, d_mps,
                              d_mp_desc, d_nmps, mp_stride, m->dCellStart.as<int32_t>(),
                              m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
-                             m->dNcand.as<int32_t>(), d_kp_match, d_nmatches, n_problems, s));
+                             m->dNcand.as<int32_t>(), d_kp_match, d_nmatches, n_problems,
+                             m->dJac.as<int32_t>(), s));
   PROF_REC(ev, pf.e(ev, 2), s);
   PROF_REC(ev, pf.t1(ev), s);
   return ORB_OK;
@@ -1726,6 +1731,8 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   const uint8_t* lk = kp_locked ? m->dLocked.as<uint8_t>() : nullptr;
   const bool stage = N <= orb_k_grid_stage_max();
   if (stage && (st = m->dProjStage.ensure((size_t)N * 16))) return st;
+  const size_t jb = orb_k_proj_jacobi_bytes(N, std::max(M, 1), 1);
+  if (jb && (st = m->dJac.ensure(jb))) return st;
   if (stage)
     HIP_TRY(orb_k_grid_build_staged(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), lk, ur,
                                     N, P.minX, P.minY, P.invW, P.invH,
@@ -1747,7 +1754,8 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
                              m->dMpDesc.as<uint8_t>(), m->dNMps.as<int32_t>(), std::max(M, 1),
                              m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
                              m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
-                             m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), 1, s));
+                             m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), 1,
+                             m->dJac.as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

@@ -114,3 +114,104 @@ def test_search_by_projection_empty(gpu, oracle):
     mps, mpd, _ = oracle.synth_local_map(1, k, d, 100, w, h)
     n, km = gpu.ORBmatcher(0.8).SearchByProjection(F0, mps, mpd, 1.0)
     assert n == 0 and len(km) == 0
+
+
+def _conflict_map(oracle, k, d, M, nsrc, seed=7):
+    rng = np.random.default_rng(seed)
+    mps = np.zeros(M, oracle.MP_TRACK_DTYPE)
+    src = rng.integers(0, nsrc, M)
+    mps["proj_x"] = k["x"][src] + rng.uniform(-2, 2, M).astype(np.float32)
+    mps["proj_y"] = k["y"][src] + rng.uniform(-2, 2, M).astype(np.float32)
+    mps["proj_xr"] = -1.0
+    mps["level"] = np.minimum(k["octave"][src] + rng.integers(0, 2, M), 7)
+    mps["view_cos"] = np.where(rng.random(M) < 0.5, 0.999, 0.9).astype(np.float32)
+    mps["in_view"] = rng.random(M) < 0.97
+    mps["bad"] = rng.random(M) < 0.02
+    mps["has_obs"] = rng.random(M) < 0.8
+    mpd = d[src].copy()
+    mpd ^= np.packbits(rng.random((M, 256)) < 0.1, axis=1, bitorder="little")
+    locked = (rng.random(len(k)) < 0.1).astype(np.uint8)
+    return mps, mpd, locked
+
+
+def test_search_by_projection_batch_large_maps(gpu, oracle):
+    """Device batch of large local maps with different sizes (30,000 / 50,000 /
+    24,000 points in a 50,000-point stride): the Jacobi rounds and, for the
+    problem with deep first-come chains, the windowed fixed-point fallback."""
+    torch = pytest.importorskip("torch")
+    w, h, nf = 1920, 1080, 4000
+    k, d, scale = _frame(gpu, oracle, w, h, nf, 5)
+    maps = [oracle.synth_local_map(5, k, d, 30000, w, h), oracle.synth_local_map(6, k, d, 50000, w, h),
+            _conflict_map(oracle, k, d, 24000, 200)]
+    P, S = len(maps), 50000
+    ext = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    cap = ext.capacity(w, h)
+    kk = np.zeros((P, cap), oracle.KEYPOINT_DTYPE)
+    dd = np.zeros((P, cap, 32), np.uint8)
+    lk = np.zeros((P, cap), np.uint8)
+    mp = np.zeros((P, S), oracle.MP_TRACK_DTYPE)
+    md = np.zeros((P, S, 32), np.uint8)
+    for i, (a, b, c) in enumerate(maps):
+        kk[i, :len(k)], dd[i, :len(k)], lk[i, :len(k)] = k, d, c
+        mp[i, :len(a)], md[i, :len(a)] = a, b
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).cuda()
+    dk, dde, dl, dm, dmd = t(kk), t(dd), t(lk), t(mp), t(md)
+    dn = torch.full((P,), len(k), dtype=torch.int32, device="cuda")
+    dnm = torch.tensor([len(a) for a, _, _ in maps], dtype=torch.int32, device="cuda")
+    km = torch.zeros((P, cap), dtype=torch.int32, device="cuda")
+    nm = torch.zeros(P, dtype=torch.int32, device="cuda")
+    m = gpu.ORBmatcher(0.8)
+    for _ in range(2):  # the second call reuses the scratch of the first
+        m.search_by_projection_batch(P, dk.data_ptr(), dde.data_ptr(), dn.data_ptr(), dl.data_ptr(),
+                                     cap, dm.data_ptr(), dmd.data_ptr(), dnm.data_ptr(), S, w, h,
+                                     scale, 1.0, km.data_ptr(), nm.data_ptr())
+        torch.cuda.synchronize()
+        for i, (a, b, c) in enumerate(maps):
+            n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, a, b, 1.0, 0.8, c)
+            assert int(nm[i]) == n_ref, i
+            assert np.array_equal(km[i, :len(k)].cpu().numpy(), km_ref), i
+
+
+@pytest.mark.parametrize("env", [{"ORB_JACOBI_ROUNDS": "1"}, {"ORB_JACOBI_ROUNDS": "48"},
+                                 {"ORB_RESOLVE_JACOBI": "0"}])
+def test_search_by_projection_resolve_schedules(gpu, oracle, tmp_path, env):
+    """The large-map resolve under each schedule (read once per process, so in
+    a child): one Jacobi round then the windowed fallback, up to 48 rounds,
+    and the windowed kernel alone; C5's map and a deep-conflict map."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    w, h = 1920, 1080
+    k, d, scale = _frame(gpu, oracle, w, h, 4000, 5)
+    cases = [oracle.synth_local_map(5, k, d, 50000, w, h), _conflict_map(oracle, k, d, 24000, 120)]
+    for i, (a, b, c) in enumerate(cases):
+        np.save(tmp_path / f"mps{i}.npy", a)
+        np.save(tmp_path / f"mpd{i}.npy", b)
+        np.save(tmp_path / f"lk{i}.npy", c)
+    np.save(tmp_path / "k.npy", k)
+    np.save(tmp_path / "d.npy", d)
+    np.save(tmp_path / "scale.npy", scale)
+    code = f"""
+import sys, numpy as np
+sys.path.insert(0, {str(root)!r}); sys.path.insert(0, {str(root / 'tests')!r})
+from conftest import load_pkg
+orb = load_pkg()
+T = {str(tmp_path)!r}
+k, d, scale = np.load(T + '/k.npy'), np.load(T + '/d.npy'), np.load(T + '/scale.npy')
+F = orb.Frame(k, d, scale, {w}, {h})
+for i in range(2):
+    n, km = orb.ORBmatcher(0.8).SearchByProjection(F, np.load(T + f'/mps{{i}}.npy'),
+                                                   np.load(T + f'/mpd{{i}}.npy'), 1.0,
+                                                   np.load(T + f'/lk{{i}}.npy'))
+    np.save(T + f'/km{{i}}.npy', km)
+    open(T + f'/n{{i}}.txt', 'w').write(str(n))
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-2000:]
+    for i, (a, b, c) in enumerate(cases):
+        n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, a, b, 1.0, 0.8, c)
+        assert int((tmp_path / f"n{i}.txt").read_text()) == n_ref, i
+        assert np.array_equal(np.load(tmp_path / f"km{i}.npy"), km_ref), i
