@@ -20,3 +20,5 @@ print("host", r["host_input"]["frames_per_s"])
 PY
 bash tools/r04/fast_attr.sh > "$O/s1_fattr.log" 2>&1 || { tail -20 "$O/s1_fattr.log"; exit 1; }
 tail -14 "$O/s1_fattr.log"
+bash tools/r04/gpu_sched_ab.sh > "$O/s1_sched.log" 2>&1 || { tail -20 "$O/s1_sched.log"; exit 1; }
+cat "$O/s1_sched.log"
