@@ -186,7 +186,8 @@ __global__ __launch_bounds__(64) void k_grid_build(const orb_keypoint_t* __restr
 #ifndef PROJ_WG
 #define PROJ_WG 512  // map points per workgroup (grid staged once per workgroup; swept 256-1024)
 #endif
-__global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
+template <int WG>
+__global__ __launch_bounds__(WG) void k_proj_candidates(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked, int kpStride,
     const int32_t* __restrict__ nkeys, const orb_mp_track_t* __restrict__ mps,
@@ -221,13 +222,13 @@ __global__ __launch_bounds__(PROJ_WG) void k_proj_candidates(
   for (int i = 0; i < ORB_MAX_LEVELS; ++i)
     if (tid == i) sScale[i] = P.scale[i];
   if (staged) {
-    for (int i = tid; i <= GRID_CELLS; i += PROJ_WG) sCS[i] = cs[i];
+    for (int i = tid; i <= GRID_CELLS; i += WG) sCS[i] = cs[i];
     const int nInGrid = cs[GRID_CELLS];
     if (stagedGrid) {
       const uint4* sg = stagedGrid + (size_t)p * kpStride;
-      for (int j = tid; j < nInGrid; j += PROJ_WG) sKp[j] = sg[j];
+      for (int j = tid; j < nInGrid; j += WG) sKp[j] = sg[j];
     } else {
-    for (int j = tid; j < nInGrid; j += PROJ_WG) {
+    for (int j = tid; j < nInGrid; j += WG) {
       const int idx = ci[j];
       const orb_keypoint_t kp = K[idx];
       uint4 e;
@@ -821,15 +822,27 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
   // dynamic LDS: the staged keypoints of a frame, sized to the key capacity
   const int stageCap = std::min(kpStride, PROJ_STAGE);
   const size_t lds = (size_t)stageCap * sizeof(uint4);
+  // Large problems (C5: 4,000 keypoints staged = 76 KB of LDS per workgroup,
+  // 50,000 points) take 1024-point workgroups: half the staging per point
+  // (ORB_PROJ_WG_LARGE=512 keeps the batch shape)
+  static const int wgLarge =
+      getenv("ORB_PROJ_WG_LARGE") ? atoi(getenv("ORB_PROJ_WG_LARGE")) : 1024;
+  const bool large = wgLarge == 1024 && stageCap > 2048 && mpMax >= 20000;
+  const void* fn = large ? (const void*)k_proj_candidates<1024> : (const void*)k_proj_candidates<PROJ_WG>;
   if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {  // with the static grid table
-    hipError_t e = hipFuncSetAttribute((const void*)k_proj_candidates,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_proj_candidates, dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems),
-                     dim3(PROJ_WG), lds, s,
-                     keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
-                     cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P, topk, ncand);
+  if (large)
+    hipLaunchKernelGGL(k_proj_candidates<1024>, dim3((mpMax + 1023) / 1024, nproblems), dim3(1024),
+                       lds, s, keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps,
+                       mpStride, cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P, topk,
+                       ncand);
+  else
+    hipLaunchKernelGGL(k_proj_candidates<PROJ_WG>, dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems),
+                       dim3(PROJ_WG), lds, s,
+                       keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
+                       cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P, topk, ncand);
   return hipGetLastError();
 }
 

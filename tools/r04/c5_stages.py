@@ -47,5 +47,7 @@ for B in [int(a) for a in sys.argv[1:]] or [16, 128]:
         name, ms, cnt = mt.profile_read(stg)
         parts.append(f"{name} {ms / n:.4f}")
     mt.profile(False)
-    print(f"C5 B={B}: pipelined {r['value']:.0f} problems/s, match alone "
+    import os
+    knobs = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith(("ORB_PROJ", "ORB_RESOLVE", "ORB_JACOBI")))
+    print(f"[{knobs}] C5 B={B}: pipelined {r['value']:.0f} problems/s, match alone "
           f"{r['match_only_problems_per_s']:.0f}; stages ms/call: " + "; ".join(parts), flush=True)

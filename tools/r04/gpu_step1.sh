@@ -5,6 +5,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p "$O"; cd "$R"
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > "$O/s1_tests.log" 2>&1 || { tail -30 "$O/s1_tests.log"; exit 1; }
 tail -2 "$O/s1_tests.log"
 timeout -k 10 200 python -u tools/r04/c5_stages.py 16 128 > "$O/s1_c5.log" 2>&1
+ORB_PROJ_WG_LARGE=512 timeout -k 10 200 python -u tools/r04/c5_stages.py 16 >> "$O/s1_c5.log" 2>&1
+ORB_RESOLVE_JACOBI=0 timeout -k 10 200 python -u tools/r04/c5_stages.py 16 >> "$O/s1_c5.log" 2>&1
+for R in 2 3 6; do ORB_JACOBI_ROUNDS=$R timeout -k 10 200 python -u tools/r04/c5_stages.py 16 >> "$O/s1_c5.log" 2>&1; done
 cat "$O/s1_c5.log"
 timeout -k 10 400 python bench.py > "$O/s1_bench.json" 2> "$O/s1_bench.err"
 python - <<'PY'
