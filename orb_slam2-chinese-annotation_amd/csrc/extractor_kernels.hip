@@ -798,16 +798,29 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define FC_STUB 0
 #endif
 
-// LDS row pitch (bytes) of a cell ROI C pixels wide: byte 8 is interior column
-// 0 (ROI column 3), groups of 8 interior pixels read [8k, 8k + 24)
-__host__ __device__ inline int fc_pitch(int C) { return ((C + 20) & ~7) + FC_PAD; }
+// LDS row pitch (bytes) of a cell ROI C pixels wide: byte 5 is ROI column 0,
+// byte 8 interior column 0 (ROI column 3); groups of 8 interior pixels read
+// [8k, 8k + 24).  FC_TIGHT: the pitch only has to hold the row (bytes 0 ..
+// C + 4, a multiple of 8 for the b64 reads): a row's last group may read up to
+// 12 bytes into the next row, but only for pixels past the interior, which the
+// pass mask drops (every ORB-SLAM2 grid: ROI widths 36-43 -> 48 instead of 56
+// bytes, and with the NMS bitmap gone from the row-major path, 7.0 -> 5.9 KB
+// of LDS per wave: 22 -> 27 waves per CU, the limit of this kernel's occupancy)
+#ifndef FC_TIGHT
+#define FC_TIGHT 1
+#endif
+__host__ __device__ inline int fc_pitch(int C) {
+  return (FC_TIGHT ? ((C + 12) & ~7) : ((C + 20) & ~7)) + FC_PAD;
+}
 __host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
   return (maxRows * fc_pitch(maxCols) + 15) & ~15;  // 16-byte aligned strength map
 }
 __host__ __device__ inline int fc_wave_bytes(int tileElems) {
-  // byte tile + strengths + queue + corners + 64 rows x 64-bit bitmap
-  return ((2 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + 512) + 15) & ~15;
+  // byte tile + strengths + queue + corners (+ 64 rows x 64-bit NMS bitmap,
+  // column-major path only)
+  return ((2 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + ((FC_ROWMAJOR && FC_TIGHT) ? 0 : 512)) + 15) & ~15;
 }
+#define FC_CONST_PITCH (FC_TIGHT ? 48 : 56)  // the compile-time instance
 
 // f16 pair {byte i0, byte i1} of the 8 bytes {hi:lo} (i in 0..7, lo first)
 __device__ __forceinline__ uint32_t byte_pair(uint32_t hi, uint32_t lo, int i0, int i1) {
@@ -965,7 +978,7 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
 #else
   if (!tiny && lane < R) {
 #endif
-    const int nS = ((C + 20) & ~7) >> 2;  // dwords per row (<= 14, host-checked)
+    const int nS = P >> 2;  // dwords per row (<= 14, host-checked): the row, no further
     uint2* dst = reinterpret_cast<uint2*>(tile + lane * P);
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
@@ -2761,10 +2774,10 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
   const int tileElems = fc_tile_elems(mr, mc);
   const size_t lds = orb_k_fast_cells_lds(mr, mc);
   // every W = 30 cell grid of the ORB-SLAM2 configurations has ROI widths of
-  // 36-43 pixels: pitch 56, the compile-time instance
+  // 36-43 pixels: pitch 48 (56 without FC_TIGHT), the compile-time instance
   static const bool noConstPitch = getenv("ORB_FAST_RT_PITCH") && atoi(getenv("ORB_FAST_RT_PITCH")) > 0;
-  const bool p56 = fc_pitch(mc) == 56 && !noConstPitch;
-  const void* fn = p56 ? (const void*)k_fast_cells<56> : (const void*)k_fast_cells<0>;
+  const bool p56 = fc_pitch(mc) == FC_CONST_PITCH && !noConstPitch;
+  const void* fn = p56 ? (const void*)k_fast_cells<FC_CONST_PITCH> : (const void*)k_fast_cells<0>;
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -2772,7 +2785,7 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
   const int n = cellEnd - cellBeg;
   dim3 grid((n + FC_WAVES * FC_CPW - 1) / (FC_WAVES * FC_CPW), nimg), block(64 * FC_WAVES);
   if (p56)
-    hipLaunchKernelGGL(k_fast_cells<56>, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
+    hipLaunchKernelGGL(k_fast_cells<FC_CONST_PITCH>, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
                        arenaPitch, *plan, cells, cellKeys, cellCount, tileElems, cellBeg, cellEnd,
                        errFlag);
   else

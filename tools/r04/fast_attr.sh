@@ -4,7 +4,7 @@
 # (fast_attr.py) and counted in one rocprofv3 SQ pass.
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/fattr; mkdir -p "$O"; cd "$R"
-V="default fstub1 fstub2 fstub3 fstub4 fstub5"
+V="default tight0 fstub1 fstub2 fstub3 fstub4 fstub5"
 for v in $V; do
   lib=$R/orb_slam2-chinese-annotation_amd/lib/liborb_amd.so
   [ "$v" != default ] && lib=$R/orb_slam2-chinese-annotation_amd/lib/variants/$v.so
