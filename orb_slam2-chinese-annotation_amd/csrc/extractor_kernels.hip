@@ -2216,6 +2216,13 @@ struct DescWaveLds {
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
+// Attribution builds (tools/r04/orient_attr; results WRONG, never shipped):
+// DESC_STUB = k drops the last k phases of a pair, the work before it kept
+// alive through a sink: 1 rBRIEF sampling, 2 + row pass (row-sum stores),
+// 3 + IC_Angle moments, 4 + fastAtan2 / pinned sincos, 5 + window loads.
+#ifndef DESC_STUB
+#define DESC_STUB 0
+#endif
 
 template <int PPW>
 __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
@@ -2327,6 +2334,10 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // loads) from the 4-aligned byte at or below column cx-21
   uint32_t ra[12], rb[12], sha = 0, shb = 0;
   auto issue = [&](const Pair& P) {
+#if DESC_STUB >= 5
+    sha = shb = (uint32_t)P.cx & 3u;
+    return;
+#endif
     const OrbLevelDesc& L = plan.lv[P.l];
     const uint8_t* lvl;
     int pitch;
@@ -2415,10 +2426,19 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       m10 += (int)rm - 16 * (int)rs;
       m01 += (ri - 15) * (int)rs;
     };
+#if DESC_STUB >= 3
+    {
+      uint32_t x = 0;
+      for (int k = 0; k < 12; ++k) x ^= ra[k] ^ rb[k];
+      m01 = (int)(x & 0xFF);
+      m10 = (int)((x >> 8) & 0xFF) + 1;
+    }
+#else
     if (P.valid && second) {
       if (2 * hl >= 6 && 2 * hl <= 36) ic_row(ra, mka, 2 * hl - 6);
       if (2 * hl + 1 >= 6 && 2 * hl + 1 <= 36) ic_row(rb, mkb, 2 * hl + 1 - 6);
     }
+#endif
     // (the rows stay in registers through the row pass: the next pair's loads
     // go out after it)
     if (!P.valid && j + 1 < ppw) {
@@ -2509,7 +2529,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     }
 #else
     // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
-    if (second) {  // the lane's row pair from registers, group by group
+    if (second && !(DESC_STUB >= 2)) {  // the lane's row pair from registers, group by group
       // (samples reach columns 0..36 only: |rotated pattern point| <= 18.4,
       // so the last group computes column 36 alone)
 #pragma unroll
@@ -2546,19 +2566,28 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     }
     m01 = half_sum(m01);
     m10 = half_sum(m10);
+#if DESC_STUB >= 4
+    const float angle = (float)(m01 & 7);
+#else
     const float angle = fast_atan2_deg((float)m01, (float)m10);
+#endif
     wave_lds_sync();
     // ---- rBRIEF sampling the blur directly: blurred pixel (ry, rx) of the
     // patch = column pass of row-sum rows 18+ry .. 24+ry at column 18+rx,
     // i.e. the four pairs (18+ry)/2 .. +3 with the parity's weights
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float a, b;
+#if DESC_STUB >= 4
+    a = angle;
+    b = angle * 0.5f;
+#else
     {
       float sn, cs;
       pinned_sincos(angle * factorPI, &sn, &cs);
       a = cs;
       b = sn;
     }
+#endif
     const uint32_t wE[4] = {__builtin_bit_cast(uint32_t, E0), __builtin_bit_cast(uint32_t, E1),
                             __builtin_bit_cast(uint32_t, E2), __builtin_bit_cast(uint32_t, E3)};
     const uint32_t wO[4] = {__builtin_bit_cast(uint32_t, O0), __builtin_bit_cast(uint32_t, O1),
@@ -2617,6 +2646,11 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     };
 #endif
     unsigned long long words[8];
+#if DESC_STUB >= 1
+#pragma unroll
+    for (int kq = 0; kq < 8; ++kq) words[kq] = __ballot(((int)(a * 8.f) ^ kq) & 1);
+    if (false)
+#endif
 #pragma unroll
     for (int kq = 0; kq < 8; ++kq) {
       const int test = hl + 32 * kq;

@@ -1,10 +1,12 @@
 #!/bin/bash
-# k_fast_cells attribution: the default library and the FC_STUB=1..5 builds
-# (tools/build_variant.sh fstubK "-DFC_STUB=K"), each timed alone
-# (fast_attr.py) and counted in one rocprofv3 SQ pass.
+# Kernel attribution: the default library and the variant builds named (each
+# tools/build_variant.sh NAME FLAGS), each timed alone (fast_attr.py: every
+# stage one after another on one stream) and counted in one rocprofv3 SQ pass.
+# Usage: tools/r04/attr.sh <tag> <kernel> <variant> ...
 set -eo pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/fattr; mkdir -p "$O"; cd "$R"
-V="default tight0 fstub1 fstub2 fstub3 fstub4 fstub5"
+TAG=$1; K=$2; shift 2
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/attr_$TAG; mkdir -p "$O"; cd "$R"
+V="default $*"
 for v in $V; do
   lib=$R/orb_slam2-chinese-annotation_amd/lib/liborb_amd.so
   [ "$v" != default ] && lib=$R/orb_slam2-chinese-annotation_amd/lib/variants/$v.so
@@ -19,4 +21,4 @@ for v in $V; do
     -d "$O/pmc_$v" -o run --output-format csv -- python3 "$R/tools/r04/fast_attr.py" > "$O/pmc_$v.log" 2>&1
 done
 cd "$R"
-python3 tools/r04/pmc_kernel.py k_fast_cells $(for v in $V; do echo "$O/pmc_$v"; done) | tee "$O/pmc.txt"
+python3 tools/r04/pmc_kernel.py "$K" $(for v in $V; do echo "$O/pmc_$v"; done) | tee "$O/pmc.txt"

@@ -5,7 +5,7 @@
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/sched; mkdir -p "$O"; cd "$R"
 ARGS="--no-cpu --no-dropin --host-frames 0 --steps 40"
-for i in 1 2; do
+for i in 1; do
   for v in side inline; do
     E=""; [ $v = inline ] && E="ORB_FAST_L0_INLINE=1"
     env $E timeout -k 10 300 python bench.py $ARGS > "$O/$v$i.json" 2> "$O/$v$i.err"
