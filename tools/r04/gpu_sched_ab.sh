@@ -5,13 +5,16 @@
 #           one launch after the resize chain)
 #   jac     C4's SearchByProjection through the Jacobi resolve too
 #           (ORB_RESOLVE_FP_MIN=1000; default: local maps of 20,000+ points)
+#   inlane  each lane runs its launch's matcher after its extraction on its own
+#           stream (no match stream)
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/sched; mkdir -p "$O"; cd "$R"
 ARGS="--no-cpu --no-dropin --host-frames 0 --steps 40"
-for v in side inline jac side2; do
+for v in side inline jac inlane side2; do
   E="ORB_NOTHING=1"
   [ $v = inline ] && E="ORB_FAST_L0_INLINE=1"
   [ $v = jac ] && E="ORB_RESOLVE_FP_MIN=1000"
+  [ $v = inlane ] && E="ORB_BENCH_LANE_MATCH=inlane"
   env $E timeout -k 10 300 python bench.py $ARGS > "$O/$v.json" 2> "$O/$v.err"
   python3 -c "
 import json; r=json.loads(open('$O/$v.json').read().strip().splitlines()[-1])
