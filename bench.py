@@ -281,7 +281,7 @@ _STREAMS = {}
 # extractor's side stream is low priority (its own pool); the extraction
 # stream is normal priority and the match and copy streams high priority, so
 # no two of the concurrently busy streams can share a queue
-# (tools/probe/c5_swap.py, profiles/r03_streams.txt)
+# (tools/archive/r03/c5_swap.py, profiles/r03_streams.txt)
 _STREAM_PRIO = {"extract": "normal", "match": "greatest", "h2d": "greatest", "d2h": "greatest"}
 _STREAM_PRIO.update({f"extract{i}": "normal" for i in range(1, 4)})
 
