@@ -4,7 +4,7 @@ across each proj_workload call (shifting where its buffers land), then freed."""
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[3]))
 import torch  # noqa: E402
 
 import bench  # noqa: E402

@@ -4,7 +4,7 @@ Stage profiler on for the extractor and the matcher inside proj_workload."""
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[3]))
 import torch  # noqa: E402
 
 import bench  # noqa: E402

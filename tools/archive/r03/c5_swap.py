@@ -5,7 +5,7 @@ state; between timed runs, move one group of buffers to a new allocation
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[3]))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

@@ -5,7 +5,7 @@ lands in the slow mode and one in the fast mode (tools/probe/c5_streams.py)."""
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[3]))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
