@@ -2213,6 +2213,9 @@ struct DescWaveLds {
 #ifndef DESC_ROW37
 #define DESC_ROW37 1     // row pass stops at column 36, the last one a sample reaches
 #endif
+#ifndef DESC_PK_ROT
+#define DESC_PK_ROT 0    // rBRIEF point rotation + rounding adder as packed f32 (A/B knob)
+#endif
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
@@ -2608,9 +2611,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     // read the same bits; its low 24 bits 0x400000 keep the signed 24-bit
     // multiply's operand positive)
     rsc -= 0x400000 * (DESC_RS_DW / 2) + 0x4B400000;
-    auto blurred = [&](float fy, float fx) -> int {
-      const int by = __builtin_bit_cast(int, fy + 12582912.0f);
-      const int bx = __builtin_bit_cast(int, fx + 12582912.0f);
+    // (by, bx): the adder's bit patterns of the rotated coordinates
+    auto blurred = [&](int by, int bx) -> int {
       const uint32_t* p = rs0 + (rsc + __mul24(by & ~1, DESC_RS_DW / 2) + bx);
       const uint4 wv = sW[by & 1];
 #else
@@ -2661,8 +2663,27 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
       const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
 #endif
+#if DESC_LDS_TABLES && DESC_MAGIC_ROUND && DESC_PK_ROT
+      // both coordinates of a point in one packed-f32 chain: {px b, px a} +
+      // {py a, -(py b)}, then + the adder (IEEE per component, no contraction:
+      // the same floats as the scalar expressions)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 ba = {b, a}, ab = {a, b}, mg = {12582912.0f, 12582912.0f};
+      f2 q0 = (f2){py0, py0} * ab, q1 = (f2){py1, py1} * ab;
+      q0.y = -q0.y;
+      q1.y = -q1.y;
+      const f2 r0 = ((f2){px0, px0} * ba + q0) + mg, r1 = ((f2){px1, px1} * ba + q1) + mg;
+      const int v0 = blurred(__builtin_bit_cast(int, r0.x), __builtin_bit_cast(int, r0.y));
+      const int v1 = blurred(__builtin_bit_cast(int, r1.x), __builtin_bit_cast(int, r1.y));
+#elif DESC_MAGIC_ROUND
+      const int v0 = blurred(__builtin_bit_cast(int, (px0 * b + py0 * a) + 12582912.0f),
+                             __builtin_bit_cast(int, (px0 * a - py0 * b) + 12582912.0f));
+      const int v1 = blurred(__builtin_bit_cast(int, (px1 * b + py1 * a) + 12582912.0f),
+                             __builtin_bit_cast(int, (px1 * a - py1 * b) + 12582912.0f));
+#else
       const int v0 = blurred(px0 * b + py0 * a, px0 * a - py0 * b);
       const int v1 = blurred(px1 * b + py1 * a, px1 * a - py1 * b);
+#endif
       words[kq] = __ballot(v0 < v1);
     }
     if (P.active && hl == 0) {
