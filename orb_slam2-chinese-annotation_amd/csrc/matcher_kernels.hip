@@ -869,7 +869,10 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   // Large maps: Jacobi rounds over the whole chip first (k_proj_jacobi), the
   // windowed fixed-point kernel after them for any problem not yet settled
   // (ORB_RESOLVE_JACOBI=0: the windowed kernel alone; ORB_JACOBI_ROUNDS = R)
-  static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 1;
+  // (off by default: at C5, B = 16, four rounds of ~20 us leave most problems
+  // unsettled, and the windowed kernel then runs after them: resolve 0.280 ms
+  // against 0.180 ms alone; profiles/r04_c5_stages.txt)
+  static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 0;
   static const int jacR =
       getenv("ORB_JACOBI_ROUNDS") ? std::max(1, std::min(48, atoi(getenv("ORB_JACOBI_ROUNDS")))) : 4;
   const bool fp = mpStride >= fpMin && fpMode > 0 && ldsFp <= 64 * 1024;
