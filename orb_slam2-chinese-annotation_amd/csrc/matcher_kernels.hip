@@ -937,7 +937,8 @@ size_t orb_k_proj_params_size(void) { return sizeof(ProjParams); }
 // bytes of Jacobi-resolve scratch for n problems (0: the windowed kernel only)
 size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems) {
   static const int fpMin = getenv("ORB_RESOLVE_FP_MIN") ? atoi(getenv("ORB_RESOLVE_FP_MIN")) : 20000;
-  if (mpStride < fpMin) return 0;
+  static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 0;
+  if (mpStride < fpMin || jacOn <= 0) return 0;
   return (size_t)jacobi_stride(kpStride, mpStride) * 4 * (size_t)nproblems;
 }
 
