@@ -172,12 +172,15 @@ def test_search_by_projection_batch_large_maps(gpu, oracle):
             assert np.array_equal(km[i, :len(k)].cpu().numpy(), km_ref), i
 
 
-@pytest.mark.parametrize("env", [{"ORB_JACOBI_ROUNDS": "1"}, {"ORB_JACOBI_ROUNDS": "48"},
+@pytest.mark.parametrize("env", [{"ORB_RESOLVE_JACOBI": "1", "ORB_JACOBI_ROUNDS": "1"},
+                                 {"ORB_RESOLVE_JACOBI": "1"},
+                                 {"ORB_RESOLVE_JACOBI": "1", "ORB_JACOBI_ROUNDS": "48"},
                                  {"ORB_RESOLVE_JACOBI": "0"}])
 def test_search_by_projection_resolve_schedules(gpu, oracle, tmp_path, env):
     """The large-map resolve under each schedule (read once per process, so in
-    a child): one Jacobi round then the windowed fallback, up to 48 rounds,
-    and the windowed kernel alone; C5's map and a deep-conflict map."""
+    a child): Jacobi rounds (1, the default 4, up to 48) with the windowed
+    fallback, and the windowed kernel alone (the default); C5's map and a
+    deep-conflict map."""
     import os
     import subprocess
     import sys
