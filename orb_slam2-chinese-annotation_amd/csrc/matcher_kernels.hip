@@ -163,6 +163,132 @@ __global__ __launch_bounds__(64) void k_grid_build(const orb_keypoint_t* __restr
   }
 }
 
+// Four waves per frame for frames with many keypoint slots (C5: 4,000
+// keypoints; the one-wave scatter takes 63 dependent rounds there): wave w
+// takes the contiguous keys [w n / 4, (w + 1) n / 4).  Per (cell, wave) counts
+// ride in u16 halves, two waves per dword (36 KB of LDS with the cell starts),
+// the cell starts come from one block scan, and wave w's cursor in cell c is
+// the cell's start plus the counts of waves 0..w-1 there, so the four waves
+// scatter at once and the lists stay in ascending keypoint order.
+#define GB4_MIN_SLOTS 1536  // frames with more keypoint slots take k_grid_build4
+__global__ __launch_bounds__(256) void k_grid_build4(const orb_keypoint_t* __restrict__ keys,
+                                                     const int32_t* __restrict__ nkeys, int kpStride,
+                                                     float minX, float minY, float invW, float invH,
+                                                     int32_t* __restrict__ cellStart,
+                                                     int32_t* __restrict__ cellIdx,
+                                                     const uint8_t* __restrict__ locked,
+                                                     const float* __restrict__ uright,
+                                                     uint4* __restrict__ staged) {
+  __shared__ uint32_t c2[GRID_CELLS][2];  // waves (0, 1) and (2, 3): counts, then cursors
+  __shared__ int start[GRID_CELLS];
+  __shared__ int tmp[20];
+  const int p = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = min(max(nkeys[p], 0), 65535);
+  const int kb = (int)((long long)n * w / 4), ke = (int)((long long)n * (w + 1) / 4);
+  const int half = w >> 1, sh = 16 * (w & 1);
+  const orb_keypoint_t* K = keys + (size_t)p * kpStride;
+  for (int i = t; i < GRID_CELLS * 2; i += 256) (&c2[0][0])[i] = 0u;
+  __syncthreads();
+  for (int base = kb; base < ke; base += 256) {
+    int c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = base + 64 * j + lane;
+      c[j] = k < ke ? grid_cell(K[k], minX, minY, invW, invH) : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (c[j] >= 0) atomicAdd(&c2[c[j]][half], 1u << sh);
+  }
+  __syncthreads();
+  {
+    constexpr int per = GRID_CELLS / 256;
+    static_assert(per * 256 == GRID_CELLS, "cells split evenly over the threads");
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+      const uint32_t a = c2[t * per + i][0], b = c2[t * per + i][1];
+      s += (int)((a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16));
+    }
+    int tot;
+    int ex = block_excl_scan(s, tmp, &tot);
+    int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+      const int c = t * per + i;
+      const uint32_t a = c2[c][0], b = c2[c][1];
+      const uint32_t n0 = a & 0xFFFFu, n1 = a >> 16, n2 = b & 0xFFFFu, n3 = b >> 16;
+      start[c] = ex;
+      cs[c] = ex;
+      // wave cursors inside the cell: 0, n0, n0 + n1, n0 + n1 + n2
+      c2[c][0] = (n0 << 16);
+      c2[c][1] = (n0 + n1) | ((n0 + n1 + n2) << 16);
+      ex += (int)(n0 + n1 + n2 + n3);
+    }
+    if (t == 255) cs[GRID_CELLS] = tot;
+  }
+  __syncthreads();
+  int32_t* ci = cellIdx + (size_t)p * kpStride;
+  const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
+  const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
+  uint4* sg = staged ? staged + (size_t)p * kpStride : nullptr;
+  const unsigned long long ltMask = (1ull << lane) - 1ull;
+  float nx = 0.f, ny = 0.f, nu = -1.f;
+  int noct = 0, nlk = 0;
+  auto load = [&](int k) {
+    if (k < ke) {
+      nx = K[k].x;
+      ny = K[k].y;
+      if (sg) {
+        noct = K[k].octave;
+        nlk = LK ? LK[k] : 0;
+        nu = UR ? UR[k] : -1.0f;
+      }
+    }
+  };
+  load(kb + lane);
+  for (int base = kb; base < ke; base += 64) {
+    const int k = base + lane;
+    const float x = nx, y = ny, u = nu;
+    const int oct = noct, lk = nlk;
+    load(k + 64);
+    int c = -1;
+    if (k < ke) {
+      orb_keypoint_t kp;
+      kp.x = x;
+      kp.y = y;
+      c = grid_cell(kp, minX, minY, invW, invH);
+    }
+    const int id = c < 0 ? 4095 : c;
+    unsigned long long peers = __ballot(1);
+#pragma unroll
+    for (int bit = 0; bit < 12; ++bit) {
+      const unsigned long long m = __ballot((id >> bit) & 1);
+      peers &= ((id >> bit) & 1) ? m : ~m;
+    }
+    int pos = 0;
+    if (c >= 0) pos = start[c] + (int)((c2[c][half] >> sh) & 0xFFFFu) + __popcll(peers & ltMask);
+    __builtin_amdgcn_wave_barrier();
+    if (c >= 0) {
+      ci[pos] = k;
+      if (sg) {
+        uint4 e;
+        e.x = __float_as_uint(x);
+        e.y = __float_as_uint(y);
+        e.z = (uint32_t)k | ((uint32_t)oct << 24) | (lk ? 0x80000000u : 0u);
+        e.w = __float_as_uint(u);
+        sg[pos] = e;
+      }
+      // the group's highest lane advances this wave's cursor (the other half
+      // of the dword is another wave's: an atomic add keeps both)
+      if ((peers >> lane) == 1ull) atomicAdd(&c2[c][half], (uint32_t)__popcll(peers) << sh);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // ------------------------------------------ SearchByProjection(F, localMap)
 // Per map point: candidate scan + first-K in (dist, scan order); counts every
 // candidate that could ever be best/second (dist < 256, not pre-locked, passes
@@ -786,11 +912,22 @@ hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out
   return hipGetLastError();
 }
 
+static bool grid4(int kpStride) {
+  static const int env = getenv("ORB_GRID_WAVES") ? atoi(getenv("ORB_GRID_WAVES")) : 0;
+  if (env == 1) return false;
+  if (env == 4) return kpStride < 65536;
+  return kpStride > GB4_MIN_SLOTS && kpStride < 65536;
+}
+
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
                             int32_t* cellIdx, int nproblems, hipStream_t s) {
-  hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride, minX,
-                     minY, invW, invH, cellStart, cellIdx, nullptr, nullptr, nullptr);
+  if (grid4(kpStride))
+    hipLaunchKernelGGL(k_grid_build4, dim3(nproblems), dim3(256), 0, s, keys, nkeys, kpStride, minX,
+                       minY, invW, invH, cellStart, cellIdx, nullptr, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride, minX,
+                       minY, invW, invH, cellStart, cellIdx, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -802,8 +939,12 @@ hipError_t orb_k_grid_build_staged(const orb_keypoint_t* keys, const int32_t* nk
                                    int32_t* cellStart, int32_t* cellIdx, void* staged,
                                    int nproblems, hipStream_t s) {
   if (kpStride > GB_LDS_KEYS) return hipErrorNotSupported;
-  hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride, minX,
-                     minY, invW, invH, cellStart, cellIdx, locked, uright, (uint4*)staged);
+  if (grid4(kpStride))
+    hipLaunchKernelGGL(k_grid_build4, dim3(nproblems), dim3(256), 0, s, keys, nkeys, kpStride, minX,
+                       minY, invW, invH, cellStart, cellIdx, locked, uright, (uint4*)staged);
+  else
+    hipLaunchKernelGGL(k_grid_build, dim3(nproblems), dim3(64), 0, s, keys, nkeys, kpStride, minX,
+                       minY, invW, invH, cellStart, cellIdx, locked, uright, (uint4*)staged);
   return hipGetLastError();
 }
 
