@@ -718,7 +718,7 @@ static void features_in_area(const Grid& g, const KP* keys, float x, float y, fl
 static int search_by_projection_local(const orb_frame_t* F, const uint8_t* kp_locked, int nmp,
                                       const orb_mp_track_t* mps, const uint8_t* mp_desc,
                                       float th, float nnratio, int32_t* kp_match) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, F->keys, F->n, F->min_x, F->max_x, F->min_y, F->max_y);
   // lock[i]: F.mvpMapPoints[i] && ->Observations() > 0 ; updated by claims of has_obs points
   std::vector<uint8_t> lock(F->n);
@@ -922,7 +922,7 @@ static int search_by_projection_frame(const orb_frame_t* C, const uint8_t* kp_lo
                                       const orb_last_mp_t* last, const uint8_t* last_desc,
                                       const orb_camera_t* cam, float tlc_z, float th, int mono,
                                       int checkOri, int32_t* kp_match) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, C->keys, C->n, C->min_x, C->max_x, C->min_y, C->max_y);
   // state[i]: 0 untouched, 1 assigned this call (holder slot[i]), 2 cleared this call
   std::vector<int> slot(C->n, -1), state(C->n, 0);
@@ -1136,7 +1136,7 @@ static void stereo_matches(const orb_stereo_input_t* in, float* uRight, float* d
 // prev is vbPrevMatched as (x, y) pairs, updated in place; m12 = vnMatches12.
 static int search_for_initialization(const orb_frame_t* F1, const orb_frame_t* F2, float* prev,
                                      int windowSize, float nnratio, int checkOri, int32_t* m12) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, F2->keys, F2->n, F2->min_x, F2->max_x, F2->min_y, F2->max_y);
   const int N1 = F1->n, N2 = F2->n;
   int nmatches = 0;
@@ -1290,7 +1290,7 @@ static int search_by_projection_reloc(const orb_frame_t* F, const uint8_t* kp_lo
                                       float logScale, int n, const orb_map_point_t* mps,
                                       const uint8_t* mpDesc, const float* kfAngle, float th,
                                       int orbDist, int checkOri, int32_t* kp_match) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, F->keys, F->n, F->min_x, F->max_x, F->min_y, F->max_y);
   std::vector<uint8_t> locked(F->n, 0);
   for (int j = 0; j < F->n; ++j) {
@@ -1349,7 +1349,7 @@ static int search_by_projection_sim3(const orb_frame_t* K, const float* Scw,
                                      const orb_camera_t* cam, float logScale, int n,
                                      const orb_map_point_t* mps, const uint8_t* mpDesc, float th,
                                      int32_t* kp_matched) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, K->keys, K->n, K->min_x, K->max_x, K->min_y, K->max_y);
   const Rt T = sim3_pose(Scw);
   std::vector<size_t> idxs;
@@ -1398,7 +1398,7 @@ static int fuse_candidates(const orb_frame_t* K, const float* invSigma2, const o
                            const orb_camera_t* cam, float logScale, int n,
                            const orb_map_point_t* mps, const uint8_t* mpDesc, float th,
                            int32_t* best) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, K->keys, K->n, K->min_x, K->max_x, K->min_y, K->max_y);
   std::vector<size_t> idxs;
   int nf = 0;
@@ -1454,7 +1454,7 @@ static int fuse_candidates(const orb_frame_t* K, const float* invSigma2, const o
 static int fuse_sim3_candidates(const orb_frame_t* K, const float* Scw, const orb_camera_t* cam,
                                 float logScale, int n, const orb_map_point_t* mps,
                                 const uint8_t* mpDesc, float th, int32_t* best) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, K->keys, K->n, K->min_x, K->max_x, K->min_y, K->max_y);
   const Rt T = sim3_pose(Scw);
   std::vector<size_t> idxs;
@@ -1503,7 +1503,7 @@ static void sim3_direction(const orb_frame_t* B, float logScaleB, const orb_came
                            int nA, const orb_map_point_t* mpsA, const uint8_t* validA,
                            const uint8_t* alreadyA, const uint8_t* descA, float th,
                            int32_t* out) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, B->keys, B->n, B->min_x, B->max_x, B->min_y, B->max_y);
   std::vector<size_t> idxs;
   for (int i = 0; i < nA; ++i) {
@@ -1966,7 +1966,7 @@ int oracle_stereo_match(const orb_stereo_input_t* in, float* u_right, float* dep
 // Grid CSR of a frame: cell_start[64*48+1] (cell index = ix*48 + iy), idx[].
 int oracle_grid(const orb_keypoint_t* keys, int n, float minX, float maxX, float minY,
                 float maxY, int32_t* cell_start, int32_t* idx) {
-  static Grid g;
+  thread_local Grid g;  // per thread: the oracle runs on many host threads (bench.py cpu_all_cores)
   assign_grid(g, keys, n, minX, maxX, minY, maxY);
   int off = 0;
   for (int ix = 0; ix < ORB_GRID_COLS; ++ix)
