@@ -930,7 +930,7 @@ def main():
     # shadow, so matcher kernel times include time-sharing with the next
     # launch's extraction): the roofline kernel is the longest extraction kernel.
     # the profiled handle is lane 0's: it ran every L-th launch of the region
-    n_prof = sum(1 for gg in range(g_first, g) if gg % L == 0)
+    n_prof = max(1, sum(1 for gg in range(g_first, g) if gg % L == 0))
     kern, ext_kern = {}, []
     for st in range(6):
         name, ms, n = ext.profile_read(st)
