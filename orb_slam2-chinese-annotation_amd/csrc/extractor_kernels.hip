@@ -778,6 +778,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef FC_PAD
 #define FC_PAD 0        // extra LDS row pitch (bytes, multiple of 8)
 #endif
+#ifndef FC_LOAD3
+#define FC_LOAD3 0      // three 16-byte row loads instead of four where the ROI fits (A/B knob)
+#endif
 #ifndef FC_ROWMAJOR
 #define FC_ROWMAJOR 1   // candidates queued in row-major order, keys written by NMS in order
 #endif
@@ -952,8 +955,17 @@ __global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
     const uint32_t o = (uint32_t)((q.y0 + r) * pitch + q.x0 - FAST_LPAD) + im.sh;
     rsh = o & 3u;
     const uint32_t a0 = o & ~3u;
+#if FC_LOAD3
+    // the row's bytes 0 .. C + 4 end inside the first 48 loaded bytes unless
+    // the cell is wider than 40 - rsh: the 4th 16-byte load only then (the
+    // stored bytes past C + 4 are never read for an interior pixel)
+    const int nLoads = (int)rsh + (q.x1 - q.x0) + FAST_LPAD > 48 ? 4 : 3;
+#else
+    const int nLoads = 4;
+#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      if (k == 3 && nLoads < 4) break;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(im.r, (int)(a0 + 16 * k), 0, 0);
       raw[4 * k] = (uint32_t)v[0];
       raw[4 * k + 1] = (uint32_t)v[1];
@@ -2216,6 +2228,9 @@ struct DescWaveLds {
 #ifndef DESC_PK_ROT
 #define DESC_PK_ROT 0    // rBRIEF point rotation + rounding adder as packed f32 (A/B knob)
 #endif
+#ifndef DESC_DBUF
+#define DESC_DBUF 0      // double-buffered window rows (A/B knob)
+#endif
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
@@ -2411,6 +2426,27 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       realign(ra, sha);
       realign(rb, shb);
     }
+#if DESC_DBUF
+    // double-buffered window rows: the pair's realigned rows move to working
+    // registers and the next pair's loads go out at once, so they overlap
+    // IC_Angle, the row pass and the sampling (24 more VGPRs: still 4 waves
+    // per SIMD, the occupancy the kernel already has)
+    uint32_t wa[12], wb[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      wa[k] = ra[k];
+      wb[k] = rb[k];
+    }
+    if (j + 1 < ppw) {
+      cur = setup(j + 1);
+      if (cur.valid) issue(cur);
+    }
+#define RA wa
+#define RB wb
+#else
+#define RA ra
+#define RB rb
+#endif
     // ---- IC_Angle from the rows in registers: row v = ri - 15 is staged row
     // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
     // by one byte; reading dwords 1..9 as loaded under byte-shifted masks
@@ -2432,19 +2468,19 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
 #if DESC_STUB >= 3
     {
       uint32_t x = 0;
-      for (int k = 0; k < 12; ++k) x ^= ra[k] ^ rb[k];
+      for (int k = 0; k < 12; ++k) x ^= RA[k] ^ RB[k];
       m01 = (int)(x & 0xFF);
       m10 = (int)((x >> 8) & 0xFF) + 1;
     }
 #else
     if (P.valid && second) {
-      if (2 * hl >= 6 && 2 * hl <= 36) ic_row(ra, mka, 2 * hl - 6);
-      if (2 * hl + 1 >= 6 && 2 * hl + 1 <= 36) ic_row(rb, mkb, 2 * hl + 1 - 6);
+      if (2 * hl >= 6 && 2 * hl <= 36) ic_row(RA, mka, 2 * hl - 6);
+      if (2 * hl + 1 >= 6 && 2 * hl + 1 <= 36) ic_row(RB, mkb, 2 * hl + 1 - 6);
     }
 #endif
     // (the rows stay in registers through the row pass: the next pair's loads
     // go out after it)
-    if (!P.valid && j + 1 < ppw) {
+    if (!DESC_DBUF && !P.valid && j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
@@ -2464,8 +2500,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       // take their REFLECT_101 column, and come back patched
       uint32_t* scr = &rsp[0][0] + 24 * hl;  // rows 2 hl, 2 hl + 1: 12 dwords each
       if (second) {
-        store_row(scr, ra);
-        store_row(scr + 12, rb);
+        store_row(scr, RA);
+        store_row(scr + 12, RB);
         for (int s2 = 0; s2 < 2; ++s2) {
           uint8_t* rp = reinterpret_cast<uint8_t*>(scr + 12 * s2);
           for (int b = 0; b < -colA; ++b) rp[b] = rp[-(colA + b) - colA];
@@ -2473,8 +2509,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
         }
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
-          ra[k] = scr[k];
-          rb[k] = scr[12 + k];
+          RA[k] = scr[k];
+          RB[k] = scr[12 + k];
         }
       }
       wave_lds_sync();
@@ -2493,10 +2529,10 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       uint4* st0 = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(&rsp[0][0]) + 128 * hl);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        st0[q] = make_uint4(ra[4 * q] ^ 0x80808080u, ra[4 * q + 1] ^ 0x80808080u,
-                            ra[4 * q + 2] ^ 0x80808080u, ra[4 * q + 3] ^ 0x80808080u);
-        st0[4 + q] = make_uint4(rb[4 * q] ^ 0x80808080u, rb[4 * q + 1] ^ 0x80808080u,
-                                rb[4 * q + 2] ^ 0x80808080u, rb[4 * q + 3] ^ 0x80808080u);
+        st0[q] = make_uint4(RA[4 * q] ^ 0x80808080u, RA[4 * q + 1] ^ 0x80808080u,
+                            RA[4 * q + 2] ^ 0x80808080u, RA[4 * q + 3] ^ 0x80808080u);
+        st0[4 + q] = make_uint4(RB[4 * q] ^ 0x80808080u, RB[4 * q + 1] ^ 0x80808080u,
+                                RB[4 * q + 2] ^ 0x80808080u, RB[4 * q + 3] ^ 0x80808080u);
       }
     }
     wave_lds_sync();
@@ -2538,15 +2574,15 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
 #pragma unroll
       for (int g = 0; g < 10; ++g) {
         if (DESC_ROW37 && g == 9) {
-          const uint32_t c0 = __builtin_amdgcn_udot4(ra[9], T0a, __builtin_amdgcn_udot4(ra[10], T0b, 0u, false), false);
-          const uint32_t c1 = __builtin_amdgcn_udot4(rb[9], T0a, __builtin_amdgcn_udot4(rb[10], T0b, 0u, false), false);
+          const uint32_t c0 = __builtin_amdgcn_udot4(RA[9], T0a, __builtin_amdgcn_udot4(RA[10], T0b, 0u, false), false);
+          const uint32_t c1 = __builtin_amdgcn_udot4(RB[9], T0a, __builtin_amdgcn_udot4(RB[10], T0b, 0u, false), false);
           rsp[hl][36] = __builtin_amdgcn_perm(c1, c0, 0x05040100u);
           break;
         }
         uint32_t o[2][4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const uint32_t* rw = h ? rb : ra;
+          const uint32_t* rw = h ? RB : RA;
           const uint32_t w0 = rw[g], w1 = rw[g + 1], w2 = rw[g + 2];
           o[h][0] = __builtin_amdgcn_udot4(w0, T0a, __builtin_amdgcn_udot4(w1, T0b, 0u, false), false);
           o[h][1] = __builtin_amdgcn_udot4(w0, T1a, __builtin_amdgcn_udot4(w1, T1b, 0u, false), false);
@@ -2563,7 +2599,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       }
     }
 #endif
-    if (j + 1 < ppw) {
+    if (!DESC_DBUF && j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
@@ -2704,6 +2740,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       kp.class_id = -1;
       kps[o] = kp;
     }
+#undef RA
+#undef RB
     // the next pair's staging overwrites raw: every lane's patch reads are done
     wave_lds_sync();
   }

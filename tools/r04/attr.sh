@@ -13,6 +13,7 @@ for v in $V; do
   ORB_AMD_LIB=$lib timeout -k 10 120 python -u tools/r04/fast_attr.py >> "$O/times.txt" 2>> "$O/err.txt"
 done
 cat "$O/times.txt"
+[ -n "$ATTR_NOPMC" ] && exit 0
 cd /tmp && export TMPDIR=/tmp
 for v in $V; do
   lib=$R/orb_slam2-chinese-annotation_amd/lib/liborb_amd.so
