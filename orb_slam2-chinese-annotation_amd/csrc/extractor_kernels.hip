@@ -770,7 +770,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define FC_CPW 4        // cells per wave (software-pipelined ROI loads)
 #endif
 #ifndef FC_QCAP
-#define FC_QCAP 768     // candidate queue per wave (one pretest round adds <= 512)
+// candidate queue per wave (one pretest round adds <= 512; a flush once it
+// holds more than 128): 640 against 768 trims the wave's LDS slice to 5.7 KB,
+// FAST alone 1.334 -> 1.283 ms per 1024 frames (profiles/r04_variants.txt)
+#define FC_QCAP 640
 #endif
 #ifndef FC_CCAP
 #define FC_CCAP 256     // corner list per wave; beyond it the NMS runs densely
@@ -2226,7 +2229,10 @@ struct DescWaveLds {
 #define DESC_ROW37 1     // row pass stops at column 36, the last one a sample reaches
 #endif
 #ifndef DESC_PK_ROT
-#define DESC_PK_ROT 0    // rBRIEF point rotation + rounding adder as packed f32 (A/B knob)
+// rBRIEF point rotation + rounding adder as packed f32 (v_pk_mul / v_pk_add:
+// the same IEEE operations per component): orient alone 0.829 -> 0.779 ms per
+// 1024 frames, VALU 4.23e8 -> 3.97e8 (profiles/r04_variants.txt, r04_orient_attr.txt)
+#define DESC_PK_ROT 1
 #endif
 #ifndef DESC_DBUF
 #define DESC_DBUF 0      // double-buffered window rows (A/B knob)
