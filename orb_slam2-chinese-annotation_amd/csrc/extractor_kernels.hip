@@ -2230,9 +2230,10 @@ struct DescWaveLds {
 #endif
 #ifndef DESC_PK_ROT
 // rBRIEF point rotation + rounding adder as packed f32 (v_pk_mul / v_pk_add:
-// the same IEEE operations per component): orient alone 0.829 -> 0.779 ms per
-// 1024 frames, VALU 4.23e8 -> 3.97e8 (profiles/r04_variants.txt, r04_orient_attr.txt)
-#define DESC_PK_ROT 1
+// the same IEEE operations per component).  A/B knob: its first build took
+// the x coordinate from the y one (a clang lowering of bit_cast on a vector
+// component); the 0.829 -> 0.779 ms it measured was that bug
+#define DESC_PK_ROT 0
 #endif
 #ifndef DESC_DBUF
 #define DESC_DBUF 0      // double-buffered window rows (A/B knob)
@@ -2715,8 +2716,11 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       q0.y = -q0.y;
       q1.y = -q1.y;
       const f2 r0 = ((f2){px0, px0} * ba + q0) + mg, r1 = ((f2){px1, px1} * ba + q1) + mg;
-      const int v0 = blurred(__builtin_bit_cast(int, r0.x), __builtin_bit_cast(int, r0.y));
-      const int v1 = blurred(__builtin_bit_cast(int, r1.x), __builtin_bit_cast(int, r1.y));
+      // (components into scalars first: ROCm 7.2 clang lowers
+      // __builtin_bit_cast(int, v.y) of an ext_vector component to element 0)
+      const float y0 = r0.x, x0 = r0.y, y1 = r1.x, x1 = r1.y;
+      const int v0 = blurred(__builtin_bit_cast(int, y0), __builtin_bit_cast(int, x0));
+      const int v1 = blurred(__builtin_bit_cast(int, y1), __builtin_bit_cast(int, x1));
 #elif DESC_MAGIC_ROUND
       const int v0 = blurred(__builtin_bit_cast(int, (px0 * b + py0 * a) + 12582912.0f),
                              __builtin_bit_cast(int, (px0 * a - py0 * b) + 12582912.0f));
