@@ -1498,6 +1498,10 @@ struct orb_matcher {
   DevBuf dRKeys, dRDesc, dNR, dPyr, dPairLv, dDepth, dSad, dBowA, dBowB, dBowC, dBowD, dBowE,
       dBowF, dBowG, dBowH, dBowI, dBowJ, dBowK;
   HostBuf hPyr;  // pinned staging of the host stereo pyramids (one DMA)
+  // orb_match_projection_local: every input in one pinned block / one DMA, and
+  // the matches + count back in one
+  HostBuf hIn, hOutM;
+  DevBuf dIn;
   // frustum scratch
   DevBuf dMapPts, dPose, dTracks, dNInView;
   // SearchForInitialization / ComputeDistinctiveDescriptors scratch
@@ -1567,6 +1571,9 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dInitStage, &m->dInitCounts};
   for (DevBuf* b : bufs) b->release();
   m->hPyr.release();
+  m->hIn.release();
+  m->hOutM.release();
+  m->dIn.release();
   for (DevBuf& b : m->sx) b.release();
   m->prof.destroy();
   hipStreamDestroy(m->stream);
@@ -1703,62 +1710,80 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   if ((st = m->dMps.ensure((size_t)std::max(M, 1) * sizeof(orb_mp_track_t)))) return st;
   if ((st = m->dMpDesc.ensure((size_t)std::max(M, 1) * 32))) return st;
   if ((st = m->dNMps.ensure(16))) return st;
-  if ((st = m->dKpMatch.ensure((size_t)N * 4))) return st;
+  if ((st = m->dKpMatch.ensure((size_t)N * 4 + 16))) return st;  // + the count (one D2H)
   if ((st = m->dNMatch.ensure(16))) return st;
   if ((st = m->dCellStart.ensure((size_t)(ORB_GRID_COLS * ORB_GRID_ROWS + 1) * 4))) return st;
   if ((st = m->dCellIdx.ensure((size_t)N * 4))) return st;
   if ((st = m->dTopk.ensure((size_t)std::max(M, 1) * 16))) return st;
   if ((st = m->dNcand.ensure((size_t)std::max(M, 1) * 4))) return st;
   hipStream_t s = m->stream;
-  HIP_TRY(hipMemcpyAsync(m->dKeys.p, F->keys, (size_t)N * sizeof(orb_keypoint_t),
-                         hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(m->dDesc.p, F->descriptors, (size_t)N * 32, hipMemcpyHostToDevice, s));
-  if (F->u_right)
-    HIP_TRY(hipMemcpyAsync(m->dUr.p, F->u_right, (size_t)N * 4, hipMemcpyHostToDevice, s));
-  if (kp_locked)
-    HIP_TRY(hipMemcpyAsync(m->dLocked.p, kp_locked, (size_t)N, hipMemcpyHostToDevice, s));
+  // every input in one pinned block, one DMA in (six pageable copies each
+  // staged by the runtime cost more than the kernels): [nk, nm | keys |
+  // descriptors | uR | locked | tracks | map-point descriptors], 16-B aligned
+  auto al16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  const size_t oKeys = 16, oDesc = al16(oKeys + (size_t)N * sizeof(orb_keypoint_t));
+  const size_t oUr = al16(oDesc + (size_t)N * 32), oLk = al16(oUr + (size_t)N * 4);
+  const size_t oMps = al16(oLk + (size_t)N), oMpd = al16(oMps + (size_t)M * sizeof(orb_mp_track_t));
+  const size_t inBytes = al16(oMpd + (size_t)M * 32);
+  if ((st = m->hIn.ensure(inBytes))) return st;
+  if ((st = m->dIn.ensure(inBytes))) return st;
+  if ((st = m->hOutM.ensure((size_t)N * 4 + 16))) return st;
+  uint8_t* hin = m->hIn.as<uint8_t>();
   const int32_t nk = N, nm = M;
-  HIP_TRY(hipMemcpyAsync(m->dNKeys.p, &nk, 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(m->dNMps.p, &nm, 4, hipMemcpyHostToDevice, s));
+  memcpy(hin, &nk, 4);
+  memcpy(hin + 4, &nm, 4);
+  memcpy(hin + oKeys, F->keys, (size_t)N * sizeof(orb_keypoint_t));
+  memcpy(hin + oDesc, F->descriptors, (size_t)N * 32);
+  if (F->u_right) memcpy(hin + oUr, F->u_right, (size_t)N * 4);
+  if (kp_locked) memcpy(hin + oLk, kp_locked, (size_t)N);
   if (M > 0) {
-    HIP_TRY(hipMemcpyAsync(m->dMps.p, mps, (size_t)M * sizeof(orb_mp_track_t),
-                           hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(m->dMpDesc.p, mp_desc, (size_t)M * 32, hipMemcpyHostToDevice, s));
+    memcpy(hin + oMps, mps, (size_t)M * sizeof(orb_mp_track_t));
+    memcpy(hin + oMpd, mp_desc, (size_t)M * 32);
   }
+  HIP_TRY(hipMemcpyAsync(m->dIn.p, hin, inBytes, hipMemcpyHostToDevice, s));
+  uint8_t* din = m->dIn.as<uint8_t>();
+  const orb_keypoint_t* dKeys = reinterpret_cast<const orb_keypoint_t*>(din + oKeys);
+  const uint8_t* dDesc = din + oDesc;
+  const int32_t* dNK = reinterpret_cast<const int32_t*>(din);
+  const int32_t* dNM = reinterpret_cast<const int32_t*>(din + 4);
+  const orb_mp_track_t* dMps = reinterpret_cast<const orb_mp_track_t*>(din + oMps);
+  const uint8_t* dMpd = din + oMpd;
   const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
                                        F->scale_factors, th, nnratio);
-  const float* ur = F->u_right ? m->dUr.as<float>() : nullptr;
-  const uint8_t* lk = kp_locked ? m->dLocked.as<uint8_t>() : nullptr;
+  const float* ur = F->u_right ? reinterpret_cast<const float*>(din + oUr) : nullptr;
+  const uint8_t* lk = kp_locked ? din + oLk : nullptr;
   const bool stage = N <= orb_k_grid_stage_max();
   if (stage && (st = m->dProjStage.ensure((size_t)N * 16))) return st;
   const size_t jb = orb_k_proj_jacobi_bytes(N, std::max(M, 1), 1);
   if (jb && (st = m->dJac.ensure(jb))) return st;
   if (stage)
-    HIP_TRY(orb_k_grid_build_staged(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), lk, ur,
+    HIP_TRY(orb_k_grid_build_staged(dKeys, dNK, lk, ur,
                                     N, P.minX, P.minY, P.invW, P.invH,
                                     m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
                                     m->dProjStage.p, 1, s));
   else
-    HIP_TRY(orb_k_grid_build(m->dKeys.as<orb_keypoint_t>(), m->dNKeys.as<int32_t>(), N, P.minX,
+    HIP_TRY(orb_k_grid_build(dKeys, dNK, N, P.minX,
                              P.minY, P.invW, P.invH, m->dCellStart.as<int32_t>(),
                              m->dCellIdx.as<int32_t>(), 1, s));
-  HIP_TRY(orb_k_proj_candidates(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(), ur, lk, N,
-                                m->dNKeys.as<int32_t>(),
-                                m->dMps.as<orb_mp_track_t>(), m->dMpDesc.as<uint8_t>(),
-                                m->dNMps.as<int32_t>(), std::max(M, 1), M,
+  HIP_TRY(orb_k_proj_candidates(dKeys, dDesc, ur, lk, N,
+                                dNK,
+                                dMps, dMpd,
+                                dNM, std::max(M, 1), M,
                                 m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
                                 stage ? m->dProjStage.p : nullptr, &P,
                                 m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(), 1, s));
-  HIP_TRY(orb_k_proj_resolve(m->dKeys.as<orb_keypoint_t>(), m->dDesc.as<uint8_t>(), ur, lk,
-                             m->dNKeys.as<int32_t>(), N, m->dMps.as<orb_mp_track_t>(),
-                             m->dMpDesc.as<uint8_t>(), m->dNMps.as<int32_t>(), std::max(M, 1),
+  HIP_TRY(orb_k_proj_resolve(dKeys, dDesc, ur, lk,
+                             dNK, N, dMps,
+                             dMpd, dNM, std::max(M, 1),
                              m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
                              m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
-                             m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), 1,
+                             m->dKpMatch.as<int32_t>(), m->dKpMatch.as<int32_t>() + N, 1,
                              m->dJac.as<int32_t>(), s));
-  HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
+  // one DMA out (count, then the matches) into pinned memory
+  HIP_TRY(hipMemcpyAsync(m->hOutM.p, m->dKpMatch.p, (size_t)N * 4 + 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  memcpy(kp_match, m->hOutM.p, (size_t)N * 4);
+  memcpy(nmatches, m->hOutM.as<uint8_t>() + (size_t)N * 4, 4);
   return ORB_OK;
 }
 

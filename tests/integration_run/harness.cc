@@ -637,6 +637,34 @@ static int run_time() {
       matches += n;
     }
   }
+  // the flatten alone (the calls integration/ORBmatcher.cc makes per point
+  // before the kernels: track fields, isBad, Observations, GetDescriptor)
+  std::vector<double> tFl;
+  {
+    std::vector<orb_mp_track_t> trk2(NMP);
+    std::vector<uint8_t> dsc(NMP * 32);
+    for (int it = 0; it < std::min(ITERS, 100); ++it) {
+      const std::vector<MapPoint*>& vp = maps[it % NFR];
+      const double t0 = now_ms();
+      for (int i = 0; i < NMP; ++i) {
+        MapPoint* q = vp[i];
+        orb_mp_track_t& t = trk2[i];
+        t.proj_x = q->mTrackProjX;
+        t.proj_y = q->mTrackProjY;
+        t.proj_xr = q->mTrackProjXR;
+        t.view_cos = q->mTrackViewCos;
+        t.level = q->mnTrackScaleLevel;
+        t.in_view = q->mbTrackInView ? 1 : 0;
+        t.bad = q->isBad() ? 1 : 0;
+        t.has_obs = q->Observations() > 0 ? 1 : 0;
+        if (t.in_view && !t.bad) {
+          const cv::Mat dd = q->GetDescriptor();
+          memcpy(&dsc[(size_t)i * 32], dd.ptr<uint8_t>(), 32);
+        }
+      }
+      tFl.push_back(now_ms() - t0);
+    }
+  }
   ORBextractor L(2 * NF, 1.2f, 8, 20, 7), R(2 * NF, 1.2f, 8, 20, 7);
   std::vector<double> tSt;
   for (int it = -3; it < ITERS; ++it) {
@@ -658,8 +686,9 @@ static int run_time() {
   snprintf(buf, sizeof buf,
            "{\"mono_extract_ms\": %.5f, \"mono_search_by_projection_ms\": %.5f, "
            "\"mono_frame_ms\": %.5f, \"stereo_pair_ms\": %.5f, \"frames\": %d, "
-           "\"mean_matches\": %.2f}\n",
-           median(tExt), median(tMatch), median(tTot), median(tSt), ITERS, (double)matches / ITERS);
+           "\"mean_matches\": %.2f, \"map_flatten_ms\": %.5f}\n",
+           median(tExt), median(tMatch), median(tTot), median(tSt), ITERS, (double)matches / ITERS,
+           median(tFl));
   wr("time.json", buf, strlen(buf));
   for (auto& v : maps)
     for (MapPoint* p : v) delete p;
