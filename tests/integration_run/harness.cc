@@ -218,6 +218,7 @@ void MapPoint::Replace(MapPoint* pMP) {
   extraObs_ = 0;
 }
 cv::Mat MapPoint::GetDescriptor() { return desc_.clone(); }
+void MapPoint::CopyDescriptor(unsigned char* dst) { memcpy(dst, desc_.data, 32); }  // INTEGRATION CHANGE
 float MapPoint::GetMinDistance() { return mfMinDistance; }
 float MapPoint::GetMaxDistance() { return mfMaxDistance; }
 }  // namespace ORB_SLAM2
@@ -638,7 +639,7 @@ static int run_time() {
     }
   }
   // the flatten alone (the calls integration/ORBmatcher.cc makes per point
-  // before the kernels: track fields, isBad, Observations, GetDescriptor)
+  // before the kernels: track fields, isBad, Observations, CopyDescriptor)
   std::vector<double> tFl;
   {
     std::vector<orb_mp_track_t> trk2(NMP);
@@ -657,10 +658,7 @@ static int run_time() {
         t.in_view = q->mbTrackInView ? 1 : 0;
         t.bad = q->isBad() ? 1 : 0;
         t.has_obs = q->Observations() > 0 ? 1 : 0;
-        if (t.in_view && !t.bad) {
-          const cv::Mat dd = q->GetDescriptor();
-          memcpy(&dsc[(size_t)i * 32], dd.ptr<uint8_t>(), 32);
-        }
+        if (t.in_view && !t.bad) q->CopyDescriptor(&dsc[(size_t)i * 32]);
       }
       tFl.push_back(now_ms() - t0);
     }

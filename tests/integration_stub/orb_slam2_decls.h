@@ -221,6 +221,7 @@ class MapPoint {
   float mTrackViewCos;
   float GetMinDistance();  // INTEGRATION CHANGE (include/MapPoint.h): mfMinDistance under mMutexPos
   float GetMaxDistance();  // INTEGRATION CHANGE (include/MapPoint.h): mfMaxDistance under mMutexPos
+  void CopyDescriptor(unsigned char* dst);  // INTEGRATION CHANGE (include/MapPoint.h): mDescriptor's 32 bytes under mMutexFeatures
  protected:
   float mfMinDistance;
   float mfMaxDistance;
