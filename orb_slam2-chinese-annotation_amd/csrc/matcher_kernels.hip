@@ -312,7 +312,19 @@ __global__ __launch_bounds__(256) void k_grid_build4(const orb_keypoint_t* __res
 #ifndef PROJ_WG
 #define PROJ_WG 512  // map points per workgroup (grid staged once per workgroup; swept 256-1024)
 #endif
-template <int WG>
+// DIRECT: the staged grid and the cell table are read where k_grid_build left
+// them (L2-resident: 64 KB + 12 KB per C5 frame, the problem's workgroups
+// share one XCD) instead of being copied into LDS by every workgroup; the
+// workgroup then holds no LDS and the chip is not limited to two 1024-point
+// workgroups per CU
+// ncand of the projection matcher: the candidate count, with the point's
+// has_obs (a claim by it locks the keypoint) in bit 30, so the resolve reads one
+// word per point for both; -1 = not in view / bad
+#define NC_OBS 0x40000000
+__device__ __forceinline__ int nc_count(int v) { return v < 0 ? v : (v & (NC_OBS - 1)); }
+__device__ __forceinline__ bool nc_obs(int v) { return v >= 0 && (v & NC_OBS) != 0; }
+
+template <int WG, bool DIRECT = false>
 __global__ __launch_bounds__(WG) void k_proj_candidates(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked, int kpStride,
@@ -321,7 +333,7 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
     const int32_t* __restrict__ cellStart, const int32_t* __restrict__ cellIdx,
     const uint4* __restrict__ stagedGrid, int stageCap, ProjParams P,
     uint32_t* __restrict__ topk, int32_t* __restrict__ ncand) {
-  __shared__ int sCS[GRID_CELLS + 1];
+  __shared__ int sCS[DIRECT ? 1 : GRID_CELLS + 1];
   extern __shared__ __attribute__((aligned(16))) uint4 sKp[];  // min(kpStride, PROJ_STAGE)
   __shared__ float sScale[ORB_MAX_LEVELS];
   // XCD-contiguous order: a problem's workgroups share one L2, which then
@@ -343,11 +355,18 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
   const float* UR = uright ? uright + (size_t)p * kpStride : nullptr;
   const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
   const int32_t* ci = cellIdx + (size_t)p * kpStride;
-  const bool staged = N <= stageCap;
+  const bool staged = DIRECT || N <= stageCap;
 #pragma unroll
   for (int i = 0; i < ORB_MAX_LEVELS; ++i)
     if (tid == i) sScale[i] = P.scale[i];
-  if (staged) {
+  // the cell table and the cell-ordered keypoints scanned below: LDS copies,
+  // or (DIRECT) the global arrays themselves
+  const int* gCS = sCS;
+  const uint4* gKp = sKp;
+  if (DIRECT) {
+    gCS = cs;
+    gKp = stagedGrid + (size_t)p * kpStride;
+  } else if (staged) {
     for (int i = tid; i <= GRID_CELLS; i += WG) sCS[i] = cs[i];
     const int nInGrid = cs[GRID_CELLS];
     if (stagedGrid) {
@@ -427,9 +446,9 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
       for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
         for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
           const int c = ix * ORB_GRID_ROWS + iy;
-          const int e = sCS[c + 1];
-          for (int j = sCS[c]; j < e; ++j) {
-            const uint4 E = sKp[j];
+          const int e = gCS[c + 1];
+          for (int j = gCS[c]; j < e; ++j) {
+            const uint4 E = gKp[j];
             const int oct = (int)((E.z >> 24) & 0x7Fu);
             if (oct < minL || oct > maxL) continue;
             const float dx = __uint_as_float(E.x) - x, dy = __uint_as_float(E.y) - y;
@@ -455,7 +474,7 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
                          });
   }
   top.store(topk + mg * TOPK);
-  ncand[mg] = count;
+  ncand[mg] = count | (mp.has_obs ? NC_OBS : 0);
 }
 
 // Sequential-semantics resolve, one workgroup per problem, speculatively a
@@ -516,8 +535,9 @@ __global__ __launch_bounds__(64 * NW) void k_proj_resolve(
         const int m = cb + j;
         if (m < M) {
           cTop[j] = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
-          cN[j] = ncand[pbase + m];
-          cObs[j] = mps[pbase + m].has_obs;
+          const int v = ncand[pbase + m];
+          cN[j] = nc_count(v);
+          cObs[j] = nc_obs(v);
         }
       }
       __syncthreads();
@@ -639,6 +659,45 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// The exact scan of a point whose top-K ran dry (more than K candidates, too
+// many of them taken): GetFeaturesInArea under the same "taken" test.  Not
+// inlined: its global loads would otherwise sit inside k_proj_resolve_fp's
+// round loop, and the compiler's wait for them at the loop head (one vmcnt
+// counter, in order) also waited for the next windows' inputs in flight; as
+// a call the waits stay on the (rare: never in C5) path that takes it.
+__device__ __noinline__ int fp_slow(int m, const int* cur, const orb_mp_track_t* mpp,
+                                    const uint8_t* mpd, const orb_keypoint_t* K, const uint8_t* D,
+                                    const uint8_t* LK, const float* UR, const int32_t* cs,
+                                    const int32_t* ci, const ProjParams P) {
+  // (P by value: a reference would put the caller's copy in scratch memory
+  // and every fp_choose would read nnratio from there)
+  const orb_mp_track_t mp = *mpp;
+  const int lvl = mp.level;
+  float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;
+  if (P.th != 1.0f) r *= P.th;
+  const float rs = r * P.scale[lvl];
+  const ulonglong4 qd = load_desc(mpd);
+  int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+  for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
+                       [&](int idx, const orb_keypoint_t& kp) {
+                         if ((LK && LK[idx]) || cur[idx] < m) return;
+                         if (UR && UR[idx] > 0) {
+                           const float er = fabsf(mp.proj_xr - UR[idx]);
+                           if (er > rs) return;
+                         }
+                         const int dist = hamming256(qd, load_desc(D + (size_t)idx * 32));
+                         if (dist < bestDist) {
+                           bestDist2 = bestDist; bestDist = dist;
+                           bestLevel2 = bestLevel; bestLevel = kp.octave; bestIdx = idx;
+                         } else if (dist < bestDist2) {
+                           bestLevel2 = kp.octave; bestDist2 = dist;
+                         }
+                       });
+  const bool accept = bestIdx >= 0 && bestDist <= 100 &&
+                      !(bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2);
+  return accept ? bestIdx : -1;
+}
+
 // One point's SearchByProjection decision (src/ORBmatcher.cc:83-132) with
 // "keypoint k taken before point m" = cur[k] < m (committed locks are -1,
 // claims of the current window hold the claiming point): the keypoint it
@@ -664,31 +723,8 @@ __device__ __forceinline__ int fp_choose(const uint32_t (&e)[TOPK], int nc, int 
     }
     found += use ? 1 : 0;
   }
-  if (nc > TOPK && found < 2) {
-    // top-K ran dry: exact scan of the point's area under the same locks
-    const orb_mp_track_t mp = *mpp;
-    const int lvl = mp.level;
-    float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;
-    if (P.th != 1.0f) r *= P.th;
-    const float rs = r * P.scale[lvl];
-    const ulonglong4 qd = load_desc(mpd);
-    bestDist = 256; bestLevel = -1; bestDist2 = 256; bestLevel2 = -1; bestIdx = -1;
-    for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
-                         [&](int idx, const orb_keypoint_t& kp) {
-                           if ((LK && LK[idx]) || cur[idx] < m) return;
-                           if (UR && UR[idx] > 0) {
-                             const float er = fabsf(mp.proj_xr - UR[idx]);
-                             if (er > rs) return;
-                           }
-                           const int dist = hamming256(qd, load_desc(D + (size_t)idx * 32));
-                           if (dist < bestDist) {
-                             bestDist2 = bestDist; bestDist = dist;
-                             bestLevel2 = bestLevel; bestLevel = kp.octave; bestIdx = idx;
-                           } else if (dist < bestDist2) {
-                             bestLevel2 = kp.octave; bestDist2 = dist;
-                           }
-                         });
-  }
+  // top-K ran dry: exact scan of the point's area under the same locks
+  if (nc > TOPK && found < 2) return fp_slow(m, cur, mpp, mpd, K, D, LK, UR, cs, ci, P);
   const bool accept = bestIdx >= 0 && bestDist <= 100 &&
                       !(bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2);
   return accept ? bestIdx : -1;
@@ -702,10 +738,29 @@ __device__ __forceinline__ int fp_choose(const uint32_t (&e)[TOPK], int nc, int 
 // The sequential result is the unique fixed point (the smallest point whose
 // choice differs from it sees a correct claim set and becomes correct next
 // round), so the loop ends after at most one round per point; C5 windows
-// settle in 2.2 rounds on average.  Claims are double-buffered (round r reads
-// buffer (r-1)&1, writes r&1); a committed lock is -1 in both buffers.  The
-// next window's inputs are loaded while the current one iterates, and rounds
-// synchronise on LDS only.
+// settle in 2.2 rounds on average (tools/r04/c5_stats.cpp: the deepest claim
+// chain of a 1024-point window is 0.5 on average, 2 at most, and no C5 point
+// ever needs more than its top 4 candidates).  Claims are double-buffered
+// (round r reads buffer (r-1)&1, writes r&1); a committed lock is -1 in both
+// buffers.  Every memory access of the window loop is LDS: the inputs of the
+// windows two and three ahead are loaded while the current one iterates
+// (FP_AHEAD), and the keypoint -> point result (kpMatch) is kept in LDS and
+// written out once at the end, so no wait on a global access (loads, or the
+// kpMatch atomics, which share the in-order vmcnt counter with the loads on
+// gfx9) sits inside the loop; rounds synchronise on LDS only.
+#ifndef FP_AHEAD
+#define FP_AHEAD 2  // windows of inputs in flight ahead of the current one (1 or 2)
+#endif
+#ifndef FP_DEBUG
+#define FP_DEBUG 0  // diagnostic build: per-window rounds and clock stamps of problem 0
+#endif
+#if FP_DEBUG
+// [0] windows, then per window: rounds, cycles (s_memtime) at its end
+__device__ unsigned long long g_fp_dbg[2 + 2 * 256];
+extern "C" hipError_t orb_k_fp_debug(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fp_dbg), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 template <int T>
 __global__ __launch_bounds__(T) void k_proj_resolve_fp(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
@@ -717,18 +772,18 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
     int32_t* __restrict__ kpMatch, int32_t* __restrict__ nmatches,
     const int32_t* __restrict__ done, long long doneStride) {
   constexpr int NOCLAIM = 0x7FFFFFFF;
-  extern __shared__ __attribute__((aligned(16))) int claims[];  // 2 x kpStride
+  // 2 x kpStride claims, kpStride kpMatch
+  extern __shared__ __attribute__((aligned(16))) int claims[];
   __shared__ int sCount[T / 64];
   __shared__ int sChanged[2];
   const int p = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   // after the Jacobi rounds (k_proj_jacobi): only problems they left unsettled
   if (done && done[(long long)p * doneStride] != 0) return;
   const int n = nkeys[p], M = nmps[p];
+  int* skm = claims + 2 * kpStride;
   if (t < 2) sChanged[t] = 0;
   for (int i = t; i < 2 * kpStride; i += T) claims[i] = NOCLAIM;
-  int32_t* km = kpMatch + (size_t)p * kpStride;
-  for (int i = t; i < n; i += T) km[i] = -1;
-  __syncthreads();  // kpMatch reset before any window's atomicMax
+  for (int i = t; i < n; i += T) skm[i] = -1;
   const size_t pbase = (size_t)p * mpStride;
   const orb_keypoint_t* K = keys + (size_t)p * kpStride;
   const uint8_t* D = desc + (size_t)p * kpStride * 32;
@@ -737,25 +792,39 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
   const int32_t* cs = cellStart + (size_t)p * (GRID_CELLS + 1);
   const int32_t* ci = cellIdx + (size_t)p * kpStride;
   int matches = 0;
-  // inputs of the window starting at `start`, loaded one window ahead
-  uint4 nE = make_uint4(0, 0, 0, 0);
-  int nNc = -1, nObs = 0;
-  auto load = [&](int m) {
-    nNc = -1;
-    if (m < M) {
-      nE = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
-      nNc = ncand[pbase + m];
-      nObs = mps[pbase + m].has_obs;
-    }
+  // inputs of the windows ahead (A: next, B: the one after)
+  struct In {
+    uint4 e;
+    int nc;  // count | NC_OBS
   };
-  load(t);
+  // issued by every lane on every path (index clamped, the count masked
+  // after the wait): the compiler then counts the loads in flight exactly and
+  // waits for a window's inputs only, not for the later windows' too
+  auto load = [&](In& in, int m) {
+    const size_t mg = pbase + (size_t)max(0, min(m, M - 1));
+    in.e = *reinterpret_cast<const uint4*>(topk + mg * TOPK);
+    in.nc = ncand[mg];
+  };
+  In inA, inB;
+  load(inA, t);
+#if FP_AHEAD > 1
+  asm volatile("" ::: "memory");  // A's loads all issue before B's (in-order counts)
+  __builtin_amdgcn_sched_barrier(0);
+  load(inB, T + t);
+#endif
+  __syncthreads();  // LDS reset before any window's claims
   int round = 0;  // global round counter: buffer parity and change flags
-  for (int start = 0; start < M; start += T) {
+#if FP_DEBUG
+  int dbgW = 0;
+  if (p == 0 && t == 0) g_fp_dbg[1] = __builtin_amdgcn_s_memtime();
+#endif
+  // one window: its inputs leave `in` (loaded FP_AHEAD windows earlier) and
+  // `in` is reloaded with the inputs FP_AHEAD windows on
+  auto window = [&](int start, In& in) {
     const int m = start + t;
-    const uint32_t e[TOPK] = {nE.x, nE.y, nE.z, nE.w};
-    const int nc = nNc;
-    const bool obs = nObs != 0;
-    load(start + T + t);
+    const uint32_t e[TOPK] = {in.e.x, in.e.y, in.e.z, in.e.w};
+    const int nc = m < M ? nc_count(in.nc) : -1;
+    const bool obs = m < M && nc_obs(in.nc);
     int prev = -1;  // this point's claim in the previous round
     int acc = -1;
     while (true) {
@@ -780,15 +849,37 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
     }
     // commit: the final claims become committed locks in both buffers
     if (acc >= 0) {
-      atomicMax(&km[acc], m);
+      atomicMax(&skm[acc], m);
       if (obs) {
         claims[acc] = -1;
         claims[kpStride + acc] = -1;
       }
       ++matches;
     }
+    // reloaded only now, when this window's inputs are dead: the loads land in
+    // the registers they came from (no copy, so no wait for them before the
+    // window that uses them)
+    load(in, start + FP_AHEAD * T + t);
     lds_barrier();
+#if FP_DEBUG
+    if (p == 0 && t == 0 && dbgW < 256) {
+      g_fp_dbg[2 + 2 * dbgW] = (unsigned long long)round;
+      g_fp_dbg[3 + 2 * dbgW] = __builtin_amdgcn_s_memtime();
+      g_fp_dbg[0] = (unsigned long long)(dbgW + 1);
+    }
+    ++dbgW;
+#endif
+  };
+#if FP_AHEAD > 1
+  for (int start = 0; start < M; start += 2 * T) {
+    window(start, inA);
+    window(start + T, inB);  // (past M: one round in which nothing changes)
   }
+#else
+  for (int start = 0; start < M; start += T) window(start, inA);
+#endif
+  int32_t* km = kpMatch + (size_t)p * kpStride;
+  for (int i = t; i < n; i += T) km[i] = skm[i];
   matches = wave_sum(matches);
   if (lane == 0) sCount[wv] = matches;
   __syncthreads();
@@ -882,7 +973,9 @@ __global__ __launch_bounds__(JAC_T) void k_proj_jacobi(
   for (int i = blockIdx.x * JAC_T + t; i < kpStride; i += gridDim.x * JAC_T) clr[i] = 0x7FFFFFFF;
   bool changed = false;
   if (m < M) {
-    const int nc = ncand[pbase + m];
+    const int ncv = ncand[pbase + m];
+    const int nc = nc_count(ncv);
+    const bool hasObs = nc_obs(ncv);
     int acc = -1;
     if (nc > 0) {
       const uint4 q = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
@@ -895,9 +988,9 @@ __global__ __launch_bounds__(JAC_T) void k_proj_jacobi(
     }
     const int old = r > 0 ? dec[m] : -1;
     dec[m] = acc;
-    const bool obs = acc >= 0 && mps[pbase + m].has_obs != 0;
+    const bool obs = acc >= 0 && hasObs;
     if (obs) atomicMin(&nxt[acc], m);
-    const int oldClaim = (old >= 0 && mps[pbase + m].has_obs != 0) ? old : -1;
+    const int oldClaim = (old >= 0 && hasObs) ? old : -1;
     changed = (obs ? acc : -1) != oldClaim;
   }
   if (__ballot(changed) != 0ull && lane == 0) S[r] = 1;
@@ -969,6 +1062,21 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
   static const int wgLarge =
       getenv("ORB_PROJ_WG_LARGE") ? atoi(getenv("ORB_PROJ_WG_LARGE")) : 1024;
   const bool large = wgLarge == 1024 && stageCap > 2048 && mpMax >= 20000;
+  // ORB_PROJ_DIRECT=1: scan the staged grid in global memory (no LDS copy)
+  static const int direct = getenv("ORB_PROJ_DIRECT") ? atoi(getenv("ORB_PROJ_DIRECT")) : 0;
+  if (direct && stagedGrid) {
+    if (large)
+      hipLaunchKernelGGL((k_proj_candidates<1024, true>), dim3((mpMax + 1023) / 1024, nproblems),
+                         dim3(1024), 0, s, keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc,
+                         nmps, mpStride, cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P,
+                         topk, ncand);
+    else
+      hipLaunchKernelGGL((k_proj_candidates<PROJ_WG, true>),
+                         dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems), dim3(PROJ_WG), 0, s, keys,
+                         desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart,
+                         cellIdx, (const uint4*)stagedGrid, stageCap, P, topk, ncand);
+    return hipGetLastError();
+  }
   const void* fn = large ? (const void*)k_proj_candidates<1024> : (const void*)k_proj_candidates<PROJ_WG>;
   if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {  // with the static grid table
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1006,7 +1114,7 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   // 39.8k/37.1k/28.7k).  ORB_RESOLVE_FP=0 selects the prefix kernel.
   static const int fpMode = getenv("ORB_RESOLVE_FP") ? atoi(getenv("ORB_RESOLVE_FP")) : 1;
   static const int fpMin = getenv("ORB_RESOLVE_FP_MIN") ? atoi(getenv("ORB_RESOLVE_FP_MIN")) : 20000;
-  const size_t ldsFp = (size_t)kpStride * 8;
+  const size_t ldsFp = (size_t)kpStride * 12;  // claims x 2 + kpMatch
   // Large maps: Jacobi rounds over the whole chip first (k_proj_jacobi), the
   // windowed fixed-point kernel after them for any problem not yet settled
   // (ORB_RESOLVE_JACOBI=0: the windowed kernel alone; ORB_JACOBI_ROUNDS = R)
@@ -1016,7 +1124,14 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 0;
   static const int jacR =
       getenv("ORB_JACOBI_ROUNDS") ? std::max(1, std::min(48, atoi(getenv("ORB_JACOBI_ROUNDS")))) : 4;
-  const bool fp = mpStride >= fpMin && fpMode > 0 && ldsFp <= 64 * 1024;
+  const bool fp = mpStride >= fpMin && fpMode > 0 && ldsFp <= 160 * 1024 - 1024;
+  if (fp && ldsFp > 64 * 1024) {
+    const void* fn = fpMode == 256   ? (const void*)k_proj_resolve_fp<256>
+                     : fpMode == 512 ? (const void*)k_proj_resolve_fp<512>
+                                     : (const void*)k_proj_resolve_fp<1024>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsFp);
+    if (e != hipSuccess) return e;
+  }
   const int32_t* done = nullptr;
   long long doneStride = 0;
   if (fp && jacOn > 0 && jacScratch) {

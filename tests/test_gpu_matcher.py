@@ -175,12 +175,16 @@ def test_search_by_projection_batch_large_maps(gpu, oracle):
 @pytest.mark.parametrize("env", [{"ORB_RESOLVE_JACOBI": "1", "ORB_JACOBI_ROUNDS": "1"},
                                  {"ORB_RESOLVE_JACOBI": "1"},
                                  {"ORB_RESOLVE_JACOBI": "1", "ORB_JACOBI_ROUNDS": "48"},
-                                 {"ORB_RESOLVE_JACOBI": "0"}])
+                                 {"ORB_RESOLVE_JACOBI": "0"},
+                                 {"ORB_RESOLVE_FP": "256"}, {"ORB_RESOLVE_FP": "512"},
+                                 {"ORB_PROJ_DIRECT": "1"}])
 def test_search_by_projection_resolve_schedules(gpu, oracle, tmp_path, env):
     """The large-map resolve under each schedule (read once per process, so in
     a child): Jacobi rounds (1, the default 4, up to 48) with the windowed
-    fallback, and the windowed kernel alone (the default); C5's map and a
-    deep-conflict map."""
+    fallback, the windowed kernel alone (the default) at 1024, 256 and 512
+    points per window, and the candidate scan reading the staged grid from
+    global memory (ORB_PROJ_DIRECT); C5's map and a deep-conflict map (whose
+    points run out of top-4 candidates: the exact re-scan)."""
     import os
     import subprocess
     import sys
