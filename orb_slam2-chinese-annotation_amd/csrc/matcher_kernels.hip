@@ -324,7 +324,9 @@ __global__ __launch_bounds__(256) void k_grid_build4(const orb_keypoint_t* __res
 __device__ __forceinline__ int nc_count(int v) { return v < 0 ? v : (v & (NC_OBS - 1)); }
 __device__ __forceinline__ bool nc_obs(int v) { return v >= 0 && (v & NC_OBS) != 0; }
 
-template <int WG, bool DIRECT = false>
+// PPT: map points per thread (a workgroup covers WG * PPT points, the grid
+// staged once for all of them)
+template <int WG, bool DIRECT = false, int PPT = 1>
 __global__ __launch_bounds__(WG) void k_proj_candidates(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked, int kpStride,
@@ -346,9 +348,8 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
   p = blockIdx.y;
 #endif
   const int tid = threadIdx.x;
-  const int m = bx * blockDim.x + tid;
   const int M = nmps[p], N = nkeys[p];
-  if ((int)(bx * blockDim.x) >= M) return;  // whole workgroup idle (uniform)
+  if (bx * WG * PPT >= M) return;  // whole workgroup idle (uniform)
   const orb_keypoint_t* K = keys + (size_t)p * kpStride;
   const uint8_t* D = desc + (size_t)p * kpStride * 32;
   const uint8_t* LK = locked ? locked + (size_t)p * kpStride : nullptr;
@@ -386,12 +387,14 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
     }
   }
   __syncthreads();
-  if (m >= M) return;
+  for (int pk = 0; pk < PPT; ++pk) {
+  const int m = (bx * PPT + pk) * WG + tid;
+  if (m >= M) break;
   const size_t mg = (size_t)p * mpStride + m;
   const orb_mp_track_t mp = mps[mg];
   if (!mp.in_view || mp.bad) {
     ncand[mg] = -1;
-    return;
+    continue;
   }
   const int lvl = mp.level;
   float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:135-141)
@@ -475,6 +478,7 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
   }
   top.store(topk + mg * TOPK);
   ncand[mg] = count | (mp.has_obs ? NC_OBS : 0);
+  }
 }
 
 // Sequential-semantics resolve, one workgroup per problem, speculatively a
@@ -1062,8 +1066,24 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
   static const int wgLarge =
       getenv("ORB_PROJ_WG_LARGE") ? atoi(getenv("ORB_PROJ_WG_LARGE")) : 1024;
   const bool large = wgLarge == 1024 && stageCap > 2048 && mpMax >= 20000;
+  // points per thread for large maps: 2 puts C5's 16 x 50,000 points in 400
+  // workgroups, one pass over the chip's 512 two-per-CU slots (1: 784, a
+  // second, half-empty pass)
+  static const int pptLarge = getenv("ORB_PROJ_PPT") ? atoi(getenv("ORB_PROJ_PPT")) : 1;
   // ORB_PROJ_DIRECT=1: scan the staged grid in global memory (no LDS copy)
   static const int direct = getenv("ORB_PROJ_DIRECT") ? atoi(getenv("ORB_PROJ_DIRECT")) : 0;
+  if (large && pptLarge == 2 && !(direct && stagedGrid)) {
+    const void* f2 = (const void*)k_proj_candidates<1024, false, 2>;
+    if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {
+      hipError_t e = hipFuncSetAttribute(f2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((k_proj_candidates<1024, false, 2>), dim3((mpMax + 2047) / 2048, nproblems),
+                       dim3(1024), lds, s, keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc,
+                       nmps, mpStride, cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P,
+                       topk, ncand);
+    return hipGetLastError();
+  }
   if (direct && stagedGrid) {
     if (large)
       hipLaunchKernelGGL((k_proj_candidates<1024, true>), dim3((mpMax + 1023) / 1024, nproblems),

@@ -109,6 +109,47 @@ int main(int argc, char** argv) {
       printf("  T=%d: windows %d, mean max-depth %.2f, worst %d\n", T, nw, (double)sumDepth / nw,
              maxD);
     }
+    // the fixed-point (Jacobi) iteration itself over windows of T points:
+    // rounds until no claim changes (k_proj_resolve_fp / k_proj_jacobi)
+    for (int T : {1024, 4096, 16384, M}) {
+      std::vector<int> lockC(lk.begin(), lk.end());  // committed: 1
+      long long sumR = 0;
+      int maxR = 0, nw = 0;
+      for (int s0 = 0; s0 < M; s0 += T) {
+        const int e0 = std::min(M, s0 + T);
+        std::vector<int> claimPrev(n, INT32_MAX), claimCur(n, INT32_MAX), dec(e0 - s0, -2);
+        int rounds = 0;
+        while (true) {
+          ++rounds;
+          std::fill(claimCur.begin(), claimCur.end(), INT32_MAX);
+          bool changed = false;
+          for (int m = s0; m < e0; ++m) {
+            int found = 0, bd = 256, bl = -1, bd2 = 256, bl2 = -1, bi = -1;
+            for (auto& c : cand[m]) {
+              const int i = c.second;
+              if (lockC[i] || claimPrev[i] < m) continue;
+              if (found == 0) { bd = c.first; bl = kp[i].octave; bi = i; }
+              else { bd2 = c.first; bl2 = kp[i].octave; }
+              if (++found == 2) break;
+            }
+            int acc = (bi >= 0 && bd <= 100 && !(bl == bl2 && (float)bd > 0.8f * (float)bd2)) ? bi : -1;
+            const int claim = mps[m].has_obs ? acc : -1;
+            if (claim >= 0) claimCur[claim] = std::min(claimCur[claim], m);
+            if (dec[m - s0] != claim) changed = true;
+            dec[m - s0] = claim;
+          }
+          std::swap(claimPrev, claimCur);
+          if (!changed) break;
+        }
+        for (int m = s0; m < e0; ++m)
+          if (dec[m - s0] >= 0) lockC[dec[m - s0]] = 1;
+        sumR += rounds;
+        maxR = std::max(maxR, rounds);
+        ++nw;
+      }
+      printf("  Jacobi T=%d: windows %d, rounds mean %.2f max %d (total %lld)\n", T, nw,
+             (double)sumR / nw, maxR, sumR);
+    }
     printf("problem %d: n %d, in view %lld, mean cand %.2f, nc hist 0..5+ %d %d %d %d %d %d, "
            "slow K=4 %d K=8 %d K=16 %d, matches %d\n",
            p, n, nIn, (double)ncTot / nIn, hist[0], hist[1], hist[2], hist[3], hist[4], hist[5],
