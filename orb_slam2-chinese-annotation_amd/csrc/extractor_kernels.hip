@@ -215,6 +215,81 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   }
 }
 
+// ============================================================ k_pyr_chain
+// The whole resize chain of one or two frames in ONE launch (the single-frame
+// call's seven dependent k_pyr_resize launches cost ~4.7 us each, most of it
+// launch and ramp): blockIdx.x = band (OrbChainBand, host-planned), blockIdx.y
+// = image.  Level by level, the band computes the rows of level l that its own
+// rows of levels >= l need, from the previous level's rows in LDS (two
+// buffers, even / odd levels), and writes the rows it owns.  Rows in a halo
+// are computed by two bands (same inputs, same result).  The taps are
+// k_pyr_resize's integer expressions (OpenCV's 11-bit fixed point), so the
+// pyramid is bit-identical.
+template <int T>
+__global__ __launch_bounds__(T) void k_pyr_chain(const uint8_t* __restrict__ img0, long long imgPitch,
+                                                 int img0Stride, uint8_t* __restrict__ arena,
+                                                 long long arenaPitch, OrbPlanDesc plan,
+                                                 const int32_t* __restrict__ rt,
+                                                 const OrbChainBand* __restrict__ bands, int buf1Off) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  const int tid = threadIdx.x;
+  const OrbChainBand& B = bands[blockIdx.x];
+  const int img = blockIdx.y;
+  uint8_t* A = arena + (long long)img * arenaPitch;
+  {
+    // level 0 rows [lo, hi) into buffer 0, dword by dword, realigned from any
+    // caller stride / base alignment (buffer loads past the image read 0)
+    const int lo = B.lo[0], hi = B.hi[0], w = plan.lv[0].w, h = plan.lv[0].h;
+    const int nd = orb_chain_pitch(w) >> 2;
+    const ImgRsrc im = img_rsrc(img0 + (long long)img * imgPitch, (uint32_t)((h - 1) * img0Stride + w));
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(sm);
+    for (int i = tid; i < (hi - lo) * nd; i += T) {
+      const int r = i / nd, c = i - r * nd;
+      const uint32_t o = (uint32_t)((lo + r) * img0Stride + 4 * c) + im.sh;
+      const uint32_t a = o & ~3u, sh = o & 3u;
+      const uint32_t w0 = buf_ld32(im.r, a), w1 = buf_ld32(im.r, a + 4);
+      d32[i] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+  }
+  __syncthreads();
+  for (int l = 1; l < plan.nlevels; ++l) {
+    const OrbLevelDesc& d = plan.lv[l];
+    const int sw = plan.lv[l - 1].w, sh = plan.lv[l - 1].h;
+    const uint8_t* S = sm + ((l - 1) & 1) * buf1Off;
+    uint8_t* Dl = sm + (l & 1) * buf1Off;
+    const int sp = orb_chain_pitch(sw), dp = orb_chain_pitch(d.w), slo = B.lo[l - 1];
+    const int lo = B.lo[l], hi = B.hi[l], own = B.own[l], ownE = B.ownEnd[l];
+    const int ng = (d.w + 3) >> 2, n = (hi - lo) * ng;
+    const int32_t* xo = rt + d.rtabX;
+    const int32_t* al = xo + d.w;
+    const int32_t* yo = rt + d.rtabY;
+    const int32_t* be = yo + d.h;
+    for (int i = tid; i < n; i += T) {
+      const int r = i / ng, c = i - r * ng;
+      const int y = lo + r, x = 4 * c;
+      const int yy = yo[y];
+      const uint32_t bb = (uint32_t)be[y], b0 = bb & 0xFFFFu, b1 = bb >> 16;
+      const uint8_t* R0 = S + (min(max(yy, 0), sh - 1) - slo) * sp;
+      const uint8_t* R1 = S + (min(max(yy + 1, 0), sh - 1) - slo) * sp;
+      uint32_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int dx = min(x + j, d.w - 1);
+        const int sx = xo[dx], sx1 = min(sx + 1, sw - 1);  // (weight 0 where sx + 1 >= sw)
+        const uint32_t aa = (uint32_t)al[dx], a0 = aa & 0xFFFFu, a1 = aa >> 16;
+        const uint32_t h0 = a0 * R0[sx] + a1 * R0[sx1], h1 = a0 * R1[sx] + a1 * R1[sx1];
+        int v = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
+        __asm__ volatile("" : "+v"(v));  // see k_pyr_resize: keep the byte pack opaque
+        packed |= (uint32_t)v << (8 * j);
+      }
+      *reinterpret_cast<uint32_t*>(Dl + r * dp + x) = packed;
+      if (y >= own && y < ownE)
+        *reinterpret_cast<uint32_t*>(A + d.arenaOff + (long long)y * d.pitch + x) = packed;
+    }
+    __syncthreads();
+  }
+}
+
 // ============================================================ k_fast_band
 // FAST arc strength at the pixel `c` points to (LDS band of biased f16 pixels,
 // row pitch `p` elements): m = max(best dark 9-arc, best bright 9-arc), where
@@ -2815,6 +2890,76 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   else ORB_RESIZE_LAUNCH(false, PYR_SROWS_WIDE, PYR_SW_WIDE);
 #undef ORB_RESIZE_LAUNCH
   return hipGetLastError();
+}
+
+// the resize chain of nimg (1 or 2) images in one launch; bands and the two
+// LDS buffers' sizes (even levels, odd levels) from orb_pyr_chain_plan
+hipError_t orb_k_pyr_chain(const uint8_t* img0, long long imgPitch, int img0Stride, uint8_t* arena,
+                           long long arenaPitch, const OrbPlanDesc* plan, const int32_t* rt,
+                           const void* bands, int nb, const int* bufBytes, int nimg, hipStream_t s) {
+  const size_t lds = (size_t)bufBytes[0] + bufBytes[1];
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_pyr_chain<512>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_pyr_chain<512>, dim3(nb, nimg), dim3(512), lds, s, img0, imgPitch, img0Stride,
+                     arena, arenaPitch, *plan, rt, (const OrbChainBand*)bands, bufBytes[0]);
+  return hipGetLastError();
+}
+
+// Plans k_pyr_chain's bands for a plan whose resize tables are `rtab` (host
+// copy): the smallest band count from 16 up (doubling) whose two LDS buffers
+// (rows of the even levels, of the odd levels; bufBytes[0], bufBytes[1]) fit
+// `ldsMax` bytes together; returns the band count (0: none fits) and fills `out`.
+int orb_pyr_chain_plan(const OrbPlanDesc* plan, const int32_t* rtab, size_t ldsMax, void* out,
+                       int maxBands, int* bufBytes) {
+  const int L = plan->nlevels;
+  OrbChainBand* bd = (OrbChainBand*)out;
+  for (int nb = 16; nb <= maxBands; nb *= 2) {
+    int need[2] = {0, 0};
+    bool ok = true;
+    for (int b = 0; b < nb && ok; ++b) {
+      OrbChainBand& B = bd[b];
+      for (int l = 0; l < L; ++l) {
+        const int h = plan->lv[l].h;
+        B.own[l] = (int16_t)((long long)b * h / nb);
+        B.ownEnd[l] = (int16_t)((long long)(b + 1) * h / nb);
+      }
+      if (L > 0) {
+        B.lo[L - 1] = B.own[L - 1];
+        B.hi[L - 1] = B.ownEnd[L - 1];
+      }
+      for (int l = L - 1; l >= 1; --l) {
+        const OrbLevelDesc& d = plan->lv[l];
+        const int sh = plan->lv[l - 1].h;
+        int lo = B.own[l - 1], hi = B.ownEnd[l - 1];
+        if (B.hi[l] > B.lo[l]) {
+          const int32_t* yo = rtab + d.rtabY;
+          int a = 1 << 30, e = -1;
+          for (int y = B.lo[l]; y < B.hi[l]; ++y) {
+            a = std::min(a, std::min(std::max(yo[y], 0), sh - 1));
+            e = std::max(e, std::min(std::max(yo[y] + 1, 0), sh - 1) + 1);
+          }
+          if (hi <= lo) { lo = a; hi = e; }
+          else { lo = std::min(lo, a); hi = std::max(hi, e); }
+        }
+        B.lo[l - 1] = (int16_t)lo;
+        B.hi[l - 1] = (int16_t)std::max(lo, hi);
+      }
+      for (int l = 0; l < L; ++l) {
+        const int bytes = (B.hi[l] - B.lo[l]) * orb_chain_pitch(plan->lv[l].w);
+        need[l & 1] = std::max(need[l & 1], bytes);
+      }
+    }
+    const int b0 = (need[0] + 15) & ~15, b1 = (need[1] + 15) & ~15;
+    if (ok && (size_t)b0 + b1 <= ldsMax) {
+      bufBytes[0] = b0;
+      bufBytes[1] = b1;
+      return nb;
+    }
+  }
+  return 0;
 }
 
 // Dynamic LDS of k_fast_band for bands of up to `bandElems` elements (rows x

@@ -70,3 +70,14 @@ struct OrbTileDesc {
 };
 #define ORB_BLUR_TW 128
 #define ORB_BLUR_TH 32
+
+// k_pyr_chain (one or two frames per call): workgroup b computes rows
+// [lo[l], hi[l]) of every level l >= 1 from the previous level's rows held in
+// LDS (level 0: rows [lo[0], hi[0]) of the caller's image, staged) and writes
+// the rows it owns, [own[l], ownEnd[l]), to the arena.  The owned rows split
+// each level evenly over the bands; lo / hi add the rows the band's owned rows
+// of the levels above need.
+struct OrbChainBand {
+  int16_t lo[ORB_MAX_LEVELS], hi[ORB_MAX_LEVELS], own[ORB_MAX_LEVELS], ownEnd[ORB_MAX_LEVELS];
+};
+__host__ __device__ inline int orb_chain_pitch(int w) { return (w + 3) & ~3; }

@@ -27,6 +27,11 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
                             int dh, const int* xofs, const void* alpha, const int* yofs,
                             const void* beta, int xmax, int nimg, hipStream_t s);
+hipError_t orb_k_pyr_chain(const uint8_t* img0, long long imgPitch, int img0Stride, uint8_t* arena,
+                           long long arenaPitch, const OrbPlanDesc* plan, const int32_t* rt,
+                           const void* bands, int nb, const int* bufBytes, int nimg, hipStream_t s);
+int orb_pyr_chain_plan(const OrbPlanDesc* plan, const int32_t* rtab, size_t ldsMax, void* out,
+                       int maxBands, int* bufBytes);
 size_t orb_k_fast_band_lds(int bandElems);
 size_t orb_k_fast_cells_lds(int maxRows, int maxCols);
 bool orb_k_fast_cells_fits(const OrbPlanDesc* plan);
@@ -371,6 +376,9 @@ struct orb_extractor {
   long long arenaBytes = 0, blurBytes = 0;
   int maxCellsPerLevel = 0, nodeCapMax = 0, ldsKeyCap = 0;
   DevBuf dCells, dRtab, dTiles, dBands;
+  // k_pyr_chain bands (the one-launch resize chain of one- or two-frame calls)
+  DevBuf dChain;
+  int chainNb = 0, chainBuf[2] = {0, 0};
 
   // batch scratch
   int batchCap = 0;
@@ -660,7 +668,22 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (!rtab.empty())
     HIP_TRY(hipMemcpyAsync(h->dRtab.p, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice,
                            h->stream));
+  // the one-launch resize chain for small calls: 16-128 bands whose LDS rows fit
+  // 150 KB (one workgroup per CU; none fits: the per-level launches)
+  std::vector<OrbChainBand> chain(128);
+  int chainBuf[2] = {0, 0};
+  const int chainNb = P.nlevels > 1 ? orb_pyr_chain_plan(&P, rtab.data(), 150 * 1024, chain.data(), 128,
+                                                         chainBuf)
+                                    : 0;
+  if (chainNb > 0) {
+    if ((st = h->dChain.ensure((size_t)chainNb * sizeof(OrbChainBand)))) return st;
+    HIP_TRY(hipMemcpyAsync(h->dChain.p, chain.data(), (size_t)chainNb * sizeof(OrbChainBand),
+                           hipMemcpyHostToDevice, h->stream));
+  }
   HIP_TRY(hipStreamSynchronize(h->stream));
+  h->chainNb = chainNb;
+  h->chainBuf[0] = chainBuf[0];
+  h->chainBuf[1] = chainBuf[1];
   h->plan = P;
   h->cells.swap(cells);
   h->arenaBytes = (arena + 255) & ~255LL;
@@ -813,7 +836,14 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   }
   PROF_REC(ev, pf.b(ev, 0), cs);
   int fastSeg = 0;
-  for (int l = 1; l < P.nlevels; ++l) {
+  // one or two frames through the band kernels: the resize chain as one launch
+  // (k_pyr_chain; ORB_PYR_CHAIN=0 keeps the per-level launches)
+  static const int chainEnv = getenv("ORB_PYR_CHAIN") ? atoi(getenv("ORB_PYR_CHAIN")) : 1;
+  const bool chain = chainEnv > 0 && useBands && B <= 2 && h->chainNb > 0 && !l0Side;
+  if (chain)
+    HIP_TRY(orb_k_pyr_chain(d_images, (long long)imgPitch, (int)stride, arena, ap, &P, rt,
+                            h->dChain.p, h->chainNb, h->chainBuf, B, cs));
+  for (int l = chain ? P.nlevels : 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
     const OrbLevelDesc& sd = P.lv[l - 1];
     const uint8_t* src = l == 1 ? d_images : arena + sd.arenaOff;

@@ -1,10 +1,11 @@
 #!/bin/bash
-# round-4 step 10: fixed-point resolve clocks (FP_DEBUG build); drop-in with the
+# round-4 step 10: the one-launch resize chain for single frames (extractor
+# parity, drop-in timing); fixed-point resolve clocks (FP_DEBUG build); drop-in with the
 # fixed-point resolve for 5,000-point maps; headline bench with the candidate
 # scan reading the staged grid from global (no LDS beside the extraction)
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p "$O"; cd "$R"
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_matcher.py -k resolve_schedules > "$O/s10_tests.log" 2>&1 || { tail -30 "$O/s10_tests.log"; exit 1; }
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_extractor.py tests/test_gpu_matcher.py tests/test_cpp_host.py > "$O/s10_tests.log" 2>&1 || { tail -30 "$O/s10_tests.log"; exit 1; }
 tail -1 "$O/s10_tests.log"
 for env in "" "ORB_PROJ_PPT=2"; do
   env $env timeout -k 10 150 python -u tools/r04/c5_stages.py 16 >> "$O/s10_c5.log" 2>&1 || { tail -20 "$O/s10_c5.log"; exit 1; }
