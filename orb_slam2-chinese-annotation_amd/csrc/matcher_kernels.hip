@@ -765,7 +765,8 @@ extern "C" hipError_t orb_k_fp_debug(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fp_dbg), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif
-template <int T>
+// PPT points per thread: a window of T * PPT points
+template <int T, int PPT = 1>
 __global__ __launch_bounds__(T) void k_proj_resolve_fp(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked,
@@ -809,12 +810,15 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
     in.e = *reinterpret_cast<const uint4*>(topk + mg * TOPK);
     in.nc = ncand[mg];
   };
-  In inA, inB;
-  load(inA, t);
+  constexpr int W = T * PPT;  // points per window
+  In inA[PPT], inB[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) load(inA[k], k * T + t);
 #if FP_AHEAD > 1
   asm volatile("" ::: "memory");  // A's loads all issue before B's (in-order counts)
   __builtin_amdgcn_sched_barrier(0);
-  load(inB, T + t);
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) load(inB[k], W + k * T + t);
 #endif
   __syncthreads();  // LDS reset before any window's claims
   int round = 0;  // global round counter: buffer parity and change flags
@@ -824,46 +828,65 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
 #endif
   // one window: its inputs leave `in` (loaded FP_AHEAD windows earlier) and
   // `in` is reloaded with the inputs FP_AHEAD windows on
-  auto window = [&](int start, In& in) {
-    const int m = start + t;
-    const uint32_t e[TOPK] = {in.e.x, in.e.y, in.e.z, in.e.w};
-    const int nc = m < M ? nc_count(in.nc) : -1;
-    const bool obs = m < M && nc_obs(in.nc);
-    int prev = -1;  // this point's claim in the previous round
-    int acc = -1;
+  auto window = [&](int start, In (&in)[PPT]) {
+    uint32_t e[PPT][TOPK];
+    int nc[PPT], prev[PPT], acc[PPT];
+    bool obs[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int m = start + k * T + t;
+      e[k][0] = in[k].e.x; e[k][1] = in[k].e.y; e[k][2] = in[k].e.z; e[k][3] = in[k].e.w;
+      nc[k] = m < M ? nc_count(in[k].nc) : -1;
+      obs[k] = m < M && nc_obs(in[k].nc);
+      prev[k] = -1;  // this point's claim in the previous round
+      acc[k] = -1;
+    }
     while (true) {
       const int* cur = claims + ((round + 1) & 1) * kpStride;
       int* nxt = claims + (round & 1) * kpStride;
-      acc = nc > 0 ? fp_choose(e, nc, m, cur, mps + pbase + m, mpDesc + (pbase + m) * 32, K, D,
-                               LK, UR, cs, ci, P)
-                   : -1;
-      const int claim = obs ? acc : -1;
-      if (claim >= 0) atomicMin(&nxt[claim], m);
-      if (__ballot(claim != prev) != 0ull && lane == 0) sChanged[round & 1] = 1;
+      bool changed = false;
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        const int m = start + k * T + t;
+        acc[k] = nc[k] > 0 ? fp_choose(e[k], nc[k], m, cur, mps + pbase + m, mpDesc + (pbase + m) * 32,
+                                       K, D, LK, UR, cs, ci, P)
+                           : -1;
+        const int claim = obs[k] ? acc[k] : -1;
+        if (claim >= 0) atomicMin(&nxt[claim], m);
+        changed |= claim != prev[k];
+      }
+      if (__ballot(changed) != 0ull && lane == 0) sChanged[round & 1] = 1;
       lds_barrier();
       const bool any = sChanged[round & 1] != 0;
       if (t == 0) sChanged[(round + 1) & 1] = 0;  // next written after the barrier below
-      // cur is not read any more: drop this point's claim of the previous
+      // cur is not read any more: drop these points' claims of the previous
       // round from it, it collects the next round's claims
-      if (prev >= 0) claims[((round + 1) & 1) * kpStride + prev] = NOCLAIM;
+#pragma unroll
+      for (int k = 0; k < PPT; ++k)
+        if (prev[k] >= 0) claims[((round + 1) & 1) * kpStride + prev[k]] = NOCLAIM;
       ++round;
       if (!any) break;  // (uniform) claims stable: the window is at its fixed point
-      prev = claim;
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) prev[k] = obs[k] ? acc[k] : -1;
       lds_barrier();
     }
     // commit: the final claims become committed locks in both buffers
-    if (acc >= 0) {
-      atomicMax(&skm[acc], m);
-      if (obs) {
-        claims[acc] = -1;
-        claims[kpStride + acc] = -1;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      if (acc[k] >= 0) {
+        atomicMax(&skm[acc[k]], start + k * T + t);
+        if (obs[k]) {
+          claims[acc[k]] = -1;
+          claims[kpStride + acc[k]] = -1;
+        }
+        ++matches;
       }
-      ++matches;
     }
     // reloaded only now, when this window's inputs are dead: the loads land in
     // the registers they came from (no copy, so no wait for them before the
     // window that uses them)
-    load(in, start + FP_AHEAD * T + t);
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) load(in[k], start + FP_AHEAD * W + k * T + t);
     lds_barrier();
 #if FP_DEBUG
     if (p == 0 && t == 0 && dbgW < 256) {
@@ -875,12 +898,12 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
 #endif
   };
 #if FP_AHEAD > 1
-  for (int start = 0; start < M; start += 2 * T) {
+  for (int start = 0; start < M; start += 2 * W) {
     window(start, inA);
-    window(start + T, inB);  // (past M: one round in which nothing changes)
+    window(start + W, inB);  // (past M: one round in which nothing changes)
   }
 #else
-  for (int start = 0; start < M; start += T) window(start, inA);
+  for (int start = 0; start < M; start += W) window(start, inA);
 #endif
   int32_t* km = kpMatch + (size_t)p * kpStride;
   for (int i = t; i < n; i += T) km[i] = skm[i];
@@ -930,6 +953,15 @@ __global__ __launch_bounds__(JAC_T) void k_proj_jacobi_init(int32_t* __restrict_
   if (i == 0) nmatches[p] = 0;
 }
 
+// PPT points per thread (m = (blockIdx.x * PPT + k) * JAC_T + t): C5's 16 x
+// 50,000 points in 784 workgroups, every one resident at once.  Every global
+// read a round needs (the problem's flags, the points' counts, top-K and
+// previous decisions) is issued before any of them is used, so a workgroup
+// pays one memory latency, then the claim reads, then the stores.
+#ifndef JAC_PPT
+#define JAC_PPT 4
+#endif
+template <int PPT>
 __global__ __launch_bounds__(JAC_T) void k_proj_jacobi(
     const orb_keypoint_t* __restrict__ keys, const uint8_t* __restrict__ desc,
     const float* __restrict__ uright, const uint8_t* __restrict__ locked,
@@ -941,24 +973,38 @@ __global__ __launch_bounds__(JAC_T) void k_proj_jacobi(
     long long stride, int r, int R) {
   __shared__ int sCnt[JAC_T / 64];
   const int p = blockIdx.y, t = threadIdx.x, lane = t & 63;
-  const int m = blockIdx.x * JAC_T + t, M = nmps[p];
+  const int M = nmps[p];
   int32_t* S = scr + (long long)p * stride;
-  // S[R] = the launch that committed the problem, + 1: an earlier launch's
-  // commit ends the problem; a commit by another workgroup of this launch
-  // does not (this workgroup's points are still to be committed)
-  const int done = S[R];
-  if (done != 0 && done != r + 1) return;
   int32_t* claims = S + jacobi_claims_off();
   int32_t* dec = claims + 3LL * kpStride;
   const size_t pbase = (size_t)p * mpStride;
-  if (r >= 1 && S[r - 1] == 0) {
+  // every load up front (indices clamped: no branch between them)
+  const int done = S[R];
+  const int prevChanged = r >= 1 ? S[r - 1] : 1;
+  int ncv[PPT], old[PPT];
+  uint4 q[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int m = (blockIdx.x * PPT + k) * JAC_T + t;
+    const size_t mg = pbase + (size_t)max(0, min(m, M - 1));
+    ncv[k] = ncand[mg];
+    q[k] = *reinterpret_cast<const uint4*>(topk + mg * TOPK);
+    old[k] = r > 0 ? dec[mg - pbase] : -1;
+  }
+  // S[R] = the launch that committed the problem, + 1: an earlier launch's
+  // commit ends the problem; a commit by another workgroup of this launch
+  // does not (this workgroup's points are still to be committed)
+  if (done != 0 && done != r + 1) return;
+  if (r >= 1 && prevChanged == 0) {
     // round r-1 changed no claim: its decisions are the sequential result
-    int acc = -1;
-    if (m < M) {
-      acc = dec[m];
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int m = (blockIdx.x * PPT + k) * JAC_T + t;
+      const int acc = m < M ? old[k] : -1;
       if (acc >= 0) atomicMax(&kpMatch[(size_t)p * kpStride + acc], m);
+      c += __popcll(__ballot(acc >= 0));
     }
-    const int c = __popcll(__ballot(acc >= 0));
     if (lane == 0) sCnt[t >> 6] = c;
     __syncthreads();
     if (t == 0) {
@@ -976,26 +1022,26 @@ __global__ __launch_bounds__(JAC_T) void k_proj_jacobi(
   int* clr = claims + (long long)((r + 1) % 3) * kpStride;
   for (int i = blockIdx.x * JAC_T + t; i < kpStride; i += gridDim.x * JAC_T) clr[i] = 0x7FFFFFFF;
   bool changed = false;
-  if (m < M) {
-    const int ncv = ncand[pbase + m];
-    const int nc = nc_count(ncv);
-    const bool hasObs = nc_obs(ncv);
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int m = (blockIdx.x * PPT + k) * JAC_T + t;
+    if (m >= M) continue;
+    const int nc = nc_count(ncv[k]);
+    const bool hasObs = nc_obs(ncv[k]);
     int acc = -1;
     if (nc > 0) {
-      const uint4 q = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
-      const uint32_t e[TOPK] = {q.x, q.y, q.z, q.w};
+      const uint32_t e[TOPK] = {q[k].x, q[k].y, q[k].z, q[k].w};
       acc = fp_choose(e, nc, m, cur, mps + pbase + m, mpDesc + (pbase + m) * 32,
                       keys + (size_t)p * kpStride, desc + (size_t)p * kpStride * 32,
                       locked ? locked + (size_t)p * kpStride : nullptr,
                       uright ? uright + (size_t)p * kpStride : nullptr,
                       cellStart + (size_t)p * (GRID_CELLS + 1), cellIdx + (size_t)p * kpStride, P);
     }
-    const int old = r > 0 ? dec[m] : -1;
     dec[m] = acc;
     const bool obs = acc >= 0 && hasObs;
     if (obs) atomicMin(&nxt[acc], m);
-    const int oldClaim = (old >= 0 && hasObs) ? old : -1;
-    changed = (obs ? acc : -1) != oldClaim;
+    const int oldClaim = (old[k] >= 0 && hasObs) ? old[k] : -1;
+    changed |= (obs ? acc : -1) != oldClaim;
   }
   if (__ballot(changed) != 0ull && lane == 0) S[r] = 1;
 }
@@ -1144,10 +1190,16 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 0;
   static const int jacR =
       getenv("ORB_JACOBI_ROUNDS") ? std::max(1, std::min(48, atoi(getenv("ORB_JACOBI_ROUNDS")))) : 4;
+  // window size (ORB_RESOLVE_FP_PPT 1, 2, 4: 1024 points, 1024 threads x 1;
+  // 2048 points, 1024 x 2; 4096 points, 512 threads x 8, whose registers a
+  // 1024-thread workgroup does not have)
+  static const int fpPpt = getenv("ORB_RESOLVE_FP_PPT") ? atoi(getenv("ORB_RESOLVE_FP_PPT")) : 1;
   const bool fp = mpStride >= fpMin && fpMode > 0 && ldsFp <= 160 * 1024 - 1024;
   if (fp && ldsFp > 64 * 1024) {
     const void* fn = fpMode == 256   ? (const void*)k_proj_resolve_fp<256>
                      : fpMode == 512 ? (const void*)k_proj_resolve_fp<512>
+                     : fpPpt == 2    ? (const void*)k_proj_resolve_fp<1024, 2>
+                     : fpPpt == 4    ? (const void*)k_proj_resolve_fp<512, 8>
                                      : (const void*)k_proj_resolve_fp<1024>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsFp);
     if (e != hipSuccess) return e;
@@ -1159,11 +1211,11 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
     const int initN = std::max(3 * kpStride, jacR + 1);
     hipLaunchKernelGGL(k_proj_jacobi_init, dim3((initN + JAC_T - 1) / JAC_T, nproblems), dim3(JAC_T),
                        0, s, jacScratch, js, kpStride, jacR, nkeys, kpMatch, nmatches);
-    const dim3 g((mpStride + JAC_T - 1) / JAC_T, nproblems);
+    const dim3 g((mpStride + JAC_T * JAC_PPT - 1) / (JAC_T * JAC_PPT), nproblems);
     for (int r = 0; r <= jacR; ++r)
-      hipLaunchKernelGGL(k_proj_jacobi, g, dim3(JAC_T), 0, s, keys, desc, uright, locked, kpStride,
-                         mps, mpDesc, nmps, mpStride, cellStart, cellIdx, P, topk, ncand, kpMatch,
-                         nmatches, jacScratch, js, r, jacR);
+      hipLaunchKernelGGL(k_proj_jacobi<JAC_PPT>, g, dim3(JAC_T), 0, s, keys, desc, uright, locked,
+                         kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, P, topk, ncand,
+                         kpMatch, nmatches, jacScratch, js, r, jacR);
     done = jacScratch + jacR;
     doneStride = js;
   }
@@ -1173,6 +1225,14 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
                        cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
   } else if (fp && fpMode == 512) {
     hipLaunchKernelGGL(k_proj_resolve_fp<512>, dim3(nproblems), dim3(512), ldsFp, s, keys, desc,
+                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
+                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
+  } else if (fp && fpPpt == 2) {
+    hipLaunchKernelGGL((k_proj_resolve_fp<1024, 2>), dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
+                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
+                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
+  } else if (fp && fpPpt == 4) {
+    hipLaunchKernelGGL((k_proj_resolve_fp<512, 8>), dim3(nproblems), dim3(512), ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
                        cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
   } else if (fp) {

@@ -177,7 +177,8 @@ def test_search_by_projection_batch_large_maps(gpu, oracle):
                                  {"ORB_RESOLVE_JACOBI": "1", "ORB_JACOBI_ROUNDS": "48"},
                                  {"ORB_RESOLVE_JACOBI": "0"},
                                  {"ORB_RESOLVE_FP": "256"}, {"ORB_RESOLVE_FP": "512"},
-                                 {"ORB_PROJ_DIRECT": "1"}, {"ORB_PROJ_PPT": "2"}])
+                                 {"ORB_PROJ_DIRECT": "1"}, {"ORB_PROJ_PPT": "2"},
+                                 {"ORB_RESOLVE_FP_PPT": "2"}, {"ORB_RESOLVE_FP_PPT": "4"}])
 def test_search_by_projection_resolve_schedules(gpu, oracle, tmp_path, env):
     """The large-map resolve under each schedule (read once per process, so in
     a child): Jacobi rounds (1, the default 4, up to 48) with the windowed

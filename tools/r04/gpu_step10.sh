@@ -7,7 +7,7 @@ set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p "$O"; cd "$R"
 timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_extractor.py tests/test_gpu_matcher.py tests/test_cpp_host.py > "$O/s10_tests.log" 2>&1 || { tail -30 "$O/s10_tests.log"; exit 1; }
 tail -1 "$O/s10_tests.log"
-for env in "" "ORB_PROJ_PPT=2"; do
+for env in "" "ORB_PROJ_PPT=2" "ORB_RESOLVE_FP_PPT=2" "ORB_RESOLVE_FP_PPT=4" "ORB_RESOLVE_JACOBI=1 ORB_JACOBI_ROUNDS=7" "ORB_RESOLVE_JACOBI=1 ORB_JACOBI_ROUNDS=10"; do
   env $env timeout -k 10 150 python -u tools/r04/c5_stages.py 16 >> "$O/s10_c5.log" 2>&1 || { tail -20 "$O/s10_c5.log"; exit 1; }
 done
 grep C5 "$O/s10_c5.log"
