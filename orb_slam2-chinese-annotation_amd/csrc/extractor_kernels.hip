@@ -232,27 +232,37 @@ __global__ __launch_bounds__(T) void k_pyr_chain(const uint8_t* __restrict__ img
                                                  const int32_t* __restrict__ rt,
                                                  const OrbChainBand* __restrict__ bands, int buf1Off) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  // the row taps of the rows a band computes at one level (host-checked <= 512 rows)
+  __shared__ int2 sY[ORB_CHAIN_MAX_ROWS];
   const int tid = threadIdx.x;
   const OrbChainBand& B = bands[blockIdx.x];
   const int img = blockIdx.y;
   uint8_t* A = arena + (long long)img * arenaPitch;
   {
     // level 0 rows [lo, hi) into buffer 0, dword by dword, realigned from any
-    // caller stride / base alignment (buffer loads past the image read 0)
+    // caller stride / base alignment (buffer loads past the image read 0);
+    // eight dwords' loads in flight per thread before their stores
     const int lo = B.lo[0], hi = B.hi[0], w = plan.lv[0].w, h = plan.lv[0].h;
-    const int nd = orb_chain_pitch(w) >> 2;
+    const int nd = orb_chain_pitch(w) >> 2, n = (hi - lo) * nd;
+    const float invNd = 1.0f / (float)nd;  // i / nd exactly (see below)
     const ImgRsrc im = img_rsrc(img0 + (long long)img * imgPitch, (uint32_t)((h - 1) * img0Stride + w));
     uint32_t* d32 = reinterpret_cast<uint32_t*>(sm);
-    const float invNd = 1.0f / (float)nd;  // (as below: exact quotients)
-    for (int i = tid; i < (hi - lo) * nd; i += T) {
-      const int r = (int)(((float)i + 0.5f) * invNd), c = i - r * nd;
-      const uint32_t o = (uint32_t)((lo + r) * img0Stride + 4 * c) + im.sh;
-      const uint32_t a = o & ~3u, sh = o & 3u;
-      const uint32_t w0 = buf_ld32(im.r, a), w1 = buf_ld32(im.r, a + 4);
-      d32[i] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    for (int i0 = 0; i0 < n; i0 += 8 * T) {
+      uint32_t w0[8], w1[8], sh[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = min(i0 + k * T + tid, n - 1);
+        const int r = (int)(((float)i + 0.5f) * invNd), c = i - r * nd;
+        const uint32_t o = (uint32_t)((lo + r) * img0Stride + 4 * c) + im.sh;
+        sh[k] = o & 3u;
+        w0[k] = buf_ld32(im.r, o & ~3u);
+        w1[k] = buf_ld32(im.r, (o & ~3u) + 4);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (i0 + k * T + tid < n) d32[i0 + k * T + tid] = __builtin_amdgcn_alignbyte(w1[k], w0[k], sh[k]);
     }
   }
-  __syncthreads();
   for (int l = 1; l < plan.nlevels; ++l) {
     const OrbLevelDesc& d = plan.lv[l];
     const int sw = plan.lv[l - 1].w, sh = plan.lv[l - 1].h;
@@ -260,37 +270,57 @@ __global__ __launch_bounds__(T) void k_pyr_chain(const uint8_t* __restrict__ img
     uint8_t* Dl = sm + (l & 1) * buf1Off;
     const int sp = orb_chain_pitch(sw), dp = orb_chain_pitch(d.w), slo = B.lo[l - 1];
     const int lo = B.lo[l], hi = B.hi[l], own = B.own[l], ownE = B.ownEnd[l];
-    const int ng = (d.w + 3) >> 2, n = (hi - lo) * ng;
-    // i / ng as ((i + 0.5) * (1 / ng)): the quotient sits >= 0.5 / ng from an
-    // integer, the float error (< 2e-7 relative, i < 2^17) far below that
-    const float invNg = 1.0f / (float)ng;
+    const int nr = hi - lo, ng = (d.w + 3) >> 2;
     const int32_t* xo = rt + d.rtabX;
     const int32_t* al = xo + d.w;
     const int32_t* yo = rt + d.rtabY;
     const int32_t* be = yo + d.h;
-    for (int i = tid; i < n; i += T) {
-      const int r = (int)(((float)i + 0.5f) * invNg), c = i - r * ng;
-      const int y = lo + r, x = 4 * c;
-      const int yy = yo[y];
-      const uint32_t bb = (uint32_t)be[y], b0 = bb & 0xFFFFu, b1 = bb >> 16;
-      const uint8_t* R0 = S + (min(max(yy, 0), sh - 1) - slo) * sp;
-      const uint8_t* R1 = S + (min(max(yy + 1, 0), sh - 1) - slo) * sp;
-      uint32_t packed = 0;
+    __syncthreads();  // the previous level's rows written, its row taps read
+    // this level's row taps, as LDS row offsets into the source buffer
+    for (int r = tid; r < nr; r += T) {
+      const int yy = yo[lo + r];
+      sY[r] = make_int2((min(max(yy, 0), sh - 1) - slo) * sp, be[lo + r]);
+      // (second tap row: + sp unless clamped at the last source row)
+      if (min(max(yy + 1, 0), sh - 1) == min(max(yy, 0), sh - 1)) sY[r].x |= 1 << 30;
+    }
+    __syncthreads();  // this level's taps in LDS
+    // a thread keeps its 4 columns' taps for the whole level and walks rows
+    const int tc = min(ng, T), tr = T / tc;
+    for (int c0 = 0; c0 < ng; c0 += tc) {
+      const int c = c0 + tid % tc, r0 = tid / tc;
+      if (c >= ng || r0 >= tr) continue;
+      const int x = 4 * c;
+      int sx[4], sx1[4];
+      uint32_t a0[4], a1[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int dx = min(x + j, d.w - 1);
-        const int sx = xo[dx], sx1 = min(sx + 1, sw - 1);  // (weight 0 where sx + 1 >= sw)
-        const uint32_t aa = (uint32_t)al[dx], a0 = aa & 0xFFFFu, a1 = aa >> 16;
-        const uint32_t h0 = a0 * R0[sx] + a1 * R0[sx1], h1 = a0 * R1[sx] + a1 * R1[sx1];
-        int v = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
-        __asm__ volatile("" : "+v"(v));  // see k_pyr_resize: keep the byte pack opaque
-        packed |= (uint32_t)v << (8 * j);
+        sx[j] = xo[dx];
+        sx1[j] = min(sx[j] + 1, sw - 1);  // (weight 0 where sx + 1 >= sw)
+        const uint32_t aa = (uint32_t)al[dx];
+        a0[j] = aa & 0xFFFFu;
+        a1[j] = aa >> 16;
       }
-      *reinterpret_cast<uint32_t*>(Dl + r * dp + x) = packed;
-      if (y >= own && y < ownE)
-        *reinterpret_cast<uint32_t*>(A + d.arenaOff + (long long)y * d.pitch + x) = packed;
+      for (int r = r0; r < nr; r += tr) {
+        const int2 ty = sY[r];
+        const uint8_t* R0 = S + (ty.x & ~(1 << 30));
+        const uint8_t* R1 = R0 + ((ty.x >> 30) ? 0 : sp);
+        const uint32_t b0 = (uint32_t)ty.y & 0xFFFFu, b1 = (uint32_t)ty.y >> 16;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t h0 = a0[j] * R0[sx[j]] + a1[j] * R0[sx1[j]];
+          const uint32_t h1 = a0[j] * R1[sx[j]] + a1[j] * R1[sx1[j]];
+          int v = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
+          __asm__ volatile("" : "+v"(v));  // see k_pyr_resize: keep the byte pack opaque
+          packed |= (uint32_t)v << (8 * j);
+        }
+        *reinterpret_cast<uint32_t*>(Dl + r * dp + x) = packed;
+        const int y = lo + r;
+        if (y >= own && y < ownE)
+          *reinterpret_cast<uint32_t*>(A + d.arenaOff + (long long)y * d.pitch + x) = packed;
+      }
     }
-    __syncthreads();
   }
 }
 
@@ -994,8 +1024,20 @@ __device__ __forceinline__ int fast_score_u8(const uint8_t* tile, int coff, int 
 // PT > 0: the launch's LDS row pitch as a compile-time constant (every cell's
 // rows at pitch PT >= fc_pitch(C)), so every ring / neighbour / row read is an
 // immediate offset from one address; PT = 0: per-cell fc_pitch(C)
+#ifndef FC_WPE
+// waves per SIMD the register allocation must allow: 7, so that the SGPRs
+// (98 without it) do not cap the kernel below its LDS limit of 27-28 waves per
+// CU (SGPR budget 800 per SIMD in granules of 16, +16 per wave: 98 -> 6 waves,
+// <= 96 -> 7; MI355X_MICROARCH "Residency")
+#define FC_WPE 7
+#endif
 template <int PT>
-__global__ __launch_bounds__(64 * FC_WAVES) void k_fast_cells(
+#if FC_WPE > 0
+__global__ __launch_bounds__(64 * FC_WAVES) __attribute__((amdgpu_waves_per_eu(FC_WPE)))
+#else
+__global__ __launch_bounds__(64 * FC_WAVES)
+#endif
+void k_fast_cells(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
     const OrbCellDesc* __restrict__ cells, uint32_t* __restrict__ cellKeys,
@@ -2954,6 +2996,7 @@ int orb_pyr_chain_plan(const OrbPlanDesc* plan, const int32_t* rtab, size_t ldsM
       for (int l = 0; l < L; ++l) {
         const int bytes = (B.hi[l] - B.lo[l]) * orb_chain_pitch(plan->lv[l].w);
         need[l & 1] = std::max(need[l & 1], bytes);
+        if (B.hi[l] - B.lo[l] > ORB_CHAIN_MAX_ROWS) ok = false;
       }
     }
     const int b0 = (need[0] + 15) & ~15, b1 = (need[1] + 15) & ~15;

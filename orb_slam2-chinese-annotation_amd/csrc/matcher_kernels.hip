@@ -368,11 +368,26 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
     gCS = cs;
     gKp = stagedGrid + (size_t)p * kpStride;
   } else if (staged) {
-    for (int i = tid; i <= GRID_CELLS; i += WG) sCS[i] = cs[i];
+    // (batches of loads issued before their stores: a load-store loop waits
+    // one memory latency per iteration)
     const int nInGrid = cs[GRID_CELLS];
+    constexpr int CSB = (GRID_CELLS + 1 + WG - 1) / WG;
+    int csv[CSB];
+#pragma unroll
+    for (int k = 0; k < CSB; ++k) csv[k] = cs[min(tid + k * WG, GRID_CELLS)];
+#pragma unroll
+    for (int k = 0; k < CSB; ++k)
+      if (tid + k * WG <= GRID_CELLS) sCS[tid + k * WG] = csv[k];
     if (stagedGrid) {
       const uint4* sg = stagedGrid + (size_t)p * kpStride;
-      for (int j = tid; j < nInGrid; j += WG) sKp[j] = sg[j];
+      for (int j0 = 0; j0 < nInGrid; j0 += 4 * WG) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = sg[min(j0 + k * WG + tid, nInGrid - 1)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (j0 + k * WG + tid < nInGrid) sKp[j0 + k * WG + tid] = v[k];
+      }
     } else {
     for (int j = tid; j < nInGrid; j += WG) {
       const int idx = ci[j];
@@ -714,9 +729,15 @@ __device__ __forceinline__ int fp_choose(const uint32_t (&e)[TOPK], int nc, int 
   int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
   int found = 0;
   const int avail = nc < TOPK ? nc : TOPK;
+  // every claim read issued before any is used (unused slots read entry 0's
+  // keypoint again): one memory round trip, not one per candidate -- the
+  // claims are LDS in k_proj_resolve_fp but global memory in k_proj_jacobi
+  int cv[TOPK];
+#pragma unroll
+  for (int j = 0; j < TOPK; ++j) cv[j] = cur[cand_idx(j < avail ? e[j] : e[0])];
   bool taken[TOPK];
 #pragma unroll
-  for (int j = 0; j < TOPK; ++j) taken[j] = j < avail ? cur[cand_idx(e[j])] < m : true;
+  for (int j = 0; j < TOPK; ++j) taken[j] = j < avail ? cv[j] < m : true;
 #pragma unroll
   for (int j = 0; j < TOPK; ++j) {
     const bool use = found < 2 && !taken[j];

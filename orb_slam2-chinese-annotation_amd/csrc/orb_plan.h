@@ -81,3 +81,4 @@ struct OrbChainBand {
   int16_t lo[ORB_MAX_LEVELS], hi[ORB_MAX_LEVELS], own[ORB_MAX_LEVELS], ownEnd[ORB_MAX_LEVELS];
 };
 __host__ __device__ inline int orb_chain_pitch(int w) { return (w + 3) & ~3; }
+#define ORB_CHAIN_MAX_ROWS 512  // rows a band computes at one level (row-tap table in LDS)

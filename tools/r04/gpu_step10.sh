@@ -19,7 +19,7 @@ for env in "" "ORB_PROJ_DIRECT=1" "" "ORB_PROJ_DIRECT=1"; do
   env $env timeout -k 10 300 python bench.py --no-cpu --no-dropin --no-secondary --host-frames 0 --steps 40 > "$O/s10_b.json" 2> "$O/s10_b.err" || { tail -20 "$O/s10_b.err"; exit 1; }
   python3 -c "import json; r=json.loads(open('$O/s10_b.json').read().strip().splitlines()[-1]); k=r['kernels']; print('[$env]', round(r['value']), {n: (v.get('ms_per_call_isolated'), v.get('ms_per_call_pipelined')) for n, v in k.items() if 'proj' in n})"
 done
-ATTR_NOPMC=1 bash tools/r04/attr.sh v10 k_fast_cells mw5 c192 cpw8 > "$O/s10_var.log" 2>&1 || { tail -20 "$O/s10_var.log"; exit 1; }
+ATTR_NOPMC=1 bash tools/r04/attr.sh v10 k_fast_cells wpe0 wpe8 cpw8 > "$O/s10_var.log" 2>&1 || { tail -20 "$O/s10_var.log"; exit 1; }
 cat "$O/s10_var.log"
 cd /tmp && export TMPDIR=/tmp
 ORB_RESOLVE_JACOBI=1 ORB_JACOBI_ROUNDS=8 timeout -k 10 150 rocprofv3 --kernel-trace --stats -d "$O/s10_jac" -o run --output-format csv -- python3 "$R/tools/r04/c5_stages.py" 16 > "$O/s10_jac.log" 2>&1 || { tail -20 "$O/s10_jac.log"; exit 1; }
