@@ -1215,7 +1215,15 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   // 2048 points, 1024 x 2; 4096 points, 512 threads x 8, whose registers a
   // 1024-thread workgroup does not have)
   static const int fpPpt = getenv("ORB_RESOLVE_FP_PPT") ? atoi(getenv("ORB_RESOLVE_FP_PPT")) : 1;
-  const bool fp = mpStride >= fpMin && fpMode > 0 && ldsFp <= 160 * 1024 - 1024;
+  // a few problems per call (the drop-in's one frame against its local map)
+  // take the fixed-point kernel at any map size: one 1024-point window per
+  // round trip instead of 256-point prefix windows (SearchByProjection of one
+  // 5,000-point map through the drop-in 0.197 vs 0.239 ms,
+  // profiles/r04_step10.txt); batches keep the one-wave prefix kernel beside
+  // the next launch's extraction (ORB_RESOLVE_FP_FEW = the problem count)
+  static const int fpFew = getenv("ORB_RESOLVE_FP_FEW") ? atoi(getenv("ORB_RESOLVE_FP_FEW")) : 8;
+  const bool fp = (mpStride >= fpMin || nproblems <= fpFew) && fpMode > 0 &&
+                  ldsFp <= 160 * 1024 - 1024;
   if (fp && ldsFp > 64 * 1024) {
     const void* fn = fpMode == 256   ? (const void*)k_proj_resolve_fp<256>
                      : fpMode == 512 ? (const void*)k_proj_resolve_fp<512>
@@ -1227,7 +1235,8 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   }
   const int32_t* done = nullptr;
   long long doneStride = 0;
-  if (fp && jacOn > 0 && jacScratch) {
+  // (the scratch is sized by orb_k_proj_jacobi_bytes: large maps only)
+  if (fp && jacOn > 0 && jacScratch && mpStride >= fpMin) {
     const long long js = jacobi_stride(kpStride, mpStride);
     const int initN = std::max(3 * kpStride, jacR + 1);
     hipLaunchKernelGGL(k_proj_jacobi_init, dim3((initN + JAC_T - 1) / JAC_T, nproblems), dim3(JAC_T),

@@ -836,9 +836,12 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   }
   PROF_REC(ev, pf.b(ev, 0), cs);
   int fastSeg = 0;
-  // one or two frames through the band kernels: the resize chain as one launch
-  // (k_pyr_chain; ORB_PYR_CHAIN=0 keeps the per-level launches)
-  static const int chainEnv = getenv("ORB_PYR_CHAIN") ? atoi(getenv("ORB_PYR_CHAIN")) : 1;
+  // ORB_PYR_CHAIN=1: one or two frames build the pyramid in one launch
+  // (k_pyr_chain).  Off: measured slower than the seven per-level launches at
+  // one 1241x376 frame (resize stage 0.0386 vs 0.0269 ms, extraction wall
+  // 0.1445 vs 0.1319 ms, profiles/r04_step11.txt): 16 bands each walking all
+  // levels serially do more work per workgroup than a launch costs
+  static const int chainEnv = getenv("ORB_PYR_CHAIN") ? atoi(getenv("ORB_PYR_CHAIN")) : 0;
   const bool chain = chainEnv > 0 && useBands && B <= 2 && h->chainNb > 0 && !l0Side;
   if (chain)
     HIP_TRY(orb_k_pyr_chain(d_images, (long long)imgPitch, (int)stride, arena, ap, &P, rt,

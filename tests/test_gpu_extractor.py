@@ -463,3 +463,62 @@ def test_host_pyramid_mirror(gpu, oracle):
             assert np.array_equal(ext.host_pyramid(l), ref[l]), (f, l)
     with pytest.raises(gpu.OrbError):
         ext.host_pyramid(8)
+
+
+def test_pyramid_chain_option_bit_exact(gpu, oracle, tmp_path):
+    """ORB_PYR_CHAIN=1 (read once per process, so in a child): the one-launch
+    resize chain of one- and two-frame calls (k_pyr_chain, off by default)
+    gives the oracle's pyramid, keypoints and descriptors for the yaml
+    defaults, a deep pyramid, the wide-resize variant and a two-image batch."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    cases = [(1241, 376, 1000, 1.2, 8), (1241, 376, 1500, 1.2, 12), (1920, 1080, 2000, 1.5, 6)]
+    for i, (w, h, nf, sf, nl) in enumerate(cases):
+        np.save(tmp_path / f"img{i}.npy", gpu.synth_image(11 + i, 0, w, h))
+    np.save(tmp_path / "pair.npy", np.stack([gpu.synth_image(20, f, 640, 480) for f in range(2)]))
+    code = f"""
+import sys, numpy as np, torch
+sys.path.insert(0, {str(root)!r}); sys.path.insert(0, {str(root / 'tests')!r})
+from conftest import load_pkg
+orb = load_pkg()
+T = {str(tmp_path)!r}
+for i, (w, h, nf, sf, nl) in enumerate({cases!r}):
+    ext = orb.ORBextractor(nf, sf, nl, 20, 7)
+    k, d = ext(np.load(T + f'/img{{i}}.npy'))
+    np.save(T + f'/k{{i}}.npy', k); np.save(T + f'/d{{i}}.npy', d)
+    for l, lv in enumerate(ext.mvImagePyramid):
+        np.save(T + f'/p{{i}}_{{l}}.npy', np.ascontiguousarray(lv))
+pair = np.load(T + '/pair.npy')
+ext = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+cap = ext.capacity(640, 480)
+d_img = torch.from_numpy(pair).cuda()
+kk = torch.zeros((2, cap, 7), dtype=torch.int32, device='cuda')
+dd = torch.zeros((2, cap, 32), dtype=torch.uint8, device='cuda')
+nn = torch.zeros(2, dtype=torch.int32, device='cuda')
+ext.extract_batch(d_img.data_ptr(), 2, 640, 480, 640, 640 * 480, kk.data_ptr(), dd.data_ptr(), cap,
+                  nn.data_ptr())
+torch.cuda.synchronize()
+np.save(T + '/bk.npy', kk.cpu().numpy()); np.save(T + '/bd.npy', dd.cpu().numpy())
+np.save(T + '/bn.npy', nn.cpu().numpy())
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, ORB_PYR_CHAIN="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    for i, (w, h, nf, sf, nl) in enumerate(cases):
+        img = np.load(tmp_path / f"img{i}.npy")
+        k_ref, d_ref, _ = oracle.extract(img, nf, sf, nl, 20, 7)
+        assert np.load(tmp_path / f"k{i}.npy").tobytes() == k_ref.tobytes(), i
+        assert np.load(tmp_path / f"d{i}.npy").tobytes() == d_ref.tobytes(), i
+        ref_pyr = oracle.pyramid(img, sf, nl)
+        for l in range(nl):
+            assert np.load(tmp_path / f"p{i}_{l}.npy").tobytes() == ref_pyr[l].tobytes(), (i, l)
+    pair = np.load(tmp_path / "pair.npy")
+    bk, bd, bn = np.load(tmp_path / "bk.npy"), np.load(tmp_path / "bd.npy"), np.load(tmp_path / "bn.npy")
+    for f in range(2):
+        k_ref, d_ref, _ = oracle.extract(pair[f], 1000, 1.2, 8, 20, 7)
+        assert int(bn[f]) == len(k_ref)
+        assert np.ascontiguousarray(bk[f, :bn[f]]).tobytes() == k_ref.tobytes(), f
+        assert bd[f, :bn[f]].tobytes() == d_ref.tobytes(), f
