@@ -404,7 +404,8 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
     return res, dict(il=il, ir=ir, set0=sets[0], bf=bf, fx=fx)
 
 
-def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warmup=3):
+def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warmup=3,
+                  serial_calls=0):
     """extract + SearchByProjection(F, localMap) against M-point synthetic maps
     (orb_synth_local_map(seed + i, ...)), B problems (frames 0..B-1 of `seed`)
     per launch, pipelined as `pipelined`; also the matcher alone, serial on
@@ -453,12 +454,27 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
         raise RuntimeError("extract + match: an extraction reported failure (negative count)")
     with torch.cuda.stream(s0):
         msec = timed_loop(lambda: match(0, s0.cuda_stream), steps, warmup, torch)
+    serial = None
+    if serial_calls:
+        # latency shape: one call (extraction + match of the B frames) at a time,
+        # each waited for before the next is issued; median over the calls
+        ts = []
+        for i in range(serial_calls + 5):
+            t0 = time.perf_counter()
+            extract(0, s0.cuda_stream)
+            match(0, s0.cuda_stream)
+            s0.synchronize()
+            if i >= 5:
+                ts.append(time.perf_counter() - t0)
+        serial = float(np.median(ts))
     n_kp = float(sets[0]["n"].float().mean().item())
     b_lm = 60 * M + 48 * n_kp + 24576  # SURVEY §8(d) B_lm
     res = {"value": B / sec, "unit": "problems/s", "problems_per_step": B, "ms_per_step": sec * 1e3,
            "match_only_problems_per_s": B / msec, "match_only_alg_GBps": b_lm * B / msec / 1e9,
            "match_only_frac_of_8TBps": b_lm * B / msec / 8e12, "mean_keypoints": n_kp,
            "mean_matches": float(sets[0]["nm"].float().mean().item()),
+           **({"serial_ms_per_call": serial * 1e3, "serial_frames_per_s": B / serial,
+               "serial_calls": serial_calls} if serial else {}),
            "workload": f"{W}x{H}, {NF} feat, extraction + SearchByProjection vs {M:,} map points "
                        f"(frames 0..{B - 1} of seed {seed}), {B} problems per launch, pipelined "
                        "over two extraction lanes and a match stream"}
@@ -475,7 +491,19 @@ def secondary_configs(orb, torch, args, dev, threads):
     c3, _ = c3_workload(orb, torch, dev, threads, steps=40, warmup=5)
     c5, _ = proj_workload(orb, torch, dev, threads, 1920, 1080, 4000, 50000, 16, C5_SEED,
                           steps=200, warmup=10)
-    return {"C3_stereo_pairs_per_s": c3, "C5_problems_per_s": c5}
+    # C4's latency shape (1 frame per GPU per step, batches of 8 over
+    # 8 GPUs): one device-resident 1241x376 frame per call, extraction +
+    # SearchByProjection vs 5,000 map points, each call waited for; and the
+    # 8-frame batch on one GPU the same way
+    lat = {}
+    for b in (1, 8):
+        r, _ = proj_workload(orb, torch, dev, threads, 1241, 376, 1000, 5000, b, 0x4B495454,
+                             steps=50, warmup=5, serial_calls=200)
+        lat[f"frames_per_call_{b}"] = {k: r[k] for k in ("serial_ms_per_call", "serial_frames_per_s",
+                                                          "serial_calls", "mean_keypoints")}
+    lat["workload"] = ("1241x376, 1000 feat, extraction + SearchByProjection vs 5,000 map points, "
+                       "device-resident, one call at a time (synchronized), median of 200 calls")
+    return {"C3_stereo_pairs_per_s": c3, "C5_problems_per_s": c5, "C4_latency": lat}
 
 
 def host_input_leg(orb, torch, ext, matcher, imgs, args, dev, sets, d_mps, d_mpd, d_lock,
