@@ -262,6 +262,29 @@ orb_status_t orb_matcher_profile(orb_matcher_t* m, int enable);
 orb_status_t orb_matcher_profile_read(orb_matcher_t* m, int stage, double* total_ms,
                                       int* launches, const char** name);
 
+/* Resolve schedule of SearchByProjection(F, vpMapPoints)'s first-come claims
+ * (src/ORBmatcher.cc:90-93,127: a keypoint claimed by an earlier MapPoint of
+ * the same call is skipped).  Every schedule returns the reference's result;
+ * they differ in how the ordered resolve is spread over the chip (DESIGN.md
+ * §4.2).  AUTO (the default) picks by problem count and map size; JACOBI runs
+ * `jacobi_rounds` (1-48) chip-wide rounds first, then the fixed-point windows
+ * for any problem not yet settled.  Schedules that need more LDS than the
+ * frame's keypoint count allows fall back to the prefix windows. */
+#define ORB_RESOLVE_AUTO 0
+#define ORB_RESOLVE_PREFIX 1      /* speculative windows, longest conflict-free prefix kept */
+#define ORB_RESOLVE_FIXED_POINT 2 /* 1024-point windows iterated to their fixed point */
+#define ORB_RESOLVE_JACOBI 3      /* chip-wide rounds + fixed-point windows */
+orb_status_t orb_matcher_set_resolve(orb_matcher_t* m, int schedule, int jacobi_rounds);
+/* The resolve kernel the local-map matcher launches for a call of n_problems
+ * problems at these strides under the handle's schedule. */
+#define ORB_RESOLVE_KERNEL_PREFIX_W1 1   /* k_proj_resolve<1>: one wave per problem */
+#define ORB_RESOLVE_KERNEL_PREFIX_W4 4   /* k_proj_resolve<4> */
+#define ORB_RESOLVE_KERNEL_PREFIX_W8 8   /* k_proj_resolve<8> */
+#define ORB_RESOLVE_KERNEL_FIXED_POINT 16 /* k_proj_resolve_fp<1024> */
+#define ORB_RESOLVE_KERNEL_JACOBI 32     /* k_proj_jacobi rounds + k_proj_resolve_fp */
+orb_status_t orb_matcher_resolve_kernel(orb_matcher_t* m, int n_problems, int kp_stride,
+                                        int mp_stride, int* kernel);
+
 /* dist[i] = DescriptorDistance(a + 32 i, b + 32 i), device pointers. */
 orb_status_t orb_hamming_batch(orb_matcher_t* m, const uint8_t* d_a, const uint8_t* d_b,
                                int n, int32_t* d_dist, void* stream);

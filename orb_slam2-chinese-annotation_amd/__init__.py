@@ -117,6 +117,8 @@ def lib() -> ctypes.CDLL:
         "orb_matcher_destroy": (None, [vp]),
         "orb_matcher_stream": (vp, [vp]),
         "orb_matcher_profile": (i32, [vp, i32]),
+        "orb_matcher_set_resolve": (i32, [vp, i32, i32]),
+        "orb_matcher_resolve_kernel": (i32, [vp, i32, i32, i32, vp]),
         "orb_matcher_profile_read": (i32, [vp, i32, vp, vp, vp]),
         "orb_hamming_batch": (i32, [vp, vp, vp, i32, vp, vp]),
         "orb_match_projection_local": (i32, [vp, vp, vp, i32, vp, vp, f32, f32, vp, vp]),
@@ -445,6 +447,22 @@ class ORBmatcher:
 
     def stream(self) -> int:
         return lib().orb_matcher_stream(self._h) or 0
+
+    # resolve schedules of SearchByProjection(F, localMap) (orb_abi.h)
+    RESOLVE_AUTO, RESOLVE_PREFIX, RESOLVE_FIXED_POINT, RESOLVE_JACOBI = 0, 1, 2, 3
+    RESOLVE_KERNELS = {1: "k_proj_resolve<1>", 4: "k_proj_resolve<4>", 8: "k_proj_resolve<8>",
+                       16: "k_proj_resolve_fp<1024>", 32: "k_proj_jacobi+k_proj_resolve_fp"}
+
+    def set_resolve(self, schedule: int, jacobi_rounds: int = 6):
+        """Resolve schedule of the local-map matcher (every schedule is exact)."""
+        _check(lib().orb_matcher_set_resolve(self._h, schedule, jacobi_rounds), "set_resolve")
+
+    def resolve_kernel(self, n_problems: int, kp_stride: int, mp_stride: int) -> str:
+        """Name of the resolve kernel a call of this shape launches."""
+        k = ctypes.c_int(0)
+        _check(lib().orb_matcher_resolve_kernel(self._h, n_problems, kp_stride, mp_stride,
+                                                ctypes.byref(k)), "resolve_kernel")
+        return self.RESOLVE_KERNELS[k.value]
 
     def search_by_projection_batch(self, n_problems, d_keys, d_desc, d_nkeys, d_locked, kp_stride,
                                    d_mps, d_mp_desc, d_nmps, mp_stride, width, height,

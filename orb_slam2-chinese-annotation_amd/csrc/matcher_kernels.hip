@@ -1076,12 +1076,9 @@ hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out
   return hipGetLastError();
 }
 
-static bool grid4(int kpStride) {
-  static const int env = getenv("ORB_GRID_WAVES") ? atoi(getenv("ORB_GRID_WAVES")) : 0;
-  if (env == 1) return false;
-  if (env == 4) return kpStride < 65536;
-  return kpStride > GB4_MIN_SLOTS && kpStride < 65536;
-}
+// k_grid_build4 (four waves) for frames with more keypoint slots than
+// GB4_MIN_SLOTS, the one-wave k_grid_build below that
+static bool grid4(int kpStride) { return kpStride > GB4_MIN_SLOTS && kpStride < 65536; }
 
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
@@ -1114,6 +1111,20 @@ hipError_t orb_k_grid_build_staged(const orb_keypoint_t* keys, const int32_t* nk
 
 int orb_k_grid_stage_max(void) { return GB_LDS_KEYS; }
 
+// Compile-time variants of the candidate scan (tools/build_variant.sh; the
+// default build instantiates only the defaults):
+//   PROJ_DIRECT 1     scan the staged grid in global memory (no LDS copy)
+//   PROJ_PPT_LARGE 2  two map points per thread for large maps
+#ifndef PROJ_DIRECT
+#define PROJ_DIRECT 0
+#endif
+#ifndef PROJ_PPT_LARGE
+#define PROJ_PPT_LARGE 1
+#endif
+// large problems (C5: 4,000 keypoints staged = 64 KB of LDS per workgroup,
+// 50,000 points) take 1024-point workgroups: half the staging per point
+#define PROJ_LARGE_MAP 20000
+
 hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc,
                                  const float* uright, const uint8_t* locked, int kpStride,
                                  const int32_t* nkeys, const orb_mp_track_t* mps,
@@ -1126,60 +1137,87 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
   if (mpMax <= 0 || nproblems <= 0) return hipSuccess;
   // dynamic LDS: the staged keypoints of a frame, sized to the key capacity
   const int stageCap = std::min(kpStride, PROJ_STAGE);
-  const size_t lds = (size_t)stageCap * sizeof(uint4);
-  // Large problems (C5: 4,000 keypoints staged = 76 KB of LDS per workgroup,
-  // 50,000 points) take 1024-point workgroups: half the staging per point
-  // (ORB_PROJ_WG_LARGE=512 keeps the batch shape)
-  static const int wgLarge =
-      getenv("ORB_PROJ_WG_LARGE") ? atoi(getenv("ORB_PROJ_WG_LARGE")) : 1024;
-  const bool large = wgLarge == 1024 && stageCap > 2048 && mpMax >= 20000;
-  // points per thread for large maps: 2 puts C5's 16 x 50,000 points in 400
-  // workgroups, one pass over the chip's 512 two-per-CU slots (1: 784, a
-  // second, half-empty pass)
-  static const int pptLarge = getenv("ORB_PROJ_PPT") ? atoi(getenv("ORB_PROJ_PPT")) : 1;
-  // ORB_PROJ_DIRECT=1: scan the staged grid in global memory (no LDS copy)
-  static const int direct = getenv("ORB_PROJ_DIRECT") ? atoi(getenv("ORB_PROJ_DIRECT")) : 0;
-  if (large && pptLarge == 2 && !(direct && stagedGrid)) {
-    const void* f2 = (const void*)k_proj_candidates<1024, false, 2>;
-    if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {
-      hipError_t e = hipFuncSetAttribute(f2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL((k_proj_candidates<1024, false, 2>), dim3((mpMax + 2047) / 2048, nproblems),
-                       dim3(1024), lds, s, keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc,
-                       nmps, mpStride, cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P,
-                       topk, ncand);
-    return hipGetLastError();
+  const bool large = stageCap > 2048 && mpMax >= PROJ_LARGE_MAP;
+  const bool direct = PROJ_DIRECT && stagedGrid;
+  const size_t lds = direct ? 0 : (size_t)stageCap * sizeof(uint4);
+  const void* fn;
+  dim3 grid;
+  int wg;
+  if (large) {
+    constexpr int ppt = PROJ_DIRECT ? 1 : PROJ_PPT_LARGE;
+    fn = direct ? (const void*)k_proj_candidates<1024, true> : (const void*)k_proj_candidates<1024, false, ppt>;
+    grid = dim3((mpMax + 1024 * (direct ? 1 : ppt) - 1) / (1024 * (direct ? 1 : ppt)), nproblems);
+    wg = 1024;
+  } else {
+    fn = direct ? (const void*)k_proj_candidates<PROJ_WG, true> : (const void*)k_proj_candidates<PROJ_WG>;
+    grid = dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems);
+    wg = PROJ_WG;
   }
-  if (direct && stagedGrid) {
-    if (large)
-      hipLaunchKernelGGL((k_proj_candidates<1024, true>), dim3((mpMax + 1023) / 1024, nproblems),
-                         dim3(1024), 0, s, keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc,
-                         nmps, mpStride, cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P,
-                         topk, ncand);
-    else
-      hipLaunchKernelGGL((k_proj_candidates<PROJ_WG, true>),
-                         dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems), dim3(PROJ_WG), 0, s, keys,
-                         desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart,
-                         cellIdx, (const uint4*)stagedGrid, stageCap, P, topk, ncand);
-    return hipGetLastError();
-  }
-  const void* fn = large ? (const void*)k_proj_candidates<1024> : (const void*)k_proj_candidates<PROJ_WG>;
   if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {  // with the static grid table
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (large)
-    hipLaunchKernelGGL(k_proj_candidates<1024>, dim3((mpMax + 1023) / 1024, nproblems), dim3(1024),
-                       lds, s, keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps,
-                       mpStride, cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P, topk,
-                       ncand);
+  const uint4* sg = (const uint4*)stagedGrid;
+  if (large && direct)
+    hipLaunchKernelGGL((k_proj_candidates<1024, true>), grid, dim3(wg), lds, s, keys, desc, uright,
+                       locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, sg,
+                       stageCap, P, topk, ncand);
+  else if (large)
+    hipLaunchKernelGGL((k_proj_candidates<1024, false, PROJ_PPT_LARGE>), grid, dim3(wg), lds, s, keys,
+                       desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart,
+                       cellIdx, sg, stageCap, P, topk, ncand);
+  else if (direct)
+    hipLaunchKernelGGL((k_proj_candidates<PROJ_WG, true>), grid, dim3(wg), lds, s, keys, desc, uright,
+                       locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, sg,
+                       stageCap, P, topk, ncand);
   else
-    hipLaunchKernelGGL(k_proj_candidates<PROJ_WG>, dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems),
-                       dim3(PROJ_WG), lds, s,
-                       keys, desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride,
-                       cellStart, cellIdx, (const uint4*)stagedGrid, stageCap, P, topk, ncand);
+    hipLaunchKernelGGL(k_proj_candidates<PROJ_WG>, grid, dim3(wg), lds, s, keys, desc, uright, locked,
+                       kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, sg, stageCap,
+                       P, topk, ncand);
   return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- resolve
+// SearchByProjection's first-come claims (src/ORBmatcher.cc:90-93,127) are
+// resolved in map-point order by one of three exact schedules (DESIGN.md
+// §4.2); the caller's schedule (orb_matcher_set_resolve) picks among them and
+// ORB_RESOLVE_AUTO picks by shape:
+//  * k_proj_resolve<NW> (prefix windows, NW waves per problem): batches of
+//    small local maps.  >= 128 problems (the headline's 1024-frame launches,
+//    run beside the next launch's extraction) take one wave per problem: the
+//    longer per-problem chain is hidden and the extraction keeps the CU slots
+//    (bench 306.5k vs 304.9k frames/s with four, profiles/r03_resolve_nw.txt);
+//    9-127 problems four waves; maps of 20,000+ points whose fixed-point claim
+//    buffers do not fit in LDS eight.
+//  * k_proj_resolve_fp (1024-point windows iterated to their fixed point): maps
+//    of 20,000+ points (C5: 33.9k -> 40.3k problems/s over 512-point prefix
+//    windows), and calls of at most RESOLVE_FP_FEW problems at any map size
+//    (the drop-in's one frame: one 5,000-point map in 5 windows instead of 20
+//    prefix windows, SearchByProjection 0.239 -> 0.197 ms, profiles/r04_step10.txt).
+//  * k_proj_jacobi rounds over the whole chip, then k_proj_resolve_fp for any
+//    problem not settled (only on request: the rounds compete with a
+//    concurrent extraction for every CU, profiles/r04_c5_stages.txt).
+#define RESOLVE_FP_MIN_MAP 20000
+#define RESOLVE_FP_FEW 8
+#define RESOLVE_FP_LDS_MAX (160 * 1024 - 1024)
+
+int orb_k_proj_resolve_kernel(int nproblems, int kpStride, int mpStride, int schedule) {
+  const bool fpFits = (size_t)kpStride * 12 <= RESOLVE_FP_LDS_MAX;  // claims x 2 + kpMatch
+  if (fpFits) {
+    if (schedule == ORB_RESOLVE_JACOBI) return ORB_RESOLVE_KERNEL_JACOBI;
+    if (schedule == ORB_RESOLVE_FIXED_POINT) return ORB_RESOLVE_KERNEL_FIXED_POINT;
+    if (schedule == ORB_RESOLVE_AUTO && (mpStride >= RESOLVE_FP_MIN_MAP || nproblems <= RESOLVE_FP_FEW))
+      return ORB_RESOLVE_KERNEL_FIXED_POINT;
+  }
+  if (mpStride >= RESOLVE_FP_MIN_MAP) return ORB_RESOLVE_KERNEL_PREFIX_W8;
+  return nproblems >= 128 ? ORB_RESOLVE_KERNEL_PREFIX_W1 : ORB_RESOLVE_KERNEL_PREFIX_W4;
+}
+
+// bytes of Jacobi-resolve scratch for n problems (0 unless that schedule runs)
+size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems, int schedule) {
+  if (orb_k_proj_resolve_kernel(nproblems, kpStride, mpStride, schedule) != ORB_RESOLVE_KERNEL_JACOBI)
+    return 0;
+  return (size_t)jacobi_stride(kpStride, mpStride) * 4 * (size_t)nproblems;
 }
 
 hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
@@ -1188,125 +1226,59 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
                               const int32_t* nmps, int mpStride, const int32_t* cellStart,
                               const int32_t* cellIdx, const void* params, const uint32_t* topk,
                               const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
-                              int nproblems, int32_t* jacScratch, hipStream_t s) {
+                              int nproblems, int schedule, int jacobiRounds, int32_t* jacScratch,
+                              hipStream_t s) {
   const ProjParams P = *(const ProjParams*)params;
   if (nproblems <= 0) return hipSuccess;
-  const size_t words = (size_t)((kpStride + 31) / 32);
-  const size_t lds = ((words + 3) & ~(size_t)3) * 4 + (size_t)kpStride * 4;
-  // 256-point prefix windows for local maps of a few thousand points (C4: 1 to
-  // 8 waves measured equal within 2 %; the fixed-point kernel 2 % slower on
-  // the headline bench).  Large maps (C5, 50,000 points): the fixed-point
-  // kernel, 1024-point windows (SearchByProjection alone 33.9k -> 40.3k
-  // problems/s over 512-point prefix windows; 2/4/8 points per thread measured
-  // 39.8k/37.1k/28.7k).  ORB_RESOLVE_FP=0 selects the prefix kernel.
-  static const int fpMode = getenv("ORB_RESOLVE_FP") ? atoi(getenv("ORB_RESOLVE_FP")) : 1;
-  static const int fpMin = getenv("ORB_RESOLVE_FP_MIN") ? atoi(getenv("ORB_RESOLVE_FP_MIN")) : 20000;
-  const size_t ldsFp = (size_t)kpStride * 12;  // claims x 2 + kpMatch
-  // Large maps: Jacobi rounds over the whole chip first (k_proj_jacobi), the
-  // windowed fixed-point kernel after them for any problem not yet settled
-  // (ORB_RESOLVE_JACOBI=0: the windowed kernel alone; ORB_JACOBI_ROUNDS = R)
-  // (off by default: at C5, B = 16, four rounds of ~20 us leave most problems
-  // unsettled, and the windowed kernel then runs after them: resolve 0.280 ms
-  // against 0.180 ms alone; profiles/r04_c5_stages.txt)
-  static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 0;
-  static const int jacR =
-      getenv("ORB_JACOBI_ROUNDS") ? std::max(1, std::min(48, atoi(getenv("ORB_JACOBI_ROUNDS")))) : 4;
-  // window size (ORB_RESOLVE_FP_PPT 1, 2, 4: 1024 points, 1024 threads x 1;
-  // 2048 points, 1024 x 2; 4096 points, 512 threads x 8, whose registers a
-  // 1024-thread workgroup does not have)
-  static const int fpPpt = getenv("ORB_RESOLVE_FP_PPT") ? atoi(getenv("ORB_RESOLVE_FP_PPT")) : 1;
-  // a few problems per call (the drop-in's one frame against its local map)
-  // take the fixed-point kernel at any map size: one 1024-point window per
-  // round trip instead of 256-point prefix windows (SearchByProjection of one
-  // 5,000-point map through the drop-in 0.197 vs 0.239 ms,
-  // profiles/r04_step10.txt); batches keep the one-wave prefix kernel beside
-  // the next launch's extraction (ORB_RESOLVE_FP_FEW = the problem count)
-  static const int fpFew = getenv("ORB_RESOLVE_FP_FEW") ? atoi(getenv("ORB_RESOLVE_FP_FEW")) : 8;
-  const bool fp = (mpStride >= fpMin || nproblems <= fpFew) && fpMode > 0 &&
-                  ldsFp <= 160 * 1024 - 1024;
-  if (fp && ldsFp > 64 * 1024) {
-    const void* fn = fpMode == 256   ? (const void*)k_proj_resolve_fp<256>
-                     : fpMode == 512 ? (const void*)k_proj_resolve_fp<512>
-                     : fpPpt == 2    ? (const void*)k_proj_resolve_fp<1024, 2>
-                     : fpPpt == 4    ? (const void*)k_proj_resolve_fp<512, 8>
-                                     : (const void*)k_proj_resolve_fp<1024>;
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsFp);
-    if (e != hipSuccess) return e;
-  }
-  const int32_t* done = nullptr;
-  long long doneStride = 0;
-  // (the scratch is sized by orb_k_proj_jacobi_bytes: large maps only)
-  if (fp && jacOn > 0 && jacScratch && mpStride >= fpMin) {
-    const long long js = jacobi_stride(kpStride, mpStride);
-    const int initN = std::max(3 * kpStride, jacR + 1);
-    hipLaunchKernelGGL(k_proj_jacobi_init, dim3((initN + JAC_T - 1) / JAC_T, nproblems), dim3(JAC_T),
-                       0, s, jacScratch, js, kpStride, jacR, nkeys, kpMatch, nmatches);
-    const dim3 g((mpStride + JAC_T * JAC_PPT - 1) / (JAC_T * JAC_PPT), nproblems);
-    for (int r = 0; r <= jacR; ++r)
-      hipLaunchKernelGGL(k_proj_jacobi<JAC_PPT>, g, dim3(JAC_T), 0, s, keys, desc, uright, locked,
-                         kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, P, topk, ncand,
-                         kpMatch, nmatches, jacScratch, js, r, jacR);
-    done = jacScratch + jacR;
-    doneStride = js;
-  }
-  if (fp && fpMode == 256) {
-    hipLaunchKernelGGL(k_proj_resolve_fp<256>, dim3(nproblems), dim3(256), ldsFp, s, keys, desc,
-                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
-  } else if (fp && fpMode == 512) {
-    hipLaunchKernelGGL(k_proj_resolve_fp<512>, dim3(nproblems), dim3(512), ldsFp, s, keys, desc,
-                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
-  } else if (fp && fpPpt == 2) {
-    hipLaunchKernelGGL((k_proj_resolve_fp<1024, 2>), dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
-                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
-  } else if (fp && fpPpt == 4) {
-    hipLaunchKernelGGL((k_proj_resolve_fp<512, 8>), dim3(nproblems), dim3(512), ldsFp, s, keys, desc,
-                       uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
-                       cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
-  } else if (fp) {
+  const int kern = orb_k_proj_resolve_kernel(nproblems, kpStride, mpStride, schedule);
+  if (kern == ORB_RESOLVE_KERNEL_FIXED_POINT || kern == ORB_RESOLVE_KERNEL_JACOBI) {
+    const size_t ldsFp = (size_t)kpStride * 12;
+    if (ldsFp > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_proj_resolve_fp<1024>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsFp);
+      if (e != hipSuccess) return e;
+    }
+    const int32_t* done = nullptr;
+    long long doneStride = 0;
+    if (kern == ORB_RESOLVE_KERNEL_JACOBI) {
+      if (!jacScratch) return hipErrorInvalidValue;
+      const int R = std::max(1, std::min(48, jacobiRounds));
+      const long long js = jacobi_stride(kpStride, mpStride);
+      const int initN = std::max(3 * kpStride, R + 1);
+      hipLaunchKernelGGL(k_proj_jacobi_init, dim3((initN + JAC_T - 1) / JAC_T, nproblems), dim3(JAC_T),
+                         0, s, jacScratch, js, kpStride, R, nkeys, kpMatch, nmatches);
+      const dim3 g((mpStride + JAC_T * JAC_PPT - 1) / (JAC_T * JAC_PPT), nproblems);
+      for (int r = 0; r <= R; ++r)
+        hipLaunchKernelGGL(k_proj_jacobi<JAC_PPT>, g, dim3(JAC_T), 0, s, keys, desc, uright, locked,
+                           kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, P, topk, ncand,
+                           kpMatch, nmatches, jacScratch, js, r, R);
+      done = jacScratch + R;
+      doneStride = js;
+    }
     hipLaunchKernelGGL(k_proj_resolve_fp<1024>, dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
                        cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
-  } else if (mpStride >= 20000)
+    return hipGetLastError();
+  }
+  const size_t words = (size_t)((kpStride + 31) / 32);
+  const size_t lds = ((words + 3) & ~(size_t)3) * 4 + (size_t)kpStride * 4;
+  if (kern == ORB_RESOLVE_KERNEL_PREFIX_W8)
     hipLaunchKernelGGL(k_proj_resolve<8>, dim3(nproblems), dim3(512), lds, s, keys, desc, uright,
                        locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
                        P, topk, ncand, kpMatch, nmatches);
-  else {
-    // waves per problem for small maps: each problem's workgroup holds its
-    // waves for the whole sequential resolve.  Batches (>= 128 problems, run
-    // beside the next launch's extraction) take one wave per problem: the
-    // longer per-problem chain is hidden and the extraction keeps the CU slots
-    // (bench 306.5k vs 304.9k frames/s with four, profiles/r03_resolve_nw.txt);
-    // a few problems per call keep four waves for latency.  ORB_RESOLVE_NW overrides.
-    static const int nwEnv = getenv("ORB_RESOLVE_NW") ? atoi(getenv("ORB_RESOLVE_NW")) : 0;
-    const int nw = nwEnv > 0 ? nwEnv : (nproblems >= 128 ? 1 : 4);
-    if (nw == 1)
-      hipLaunchKernelGGL(k_proj_resolve<1>, dim3(nproblems), dim3(64), lds, s, keys, desc, uright,
-                         locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
-                         P, topk, ncand, kpMatch, nmatches);
-    else if (nw == 2)
-      hipLaunchKernelGGL(k_proj_resolve<2>, dim3(nproblems), dim3(128), lds, s, keys, desc, uright,
-                         locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
-                         P, topk, ncand, kpMatch, nmatches);
-    else
-      hipLaunchKernelGGL(k_proj_resolve<4>, dim3(nproblems), dim3(256), lds, s, keys, desc, uright,
-                         locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
-                         P, topk, ncand, kpMatch, nmatches);
-  }
+  else if (kern == ORB_RESOLVE_KERNEL_PREFIX_W1)
+    hipLaunchKernelGGL(k_proj_resolve<1>, dim3(nproblems), dim3(64), lds, s, keys, desc, uright,
+                       locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
+                       P, topk, ncand, kpMatch, nmatches);
+  else
+    hipLaunchKernelGGL(k_proj_resolve<4>, dim3(nproblems), dim3(256), lds, s, keys, desc, uright,
+                       locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx,
+                       P, topk, ncand, kpMatch, nmatches);
   return hipGetLastError();
 }
 
 size_t orb_k_proj_params_size(void) { return sizeof(ProjParams); }
 
-// bytes of Jacobi-resolve scratch for n problems (0: the windowed kernel only)
-size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems) {
-  static const int fpMin = getenv("ORB_RESOLVE_FP_MIN") ? atoi(getenv("ORB_RESOLVE_FP_MIN")) : 20000;
-  static const int jacOn = getenv("ORB_RESOLVE_JACOBI") ? atoi(getenv("ORB_RESOLVE_JACOBI")) : 0;
-  if (mpStride < fpMin || jacOn <= 0) return 0;
-  return (size_t)jacobi_stride(kpStride, mpStride) * 4 * (size_t)nproblems;
-}
 
 }  // extern "C"
 

@@ -90,8 +90,10 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
                               const int32_t* nmps, int mpStride, const int32_t* cellStart,
                               const int32_t* cellIdx, const void* params, const uint32_t* topk,
                               const int32_t* ncand, int32_t* kpMatch, int32_t* nmatches,
-                              int nproblems, int32_t* jacScratch, hipStream_t s);
-size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems);
+                              int nproblems, int schedule, int jacobiRounds, int32_t* jacScratch,
+                              hipStream_t s);
+int orb_k_proj_resolve_kernel(int nproblems, int kpStride, int mpStride, int schedule);
+size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems, int schedule);
 size_t orb_k_proj_params_size(void);
 size_t orb_k_stereo_params_size(void);
 hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc, const int32_t* nleft,
@@ -1524,7 +1526,9 @@ struct orb_matcher {
   StageProfiler prof;
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
-  DevBuf dJac;  // Jacobi-resolve scratch (large local maps)
+  DevBuf dJac;  // Jacobi-resolve scratch (ORB_RESOLVE_JACOBI)
+  int resolveSchedule = ORB_RESOLVE_AUTO;  // orb_matcher_set_resolve
+  int jacobiRounds = 6;
   // stereo / frame / BoW scratch
   DevBuf dStRowStart, dStRowIdx;  // stereo vRowIndices (CSR per pair)
   DevBuf dProjStage;              // cell-ordered keypoints for k_proj_candidates (16 B per slot)
@@ -1664,7 +1668,7 @@ orb_status_t orb_match_projection_local_batch(
   if ((st = m->dNcand.ensure((size_t)n_problems * std::max(mp_stride, 1) * 4))) return st;
   const bool stage = kp_stride <= orb_k_grid_stage_max();
   if (stage && (st = m->dProjStage.ensure((size_t)n_problems * kp_stride * 16))) return st;
-  const size_t jb = orb_k_proj_jacobi_bytes(kp_stride, mp_stride, n_problems);
+  const size_t jb = orb_k_proj_jacobi_bytes(kp_stride, mp_stride, n_problems, m->resolveSchedule);
   if (jb && (st = m->dJac.ensure(jb))) return st;
   StageProfiler& pf = m->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
@@ -1691,9 +1695,28 @@ orb_status_t orb_match_projection_local_batch(
                              d_mp_desc, d_nmps, mp_stride, m->dCellStart.as<int32_t>(),
                              m->dCellIdx.as<int32_t>(), &P, m->dTopk.as<uint32_t>(),
                              m->dNcand.as<int32_t>(), d_kp_match, d_nmatches, n_problems,
-                             m->dJac.as<int32_t>(), s));
+                             m->resolveSchedule, m->jacobiRounds, m->dJac.as<int32_t>(), s));
   PROF_REC(ev, pf.e(ev, 2), s);
   PROF_REC(ev, pf.t1(ev), s);
+  return ORB_OK;
+}
+
+orb_status_t orb_matcher_set_resolve(orb_matcher_t* m, int schedule, int jacobi_rounds) {
+  if (!m || schedule < ORB_RESOLVE_AUTO || schedule > ORB_RESOLVE_JACOBI ||
+      (schedule == ORB_RESOLVE_JACOBI && (jacobi_rounds < 1 || jacobi_rounds > 48)))
+    return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  m->resolveSchedule = schedule;
+  if (schedule == ORB_RESOLVE_JACOBI) m->jacobiRounds = jacobi_rounds;
+  return ORB_OK;
+}
+
+orb_status_t orb_matcher_resolve_kernel(orb_matcher_t* m, int n_problems, int kp_stride,
+                                        int mp_stride, int* kernel) {
+  if (!m || !kernel || n_problems <= 0 || kp_stride <= 0 || mp_stride < 0) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  *kernel = orb_k_proj_resolve_kernel(n_problems, kp_stride, std::max(mp_stride, 1),
+                                      m->resolveSchedule);
   return ORB_OK;
 }
 
@@ -1735,16 +1758,8 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   hipSetDevice(m->device);
   const int N = F->n, M = n_mp;
   orb_status_t st;
-  if ((st = m->dKeys.ensure((size_t)N * sizeof(orb_keypoint_t)))) return st;
-  if ((st = m->dDesc.ensure((size_t)N * 32))) return st;
-  if ((st = m->dUr.ensure((size_t)N * 4))) return st;
-  if ((st = m->dLocked.ensure((size_t)N))) return st;
-  if ((st = m->dNKeys.ensure(16))) return st;
-  if ((st = m->dMps.ensure((size_t)std::max(M, 1) * sizeof(orb_mp_track_t)))) return st;
-  if ((st = m->dMpDesc.ensure((size_t)std::max(M, 1) * 32))) return st;
-  if ((st = m->dNMps.ensure(16))) return st;
+  // (inputs live in dIn below; only the outputs and the matcher scratch here)
   if ((st = m->dKpMatch.ensure((size_t)N * 4 + 16))) return st;  // + the count (one D2H)
-  if ((st = m->dNMatch.ensure(16))) return st;
   if ((st = m->dCellStart.ensure((size_t)(ORB_GRID_COLS * ORB_GRID_ROWS + 1) * 4))) return st;
   if ((st = m->dCellIdx.ensure((size_t)N * 4))) return st;
   if ((st = m->dTopk.ensure((size_t)std::max(M, 1) * 16))) return st;
@@ -1787,7 +1802,7 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   const uint8_t* lk = kp_locked ? din + oLk : nullptr;
   const bool stage = N <= orb_k_grid_stage_max();
   if (stage && (st = m->dProjStage.ensure((size_t)N * 16))) return st;
-  const size_t jb = orb_k_proj_jacobi_bytes(N, std::max(M, 1), 1);
+  const size_t jb = orb_k_proj_jacobi_bytes(N, std::max(M, 1), 1, m->resolveSchedule);
   if (jb && (st = m->dJac.ensure(jb))) return st;
   if (stage)
     HIP_TRY(orb_k_grid_build_staged(dKeys, dNK, lk, ur,
@@ -1811,7 +1826,7 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
                              m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
                              m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
                              m->dKpMatch.as<int32_t>(), m->dKpMatch.as<int32_t>() + N, 1,
-                             m->dJac.as<int32_t>(), s));
+                             m->resolveSchedule, m->jacobiRounds, m->dJac.as<int32_t>(), s));
   // one DMA out (count, then the matches) into pinned memory
   HIP_TRY(hipMemcpyAsync(m->hOutM.p, m->dKpMatch.p, (size_t)N * 4 + 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

@@ -54,9 +54,10 @@ def test_search_by_projection_local(gpu, oracle, w, h, nf, M, th, seed):
 def test_search_by_projection_conflicts_and_flags(gpu, oracle, M, nsrc):
     """Many map points on few keypoints (deep first-come chains, top-K overflow),
     points without observations (claims that do not lock), bad / out-of-view
-    points, stereo gating through mvuRight.  24,000 points take the
-    fixed-point resolve (local maps of 20,000 points and more), 4,000 the
-    256-point prefix windows."""
+    points, stereo gating through mvuRight.  One problem per call, so the
+    default schedule takes the fixed-point resolve at both sizes; the prefix
+    kernels are held to the same maps in
+    test_search_by_projection_resolve_schedules and test_gpu_headline.py."""
     w, h = 640, 480
     k, d, scale = _frame(gpu, oracle, w, h, 1000, 3)
     rng = np.random.default_rng(7)
@@ -84,20 +85,23 @@ def test_search_by_projection_conflicts_and_flags(gpu, oracle, M, nsrc):
 
 
 def test_search_by_projection_large_frame(gpu, oracle):
-    """More than 8,192 keypoints: the one-wave grid build, the candidate scan
+    """More than 13,568 keypoints: the four-wave grid build, the candidate scan
     over the global grid (no LDS staging past 4,096 keypoints) and, with
-    20,000+ map points, the 512-point prefix resolve (the fixed-point kernel's
-    claim buffers would exceed 64 KiB of LDS)."""
+    20,000+ map points, the 512-thread prefix resolve k_proj_resolve<8> (the
+    fixed-point kernel's claim buffers, 12 B per keypoint, would exceed the
+    160 KB of LDS)."""
     w, h = 1920, 1080
     rng = np.random.default_rng(1080)
     img = rng.integers(0, 256, (h, w), dtype=np.uint8)
-    k, d, _ = oracle.extract(img, 12000, 1.2, 8, 20, 7)
-    assert len(k) > 8192
-    scale = oracle.params(12000)["scale"]
+    k, d, _ = oracle.extract(img, 15000, 1.2, 8, 20, 7)
+    assert len(k) * 12 > 160 * 1024 - 1024
+    scale = oracle.params(15000)["scale"]
     mps, mpd, locked = oracle.synth_local_map(11, k, d, 20000, w, h)
     n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, mps, mpd, 1.0, 0.8, locked)
     F = gpu.Frame(k, d, scale, w, h)
-    n_gpu, km_gpu = gpu.ORBmatcher(0.8).SearchByProjection(F, mps, mpd, 1.0, locked)
+    m = gpu.ORBmatcher(0.8)
+    assert m.resolve_kernel(1, len(k), len(mps)) == "k_proj_resolve<8>"
+    n_gpu, km_gpu = m.SearchByProjection(F, mps, mpd, 1.0, locked)
     assert n_ref > 0
     assert n_gpu == n_ref
     assert np.array_equal(km_gpu, km_ref)
@@ -136,8 +140,9 @@ def _conflict_map(oracle, k, d, M, nsrc, seed=7):
 
 def test_search_by_projection_batch_large_maps(gpu, oracle):
     """Device batch of large local maps with different sizes (30,000 / 50,000 /
-    24,000 points in a 50,000-point stride): the Jacobi rounds and, for the
-    problem with deep first-come chains, the windowed fixed-point fallback."""
+    24,000 points in a 50,000-point stride), under the default schedule (the
+    fixed-point windows) and then the Jacobi schedule (chip-wide rounds and,
+    for the problem with deep first-come chains, the windowed fallback)."""
     torch = pytest.importorskip("torch")
     w, h, nf = 1920, 1080, 4000
     k, d, scale = _frame(gpu, oracle, w, h, nf, 5)
@@ -161,7 +166,10 @@ def test_search_by_projection_batch_large_maps(gpu, oracle):
     km = torch.zeros((P, cap), dtype=torch.int32, device="cuda")
     nm = torch.zeros(P, dtype=torch.int32, device="cuda")
     m = gpu.ORBmatcher(0.8)
-    for _ in range(2):  # the second call reuses the scratch of the first
+    for it in range(3):  # the second call reuses the scratch of the first
+        if it == 2:
+            m.set_resolve(m.RESOLVE_JACOBI, 4)
+            km.fill_(-7)
         m.search_by_projection_batch(P, dk.data_ptr(), dde.data_ptr(), dn.data_ptr(), dl.data_ptr(),
                                      cap, dm.data_ptr(), dmd.data_ptr(), dnm.data_ptr(), S, w, h,
                                      scale, 1.0, km.data_ptr(), nm.data_ptr())
@@ -172,54 +180,38 @@ def test_search_by_projection_batch_large_maps(gpu, oracle):
             assert np.array_equal(km[i, :len(k)].cpu().numpy(), km_ref), i
 
 
-@pytest.mark.parametrize("env", [{"ORB_RESOLVE_JACOBI": "1", "ORB_JACOBI_ROUNDS": "1"},
-                                 {"ORB_RESOLVE_JACOBI": "1"},
-                                 {"ORB_RESOLVE_JACOBI": "1", "ORB_JACOBI_ROUNDS": "48"},
-                                 {"ORB_RESOLVE_JACOBI": "0"},
-                                 {"ORB_RESOLVE_FP": "256"}, {"ORB_RESOLVE_FP": "512"},
-                                 {"ORB_PROJ_DIRECT": "1"}, {"ORB_PROJ_PPT": "2"},
-                                 {"ORB_RESOLVE_FP_PPT": "2"}, {"ORB_RESOLVE_FP_PPT": "4"}])
-def test_search_by_projection_resolve_schedules(gpu, oracle, tmp_path, env):
-    """The large-map resolve under each schedule (read once per process, so in
-    a child): Jacobi rounds (1, the default 4, up to 48) with the windowed
-    fallback, the windowed kernel alone (the default) at 1024, 256 and 512
-    points per window, and the candidate scan reading the staged grid from
-    global memory (ORB_PROJ_DIRECT); C5's map and a deep-conflict map (whose
-    points run out of top-4 candidates: the exact re-scan)."""
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
-    w, h = 1920, 1080
-    k, d, scale = _frame(gpu, oracle, w, h, 4000, 5)
-    cases = [oracle.synth_local_map(5, k, d, 50000, w, h), _conflict_map(oracle, k, d, 24000, 120)]
-    for i, (a, b, c) in enumerate(cases):
-        np.save(tmp_path / f"mps{i}.npy", a)
-        np.save(tmp_path / f"mpd{i}.npy", b)
-        np.save(tmp_path / f"lk{i}.npy", c)
-    np.save(tmp_path / "k.npy", k)
-    np.save(tmp_path / "d.npy", d)
-    np.save(tmp_path / "scale.npy", scale)
-    code = f"""
-import sys, numpy as np
-sys.path.insert(0, {str(root)!r}); sys.path.insert(0, {str(root / 'tests')!r})
-from conftest import load_pkg
-orb = load_pkg()
-T = {str(tmp_path)!r}
-k, d, scale = np.load(T + '/k.npy'), np.load(T + '/d.npy'), np.load(T + '/scale.npy')
-F = orb.Frame(k, d, scale, {w}, {h})
-for i in range(2):
-    n, km = orb.ORBmatcher(0.8).SearchByProjection(F, np.load(T + f'/mps{{i}}.npy'),
-                                                   np.load(T + f'/mpd{{i}}.npy'), 1.0,
-                                                   np.load(T + f'/lk{{i}}.npy'))
-    np.save(T + f'/km{{i}}.npy', km)
-    open(T + f'/n{{i}}.txt', 'w').write(str(n))
-"""
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
-                       env=dict(os.environ, **env))
-    assert r.returncode == 0, r.stderr[-2000:]
-    for i, (a, b, c) in enumerate(cases):
-        n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, a, b, 1.0, 0.8, c)
-        assert int((tmp_path / f"n{i}.txt").read_text()) == n_ref, i
-        assert np.array_equal(np.load(tmp_path / f"km{i}.npy"), km_ref), i
+_SCHEDULES = [("auto", 0, 6), ("prefix", 1, 6), ("fixed_point", 2, 6), ("jacobi_r1", 3, 1),
+              ("jacobi_r6", 3, 6), ("jacobi_r48", 3, 48)]
+
+
+@pytest.mark.parametrize("name,schedule,rounds", _SCHEDULES, ids=[s[0] for s in _SCHEDULES])
+def test_search_by_projection_resolve_schedules(gpu, oracle, name, schedule, rounds):
+    """Every resolve schedule (orb_matcher_set_resolve) on one handle, in
+    process: C5's 50,000-point map and a 24,000-point deep-conflict map (points
+    that run out of top-4 candidates take the exact re-scan) on a 4,000-feature
+    1920x1080 frame, and C4's 5,000-point map plus a 5,000-point conflict map on
+    a 1241x376 frame.  Under the prefix schedule these single problems take
+    k_proj_resolve<8> (20,000+ points) and k_proj_resolve<4>."""
+    m = gpu.ORBmatcher(0.8)
+    m.set_resolve(schedule, rounds)
+    for (w, h, nf, seed, M) in ((1920, 1080, 4000, 5, 50000), (1241, 376, 1000, 0, 5000)):
+        k, d, scale = _frame(gpu, oracle, w, h, nf, seed)
+        cases = [oracle.synth_local_map(seed, k, d, M, w, h),
+                 _conflict_map(oracle, k, d, 24000 if M > 20000 else M, 120 if M > 20000 else 40)]
+        F = gpu.Frame(k, d, scale, w, h)
+        for i, (a, b, c) in enumerate(cases):
+            want = {"prefix": "k_proj_resolve<8>" if len(a) >= 20000 else "k_proj_resolve<4>",
+                    "fixed_point": "k_proj_resolve_fp<1024>", "auto": "k_proj_resolve_fp<1024>"}
+            got_kernel = m.resolve_kernel(1, len(k), len(a))
+            assert got_kernel == want.get(name, "k_proj_jacobi+k_proj_resolve_fp"), got_kernel
+            n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, a, b, 1.0, 0.8, c)
+            n, km = m.SearchByProjection(F, a, b, 1.0, c)
+            assert n == n_ref, (w, i)
+            assert np.array_equal(km, km_ref), (w, i, np.nonzero(km != km_ref)[0][:10])
+
+
+def test_resolve_schedule_rejects_bad_values(gpu):
+    m = gpu.ORBmatcher(0.8)
+    for sched, r in ((4, 6), (-1, 6), (3, 0), (3, 49)):
+        with pytest.raises(gpu.OrbError):
+            m.set_resolve(sched, r)
