@@ -100,12 +100,18 @@ typedef struct orb_matcher orb_matcher_t;
 
 /* ---------------------------------------------------------------- extractor */
 
-/* Limits (the reference has none; these are where this build stops, each a
- * status, never a silent change of results):
- *   create: 0 <= nfeatures <= 60000, 1 <= nlevels <= 16, 1 < scale_factor <= 1.9
- *     (ORB_EINVAL otherwise; every ORB-SLAM2 configuration uses 1.2).
- *   extract: every pyramid level between 40 and 4095 px in each dimension
- *     (keys pack x and y in 12 bits), FAST cells at most 64 x 64 interior
+/* Limits (the reference states none; these are where this build stops, each
+ * a status, never a silent change of results):
+ *   create: nfeatures >= 0, 1 <= nlevels <= 16, scale_factor > 1 (finite)
+ *     (ORB_EINVAL otherwise: at 1 the reference's quota series is 0 / 0,
+ *     src/ORBextractor.cc:453-455).  Every scale factor takes the same
+ *     integer resize taps; levels whose downscale the staged tiles cannot
+ *     hold (beyond ~1.9) take an untiled kernel.
+ *   extract: every pyramid level between 33 and 4095 px in each dimension
+ *     (at 32 px or less the reference's DistributeOctTree divides by zero or
+ *     sizes its root vector negatively, :562-569; keys pack x and y in 12
+ *     bits), a level's quota + 4 at most 65,534 (16-bit node labels: nfeatures
+ *     up to ~300,000 at 1.2 / 8 levels), FAST cells at most 64 x 64 interior
  *     pixels: ORB_EINVAL from the call (and orb_extractor_capacity < 0).
  *   DistributeOctTree (src/ORBextractor.cc:558-782): node tables hold
  *     quota + 4 nodes per level (the reference's list never exceeds quota + 3,

@@ -13,7 +13,7 @@
 //   k_orient_desc  x 1            IC_Angle + rBRIEF-256 with the 7x7  src/ORBextractor.cc:77-164,
 //                                 blur fused (each sample blurred     1131-1167
 //                                 from LDS row sums), two keypoints per wave, rescale
-//   (k_blur_levels + k_orient_desc_split: blurred levels on demand / split A/B mode)
+//   (k_blur_levels: one image's blurred levels on demand, orb_extractor_blurred_level)
 // Bit-exactness contract: every output byte equals the CPU oracle
 // (oracle/orb_oracle.cpp) on the same image.
 #include <stdlib.h>
@@ -33,6 +33,9 @@
 // each thread produces 4 columns x 4 rows and stores whole dwords, so a wave
 // writes two full 128-byte rows per store.
 #define PYR_TW 128
+#ifndef PYR_IMAGES_PER_WG
+#define PYR_IMAGES_PER_WG 16  // images per k_pyr_resize workgroup
+#endif
 #define PYR_TH 32
 // Staged source window (rows x dwords): >= the source rows a 32-row output
 // tile touches, multiple of 4, and >= the dwords of source row a 128-column
@@ -42,6 +45,40 @@
 #define PYR_SW 44
 #define PYR_SROWS_WIDE 64
 #define PYR_SW_WIDE 64
+
+// Levels whose tiles fit neither staged window (per-level downscales beyond
+// ~1.9): one thread per 4 output pixels, its taps read straight from the
+// source level with byte loads -- the same integer expressions as
+// k_pyr_resize, bit-identical, without the staging.
+__global__ __launch_bounds__(256) void k_pyr_resize_generic(
+    const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int sw, int sh,
+    uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride, int dw, int dh,
+    const int* __restrict__ xofs, const int* __restrict__ alpha, const int* __restrict__ yofs,
+    const int* __restrict__ beta) {
+  const int xs = 4 * (blockIdx.x * 64 + (int)(threadIdx.x & 63));
+  const int y = blockIdx.y * 4 + (int)(threadIdx.x >> 6);
+  if (xs >= dw || y >= dh) return;
+  const ImgRsrc im = img_rsrc(src + (long long)blockIdx.z * srcImgPitch,
+                              (uint32_t)((sh - 1) * srcStride + sw));
+  const int sy0 = min(max(yofs[y], 0), sh - 1), sy1 = min(max(yofs[y] + 1, 0), sh - 1);
+  const uint32_t b = (uint32_t)beta[y], b0 = b & 0xFFFFu, b1 = b >> 16;
+  const uint32_t r0 = (uint32_t)(sy0 * srcStride) + im.sh, r1 = (uint32_t)(sy1 * srcStride) + im.sh;
+  uint32_t packed = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int dx = min(xs + j, dw - 1);
+    const int sx = xofs[dx], sx1 = min(sx + 1, sw - 1);  // past xmax the weights are (2048, 0)
+    const uint32_t a = (uint32_t)alpha[dx], a0 = a & 0xFFFFu, a1 = a >> 16;
+    const uint32_t h0 = a0 * buf_ld8(im.r, r0 + sx) + a1 * buf_ld8(im.r, r0 + sx1);
+    const uint32_t h1 = a0 * buf_ld8(im.r, r1 + sx) + a1 * buf_ld8(im.r, r1 + sx1);
+    int v = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
+    __asm__ volatile("" : "+v"(v));  // see k_pyr_resize
+    packed |= (uint32_t)v << (8 * j);
+  }
+  const __amdgpu_buffer_rsrc_t rd =
+      make_rsrc(dst + (long long)blockIdx.z * dstImgPitch, (uint32_t)(dh * dstStride));
+  buf_st32(rd, (uint32_t)(y * dstStride + xs), packed);
+}
 
 // Source-window staging in 16-byte groups: element i of a window of nR rows x
 // nG groups (4 dwords each) is row i / nG, group i % nG.  One b128 load per
@@ -211,115 +248,6 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
         packed |= (uint32_t)v << (8 * j);
       }
       buf_st32(rd, (uint32_t)(y * dstStride + xs), packed);
-    }
-  }
-}
-
-// ============================================================ k_pyr_chain
-// The whole resize chain of one or two frames in ONE launch (the single-frame
-// call's seven dependent k_pyr_resize launches cost ~4.7 us each, most of it
-// launch and ramp): blockIdx.x = band (OrbChainBand, host-planned), blockIdx.y
-// = image.  Level by level, the band computes the rows of level l that its own
-// rows of levels >= l need, from the previous level's rows in LDS (two
-// buffers, even / odd levels), and writes the rows it owns.  Rows in a halo
-// are computed by two bands (same inputs, same result).  The taps are
-// k_pyr_resize's integer expressions (OpenCV's 11-bit fixed point), so the
-// pyramid is bit-identical.
-template <int T>
-__global__ __launch_bounds__(T) void k_pyr_chain(const uint8_t* __restrict__ img0, long long imgPitch,
-                                                 int img0Stride, uint8_t* __restrict__ arena,
-                                                 long long arenaPitch, OrbPlanDesc plan,
-                                                 const int32_t* __restrict__ rt,
-                                                 const OrbChainBand* __restrict__ bands, int buf1Off) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  // the row taps of the rows a band computes at one level (host-checked <= 512 rows)
-  __shared__ int2 sY[ORB_CHAIN_MAX_ROWS];
-  const int tid = threadIdx.x;
-  const OrbChainBand& B = bands[blockIdx.x];
-  const int img = blockIdx.y;
-  uint8_t* A = arena + (long long)img * arenaPitch;
-  {
-    // level 0 rows [lo, hi) into buffer 0, dword by dword, realigned from any
-    // caller stride / base alignment (buffer loads past the image read 0);
-    // eight dwords' loads in flight per thread before their stores
-    const int lo = B.lo[0], hi = B.hi[0], w = plan.lv[0].w, h = plan.lv[0].h;
-    const int nd = orb_chain_pitch(w) >> 2, n = (hi - lo) * nd;
-    const float invNd = 1.0f / (float)nd;  // i / nd exactly (see below)
-    const ImgRsrc im = img_rsrc(img0 + (long long)img * imgPitch, (uint32_t)((h - 1) * img0Stride + w));
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(sm);
-    for (int i0 = 0; i0 < n; i0 += 8 * T) {
-      uint32_t w0[8], w1[8], sh[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int i = min(i0 + k * T + tid, n - 1);
-        const int r = (int)(((float)i + 0.5f) * invNd), c = i - r * nd;
-        const uint32_t o = (uint32_t)((lo + r) * img0Stride + 4 * c) + im.sh;
-        sh[k] = o & 3u;
-        w0[k] = buf_ld32(im.r, o & ~3u);
-        w1[k] = buf_ld32(im.r, (o & ~3u) + 4);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (i0 + k * T + tid < n) d32[i0 + k * T + tid] = __builtin_amdgcn_alignbyte(w1[k], w0[k], sh[k]);
-    }
-  }
-  for (int l = 1; l < plan.nlevels; ++l) {
-    const OrbLevelDesc& d = plan.lv[l];
-    const int sw = plan.lv[l - 1].w, sh = plan.lv[l - 1].h;
-    const uint8_t* S = sm + ((l - 1) & 1) * buf1Off;
-    uint8_t* Dl = sm + (l & 1) * buf1Off;
-    const int sp = orb_chain_pitch(sw), dp = orb_chain_pitch(d.w), slo = B.lo[l - 1];
-    const int lo = B.lo[l], hi = B.hi[l], own = B.own[l], ownE = B.ownEnd[l];
-    const int nr = hi - lo, ng = (d.w + 3) >> 2;
-    const int32_t* xo = rt + d.rtabX;
-    const int32_t* al = xo + d.w;
-    const int32_t* yo = rt + d.rtabY;
-    const int32_t* be = yo + d.h;
-    __syncthreads();  // the previous level's rows written, its row taps read
-    // this level's row taps, as LDS row offsets into the source buffer
-    for (int r = tid; r < nr; r += T) {
-      const int yy = yo[lo + r];
-      sY[r] = make_int2((min(max(yy, 0), sh - 1) - slo) * sp, be[lo + r]);
-      // (second tap row: + sp unless clamped at the last source row)
-      if (min(max(yy + 1, 0), sh - 1) == min(max(yy, 0), sh - 1)) sY[r].x |= 1 << 30;
-    }
-    __syncthreads();  // this level's taps in LDS
-    // a thread keeps its 4 columns' taps for the whole level and walks rows
-    const int tc = min(ng, T), tr = T / tc;
-    for (int c0 = 0; c0 < ng; c0 += tc) {
-      const int c = c0 + tid % tc, r0 = tid / tc;
-      if (c >= ng || r0 >= tr) continue;
-      const int x = 4 * c;
-      int sx[4], sx1[4];
-      uint32_t a0[4], a1[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int dx = min(x + j, d.w - 1);
-        sx[j] = xo[dx];
-        sx1[j] = min(sx[j] + 1, sw - 1);  // (weight 0 where sx + 1 >= sw)
-        const uint32_t aa = (uint32_t)al[dx];
-        a0[j] = aa & 0xFFFFu;
-        a1[j] = aa >> 16;
-      }
-      for (int r = r0; r < nr; r += tr) {
-        const int2 ty = sY[r];
-        const uint8_t* R0 = S + (ty.x & ~(1 << 30));
-        const uint8_t* R1 = R0 + ((ty.x >> 30) ? 0 : sp);
-        const uint32_t b0 = (uint32_t)ty.y & 0xFFFFu, b1 = (uint32_t)ty.y >> 16;
-        uint32_t packed = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t h0 = a0[j] * R0[sx[j]] + a1[j] * R0[sx1[j]];
-          const uint32_t h1 = a0[j] * R1[sx[j]] + a1[j] * R1[sx1[j]];
-          int v = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
-          __asm__ volatile("" : "+v"(v));  // see k_pyr_resize: keep the byte pack opaque
-          packed |= (uint32_t)v << (8 * j);
-        }
-        *reinterpret_cast<uint32_t*>(Dl + r * dp + x) = packed;
-        const int y = lo + r;
-        if (y >= own && y < ownE)
-          *reinterpret_cast<uint32_t*>(A + d.arenaOff + (long long)y * d.pitch + x) = packed;
-      }
     }
   }
 }
@@ -2151,150 +2079,9 @@ __device__ __forceinline__ int half_sum(int v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_orient_desc_split(
-    const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
-    const uint8_t* __restrict__ arena, long long arenaPitch, const uint8_t* __restrict__ blur,
-    long long blurPitch, OrbPlanDesc plan, const uint32_t* __restrict__ outKeys,
-    const int32_t* __restrict__ outCount, const int32_t* __restrict__ errFlag,
-    orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc, int capacity,
-    int32_t* __restrict__ counts) {
-  // wave id through readfirstlane: the level and buffer descriptors derived
-  // from it are provably wave-uniform -> SGPRs, no waterfall
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int half = lane >> 5, hl = lane & 31;
-  const int img = blockIdx.y;
-  const int slot0 = (blockIdx.x * 4 + w) * 2;  // even: first slot of the wave's pair
-  const int32_t* cnts = outCount + img * plan.nlevels;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    int tot = 0;
-    for (int i = 0; i < plan.nlevels; ++i) tot += cnts[i];
-    counts[img] = errFlag[img] ? (int32_t)ORB_EDEVICE : tot;  // failed image: negative count
-  }
-  if (slot0 >= plan.slotsPerImage) return;
-  int l = 0;
-  while (l + 1 < plan.nlevels && plan.lv[l + 1].outOff <= slot0) ++l;
-  const int i0 = slot0 - plan.lv[l].outOff, nl = cnts[l];
-  if (i0 >= nl) return;
-  const bool active = i0 + half < nl;  // the pair's second slot may be past the level's count
-  const int i = i0 + (active ? half : 0);
-  int base = 0;
-  for (int j = 0; j < l; ++j) base += cnts[j];
-  const uint32_t key = outKeys[(long long)img * plan.slotsPerImage + plan.lv[l].outOff + i];
-  const int cx = key_x(key), cy = key_y(key);
-  const OrbLevelDesc& L = plan.lv[l];
-  const uint8_t* lvl;
-  int pitch;
-  if (l == 0) {
-    lvl = img0 + (long long)img * img0Pitch;
-    pitch = img0Stride;
-  } else {
-    lvl = arena + (long long)img * arenaPitch + L.arenaOff;
-    pitch = L.pitch;
-  }
-  // The blurred 37 x 37 patch the descriptor samples (rotated pattern within
-  // +-18 px, max radius 18.38) does not depend on the angle: its loads are
-  // issued first, in flight together with the IC_Angle loads (one memory
-  // round trip per wave).  37 rows x 11 dwords per keypoint, 13 per lane.
-  __shared__ __attribute__((aligned(16))) uint32_t patch[4][2][37][ORB_PATCH_DW];
-  const int bp = L.blurPitch;
-  const __amdgpu_buffer_rsrc_t rb =
-      make_rsrc(blur + (long long)img * blurPitch + L.blurOff, (uint32_t)(L.h * bp));
-  const int colA = cx - 18, psh = colA & 3;  // per-keypoint (half-wave) alignment
-  uint32_t pv[13];
-  {
-    const uint32_t pbase = (uint32_t)((cy - 18) * bp + (colA & ~3));
-#pragma unroll
-    for (int q = 0; q < 13; ++q) {
-      const int ii = min(hl + 32 * q, 37 * 11 - 1);
-      const int r = ii / 11, k = ii - r * 11;
-      pv[q] = buf_ld32(rb, pbase + (uint32_t)(r * bp + 4 * k));
-    }
-  }
-  // ---- IC_Angle, exact integer moments.  Row sum and u-moment are v_dot4
-  // products over 16-byte halves masked to |u| <= umax[|v|]:
-  // m10 = sum (u+16)*I - 16*sum I, m01 = sum v * rowsum.
-  int m01 = 0, m10 = 0;
-  {
-    const int ri = hl;
-    if (ri < 31) {
-      const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
-      const uint32_t o0 = (uint32_t)((cy + ri - 15) * pitch + cx - 16) + im.sh;
-      const uint32_t sh = o0 & 3u, a0 = o0 & ~3u;
-      uint32_t wv[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) wv[k] = buf_ld32(im.r, a0 + 4 * k);
-      uint32_t rs = 0, rm = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t d = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh) & c_icmask[ri][k];
-        const uint32_t wt = (uint32_t)(4 * k) * 0x01010101u + 0x03020100u;  // u + 16
-        rs = __builtin_amdgcn_udot4(d, 0x01010101u, rs, false);
-        rm = __builtin_amdgcn_udot4(d, wt, rm, false);
-      }
-      m10 = (int)rm - 16 * (int)rs;
-      m01 = (ri - 15) * (int)rs;
-    }
-  }
-  m01 = half_sum(m01);
-  m10 = half_sum(m10);
-  const float angle = fast_atan2_deg((float)m01, (float)m10);
-  // ---- rBRIEF on the blurred level
-  const float factorPI = (float)(3.14159265358979323846 / 180.f);
-  float a, b;
-  {
-    float sn, cs;
-    pinned_sincos(angle * factorPI, &sn, &cs);
-    a = cs;
-    b = sn;
-  }
-#pragma unroll
-  for (int q = 0; q < 13; ++q) {
-    const int ii = hl + 32 * q;
-    if (ii < 37 * 11) {
-      const int r = ii / 11, k = ii - r * 11;
-      patch[w][half][r][k] = pv[q];
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint8_t* pb = reinterpret_cast<const uint8_t*>(&patch[w][half][0][0]) +
-                      18 * (ORB_PATCH_DW * 4) + 18 + psh;
-  unsigned long long words[8];
-#pragma unroll
-  for (int kq = 0; kq < 8; ++kq) {
-    const int test = hl + 32 * kq;
-    // one 4-byte load per test (x0, y0, x1, y1 as int8)
-    const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
-    const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
-    // |rounded offsets| <= 19: 24-bit multiplies
-    const int v0 = pb[__mul24(cv_round(px0 * b + py0 * a), ORB_PATCH_DW * 4) + cv_round(px0 * a - py0 * b)];
-    const int v1 = pb[__mul24(cv_round(px1 * b + py1 * a), ORB_PATCH_DW * 4) + cv_round(px1 * a - py1 * b)];
-    words[kq] = __ballot(v0 < v1);
-  }
-  if (active && hl == 0) {
-    const long long o = (long long)img * capacity + base + i;
-    uint32_t d[8];
-#pragma unroll
-    for (int kq = 0; kq < 8; ++kq) d[kq] = (uint32_t)(words[kq] >> (32 * half));
-    uint4* dst = reinterpret_cast<uint4*>(desc + o * 32);
-    dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
-    dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
-    orb_keypoint_t kp;
-    kp.x = l ? (float)cx * L.scale : (float)cx;  // pt *= mvScaleFactor[level] (:1157-1165)
-    kp.y = l ? (float)cy * L.scale : (float)cy;
-    kp.size = L.sizeF;
-    kp.angle = angle;
-    kp.response = (float)key_s(key);
-    kp.octave = l;
-    kp.class_id = -1;
-    kps[o] = kp;
-  }
-}
-
 // ===================================================== k_orient_desc (fused)
 // IC_Angle + GaussianBlur 7x7 + rBRIEF + rescale in one pass, two keypoints
-// per wave (half-wave per keypoint, slot pairing as in k_orient_desc_split).
+// per wave (half-wave per keypoint, slot pairing as described above).
 // The blurred level is never materialised: descriptors sample only the 37 x 37
 // blurred patch around a keypoint (rotated pattern within +-18 px), and that
 // patch depends only on the 43 x 43 raw window around it, so each keypoint
@@ -2913,15 +2700,20 @@ hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s) {
 hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sw,
                             int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
                             int dh, const int* xofs, const void* alpha, const int* yofs,
-                            const void* beta, int xmax, int nimg, hipStream_t s) {
-  (void)xmax;  // folded into the alpha table: (2048, 0) past xmax
-  // tile bounds: narrow variant for a per-level downscale <= 1.25, wide <= 1.9
-  const bool wide = (double)sw / dw > 1.25 || (double)sh / dh > 1.25;
-  // each workgroup resizes one tile of ORB_RESIZE_IMAGES_PER_WG images (default
+                            const void* beta, int mode, int nimg, hipStream_t s) {
+  if (mode == ORB_RESIZE_GENERIC) {
+    hipLaunchKernelGGL(k_pyr_resize_generic, dim3((dw + 255) / 256, (dh + 3) / 4, nimg), dim3(256), 0,
+                       s, src, srcImgPitch, srcStride, sw, sh, dst, dstImgPitch, dstStride, dw, dh,
+                       xofs, (const int*)alpha, yofs, (const int*)beta);
+    return hipGetLastError();
+  }
+  // tile bounds (the planner picked the variant every tile of the level fits):
+  // narrow for a per-level downscale <= 1.25, wide beyond
+  const bool wide = mode == ORB_RESIZE_WIDE;
+  // each workgroup resizes one tile of PYR_IMAGES_PER_WG images (default
   // 16: with two extraction lanes 12 / 16 / 24 measured 323.8k / 322.3-324.4k /
   // 324.7k against 321.3-321.8k frames/s for 8, profiles/r03_lanes.txt)
-  static const int perWg =
-      getenv("ORB_RESIZE_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_RESIZE_IMAGES_PER_WG"))) : 16;
+  constexpr int perWg = PYR_IMAGES_PER_WG;
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, (nimg + perWg - 1) / perWg),
       block(256);
   // every image base and row start 4-aligned: one load per staged dword
@@ -2936,77 +2728,6 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   else ORB_RESIZE_LAUNCH(false, PYR_SROWS_WIDE, PYR_SW_WIDE);
 #undef ORB_RESIZE_LAUNCH
   return hipGetLastError();
-}
-
-// the resize chain of nimg (1 or 2) images in one launch; bands and the two
-// LDS buffers' sizes (even levels, odd levels) from orb_pyr_chain_plan
-hipError_t orb_k_pyr_chain(const uint8_t* img0, long long imgPitch, int img0Stride, uint8_t* arena,
-                           long long arenaPitch, const OrbPlanDesc* plan, const int32_t* rt,
-                           const void* bands, int nb, const int* bufBytes, int nimg, hipStream_t s) {
-  const size_t lds = (size_t)bufBytes[0] + bufBytes[1];
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_pyr_chain<512>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(k_pyr_chain<512>, dim3(nb, nimg), dim3(512), lds, s, img0, imgPitch, img0Stride,
-                     arena, arenaPitch, *plan, rt, (const OrbChainBand*)bands, bufBytes[0]);
-  return hipGetLastError();
-}
-
-// Plans k_pyr_chain's bands for a plan whose resize tables are `rtab` (host
-// copy): the smallest band count from 16 up (doubling) whose two LDS buffers
-// (rows of the even levels, of the odd levels; bufBytes[0], bufBytes[1]) fit
-// `ldsMax` bytes together; returns the band count (0: none fits) and fills `out`.
-int orb_pyr_chain_plan(const OrbPlanDesc* plan, const int32_t* rtab, size_t ldsMax, void* out,
-                       int maxBands, int* bufBytes) {
-  const int L = plan->nlevels;
-  OrbChainBand* bd = (OrbChainBand*)out;
-  for (int nb = 16; nb <= maxBands; nb *= 2) {
-    int need[2] = {0, 0};
-    bool ok = true;
-    for (int b = 0; b < nb && ok; ++b) {
-      OrbChainBand& B = bd[b];
-      for (int l = 0; l < L; ++l) {
-        const int h = plan->lv[l].h;
-        B.own[l] = (int16_t)((long long)b * h / nb);
-        B.ownEnd[l] = (int16_t)((long long)(b + 1) * h / nb);
-      }
-      if (L > 0) {
-        B.lo[L - 1] = B.own[L - 1];
-        B.hi[L - 1] = B.ownEnd[L - 1];
-      }
-      for (int l = L - 1; l >= 1; --l) {
-        const OrbLevelDesc& d = plan->lv[l];
-        const int sh = plan->lv[l - 1].h;
-        int lo = B.own[l - 1], hi = B.ownEnd[l - 1];
-        if (B.hi[l] > B.lo[l]) {
-          const int32_t* yo = rtab + d.rtabY;
-          int a = 1 << 30, e = -1;
-          for (int y = B.lo[l]; y < B.hi[l]; ++y) {
-            a = std::min(a, std::min(std::max(yo[y], 0), sh - 1));
-            e = std::max(e, std::min(std::max(yo[y] + 1, 0), sh - 1) + 1);
-          }
-          if (hi <= lo) { lo = a; hi = e; }
-          else { lo = std::min(lo, a); hi = std::max(hi, e); }
-        }
-        B.lo[l - 1] = (int16_t)lo;
-        B.hi[l - 1] = (int16_t)std::max(lo, hi);
-      }
-      for (int l = 0; l < L; ++l) {
-        const int bytes = (B.hi[l] - B.lo[l]) * orb_chain_pitch(plan->lv[l].w);
-        need[l & 1] = std::max(need[l & 1], bytes);
-        if (B.hi[l] - B.lo[l] > ORB_CHAIN_MAX_ROWS) ok = false;
-      }
-    }
-    const int b0 = (need[0] + 15) & ~15, b1 = (need[1] + 15) & ~15;
-    if (ok && (size_t)b0 + b1 <= ldsMax) {
-      bufBytes[0] = b0;
-      bufBytes[1] = b1;
-      return nb;
-    }
-  }
-  return 0;
 }
 
 // Dynamic LDS of k_fast_band for bands of up to `bandElems` elements (rows x
@@ -3027,9 +2748,7 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
   // each workgroup takes ORB_FAST_BANDS_PER_WG bands (default 2; swept 1-8), prefetching the next
   // (one band per workgroup for a frame or two per call: the grid is small and
   // the per-workgroup band chain is the latency)
-  static const int perWgEnv =
-      getenv("ORB_FAST_BANDS_PER_WG") ? std::max(1, atoi(getenv("ORB_FAST_BANDS_PER_WG"))) : 0;
-  const int perWg = perWgEnv ? perWgEnv : (nimg <= 2 ? 1 : 2);
+  const int perWg = nimg <= 2 ? 1 : 2;
   if ((size_t)plan->maxBandBytes > (size_t)4 * FAST_LOADS * 256) return hipErrorInvalidValue;
   dim3 grid((nbands + perWg - 1) / perWg, nimg), block(256);
   hipLaunchKernelGGL(k_fast_band, grid, block, lds, s, img0, img0Pitch, img0Stride, arena,
@@ -3070,8 +2789,7 @@ hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0St
   const size_t lds = orb_k_fast_cells_lds(mr, mc);
   // every W = 30 cell grid of the ORB-SLAM2 configurations has ROI widths of
   // 36-43 pixels: pitch 48 (56 without FC_TIGHT), the compile-time instance
-  static const bool noConstPitch = getenv("ORB_FAST_RT_PITCH") && atoi(getenv("ORB_FAST_RT_PITCH")) > 0;
-  const bool p56 = fc_pitch(mc) == FC_CONST_PITCH && !noConstPitch;
+  const bool p56 = fc_pitch(mc) == FC_CONST_PITCH;
   const void* fn = p56 ? (const void*)k_fast_cells<FC_CONST_PITCH> : (const void*)k_fast_cells<0>;
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -3131,10 +2849,9 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
   // Batches take 256-thread workgroups: the octree alone is slower (0.150 vs
   // 0.132 ms per 512 frames) but the smaller workgroups fit better beside the
   // other lane's kernels (bench 317.0k / 316.6k vs 315.5k / 315.2k frames/s,
-  // two interleaved pairs, profiles/r03_octree256.txt); ORB_OCTREE_THREADS=512
-  // restores the old shape
-  static const int bthreads =
-      getenv("ORB_OCTREE_THREADS") && atoi(getenv("ORB_OCTREE_THREADS")) == 512 ? 512 : 256;
+  // two interleaved pairs, profiles/r03_octree256.txt); 512 threads
+  // was the old shape
+  constexpr int bthreads = 256;
   dim3 grid(nimg, levelEnd - levelBeg), block(reg ? 512 : bthreads);
 #define ORB_OCTREE_LAUNCH(R, G)                                                                 \
   hipLaunchKernelGGL((k_octree<R, G>), grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,  \
@@ -3152,27 +2869,11 @@ hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
                              int nimg, hipStream_t s) {
-  // each workgroup blurs one tile of ORB_BLUR_IMAGES_PER_WG images (default 8; swept 2-16)
-  static const int perWg =
-      getenv("ORB_BLUR_IMAGES_PER_WG") ? std::max(1, atoi(getenv("ORB_BLUR_IMAGES_PER_WG"))) : 8;
+  // each workgroup blurs one tile of 8 images (swept 2-16)
+  constexpr int perWg = 8;
   dim3 grid(plan->nBlurTiles, (nimg + perWg - 1) / perWg), block(256);
   hipLaunchKernelGGL(k_blur_levels, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
                      arenaPitch, *plan, tiles, blur, blurPitch, nimg);
-  return hipGetLastError();
-}
-
-hipError_t orb_k_orient_desc_split(const uint8_t* img0, long long img0Pitch, int img0Stride,
-                                   const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
-                                   long long blurPitch, const OrbPlanDesc* plan,
-                                   const uint32_t* outKeys, const int32_t* outCount,
-                                   const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
-                                   int capacity, int32_t* counts, int nimg, hipStream_t s) {
-  // 4 waves x 2 slots per workgroup; slotsPerImage and every level's outOff are even
-  if (plan->slotsPerImage & 1) return hipErrorInvalidValue;
-  dim3 grid((plan->slotsPerImage + 7) / 8, nimg), block(256);
-  hipLaunchKernelGGL(k_orient_desc_split, grid, block, 0, s, img0, img0Pitch, img0Stride, arena,
-                     arenaPitch, blur, blurPitch, *plan, outKeys, outCount, errFlag, kps, desc,
-                     capacity, counts);
   return hipGetLastError();
 }
 
@@ -3189,9 +2890,8 @@ hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0S
   if ((slotBeg | slotEnd) & 1) return hipErrorInvalidValue;
   // DESC_PPW keypoint pairs per wave for batches (the next pair's loads overlap
   // the current one); one pair per wave for a frame or two per call, where the
-  // grid is small and the per-wave chain is the latency (ORB_DESC_PPW overrides)
-  static const int kPpw = getenv("ORB_DESC_PPW") ? atoi(getenv("ORB_DESC_PPW")) : 0;
-  const int ppw = kPpw == 1 || kPpw == DESC_PPW ? kPpw : (nimg <= 2 ? 1 : DESC_PPW);
+  // grid is small and the per-wave chain is the latency
+  const int ppw = nimg <= 2 ? 1 : DESC_PPW;
   dim3 grid((slotEnd - slotBeg + 8 * ppw - 1) / (8 * ppw), nimg), block(256);
   if (ppw == DESC_PPW)
     hipLaunchKernelGGL(k_orient_desc<DESC_PPW>, grid, block, 0, s, img0, img0Pitch, img0Stride,

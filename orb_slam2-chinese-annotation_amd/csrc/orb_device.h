@@ -120,6 +120,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 __device__ __forceinline__ uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
 }
+__device__ __forceinline__ uint32_t buf_ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b8(r, (int)off, 0, 0);
+}
 __device__ __forceinline__ void buf_st32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
   __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
 }

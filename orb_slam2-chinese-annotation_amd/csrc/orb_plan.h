@@ -30,9 +30,14 @@ struct OrbLevelDesc {
   float sizeF;       // (float)(int)(31 * scale), src/ORBextractor.cc:874
   int rtabX, rtabY;  // offsets of this level's resize tables (x: xofs/alpha, y: yofs/beta)
   int xmax;          // first dx whose source tap sx+1 falls outside (resize)
+  int resizeMode;    // ORB_RESIZE_NARROW / _WIDE / _GENERIC: k_pyr_resize variant for this level
   int tileBeg;       // first blur tile of this level
   int cellMaxRows, cellMaxCols;  // largest cell ROI of this level (k_fast_cells LDS per launch)
 };
+
+#define ORB_RESIZE_NARROW 0   // 44 x 44-dword source windows (downscale <= 1.25)
+#define ORB_RESIZE_WIDE 1     // 64 x 64 dwords
+#define ORB_RESIZE_GENERIC 2  // untiled: each thread reads its taps from the source level
 
 struct OrbPlanDesc {
   int nlevels;
@@ -62,6 +67,7 @@ struct OrbBandDesc {
   int16_t level, y0, y1, x0, x1, nCells;
   int32_t cellBeg;
 };
+#define ORB_OCTREE_LDS_KB 52  // k_octree node tables + keys per workgroup (swept 24-64)
 #define ORB_BAND_BYTES 6656  // elements (rows x LDS pitch) of one FAST band: f16 pixels + strengths; 5 workgroups per CU (swept 4-10 K)
 
 // One ORB_BLUR_TW x ORB_BLUR_TH output tile of the 7x7 Gaussian pass over level `level`.
@@ -71,14 +77,3 @@ struct OrbTileDesc {
 #define ORB_BLUR_TW 128
 #define ORB_BLUR_TH 32
 
-// k_pyr_chain (one or two frames per call): workgroup b computes rows
-// [lo[l], hi[l]) of every level l >= 1 from the previous level's rows held in
-// LDS (level 0: rows [lo[0], hi[0]) of the caller's image, staged) and writes
-// the rows it owns, [own[l], ownEnd[l]), to the arena.  The owned rows split
-// each level evenly over the bands; lo / hi add the rows the band's owned rows
-// of the levels above need.
-struct OrbChainBand {
-  int16_t lo[ORB_MAX_LEVELS], hi[ORB_MAX_LEVELS], own[ORB_MAX_LEVELS], ownEnd[ORB_MAX_LEVELS];
-};
-__host__ __device__ inline int orb_chain_pitch(int w) { return (w + 3) & ~3; }
-#define ORB_CHAIN_MAX_ROWS 512  // rows a band computes at one level (row-tap table in LDS)

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <cmath>
 #include <vector>
 
 #include "../../include/orb_abi.h"
@@ -26,12 +27,7 @@ hipError_t orb_k_upload_umax(const int* umax16, hipStream_t s);
 hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcStride, int sw,
                             int sh, uint8_t* dst, long long dstImgPitch, int dstStride, int dw,
                             int dh, const int* xofs, const void* alpha, const int* yofs,
-                            const void* beta, int xmax, int nimg, hipStream_t s);
-hipError_t orb_k_pyr_chain(const uint8_t* img0, long long imgPitch, int img0Stride, uint8_t* arena,
-                           long long arenaPitch, const OrbPlanDesc* plan, const int32_t* rt,
-                           const void* bands, int nb, const int* bufBytes, int nimg, hipStream_t s);
-int orb_pyr_chain_plan(const OrbPlanDesc* plan, const int32_t* rtab, size_t ldsMax, void* out,
-                       int maxBands, int* bufBytes);
+                            const void* beta, int mode, int nimg, hipStream_t s);
 size_t orb_k_fast_band_lds(int bandElems);
 size_t orb_k_fast_cells_lds(int maxRows, int maxCols);
 bool orb_k_fast_cells_fits(const OrbPlanDesc* plan);
@@ -54,12 +50,6 @@ hipError_t orb_k_blur_levels(const uint8_t* img0, long long img0Pitch, int img0S
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const OrbTileDesc* tiles, uint8_t* blur, long long blurPitch,
                              int nimg, hipStream_t s);
-hipError_t orb_k_orient_desc_split(const uint8_t* img0, long long img0Pitch, int img0Stride,
-                                   const uint8_t* arena, long long arenaPitch, const uint8_t* blur,
-                                   long long blurPitch, const OrbPlanDesc* plan,
-                                   const uint32_t* outKeys, const int32_t* outCount,
-                                   const int32_t* errFlag, orb_keypoint_t* kps, uint8_t* desc,
-                                   int capacity, int32_t* counts, int nimg, hipStream_t s);
 hipError_t orb_k_orient_desc(const uint8_t* img0, long long img0Pitch, int img0Stride,
                              const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                              const uint32_t* outKeys, const int32_t* outCount,
@@ -190,6 +180,61 @@ namespace {
       return _e == hipErrorOutOfMemory ? ORB_ENOMEM : ORB_EDEVICE; \
     }                                                   \
   } while (0)
+
+// A call's launch sequence replayed as one hipGraph once the same call (same
+// key: every pointer, size and parameter its kernels capture) repeats.  Small
+// calls are launch-bound -- one frame is 7 dependent resize launches plus
+// FAST, octree and descriptors, a few microseconds each -- and a replayed
+// graph submits them at once.  The first call of a key runs directly (a
+// caller cycling through buffers never pays a capture); the second captures
+// on the handle's own stream and replays onto the caller's.
+struct CallGraph {
+  hipGraphExec_t exec = nullptr;
+  std::vector<uintptr_t> key, lastKey;
+  void reset() {
+    if (exec) hipGraphExecDestroy(exec);
+    exec = nullptr;
+    key.clear();
+  }
+};
+template <class F>
+static orb_status_t run_graphed(CallGraph& g, const std::vector<uintptr_t>& key,
+                                hipStream_t capStream, hipStream_t s, F&& enqueue) {
+  // a caller capturing its own graph gets the launches themselves
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cst) != hipSuccess || cst != hipStreamCaptureStatusNone)
+    return enqueue(s, false);
+  if (g.exec && key == g.key) {
+    if (hipGraphLaunch(g.exec, s) != hipSuccess) return ORB_EDEVICE;
+    return ORB_OK;
+  }
+  if (key != g.lastKey) {
+    g.lastKey = key;
+    return enqueue(s, false);
+  }
+  g.reset();
+  hipGraph_t graph = nullptr;
+  if (hipStreamBeginCapture(capStream, hipStreamCaptureModeThreadLocal) != hipSuccess)
+    return ORB_EDEVICE;
+  const orb_status_t st = enqueue(capStream, true);
+  const hipError_t ce = hipStreamEndCapture(capStream, &graph);
+  if (st) {
+    if (graph) hipGraphDestroy(graph);
+    return st;
+  }
+  if (ce != hipSuccess) return ORB_EDEVICE;
+  const hipError_t ie = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  if (ie != hipSuccess) {
+    g.exec = nullptr;
+    return ORB_EDEVICE;
+  }
+  g.key = key;
+  if (hipGraphLaunch(g.exec, s) != hipSuccess) return ORB_EDEVICE;
+  return ORB_OK;
+}
+// calls of at most this many frames / problems replay graphs
+#define GRAPH_MAX_BATCH 16
 
 static inline int cvRoundF(float v) { return (int)lrintf(v); }
 static inline short satShort(int v) { return (short)std::min(std::max(v, -32768), 32767); }
@@ -360,13 +405,10 @@ struct orb_extractor {
   std::vector<int> quota;
   int umax[16];
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // side stream: FAST beside the resize chain (blur in split mode)
-  bool sharedSide = false;        // stream2 is the device's shared side stream (not destroyed)
+  hipStream_t stream2 = nullptr;  // the device's shared side stream: FAST beside the resize chain
   hipStream_t privSide = nullptr; // this handle's side stream while its caller's stream is captured
-  hipStream_t stream3 = nullptr;  // resize chain, high priority (ORB_CHAIN_STREAM=1)
-  hipEvent_t evFork = nullptr, evJoin = nullptr;
   hipEvent_t evL0Fork = nullptr, evL0Join = nullptr;  // level-0 FAST beside the resize chain
-  hipEvent_t evLvl[ORB_MAX_LEVELS] = {};  // level l written by the resize chain (per-level FAST)
+  hipEvent_t evLvl = nullptr;  // the resize chain has written level FAST_SIDE_LEVELS
   hipEvent_t evBatch = nullptr;  // recorded at the end of every run_batch on its stream
   bool ownStream = false;
   std::mutex mu;
@@ -378,13 +420,11 @@ struct orb_extractor {
   long long arenaBytes = 0, blurBytes = 0;
   int maxCellsPerLevel = 0, nodeCapMax = 0, ldsKeyCap = 0;
   DevBuf dCells, dRtab, dTiles, dBands;
-  // k_pyr_chain bands (the one-launch resize chain of one- or two-frame calls)
-  DevBuf dChain;
-  int chainNb = 0, chainBuf[2] = {0, 0};
 
   // batch scratch
   int batchCap = 0;
-  DevBuf dArena, dBlur, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
+  DevBuf dBlur;  // one image's blurred levels (orb_extractor_blurred_level, on demand)
+  DevBuf dArena, dCellKeys, dCellCount, dGKeys, dGNid, dOutKeys, dOutCount, dErr;
   DevBuf dOctNodes;            // octree node tables in global memory (large nfeatures)
   long long octNodeBytes = 0;  // per (image, level) slice; 0: node tables in LDS
   // single-image API scratch
@@ -403,6 +443,7 @@ struct orb_extractor {
   // plan; keyed by the buffers it captured (any reallocation re-captures)
   hipGraphExec_t oneExec = nullptr;
   std::vector<const void*> oneKey;
+  CallGraph batchGraph;  // small extract_batch calls (run_graphed)
   int lastW = 0, lastH = 0;
   size_t lastImgStride = 0;
   const uint8_t* lastImg0 = nullptr;  // level 0 of the last batch (device)
@@ -470,16 +511,17 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   std::vector<OrbTileDesc> tiles;
   std::vector<OrbBandDesc> bands;
   int maxBandBytes = 0;
-  static const int bandBudget =
-      getenv("ORB_BAND_BYTES") ? std::min(8192, std::max(2048, atoi(getenv("ORB_BAND_BYTES"))))
-                               : ORB_BAND_BYTES;  // k_fast_band stages <= 8192 elements per pass
+  const int bandBudget = ORB_BAND_BYTES;  // k_fast_band stages <= 8192 elements per pass
   long long arena = 0, blurArena = 0;
   int keyCap = 1, maxRows = 7, maxCols = 7, maxCellsPerLevel = 1, nodeCapMax = 1, slots = 0;
   for (int l = 0; l < L; ++l) {
     OrbLevelDesc& d = P.lv[l];
     d.w = l ? cvRoundF((float)W * h->invScale[l]) : W;  // src/ORBextractor.cc:1180
     d.h = l ? cvRoundF((float)H * h->invScale[l]) : H;
-    if (d.w < 40 || d.h < 40 || d.w > 4095 || d.h > 4095) return ORB_EINVAL;
+    // a level needs more than the 2 x 16 px FAST border in each direction
+    // (src/ORBextractor.cc:797-800); at 32 px or less the reference's
+    // DistributeOctTree divides by zero or sizes a vector negatively (:562-569)
+    if (d.w < 33 || d.h < 33 || d.w > 4095 || d.h > 4095) return ORB_EINVAL;
     d.pitch = ((d.w + 127) & ~127) | 128;  // odd multiple of 128 B: whole-line rows, channel spread
     d.arenaOff = l ? arena : 0;
     if (l) arena += (long long)d.pitch * d.h;
@@ -537,7 +579,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     }
     d.cellEnd = (int)cells.size();
     // FAST bands: runs of consecutive cells of one cell row whose union ROI
-    // fits the band LDS budget (k_fast_band; ORB_BAND_BYTES, env ORB_BAND_BYTES)
+    // fits the band LDS budget (k_fast_band; ORB_BAND_BYTES)
     for (int c = d.cellBeg; c < d.cellEnd;) {
       OrbBandDesc b;
       b.level = (int16_t)l;
@@ -569,9 +611,17 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     d.Wr = maxBX - minBX;
     d.Hr = maxBY - minBY;
     d.nIni = (int)roundf((float)d.Wr / d.Hr);
-    if (d.nIni <= 0) return ORB_EINVAL;
+    // no root at all (width under half the height): the reference indexes an
+    // empty root vector for every key (:569,588); a level without cells has no
+    // keys, so one root stands in for none
+    if (d.nIni <= 0 && d.cellEnd > d.cellBeg) return ORB_EINVAL;
+    d.nIni = std::max(d.nIni, 1);
     d.hX = (float)d.Wr / d.nIni;
     d.nodeCap = (std::max(d.quota + 4, 4 * d.nIni + 4) + 1) & ~1;  // even: k_orient_desc slot pairs
+    // k_octree labels a level's keys with 16-bit node indices (its final-phase
+    // sort key packs size 24 | creation order 24 | node 16 bits): a level's
+    // quota may reach 65,530 (nfeatures ~300,000 at 1.2 / 8 levels)
+    if (d.nodeCap > 65534) return ORB_EINVAL;
     nodeCapMax = std::max(nodeCapMax, d.nodeCap);
     d.outOff = slots;
     slots += d.nodeCap;
@@ -607,24 +657,34 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
         rtab[d.rtabY + d.h + dy] = (int32_t)(((uint32_t)(uint16_t)b1 << 16) | (uint16_t)b0);
       }
       // k_pyr_resize stages each 128 x 32 output tile's source window in LDS
-      // (narrow 44 x 44 dwords up to a 1.25 downscale, wide 64 x 64 beyond):
-      // every tile of this level must fit the variant orb_k_pyr_resize picks
-      const bool wide = (double)sw / d.w > 1.25 || (double)sh / d.h > 1.25;
-      const int SR = wide ? 64 : 44, SWd = wide ? 64 : 44;
+      // (narrow 44 x 44 dwords up to a 1.25 downscale, wide 64 x 64 beyond),
+      // and each thread's 4 columns read 8 staged source bytes: the level takes
+      // the first variant every tile fits, else the untiled generic kernel
+      // (per-level downscales beyond ~1.9: scaleFactor > 1.9, which no
+      // ORB-SLAM2 configuration uses)
       const int32_t* xo = &rtab[d.rtabX];
       const int32_t* yo = &rtab[d.rtabY];
-      for (int x0 = 0; x0 < d.w; x0 += 128) {
-        const int xl = std::min(x0 + 127, d.w - 1), xt = std::min(x0 + 124, d.w - 1);
-        const int colBase = xo[x0] & ~3, sxB = std::min(xo[xl] + 1, sw - 1);
-        const int nW = ((sxB - colBase) >> 2) + 1, lastRead = ((xo[xt] - colBase) >> 2) + 2;
-        if (nW > 64 || nW > SWd || lastRead >= SWd) return ORB_EINVAL;
-      }
-      for (int y0 = 0; y0 < d.h; y0 += 32) {
-        const int yl = std::min(y0 + 31, d.h - 1);
-        const int syA = std::min(std::max(yo[y0], 0), sh - 1);
-        const int syB = std::min(std::max(yo[yl] + 1, 0), sh - 1);
-        if (syB - syA + 1 > SR) return ORB_EINVAL;
-      }
+      auto tiles_fit = [&](int SR, int SWd) {
+        for (int x = 0; x < d.w; x += 4)
+          if (xo[std::min(x + 3, d.w - 1)] - xo[x] > 6) return false;
+        for (int x0 = 0; x0 < d.w; x0 += 128) {
+          const int xl = std::min(x0 + 127, d.w - 1), xt = std::min(x0 + 124, d.w - 1);
+          const int colBase = xo[x0] & ~3, sxB = std::min(xo[xl] + 1, sw - 1);
+          const int nW = ((sxB - colBase) >> 2) + 1, lastRead = ((xo[xt] - colBase) >> 2) + 2;
+          if (nW > 64 || nW > SWd || lastRead >= SWd) return false;
+        }
+        for (int y0 = 0; y0 < d.h; y0 += 32) {
+          const int yl = std::min(y0 + 31, d.h - 1);
+          const int syA = std::min(std::max(yo[y0], 0), sh - 1);
+          const int syB = std::min(std::max(yo[yl] + 1, 0), sh - 1);
+          if (syB - syA + 1 > SR) return false;
+        }
+        return true;
+      };
+      const bool narrowOk = (double)sw / d.w <= 1.25 && (double)sh / d.h <= 1.25;
+      d.resizeMode = narrowOk && tiles_fit(44, 44) ? ORB_RESIZE_NARROW
+                     : tiles_fit(64, 64)          ? ORB_RESIZE_WIDE
+                                                  : ORB_RESIZE_GENERIC;
     }
   }
   // k_fast_band: one band = at least one cell; its pixels and scores + the
@@ -639,11 +699,10 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   P.maxCellRows = maxRows;
   P.maxCellCols = maxCols;
   // octree LDS: node tables + keys within ~52 KiB (three workgroups per CU
-  // overlap their latency-bound passes); a level with more candidate keys
-  // keeps them in global scratch instead (ORB_OCTREE_LDS_KB overrides)
+  // overlap their latency-bound passes; budgets of 24-64 KiB measured 52 +- 1 %);
+  // a level with more candidate keys keeps them in global scratch instead
   const size_t nodeBytes = orb_k_octree_lds(nodeCapMax, maxCellsPerLevel, 0);
-  const char* lk = getenv("ORB_OCTREE_LDS_KB");
-  const size_t budget = (size_t)(lk ? std::max(16, std::min(150, atoi(lk))) : 52) * 1024;
+  const size_t budget = (size_t)ORB_OCTREE_LDS_KB * 1024;
   // node tables beyond 128 KiB (nfeatures above ~7,500 at 1.2 / 8 levels) go
   // to a global scratch slice per (image, level); the LDS then holds keys only
   const bool octGlobal = nodeBytes > 128 * 1024;
@@ -670,22 +729,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (!rtab.empty())
     HIP_TRY(hipMemcpyAsync(h->dRtab.p, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice,
                            h->stream));
-  // the one-launch resize chain for small calls: 16-128 bands whose LDS rows fit
-  // 150 KB (one workgroup per CU; none fits: the per-level launches)
-  std::vector<OrbChainBand> chain(128);
-  int chainBuf[2] = {0, 0};
-  const int chainNb = P.nlevels > 1 ? orb_pyr_chain_plan(&P, rtab.data(), 150 * 1024, chain.data(), 128,
-                                                         chainBuf)
-                                    : 0;
-  if (chainNb > 0) {
-    if ((st = h->dChain.ensure((size_t)chainNb * sizeof(OrbChainBand)))) return st;
-    HIP_TRY(hipMemcpyAsync(h->dChain.p, chain.data(), (size_t)chainNb * sizeof(OrbChainBand),
-                           hipMemcpyHostToDevice, h->stream));
-  }
   HIP_TRY(hipStreamSynchronize(h->stream));
-  h->chainNb = chainNb;
-  h->chainBuf[0] = chainBuf[0];
-  h->chainBuf[1] = chainBuf[1];
   h->plan = P;
   h->cells.swap(cells);
   h->arenaBytes = (arena + 255) & ~255LL;
@@ -700,23 +744,12 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   return ORB_OK;
 }
 
-// ORB_SPLIT_BLUR=1: the round-1 split path (k_blur_levels writes every blurred
-// level, k_orient_desc_split samples them) for A/B runs; default is the fused
-// k_orient_desc, which blurs each keypoint's window in LDS.
-static bool split_blur() {
-  static const bool v = getenv("ORB_SPLIT_BLUR") && atoi(getenv("ORB_SPLIT_BLUR")) > 0;
-  return v;
-}
-
 static orb_status_t ensure_batch(orb_extractor* h, int B) {
   if (B <= h->batchCap) return ORB_OK;
   const OrbPlanDesc& P = h->plan;
   const size_t cellSlots = (size_t)B * P.ncells * P.keyCap;
   orb_status_t st;
   if ((st = h->dArena.ensure((size_t)B * h->arenaBytes))) return st;
-  // the blurred levels are materialised only in the split A/B mode
-  // (ORB_SPLIT_BLUR=1); orb_extractor_blurred_level blurs one image on demand
-  if (split_blur() && (st = h->dBlur.ensure((size_t)B * h->blurBytes))) return st;
   if ((st = h->dCellKeys.ensure(cellSlots * 4))) return st;
   if ((st = h->dGKeys.ensure(cellSlots * 4))) return st;
   if ((st = h->dGNid.ensure(cellSlots * 2))) return st;
@@ -731,124 +764,90 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
   return ORB_OK;
 }
 
-static int stream_prio(const char* var, const char* dflt);
+static int stream_prio(bool least);
+
+// Schedule constants of run_batch (compile-time A/B: tools/build_variant.sh)
+#ifndef FAST_CELLS_MIN_BATCH
+#define FAST_CELLS_MIN_BATCH 4  // smaller calls take k_fast_band on one stream
+#endif
+#ifndef FAST_SIDE_LEVELS
+// levels 1..FAST_SIDE_LEVELS follow level 0 on the side stream: extraction
+// alone 1.770 / 1.723 / 1.708 / 1.709 ms per 512 frames for 0 / 1 / 2 / 3,
+// bench 259.7k / 262.3k / 263.6k / 263.4k frames/s (profiles/r03_schedule_xcd.txt)
+#define FAST_SIDE_LEVELS 2
+#endif
+#ifndef FAST_L0_INLINE
+#define FAST_L0_INLINE 0  // 1: level 0's FAST on the caller's stream (one dispatch; PMC passes)
+#endif
 
 static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, size_t stride,
                               size_t imgPitch, orb_keypoint_t* d_kps, uint8_t* d_desc,
                               int capacity, int32_t* d_counts, hipStream_t s,
                               bool capturing = false) {
   // Stage chain: pyramid -> FAST -> octree -> orient + blur + descriptors
-  // (k_orient_desc blurs each keypoint's window in LDS).  Split A/B mode
-  // (ORB_SPLIT_BLUR=1): k_blur_levels writes every blurred level after FAST,
-  // optionally on a side stream (ORB_EXTRACT_STREAMS=2, fork/join by events).
+  // (k_orient_desc blurs each keypoint's window in LDS).
   const OrbPlanDesc& P = h->plan;
   const int32_t* rt = h->dRtab.as<int32_t>();
   uint8_t* arena = h->dArena.as<uint8_t>();
   const long long ap = h->arenaBytes;
-  static const bool sideStream =
-      getenv("ORB_EXTRACT_STREAMS") && atoi(getenv("ORB_EXTRACT_STREAMS")) > 1;
   // the side stream: the device's shared one, or -- while the caller's stream
   // is being captured into a graph -- a stream of this handle's own, so a
   // capture never pulls another handle's side work into its graph
   hipStream_t side = h->stream2;
-  if (h->sharedSide) {
+  {
     hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone) {
-      if (!h->privSide && hipStreamCreateWithPriority(&h->privSide, hipStreamNonBlocking,
-                                                      stream_prio("ORB_STREAM2_PRIO", "least")) != hipSuccess) {
+      if (!h->privSide &&
+          hipStreamCreateWithPriority(&h->privSide, hipStreamNonBlocking, stream_prio(true)) != hipSuccess) {
         h->privSide = nullptr;
         return ORB_EDEVICE;
       }
       side = h->privSide;
     }
   }
-  hipStream_t s2 = sideStream ? side : s;
   StageProfiler& pf = h->prof;
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
   // the FAST kernels clear each image's status flag (one launch fewer per call);
   // a plan without cells launches no FAST kernel
   if (P.ncells == 0) HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
-  static const bool bandFast = getenv("ORB_FAST_BANDS") && atoi(getenv("ORB_FAST_BANDS")) > 0;
-  static const int kCellsMinBatch =
-      getenv("ORB_FAST_CELLS_MIN_BATCH") ? atoi(getenv("ORB_FAST_CELLS_MIN_BATCH")) : 4;
-  static const bool noL0Overlap = getenv("ORB_FAST_L0_INLINE") && atoi(getenv("ORB_FAST_L0_INLINE")) > 0;
   // k_fast_cells (one wave per cell) unless a tiny level's cells outgrow its
-  // staging; k_fast_band (one workgroup per run of cells) otherwise or on request
-  // (a frame or two per call: the band kernel's fewer, larger workgroups and a
+  // staging; k_fast_band (one workgroup per run of cells) otherwise and for a
+  // frame or two per call (the band kernel's fewer, larger workgroups and a
   // single stream give the lower latency)
-  const bool useBands = bandFast || B < kCellsMinBatch || !orb_k_fast_cells_fits(&P);
+  const bool useBands = B < FAST_CELLS_MIN_BATCH || !orb_k_fast_cells_fits(&P);
   pf.names[2] = useBands ? "k_fast_band" : "k_fast_cells";
   // Level 0 is the caller's image: its FAST cells need no pyramid, so they run
   // on the side stream beside the latency-bound resize chain (fork / join by
   // events, graph-capturable).  Levels 1..sideLevels follow on the side stream
   // in one launch once the chain has written level sideLevels; the rest follow
-  // the chain on the main stream.
+  // the chain on the main stream.  (Measured and not kept: every level on the
+  // side stream as the chain writes it, 255k vs 260k frames/s, the chain losing
+  // its CUs to FAST, profiles/r03_fast_schedule.txt; the octree and descriptors
+  // of the side levels on the side stream too, round 4.)
   const int l0End = P.lv[0].cellEnd;
   // (profile mode 2 times each stage alone: no side stream)
-  const bool l0Side = !useBands && !noL0Overlap && !(ev && pf.serial) && l0End > 0 && P.nlevels > 1;
-  // ORB_FAST_PER_LEVEL=1 (A/B knob, off): levels >= 1 on the side stream too,
-  // each launched as soon as the chain has written its level.  Measured slower
-  // (255k vs 260k frames/s; the chain, 0.52 -> 0.81 ms, loses its CUs to FAST),
-  // with or without stream priorities (profiles/r03_fast_schedule.txt)
-  static const bool fastPerLevelEnv =
-      getenv("ORB_FAST_PER_LEVEL") && atoi(getenv("ORB_FAST_PER_LEVEL")) > 0;
-  const bool perLevel = l0Side && fastPerLevelEnv;
-  // ORB_FAST_SIDE_LEVELS=n (default 2): extraction alone 1.770 / 1.723 /
-  // 1.708 / 1.709 ms per 512 frames for n = 0 / 1 / 2 / 3, bench 259.7k /
-  // 262.3k / 263.6k / 263.4k frames/s (profiles/r03_schedule_xcd.txt)
-  static const int sideLevelsEnv =
-      getenv("ORB_FAST_SIDE_LEVELS") ? std::max(0, atoi(getenv("ORB_FAST_SIDE_LEVELS"))) : 2;
-  const int sideLevels = (l0Side && !perLevel) ? std::min(sideLevelsEnv, P.nlevels - 1) : 0;
+  const bool l0Side = !useBands && !FAST_L0_INLINE && !(ev && pf.serial) && l0End > 0 && P.nlevels > 1;
+  const int sideLevels = l0Side ? std::min(FAST_SIDE_LEVELS, P.nlevels - 1) : 0;
   const int sideEnd = sideLevels > 0 ? P.lv[sideLevels].cellEnd : l0End;
-  // ORB_SIDE_TAIL=1 (A/B knob): the side stream also runs the octree and
-  // k_orient_desc of its levels 0..sideLevels, beside the main stream's FAST /
-  // octree of the rest; the main stream's k_orient_desc (which writes the
-  // counts) waits for the side octree, and the call ends on both streams
-  static const bool sideTailEnv = getenv("ORB_SIDE_TAIL") && atoi(getenv("ORB_SIDE_TAIL")) > 0;
-  const bool sideTail = sideTailEnv && l0Side && !perLevel && !split_blur() && sideLevels > 0 &&
-                        sideLevels + 1 < P.nlevels;
-  const int tailSplit = sideLevels + 1;  // first level of the main stream's tail
-  // with a split tail, octrees run on both streams: the status flags are cleared
-  // before the fork, not by the FAST launches (which would race a side octree)
   int32_t* fastErr = h->dErr.as<int32_t>();
-  if (sideTail) {
-    HIP_TRY(hipMemsetAsync(h->dErr.p, 0, (size_t)B * 4, s));
-    fastErr = nullptr;
-  }
   if (l0Side) {
     HIP_TRY(hipEventRecord(h->evL0Fork, s));
     HIP_TRY(hipStreamWaitEvent(side, h->evL0Fork, 0));
     PROF_REC(ev, pf.b(ev, 5), side);
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), fastErr, 0, l0End, B,
-                             side));
+                             h->dCellCount.as<int32_t>(), fastErr, 0, l0End, B, side));
     PROF_REC(ev, pf.e(ev, 5), side);
-    if (!perLevel && sideLevels == 0) HIP_TRY(hipEventRecord(h->evL0Join, side));
+    if (sideLevels == 0) HIP_TRY(hipEventRecord(h->evL0Join, side));
   } else if (ev) {
     pf.not_run(5);
   }
-  // the resize chain: on the caller's stream, or (per-level mode,
-  // ORB_CHAIN_STREAM=1) on a high-priority third stream forked from it
-  hipStream_t cs = s;
-  if (l0Side && h->stream3) {
-    cs = h->stream3;
-    HIP_TRY(hipStreamWaitEvent(cs, h->evL0Fork, 0));
-  }
-  PROF_REC(ev, pf.b(ev, 0), cs);
-  int fastSeg = 0;
-  // ORB_PYR_CHAIN=1: one or two frames build the pyramid in one launch
-  // (k_pyr_chain).  Off: measured slower than the seven per-level launches at
-  // one 1241x376 frame (resize stage 0.0386 vs 0.0269 ms, extraction wall
-  // 0.1445 vs 0.1319 ms, profiles/r04_step11.txt): 16 bands each walking all
-  // levels serially do more work per workgroup than a launch costs
-  static const int chainEnv = getenv("ORB_PYR_CHAIN") ? atoi(getenv("ORB_PYR_CHAIN")) : 0;
-  const bool chain = chainEnv > 0 && useBands && B <= 2 && h->chainNb > 0 && !l0Side;
-  if (chain)
-    HIP_TRY(orb_k_pyr_chain(d_images, (long long)imgPitch, (int)stride, arena, ap, &P, rt,
-                            h->dChain.p, h->chainNb, h->chainBuf, B, cs));
-  for (int l = chain ? P.nlevels : 1; l < P.nlevels; ++l) {
+  // the resize chain on the caller's stream (one launch per level: the
+  // one-launch chain k_pyr_chain measured slower, 0.0386 vs 0.0269 ms per
+  // frame, profiles/r04_step11.txt)
+  PROF_REC(ev, pf.b(ev, 0), s);
+  for (int l = 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
     const OrbLevelDesc& sd = P.lv[l - 1];
     const uint8_t* src = l == 1 ? d_images : arena + sd.arenaOff;
@@ -856,67 +855,22 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     const int srcStride = l == 1 ? (int)stride : sd.pitch;
     HIP_TRY(orb_k_pyr_resize(src, srcPitch, srcStride, sd.w, sd.h, arena + d.arenaOff, ap, d.pitch, d.w,
                              d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
-                             rt + d.rtabY + d.h, d.xmax, B, cs));
-    if (perLevel && d.cellEnd > d.cellBeg) {
-      // level l's cells on the side stream as soon as the chain has produced it
-      HIP_TRY(hipEventRecord(h->evLvl[l], cs));
-      HIP_TRY(hipStreamWaitEvent(side, h->evLvl[l], 0));
-      PROF_REC(ev, pf.b(ev, 2, fastSeg), side);
-      HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                               h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                               h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), d.cellBeg,
-                               d.cellEnd, B, side));
-      PROF_REC(ev, pf.e(ev, 2, fastSeg), side);
-      ++fastSeg;
-    }
-    if (l == sideLevels && sideEnd > l0End) {
-      HIP_TRY(hipEventRecord(h->evLvl[l], cs));
-      HIP_TRY(hipStreamWaitEvent(side, h->evLvl[l], 0));
-      PROF_REC(ev, pf.b(ev, 5, 1), side);
-      HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                               h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                               h->dCellCount.as<int32_t>(), fastErr, l0End,
-                               sideEnd, B, side));
-      PROF_REC(ev, pf.e(ev, 5, 1), side);
-      if (ev) pf.segments(5, 2);
-    }
-    if (l == sideLevels && sideTail) {
-      // the side stream's tail: octree of levels 0..sideLevels, then their
-      // descriptors (the main stream's octree of the rest runs beside it)
-      PROF_REC(ev, pf.b(ev, 3, 1), side);
-      HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
-                           h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
-                           h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
-                           h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, tailSplit, B,
-                           h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr,
-                           h->octNodeBytes, side));
-      PROF_REC(ev, pf.e(ev, 3, 1), side);
-      HIP_TRY(hipEventRecord(h->evFork, side));  // side octree done
-      PROF_REC(ev, pf.b(ev, 4, 1), side);
-      HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                                h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
-                                h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, 0,
-                                tailSplit, side));
-      PROF_REC(ev, pf.e(ev, 4, 1), side);
-      if (ev) {
-        pf.segments(3, 2);
-        pf.segments(4, 2);
+                             rt + d.rtabY + d.h, d.resizeMode, B, s));
+    if (l == sideLevels) {
+      if (sideEnd > l0End) {
+        HIP_TRY(hipEventRecord(h->evLvl, s));
+        HIP_TRY(hipStreamWaitEvent(side, h->evLvl, 0));
+        PROF_REC(ev, pf.b(ev, 5, 1), side);
+        HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                                 h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
+                                 h->dCellCount.as<int32_t>(), fastErr, l0End, sideEnd, B, side));
+        PROF_REC(ev, pf.e(ev, 5, 1), side);
+        if (ev) pf.segments(5, 2);
       }
+      HIP_TRY(hipEventRecord(h->evL0Join, side));
     }
-    if (l == sideLevels && sideLevels > 0) HIP_TRY(hipEventRecord(h->evL0Join, side));
   }
-  PROF_REC(ev, pf.e(ev, 0), cs);
-  if (cs != s) {  // the caller's stream also follows the whole chain (levels without cells)
-    HIP_TRY(hipEventRecord(h->evLvl[0], cs));
-    HIP_TRY(hipStreamWaitEvent(s, h->evLvl[0], 0));
-  }
-  if (perLevel) {
-    HIP_TRY(hipEventRecord(h->evL0Join, side));
-    if (ev) {
-      if (fastSeg) pf.segments(2, fastSeg);
-      else pf.not_run(2);
-    }
-  } else {
+  PROF_REC(ev, pf.e(ev, 0), s);
   PROF_REC(ev, pf.b(ev, 2), s);
   if (useBands)
     HIP_TRY(orb_k_fast_band(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
@@ -926,50 +880,25 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   else
     HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
                              h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), fastErr,
-                             l0Side ? sideEnd : 0, P.ncells, B, s));
+                             h->dCellCount.as<int32_t>(), fastErr, l0Side ? sideEnd : 0, P.ncells,
+                             B, s));
   PROF_REC(ev, pf.e(ev, 2), s);
-  }
   // (level 0's octree on the side stream as well measured no gain: the octree's
   // time is its per-workgroup pass latency, not level 0's size)
-  if (l0Side && !sideTail) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));
-  const bool split = split_blur();
-  if (split) {
-    if (s2 != s) {
-      HIP_TRY(hipEventRecord(h->evFork, s));
-      HIP_TRY(hipStreamWaitEvent(s2, h->evFork, 0));
-    }
-    PROF_REC(ev, pf.b(ev, 1), s2);
-    HIP_TRY(orb_k_blur_levels(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                              h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, B,
-                              s2));
-    PROF_REC(ev, pf.e(ev, 1), s2);
-    if (s2 != s) HIP_TRY(hipEventRecord(h->evJoin, s2));
-  }
+  if (l0Side) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));
   PROF_REC(ev, pf.b(ev, 3), s);
   HIP_TRY(orb_k_octree(&P, h->dCellCount.as<int32_t>(), h->dCellKeys.as<uint32_t>(),
                        h->dGKeys.as<uint32_t>(), h->dGNid.as<uint16_t>(), h->ldsKeyCap,
                        h->nodeCapMax, h->maxCellsPerLevel, h->dOutKeys.as<uint32_t>(),
-                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), sideTail ? tailSplit : 0,
-                       P.nlevels, B, h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr,
-                       h->octNodeBytes, s));
+                       h->dOutCount.as<int32_t>(), h->dErr.as<int32_t>(), 0, P.nlevels, B,
+                       h->octNodeBytes ? h->dOctNodes.as<uint8_t>() : nullptr, h->octNodeBytes, s));
   PROF_REC(ev, pf.e(ev, 3), s);
-  // the main k_orient_desc writes every image's count: it needs the side octree
-  if (sideTail) HIP_TRY(hipStreamWaitEvent(s, h->evFork, 0));
-  if (split && s2 != s) HIP_TRY(hipStreamWaitEvent(s, h->evJoin, 0));
   PROF_REC(ev, pf.b(ev, 4), s);
-  if (split)
-    HIP_TRY(orb_k_orient_desc_split(d_images, (long long)imgPitch, (int)stride, arena, ap,
-                                    h->dBlur.as<uint8_t>(), h->blurBytes, &P,
-                                    h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
-                                    h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, s));
-  else
-    HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                              h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
-                              h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B,
-                              sideTail ? tailSplit : 0, P.nlevels, s));
+  HIP_TRY(orb_k_orient_desc(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                            h->dOutKeys.as<uint32_t>(), h->dOutCount.as<int32_t>(),
+                            h->dErr.as<int32_t>(), d_kps, d_desc, capacity, d_counts, B, 0,
+                            P.nlevels, s));
   PROF_REC(ev, pf.e(ev, 4), s);
-  if (sideTail) HIP_TRY(hipStreamWaitEvent(s, h->evL0Join, 0));  // the side tail is done
   PROF_REC(ev, pf.t1(ev), s);
   if (!capturing) HIP_TRY(hipEventRecord(h->evBatch, s));  // readbacks on the handle stream wait for it
   h->lastImg0 = d_images;
@@ -1005,26 +934,24 @@ orb_status_t orb_device_count(int* n) {
 // Side-stream priorities (A/B knobs): ORB_STREAM2_PRIO = least | normal |
 // greatest for the FAST side stream; ORB_CHAIN_STREAM=1 runs the resize chain
 // on a third stream at the greatest priority.
-static int stream_prio(const char* var, const char* dflt) {
-  int least = 0, greatest = 0;
-  hipDeviceGetStreamPriorityRange(&least, &greatest);
-  const char* v = getenv(var);
-  const std::string m = v ? v : dflt;
-  if (getenv("ORB_AMD_DEBUG"))
-    fprintf(stderr, "[orb_amd] stream priorities least %d greatest %d, %s=%s\n", least, greatest,
-            var, m.c_str());
-  return m == "least" ? least : m == "greatest" ? greatest : 0;
+// the side stream's priority: the least (least == true) or the normal stream
+// priority of the device (SIDE_PRIO: compile-time A/B, 0 least, 1 normal, 2 greatest)
+#ifndef SIDE_PRIO
+#define SIDE_PRIO 0
+#endif
+static int stream_prio(bool least) {
+  int lo = 0, hi = 0;
+  hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (!least) return 0;
+  return SIDE_PRIO == 0 ? lo : SIDE_PRIO == 1 ? 0 : hi;
 }
-static bool chain_stream() {
-  static const bool v = getenv("ORB_CHAIN_STREAM") && atoi(getenv("ORB_CHAIN_STREAM")) > 0;
-  return v;
-}
-// One side stream per device, shared by every extractor handle of the process
-// (ORB_SIDE_SHARED=0: one per handle).  Each stream holds an HSA queue, and a
-// process with more queues than the hardware maps at once (the bench with its
-// C3 / C5 handles: 11) saw the side stream's cross-queue fork / join slow its
-// extraction by 30-50 % whenever a matcher ran beside it (profiles/r03_streams.txt).
-// Handles on one device share it safely: fork / join are per-handle events.
+// One side stream per device, shared by every extractor handle of the process.
+// Each stream holds an HSA queue, and a process with more queues than the
+// hardware maps at once (the bench with its C3 / C5 handles: 11, with one
+// side stream per handle) saw the side stream's cross-queue fork / join slow
+// its extraction by 30-50 % whenever a matcher ran beside it
+// (profiles/r03_streams.txt).  Handles on one device share it safely: fork /
+// join are per-handle events.
 static hipStream_t shared_side_stream(int device, int prio) {
   static std::mutex mu;
   static hipStream_t s[64] = {};
@@ -1042,36 +969,18 @@ static bool create_side_streams(orb_extractor* h) {
   // 0's FAST with the resize chain.  Low rather than high: the chain on the
   // caller's stream then wins the CUs the side FAST also wants (extraction
   // 1.703 vs 1.727 ms per 512 frames; profiles/r03_streams.txt)
-  static const bool shared = !getenv("ORB_SIDE_SHARED") || atoi(getenv("ORB_SIDE_SHARED")) > 0;
-  const int prio = stream_prio("ORB_STREAM2_PRIO", "least");
-  if (shared) {
-    h->stream2 = shared_side_stream(h->device, prio);
-    h->sharedSide = true;
-    if (!h->stream2) return false;
-  } else if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, prio) != hipSuccess) {
-    return false;
-  }
-  if (chain_stream() &&
-      hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking,
-                                  stream_prio("ORB_CHAIN_PRIO", "greatest")) != hipSuccess)
-    return false;
-  return true;
-}
-
-static bool create_level_events(orb_extractor* h) {
-  for (hipEvent_t& e : h->evLvl)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
-  return true;
+  h->stream2 = shared_side_stream(h->device, stream_prio(true));
+  return h->stream2 != nullptr;
 }
 
 orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int ini_th_fast,
                                   int min_th_fast, int device, orb_extractor_t** out) {
   if (!out) return ORB_EINVAL;
   *out = nullptr;
-  // k_pyr_resize stages tiles sized for a per-level downscale of at most 1.9
-  // (the planner checks every tile of every level)
+  // (a scale factor of 1 makes the reference's quota series 0 / 0,
+  // src/ORBextractor.cc:453-455; the per-level node bound is the planner's)
   if (nfeatures < 0 || nlevels < 1 || nlevels > ORB_MAX_LEVELS || !(scale_factor > 1.0f) ||
-      !(scale_factor <= 1.9f) || nfeatures > 60000)
+      !std::isfinite(scale_factor))
     return ORB_EINVAL;
   orb_status_t st = check_device(device);
   if (st) return st;
@@ -1087,31 +996,21 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   hipSetDevice(device);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       !create_side_streams(h) ||
-      hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evL0Fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evL0Join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->evBatch, hipEventDisableTiming) != hipSuccess ||
-      !create_level_events(h)) {
+      hipEventCreateWithFlags(&h->evLvl, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->evBatch, hipEventDisableTiming) != hipSuccess) {
     if (h->stream) hipStreamDestroy(h->stream);
-    if (h->stream2 && !h->sharedSide) hipStreamDestroy(h->stream2);
-    if (h->stream3) hipStreamDestroy(h->stream3);
-    if (h->evFork) hipEventDestroy(h->evFork);
-    if (h->evJoin) hipEventDestroy(h->evJoin);
     if (h->evL0Fork) hipEventDestroy(h->evL0Fork);
     if (h->evL0Join) hipEventDestroy(h->evL0Join);
+    if (h->evLvl) hipEventDestroy(h->evLvl);
     if (h->evBatch) hipEventDestroy(h->evBatch);
-    for (hipEvent_t e : h->evLvl)
-      if (e) hipEventDestroy(e);
     delete h;
     return ORB_EDEVICE;
   }
   h->ownStream = true;
   h->prof.nStages = 6;
-  h->prof.maxSeg[2] = ORB_MAX_LEVELS;  // FAST of levels >= 1: one launch per level
-  h->prof.maxSeg[5] = 2;  // side-stream FAST: level 0, then levels 1..sideLevels
-  h->prof.maxSeg[3] = 2;  // octree / orient: main stream, then (split tail) side stream
-  h->prof.maxSeg[4] = 2;
+  h->prof.maxSeg[5] = 2;  // side-stream FAST: level 0, then levels 1..FAST_SIDE_LEVELS
   const char* names[6] = {"k_pyr_resize", "k_blur_levels", "k_fast_band", "k_octree",
                           "k_orient_desc", "k_fast_cells_side"};
   for (int i = 0; i < 6; ++i) {
@@ -1119,7 +1018,7 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
     h->prof.launchesPerCall[i] = 1;
   }
   h->prof.launchesPerCall[0] = std::max(nlevels - 1, 0);
-  h->prof.launchesPerCall[1] = split_blur() ? 1 : 0;  // k_blur_levels: split A/B mode only
+  h->prof.launchesPerCall[1] = 0;  // k_blur_levels: orb_extractor_blurred_level only
   if (orb_k_upload_constants(h->stream) != hipSuccess ||
       orb_k_upload_umax(h->umax, h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -1143,18 +1042,14 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   h->hLvl.release();
   h->hPyr.release();
   if (h->oneExec) hipGraphExecDestroy(h->oneExec);
+  h->batchGraph.reset();
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
-  if (h->stream2 && !h->sharedSide) hipStreamDestroy(h->stream2);
   if (h->privSide) hipStreamDestroy(h->privSide);
-  if (h->stream3) hipStreamDestroy(h->stream3);
-  if (h->evFork) hipEventDestroy(h->evFork);
-  if (h->evJoin) hipEventDestroy(h->evJoin);
   if (h->evL0Fork) hipEventDestroy(h->evL0Fork);
   if (h->evL0Join) hipEventDestroy(h->evL0Join);
+  if (h->evLvl) hipEventDestroy(h->evLvl);
   if (h->evBatch) hipEventDestroy(h->evBatch);
-  for (hipEvent_t e : h->evLvl)
-    if (e) hipEventDestroy(e);
   delete h;
 }
 
@@ -1201,8 +1096,30 @@ orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_im
   if (capacity < h->plan.slotsPerImage) return ORB_ECAPACITY;
   if ((st = ensure_batch(h, n_images))) return st;
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-  st = run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors, capacity,
-                 d_counts, s);
+  if (n_images > GRAPH_MAX_BATCH || h->prof.enabled) {
+    st = run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors, capacity,
+                   d_counts, s);
+  } else {
+    const std::vector<uintptr_t> key = {
+        (uintptr_t)d_images, (uintptr_t)n_images, (uintptr_t)width, (uintptr_t)height, stride,
+        image_pitch, (uintptr_t)d_keypoints, (uintptr_t)d_descriptors, (uintptr_t)capacity,
+        (uintptr_t)d_counts, (uintptr_t)h->dArena.p, (uintptr_t)h->dCellKeys.p,
+        (uintptr_t)h->dGKeys.p, (uintptr_t)h->dGNid.p, (uintptr_t)h->dCellCount.p,
+        (uintptr_t)h->dOutKeys.p, (uintptr_t)h->dOutCount.p, (uintptr_t)h->dErr.p,
+        (uintptr_t)h->dRtab.p, (uintptr_t)h->dBands.p, (uintptr_t)h->dCells.p,
+        (uintptr_t)h->dOctNodes.p};
+    st = run_graphed(h->batchGraph, key, h->stream, s, [&](hipStream_t cs, bool cap) {
+      return run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors,
+                       capacity, d_counts, cs, cap);
+    });
+    if (!st) {
+      // a replayed or captured call skips run_batch's bookkeeping
+      HIP_TRY(hipEventRecord(h->evBatch, s));
+      h->lastImg0 = d_images;
+      h->lastImg0Pitch = image_pitch;
+      h->lastImg0Stride = (int)stride;
+    }
+  }
   if (st) return st;
   h->lastSingle = false;
   h->lastW = width;
@@ -1249,8 +1166,7 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
                              h->stream));
     return ORB_OK;
   };
-  static const bool noGraph = getenv("ORB_NO_GRAPH") && atoi(getenv("ORB_NO_GRAPH")) > 0;
-  if (h->prof.enabled || noGraph) {
+  if (h->prof.enabled) {  // (the stage events need the launches issued one by one)
     if ((st = enqueue(false))) return st;
   } else {
     const std::vector<const void*> key = {
@@ -1400,18 +1316,16 @@ orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t*
   if (dst_stride < (size_t)L.w) return ORB_EINVAL;
   hipSetDevice(h->device);
   // The extraction never materialises blurred levels (k_orient_desc blurs
-  // each keypoint's window in LDS; in the split A/B mode they are in dBlur
-  // already): blur image 0 of the last call on demand with k_blur_levels.
+  // each keypoint's window in LDS): blur image 0 of the last call on demand
+  // with k_blur_levels.
   HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));
-  if (!split_blur()) {
-    if (!h->lastImg0) return ORB_EINVAL;
-    orb_status_t st = h->dBlur.ensure((size_t)h->blurBytes);
-    if (st) return st;
-    HIP_TRY(orb_k_blur_levels(h->lastImg0, (long long)h->lastImg0Pitch, h->lastImg0Stride,
-                              h->dArena.as<uint8_t>(), h->arenaBytes, &h->plan,
-                              h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, 1,
-                              h->stream));
-  }
+  if (!h->lastImg0) return ORB_EINVAL;
+  orb_status_t st = h->dBlur.ensure((size_t)h->blurBytes);
+  if (st) return st;
+  HIP_TRY(orb_k_blur_levels(h->lastImg0, (long long)h->lastImg0Pitch, h->lastImg0Stride,
+                            h->dArena.as<uint8_t>(), h->arenaBytes, &h->plan,
+                            h->dTiles.as<OrbTileDesc>(), h->dBlur.as<uint8_t>(), h->blurBytes, 1,
+                            h->stream));
   return copy_level_to_host(h, dst, dst_stride, h->dBlur.as<uint8_t>() + L.blurOff, L.blurPitch,
                             L.w, L.h);
 }
@@ -1527,6 +1441,7 @@ struct orb_matcher {
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
   DevBuf dJac;  // Jacobi-resolve scratch (ORB_RESOLVE_JACOBI)
+  CallGraph projGraph;  // small orb_match_projection_local_batch calls (run_graphed)
   int resolveSchedule = ORB_RESOLVE_AUTO;  // orb_matcher_set_resolve
   int jacobiRounds = 6;
   // stereo / frame / BoW scratch
@@ -1596,6 +1511,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
   if (!m) return;
   hipSetDevice(m->device);
   hipStreamSynchronize(m->stream);
+  m->projGraph.reset();
   DevBuf* bufs[] = {&m->dKeys, &m->dDesc, &m->dUr, &m->dLocked, &m->dNKeys, &m->dMps,
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
                     &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut, &m->dJac,
@@ -1671,6 +1587,7 @@ orb_status_t orb_match_projection_local_batch(
   const size_t jb = orb_k_proj_jacobi_bytes(kp_stride, mp_stride, n_problems, m->resolveSchedule);
   if (jb && (st = m->dJac.ensure(jb))) return st;
   StageProfiler& pf = m->prof;
+  auto enqueue = [&](hipStream_t s, bool) -> orb_status_t {
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
   PROF_REC(ev, pf.b(ev, 0), s);
@@ -1699,6 +1616,20 @@ orb_status_t orb_match_projection_local_batch(
   PROF_REC(ev, pf.e(ev, 2), s);
   PROF_REC(ev, pf.t1(ev), s);
   return ORB_OK;
+  };
+  if (n_problems > GRAPH_MAX_BATCH || pf.enabled) return enqueue(s, false);
+  std::vector<uintptr_t> key = {
+      (uintptr_t)n_problems, (uintptr_t)d_keys, (uintptr_t)d_desc, (uintptr_t)d_nkeys,
+      (uintptr_t)d_locked, (uintptr_t)kp_stride, (uintptr_t)d_mps, (uintptr_t)d_mp_desc,
+      (uintptr_t)d_nmps, (uintptr_t)mp_stride, (uintptr_t)d_kp_match, (uintptr_t)d_nmatches,
+      (uintptr_t)m->resolveSchedule, (uintptr_t)m->jacobiRounds, (uintptr_t)m->dCellStart.p,
+      (uintptr_t)m->dCellIdx.p, (uintptr_t)m->dTopk.p, (uintptr_t)m->dNcand.p,
+      (uintptr_t)m->dProjStage.p, (uintptr_t)m->dJac.p};
+  // the kernel parameters (bounds, scale factors, th, nnratio) by value
+  const size_t pw = (sizeof(P) + sizeof(uintptr_t) - 1) / sizeof(uintptr_t);
+  key.resize(key.size() + pw, 0);
+  memcpy(key.data() + key.size() - pw, &P, sizeof(P));
+  return run_graphed(m->projGraph, key, m->stream, s, enqueue);
 }
 
 orb_status_t orb_matcher_set_resolve(orb_matcher_t* m, int schedule, int jacobi_rounds) {

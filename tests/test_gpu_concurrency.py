@@ -158,13 +158,20 @@ def test_graph_capture_beside_another_handle(gpu):
 
 
 def test_batch_rate_with_extra_caller_streams(gpu):
-    """A caller that creates many streams of its own (ORB-SLAM2 runs extractors
-    and matchers on three threads) must not push the batch extraction into a
-    slow mode: HIP maps streams onto a few HSA queues per priority level, and
-    a library stream sharing a queue with a busy caller stream runs in
-    submission order with it.  The batch path forks nothing onto streams of
-    its own by default, so 8 extra busy streams leave its rate unchanged
-    (timed on one stream, before and after; 15 % tolerance for box noise)."""
+    """A caller that keeps many streams of its own busy (ORB-SLAM2 runs
+    extractors and matchers on three threads) must not push the batch
+    extraction into a slow mode.  HIP maps streams onto a few HSA queues per
+    priority level (GPU_MAX_HW_QUEUES, 4), and two streams on one queue run in
+    submission order.  The batch path forks level 0's FAST (then levels 1-2)
+    onto the device's shared side stream, which is created at the lowest
+    priority so it never shares a queue with a normal-priority caller stream
+    (runtime.cpp create_side_streams).  Here 8 caller threads keep 8
+    normal-priority streams continuously busy with 2 ms one-thread spin kernels
+    (torch.cuda._sleep: a queue they share is blocked, the chip is not) while
+    the batch runs on a high-priority stream: its rate must stay within 15 %
+    of the idle rate.  A side stream on a caller's queue would wait ~2 ms
+    behind a spin kernel per call (a call of 128 frames takes ~0.4 ms)."""
+    import threading
     import time
 
     import torch
@@ -176,31 +183,58 @@ def test_batch_rate_with_extra_caller_streams(gpu):
     k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
     de = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
     n = torch.zeros(B, dtype=torch.int32, device="cuda")
-    s = torch.cuda.Stream()
+    s = torch.cuda.Stream(priority=-1)  # the caller's extraction stream: high priority
 
     def rate():
         for _ in range(3):
             ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
                               n.data_ptr(), s.cuda_stream)
-        torch.cuda.synchronize()
+        s.synchronize()
         best = 0.0
-        for _ in range(3):
+        for _ in range(5):
             t0 = time.perf_counter()
             for _ in range(10):
                 ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(),
                                   cap, n.data_ptr(), s.cuda_stream)
-            torch.cuda.synchronize()
+            s.synchronize()
             best = max(best, 10 * B / (time.perf_counter() - t0))
         return best
 
     r0 = rate()
     ref = n.clone()
-    extra = [torch.cuda.Stream() for _ in range(8)]
-    bufs = [torch.zeros(1 << 16, device="cuda") for _ in extra]
-    for st, b in zip(extra, bufs):  # each stream gets work, so each holds a queue
-        with torch.cuda.stream(st):
-            b.add_(1.0)
+    # calibrate the spin kernel to ~2 ms
+    probe = torch.cuda.Stream()
+    cycles = 1 << 20
+    with torch.cuda.stream(probe):
+        torch.cuda._sleep(cycles)
+        probe.synchronize()
+        t0 = time.perf_counter()
+        torch.cuda._sleep(cycles)
+        probe.synchronize()
+    cycles = max(1 << 16, int(cycles * 2e-3 / max(time.perf_counter() - t0, 1e-6)))
+    extra = [torch.cuda.Stream() for _ in range(8)]  # normal priority, as a caller's
+    stop = threading.Event()
+    spins = [0] * len(extra)
+
+    def busy(i):
+        with torch.cuda.stream(extra[i]):
+            while not stop.is_set():
+                for _ in range(2):  # always one spin kernel queued behind the running one
+                    torch.cuda._sleep(cycles)
+                spins[i] += 2
+                extra[i].synchronize()
+
+    ths = [threading.Thread(target=busy, args=(i,)) for i in range(len(extra))]
+    for t in ths:
+        t.start()
+    try:
+        time.sleep(0.05)
+        r1 = rate()
+    finally:
+        stop.set()
+        for t in ths:
+            t.join(timeout=60)
     torch.cuda.synchronize()
-    r1 = rate()
+    assert min(spins) > 0, spins  # every caller stream really ran
     assert torch.equal(n, ref)
-    assert r1 > 0.85 * r0, (r0, r1)
+    assert r1 > 0.85 * r0, (r0, r1, cycles)

@@ -165,8 +165,12 @@ def test_batch_matches_single(gpu):
     (1241, 376, 1500, 1.2, 12),    # deep pyramid (level 11: 167 x 51)
     (640, 480, 800, 1.1, 8),       # finer scale steps
     (1920, 1080, 2000, 1.5, 6),    # wide resize variant (downscale > 1.25)
-    (1241, 376, 1000, 1.9, 4),     # widest supported downscale
+    (1241, 376, 1000, 1.9, 4),     # widest staged downscale
     (1241, 376, 1000, 1.25, 8),    # narrow variant's limit
+    (1920, 1080, 2000, 2.0, 5),    # untiled resize (every level >= 33 px)
+    (1920, 1080, 2000, 2.5, 4),
+    (1241, 376, 1000, 3.0, 3),
+    (640, 480, 1000, 1.2, 15),     # levels 12-14 (60..37 px high) have no cells
 ])
 def test_extractor_parameters(gpu, oracle, w, h, nf, sf, nl):
     """ORBextractor(nfeatures, scaleFactor, nlevels, 20, 7) for parameters other
@@ -184,9 +188,32 @@ def test_extractor_parameters(gpu, oracle, w, h, nf, sf, nl):
         assert np.ascontiguousarray(lv).tobytes() == ref_pyr[l].tobytes(), f"level {l}"
 
 
-def test_extractor_rejects_unsupported_scale(gpu):
+def test_extractor_rejects_degenerate_parameters(gpu):
+    """scaleFactor 1 (the reference's quota series is 0 / 0,
+    src/ORBextractor.cc:453-455) is rejected at construction; a pyramid level
+    of 32 px or less (where the reference's DistributeOctTree divides by zero
+    or resizes its root vector to a negative size, :562-569) by the call."""
+    for sf in (1.0, 0.5, float("nan"), float("inf")):
+        with pytest.raises(gpu.OrbError):
+            gpu.ORBextractor(1000, sf, 8, 20, 7)
+    ext = gpu.ORBextractor(1000, 2.0, 8, 20, 7)  # 1241x376: level 4 is 78 x 24
     with pytest.raises(gpu.OrbError):
-        gpu.ORBextractor(1000, 2.5, 8, 20, 7)
+        ext(gpu.synth_image(1, 0, 1241, 376))
+    assert ext.capacity(1241, 376) < 0
+
+
+def test_extractor_100k_features(gpu, oracle):
+    """nfeatures far above any ORB-SLAM2 yaml (100,000 on 1080p noise: level
+    quotas 21,700 .. 6,900, 92,610 keypoints): single frame and a batch of
+    two, bit-exact."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (1080, 1920), dtype=np.uint8)
+    k_ref, d_ref, _ = oracle.extract(img, 100000, 1.2, 8, 20, 7)
+    assert len(k_ref) > 60000
+    k_gpu, d_gpu = gpu.ORBextractor(100000, 1.2, 8, 20, 7)(img)
+    assert k_gpu.tobytes() == k_ref.tobytes(), _diff_report(k_gpu, d_gpu, k_ref, d_ref)
+    assert d_gpu.tobytes() == d_ref.tobytes()
+    _batch_vs_oracle(gpu, oracle, [img, img[:, ::-1].copy()], 100000)
 
 
 @pytest.mark.parametrize("w,h,stride,pitch,B", [
@@ -270,6 +297,7 @@ def test_batch_hard_cases_vs_oracle(gpu, oracle):
     (640, 480, 800, 1.1, 8),
     (1920, 1080, 2000, 1.5, 6),
     (1241, 376, 1000, 1.9, 4),
+    (1920, 1080, 2000, 2.5, 4),    # untiled resize
     (640, 480, 1000, 1.2, 1),
     (640, 480, 1000, 1.2, 2),      # the side stream's FAST covers every level >= 1,
     (1241, 376, 1000, 1.2, 3),     # the main stream's FAST launch is empty
@@ -402,52 +430,31 @@ print('batch:', n.tolist())
     assert out["batch"] == str([gpu.ORB_EDEVICE] * 4)
 
 
-@pytest.mark.parametrize("side_tail", ["0", "1"])
-def test_octree_12k_batch4_global_nodes(gpu, oracle, tmp_path, side_tail):
+def test_octree_12k_batch4_global_nodes(gpu, oracle):
     """12,000 features put the octree's node tables in global memory (one slice
-    per (image, level)); a batch of 4 takes the cell FAST path and, with
-    ORB_SIDE_TAIL=1, runs the octree of levels 0..2 on the side stream beside
-    levels 3..7 on the main one: the two launches must not share slices
-    (run in a child: the schedule knobs are read once per process)."""
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
+    per (image, level)); a batch of 4 takes the cell FAST path (level 0 and
+    levels 1-2 on the side stream), three calls on a stream of the caller's."""
+    torch = pytest.importorskip("torch")
     rng = np.random.default_rng(12)
     w, h, nf = 1920, 1080, 12000
     img = rng.integers(0, 256, (h, w), dtype=np.uint8)
-    np.save(tmp_path / "img.npy", img)
-    code = f"""
-import sys, numpy as np, torch
-sys.path.insert(0, {str(root)!r}); sys.path.insert(0, {str(root / 'tests')!r})
-from conftest import load_pkg
-orb = load_pkg()
-img = np.load({str(tmp_path / 'img.npy')!r})
-ext = orb.ORBextractor({nf}, 1.2, 8, 20, 7)
-cap = ext.capacity({w}, {h})
-imgs = torch.from_numpy(np.stack([img] * 4)).cuda()
-k = torch.zeros((4, cap, 7), dtype=torch.int32, device='cuda')
-d = torch.zeros((4, cap, 32), dtype=torch.uint8, device='cuda')
-n = torch.zeros(4, dtype=torch.int32, device='cuda')
-s = torch.cuda.Stream()
-for _ in range(3):
-    ext.extract_batch(imgs.data_ptr(), 4, {w}, {h}, {w}, {w * h}, k.data_ptr(), d.data_ptr(), cap,
-                      n.data_ptr(), s.cuda_stream)
-torch.cuda.synchronize()
-np.savez({str(tmp_path / 'out.npz')!r}, k=k.cpu().numpy(), d=d.cpu().numpy(), n=n.cpu().numpy())
-"""
-    import os
-    env = dict(os.environ, ORB_SIDE_TAIL=side_tail)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
-                       env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
-    out = np.load(tmp_path / "out.npz")
+    ext = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    cap = ext.capacity(w, h)
+    imgs = torch.from_numpy(np.stack([img] * 4)).cuda()
+    k = torch.zeros((4, cap, 7), dtype=torch.int32, device="cuda")
+    d = torch.zeros((4, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(4, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    for _ in range(3):
+        ext.extract_batch(imgs.data_ptr(), 4, w, h, w, w * h, k.data_ptr(), d.data_ptr(), cap,
+                          n.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
     kr, dr, _ = oracle.extract(img, nf)
+    kk, dd, nn = k.cpu().numpy().view(gpu.KEYPOINT_DTYPE).reshape(4, cap), d.cpu().numpy(), n.cpu().numpy()
     for i in range(4):
-        n = int(out["n"][i])
-        assert n == len(kr), (i, n, len(kr))
-        assert out["k"][i, :n].tobytes() == kr.tobytes()
-        assert out["d"][i, :n].tobytes() == dr.tobytes()
+        assert nn[i] == len(kr), (i, nn[i], len(kr))
+        assert kk[i, :nn[i]].tobytes() == kr.tobytes()
+        assert dd[i, :nn[i]].tobytes() == dr.tobytes()
 
 
 def test_host_pyramid_mirror(gpu, oracle):
@@ -463,62 +470,3 @@ def test_host_pyramid_mirror(gpu, oracle):
             assert np.array_equal(ext.host_pyramid(l), ref[l]), (f, l)
     with pytest.raises(gpu.OrbError):
         ext.host_pyramid(8)
-
-
-def test_pyramid_chain_option_bit_exact(gpu, oracle, tmp_path):
-    """ORB_PYR_CHAIN=1 (read once per process, so in a child): the one-launch
-    resize chain of one- and two-frame calls (k_pyr_chain, off by default)
-    gives the oracle's pyramid, keypoints and descriptors for the yaml
-    defaults, a deep pyramid, the wide-resize variant and a two-image batch."""
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
-    cases = [(1241, 376, 1000, 1.2, 8), (1241, 376, 1500, 1.2, 12), (1920, 1080, 2000, 1.5, 6)]
-    for i, (w, h, nf, sf, nl) in enumerate(cases):
-        np.save(tmp_path / f"img{i}.npy", gpu.synth_image(11 + i, 0, w, h))
-    np.save(tmp_path / "pair.npy", np.stack([gpu.synth_image(20, f, 640, 480) for f in range(2)]))
-    code = f"""
-import sys, numpy as np, torch
-sys.path.insert(0, {str(root)!r}); sys.path.insert(0, {str(root / 'tests')!r})
-from conftest import load_pkg
-orb = load_pkg()
-T = {str(tmp_path)!r}
-for i, (w, h, nf, sf, nl) in enumerate({cases!r}):
-    ext = orb.ORBextractor(nf, sf, nl, 20, 7)
-    k, d = ext(np.load(T + f'/img{{i}}.npy'))
-    np.save(T + f'/k{{i}}.npy', k); np.save(T + f'/d{{i}}.npy', d)
-    for l, lv in enumerate(ext.mvImagePyramid):
-        np.save(T + f'/p{{i}}_{{l}}.npy', np.ascontiguousarray(lv))
-pair = np.load(T + '/pair.npy')
-ext = orb.ORBextractor(1000, 1.2, 8, 20, 7)
-cap = ext.capacity(640, 480)
-d_img = torch.from_numpy(pair).cuda()
-kk = torch.zeros((2, cap, 7), dtype=torch.int32, device='cuda')
-dd = torch.zeros((2, cap, 32), dtype=torch.uint8, device='cuda')
-nn = torch.zeros(2, dtype=torch.int32, device='cuda')
-ext.extract_batch(d_img.data_ptr(), 2, 640, 480, 640, 640 * 480, kk.data_ptr(), dd.data_ptr(), cap,
-                  nn.data_ptr())
-torch.cuda.synchronize()
-np.save(T + '/bk.npy', kk.cpu().numpy()); np.save(T + '/bd.npy', dd.cpu().numpy())
-np.save(T + '/bn.npy', nn.cpu().numpy())
-"""
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
-                       env=dict(os.environ, ORB_PYR_CHAIN="1"))
-    assert r.returncode == 0, r.stderr[-2000:]
-    for i, (w, h, nf, sf, nl) in enumerate(cases):
-        img = np.load(tmp_path / f"img{i}.npy")
-        k_ref, d_ref, _ = oracle.extract(img, nf, sf, nl, 20, 7)
-        assert np.load(tmp_path / f"k{i}.npy").tobytes() == k_ref.tobytes(), i
-        assert np.load(tmp_path / f"d{i}.npy").tobytes() == d_ref.tobytes(), i
-        ref_pyr = oracle.pyramid(img, sf, nl)
-        for l in range(nl):
-            assert np.load(tmp_path / f"p{i}_{l}.npy").tobytes() == ref_pyr[l].tobytes(), (i, l)
-    pair = np.load(tmp_path / "pair.npy")
-    bk, bd, bn = np.load(tmp_path / "bk.npy"), np.load(tmp_path / "bd.npy"), np.load(tmp_path / "bn.npy")
-    for f in range(2):
-        k_ref, d_ref, _ = oracle.extract(pair[f], 1000, 1.2, 8, 20, 7)
-        assert int(bn[f]) == len(k_ref)
-        assert np.ascontiguousarray(bk[f, :bn[f]]).tobytes() == k_ref.tobytes(), f
-        assert bd[f, :bn[f]].tobytes() == d_ref.tobytes(), f
