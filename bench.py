@@ -190,7 +190,7 @@ def snapshot_sample(sets, g_end, n_sets, n_batches, B, orb, per_set=2):
     (batch gg % n_batches).  Returns [(frame index, keypoints, descriptors,
     kp_match, nmatches)]."""
     out = []
-    for gg in range(g_end - n_sets, g_end):
+    for gg in range(max(0, g_end - n_sets), g_end):  # (a short run may not have used every set)
         st, b = sets[gg % n_sets], gg % n_batches
         for q in range(per_set):
             i = (gg * 389 + q * (B // per_set) + 7) % B
@@ -217,7 +217,12 @@ def cpu_leg(imgs, maps, sample, args, scale, timed):
         ok = (k.tobytes() == kr.tobytes() and d.tobytes() == dr.tobytes() and nm == n_ref
               and np.array_equal(km, km_ref))
         if not ok:
-            bad.append(int(f))
+            bad.append({"frame": int(f), "n": int(len(k)), "n_ref": int(len(kr)),
+                        "keys": k.tobytes() == kr.tobytes(), "desc": d.tobytes() == dr.tobytes(),
+                        "nmatch": int(nm), "nmatch_ref": int(n_ref),
+                        "kp_match_diff": int(np.sum(km != km_ref)) if len(km) == len(km_ref) else -1})
+    if bad:
+        print("bench.py parity_sample mismatch:", json.dumps(bad), file=sys.stderr, flush=True)
     par = {"frames": [int(s[0]) for s in sample], "bit_exact": not bad, "mismatched": bad,
            "checked": "keypoints (28 B records, order), descriptors, SearchByProjection "
                       "kp_match and nmatches of frames taken from the timed pipeline's own "
@@ -327,6 +332,7 @@ _STREAMS = {}
 # (tools/archive/r03/c5_swap.py, profiles/r03_streams.txt)
 _STREAM_PRIO = {"extract": "normal", "match": "greatest", "h2d": "greatest", "d2h": "greatest"}
 _STREAM_PRIO.update({f"extract{i}": "normal" for i in range(1, 4)})
+_STREAM_PRIO.update({f"match{i}": "greatest" for i in range(1, 4)})
 
 
 def _hip(torch):
@@ -361,23 +367,25 @@ def new_stream(torch, dev, key):
     return _STREAMS[key]
 
 
-def pipelined(torch, dev, extract, match, n_sets, steps, warmup, lanes=None):
+def pipelined(torch, dev, extract, match, n_sets, steps, warmup, lanes=None, match_lanes=1):
     """Seconds per step of `extract(j, stream)` then `match(j, stream)` over
     buffer set j = step % n_sets, pipelined: set j's extraction runs on lane
     j % lanes (a stream of its own; each set has its own extractor handles),
-    every match on one match stream, so step k's match overlaps the next steps'
-    extraction; a set is rewritten only after its previous match has finished
-    (events).  Every step does all of its work."""
+    its match on match stream j % match_lanes, so step k's match overlaps the
+    next steps' extraction (and, with two match streams, the next set's match);
+    a set is rewritten only after its previous match has finished (events).
+    Every step does all of its work."""
     if lanes is None:
         lanes = min(n_sets, max(1, int(os.environ.get("ORB_BENCH_LANES", "2"))))
     ess = [new_stream(torch, dev, "extract" if i == 0 else f"extract{i}") for i in range(lanes)]
-    ms = new_stream(torch, dev, "match")
+    mss = [new_stream(torch, dev, "match" if i == 0 else f"match{i}") for i in range(match_lanes)]
     ext_done = [torch.cuda.Event() for _ in range(n_sets)]
     match_done = [torch.cuda.Event() for _ in range(n_sets)]
 
     def one(g):
         j = g % n_sets
         es = ess[j % lanes]
+        ms = mss[j % match_lanes]
         if g >= n_sets:
             es.wait_event(match_done[j])
         extract(j, es.cuda_stream)
@@ -448,7 +456,7 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
 
 
 def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warmup=3,
-                  serial_calls=0):
+                  serial_calls=0, match_streams2=False):
     """extract + SearchByProjection(F, localMap) against M-point synthetic maps
     (orb_synth_local_map(seed + i, ...)), B problems (frames 0..B-1 of `seed`)
     per launch, pipelined as `pipelined`; also the matcher alone, serial on
@@ -478,7 +486,9 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
     d_mpd = torch.from_numpy(mpd).to(dev)
     d_lk = torch.from_numpy(lk).to(dev)
     d_nm = torch.full((B,), M, dtype=torch.int32, device=dev)
-    mt = orb.ORBmatcher(0.8, device=dev.index)
+    # one matcher handle per buffer set: a handle's scratch serves one call at a
+    # time, and two sets' matches may run at once on two streams
+    mts = [orb.ORBmatcher(0.8, device=dev.index) for _ in range(2)]
 
     def extract(j, s):
         st = sets[j]
@@ -487,16 +497,31 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
 
     def match(j, s):
         st = sets[j]
-        mt.search_by_projection_batch(B, st["k"].data_ptr(), st["de"].data_ptr(), st["n"].data_ptr(),
-                                      d_lk.data_ptr(), cap, d_mps.data_ptr(), d_mpd.data_ptr(),
-                                      d_nm.data_ptr(), M, W, H, scale, 1.0, st["km"].data_ptr(),
-                                      st["nm"].data_ptr(), s)
+        mts[j].search_by_projection_batch(B, st["k"].data_ptr(), st["de"].data_ptr(),
+                                          st["n"].data_ptr(), d_lk.data_ptr(), cap, d_mps.data_ptr(),
+                                          d_mpd.data_ptr(), d_nm.data_ptr(), M, W, H, scale, 1.0,
+                                          st["km"].data_ptr(), st["nm"].data_ptr(), s)
 
     sec = pipelined(torch, dev, extract, match, 2, steps, warmup)
+    sec2 = pipelined(torch, dev, extract, match, 2, steps, warmup, match_lanes=2) \
+        if match_streams2 else None
     if min(int(st["n"].min().item()) for st in sets) < 0:
         raise RuntimeError("extract + match: an extraction reported failure (negative count)")
     with torch.cuda.stream(s0):
         msec = timed_loop(lambda: match(0, s0.cuda_stream), steps, warmup, torch)
+    msec2 = None
+    if match_streams2:
+        # the matcher alone with two sets in flight on two streams (set j's
+        # resolve, which holds one workgroup per problem, beside set j+1's
+        # chip-wide candidate scan)
+        s1 = new_stream(torch, dev, "match1")
+        ss = [s0.cuda_stream, s1.cuda_stream]
+        it = [0]
+
+        def two():
+            match(it[0] % 2, ss[it[0] % 2])
+            it[0] += 1
+        msec2 = timed_loop(two, steps, warmup, torch)
     serial = None
     if serial_calls:
         # latency shape: one call (extraction + match of the B frames) at a time,
@@ -515,6 +540,11 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
     res = {"value": B / sec, "unit": "problems/s", "problems_per_step": B, "ms_per_step": sec * 1e3,
            "match_only_problems_per_s": B / msec, "match_only_alg_GBps": b_lm * B / msec / 1e9,
            "match_only_frac_of_8TBps": b_lm * B / msec / 8e12, "mean_keypoints": n_kp,
+           **({"two_match_streams": {
+               "problems_per_s": B / sec2, "match_only_problems_per_s": B / msec2,
+               "note": "each set's SearchByProjection on a match stream (and matcher handle) of "
+                       "its own, so one set's resolve runs beside the next set's candidate scan"}}
+              if match_streams2 else {}),
            "mean_matches": float(sets[0]["nm"].float().mean().item()),
            **({"serial_ms_per_call": serial * 1e3, "serial_frames_per_s": B / serial,
                "serial_calls": serial_calls} if serial else {}),
@@ -533,7 +563,7 @@ def secondary_configs(orb, torch, args, dev, threads):
     # (profiles/r03_configs.txt); 200 steps repeat within 0.3 %
     c3, _ = c3_workload(orb, torch, dev, threads, steps=40, warmup=5)
     c5, _ = proj_workload(orb, torch, dev, threads, 1920, 1080, 4000, 50000, 16, C5_SEED,
-                          steps=200, warmup=10)
+                          steps=200, warmup=10, match_streams2=True)
     # C4's latency shape (1 frame per GPU per step, batches of 8 over
     # 8 GPUs): one device-resident 1241x376 frame per call, extraction +
     # SearchByProjection vs 5,000 map points, each call waited for; and the

@@ -1546,6 +1546,9 @@ __device__ __forceinline__ void oct_rank_by_count(unsigned long long* sortBuf, i
 
 #define OCT_MAX_PASSES 512
 #define OCT_REG_KEYS 8  // keys per thread held in registers (n <= 8 x 512), small batches
+#ifndef OCT_REG_THREADS
+#define OCT_REG_THREADS 512  // workgroup of the register-key octree (calls of <= 16 frames)
+#endif
 
 template <bool REG, bool GNODES>
 __global__ __launch_bounds__(512) void k_octree(
@@ -2852,7 +2855,7 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
   // two interleaved pairs, profiles/r03_octree256.txt); 512 threads
   // was the old shape
   constexpr int bthreads = 256;
-  dim3 grid(nimg, levelEnd - levelBeg), block(reg ? 512 : bthreads);
+  dim3 grid(nimg, levelEnd - levelBeg), block(reg ? OCT_REG_THREADS : bthreads);
 #define ORB_OCTREE_LAUNCH(R, G)                                                                 \
   hipLaunchKernelGGL((k_octree<R, G>), grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,  \
                      gNid, ldsKeyCap, nodeCapMax, maxCellsPerLevel, outKeys, outCount, errFlag, \

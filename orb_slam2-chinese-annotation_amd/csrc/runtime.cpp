@@ -181,61 +181,6 @@ namespace {
     }                                                   \
   } while (0)
 
-// A call's launch sequence replayed as one hipGraph once the same call (same
-// key: every pointer, size and parameter its kernels capture) repeats.  Small
-// calls are launch-bound -- one frame is 7 dependent resize launches plus
-// FAST, octree and descriptors, a few microseconds each -- and a replayed
-// graph submits them at once.  The first call of a key runs directly (a
-// caller cycling through buffers never pays a capture); the second captures
-// on the handle's own stream and replays onto the caller's.
-struct CallGraph {
-  hipGraphExec_t exec = nullptr;
-  std::vector<uintptr_t> key, lastKey;
-  void reset() {
-    if (exec) hipGraphExecDestroy(exec);
-    exec = nullptr;
-    key.clear();
-  }
-};
-template <class F>
-static orb_status_t run_graphed(CallGraph& g, const std::vector<uintptr_t>& key,
-                                hipStream_t capStream, hipStream_t s, F&& enqueue) {
-  // a caller capturing its own graph gets the launches themselves
-  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cst) != hipSuccess || cst != hipStreamCaptureStatusNone)
-    return enqueue(s, false);
-  if (g.exec && key == g.key) {
-    if (hipGraphLaunch(g.exec, s) != hipSuccess) return ORB_EDEVICE;
-    return ORB_OK;
-  }
-  if (key != g.lastKey) {
-    g.lastKey = key;
-    return enqueue(s, false);
-  }
-  g.reset();
-  hipGraph_t graph = nullptr;
-  if (hipStreamBeginCapture(capStream, hipStreamCaptureModeThreadLocal) != hipSuccess)
-    return ORB_EDEVICE;
-  const orb_status_t st = enqueue(capStream, true);
-  const hipError_t ce = hipStreamEndCapture(capStream, &graph);
-  if (st) {
-    if (graph) hipGraphDestroy(graph);
-    return st;
-  }
-  if (ce != hipSuccess) return ORB_EDEVICE;
-  const hipError_t ie = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
-  hipGraphDestroy(graph);
-  if (ie != hipSuccess) {
-    g.exec = nullptr;
-    return ORB_EDEVICE;
-  }
-  g.key = key;
-  if (hipGraphLaunch(g.exec, s) != hipSuccess) return ORB_EDEVICE;
-  return ORB_OK;
-}
-// calls of at most this many frames / problems replay graphs
-#define GRAPH_MAX_BATCH 16
-
 static inline int cvRoundF(float v) { return (int)lrintf(v); }
 static inline short satShort(int v) { return (short)std::min(std::max(v, -32768), 32767); }
 
@@ -443,7 +388,6 @@ struct orb_extractor {
   // plan; keyed by the buffers it captured (any reallocation re-captures)
   hipGraphExec_t oneExec = nullptr;
   std::vector<const void*> oneKey;
-  CallGraph batchGraph;  // small extract_batch calls (run_graphed)
   int lastW = 0, lastH = 0;
   size_t lastImgStride = 0;
   const uint8_t* lastImg0 = nullptr;  // level 0 of the last batch (device)
@@ -952,14 +896,47 @@ static int stream_prio(bool least) {
 // its extraction by 30-50 % whenever a matcher ran beside it
 // (profiles/r03_streams.txt).  Handles on one device share it safely: fork /
 // join are per-handle events.
+#ifndef SIDE_CUMASK
+#define SIDE_CUMASK 1  // the side stream on an HSA queue of its own (a full-CU-mask stream)
+#endif
 static hipStream_t shared_side_stream(int device, int prio) {
   static std::mutex mu;
   static hipStream_t s[64] = {};
   if (device < 0 || device >= 64) return nullptr;
   std::lock_guard<std::mutex> g(mu);
-  if (!s[device] && hipStreamCreateWithPriority(&s[device], hipStreamNonBlocking, prio) != hipSuccess)
-    s[device] = nullptr;
+  if (!s[device]) {
+    hipError_t e;
+    if (SIDE_CUMASK) {
+      // HIP gives a CU-masked stream an HSA queue of its own instead of a
+      // pooled one: a mask of every CU of the device
+      hipDeviceProp_t prop;
+      e = hipGetDeviceProperties(&prop, device);
+      std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+      for (int c = 0; c < prop.multiProcessorCount; ++c) mask[c >> 5] |= 1u << (c & 31);
+      if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&s[device], (uint32_t)mask.size(), mask.data());
+    } else {
+      e = hipStreamCreateWithPriority(&s[device], hipStreamNonBlocking, prio);
+    }
+    if (e != hipSuccess) s[device] = nullptr;
+  }
   return s[device];  // process lifetime
+}
+
+// A handle's own stream (single-frame calls, host-buffer matchers, readbacks,
+// graph capture) at the device's least priority.  HIP backs the streams of a
+// process by a few HSA queues per priority level and maps a new stream onto
+// the least-used queue of its level; normal-priority streams a library
+// creates early (ORB-SLAM2 builds its extractors and matchers at start-up)
+// take normal queues the caller's own streams then share: a caller's
+// high-priority stream ran 2x slower beside busy normal-priority streams
+// after three idle normal streams had been created first, with or without
+// this library (tools/probe/contention_probe.py, profiles/r05_contention.txt).
+// The least priority keeps the library in the pool of its side stream.
+#ifndef OWN_PRIO
+#define OWN_PRIO 0  // handles' own streams: 0 least priority, 1 normal (compile-time A/B)
+#endif
+static hipError_t create_own_stream(hipStream_t* s) {
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, OWN_PRIO ? 0 : stream_prio(true));
 }
 
 static bool create_side_streams(orb_extractor* h) {
@@ -994,7 +971,7 @@ orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels
   h->minTh = min_th_fast;
   compute_tables(h);
   hipSetDevice(device);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+  if (create_own_stream(&h->stream) != hipSuccess ||
       !create_side_streams(h) ||
       hipEventCreateWithFlags(&h->evL0Fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->evL0Join, hipEventDisableTiming) != hipSuccess ||
@@ -1042,7 +1019,6 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   h->hLvl.release();
   h->hPyr.release();
   if (h->oneExec) hipGraphExecDestroy(h->oneExec);
-  h->batchGraph.reset();
   h->prof.destroy();
   if (h->ownStream && h->stream) hipStreamDestroy(h->stream);
   if (h->privSide) hipStreamDestroy(h->privSide);
@@ -1096,30 +1072,8 @@ orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_im
   if (capacity < h->plan.slotsPerImage) return ORB_ECAPACITY;
   if ((st = ensure_batch(h, n_images))) return st;
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-  if (n_images > GRAPH_MAX_BATCH || h->prof.enabled) {
-    st = run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors, capacity,
-                   d_counts, s);
-  } else {
-    const std::vector<uintptr_t> key = {
-        (uintptr_t)d_images, (uintptr_t)n_images, (uintptr_t)width, (uintptr_t)height, stride,
-        image_pitch, (uintptr_t)d_keypoints, (uintptr_t)d_descriptors, (uintptr_t)capacity,
-        (uintptr_t)d_counts, (uintptr_t)h->dArena.p, (uintptr_t)h->dCellKeys.p,
-        (uintptr_t)h->dGKeys.p, (uintptr_t)h->dGNid.p, (uintptr_t)h->dCellCount.p,
-        (uintptr_t)h->dOutKeys.p, (uintptr_t)h->dOutCount.p, (uintptr_t)h->dErr.p,
-        (uintptr_t)h->dRtab.p, (uintptr_t)h->dBands.p, (uintptr_t)h->dCells.p,
-        (uintptr_t)h->dOctNodes.p};
-    st = run_graphed(h->batchGraph, key, h->stream, s, [&](hipStream_t cs, bool cap) {
-      return run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors,
-                       capacity, d_counts, cs, cap);
-    });
-    if (!st) {
-      // a replayed or captured call skips run_batch's bookkeeping
-      HIP_TRY(hipEventRecord(h->evBatch, s));
-      h->lastImg0 = d_images;
-      h->lastImg0Pitch = image_pitch;
-      h->lastImg0Stride = (int)stride;
-    }
-  }
+  st = run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors, capacity,
+                 d_counts, s);
   if (st) return st;
   h->lastSingle = false;
   h->lastW = width;
@@ -1441,7 +1395,6 @@ struct orb_matcher {
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
   DevBuf dJac;  // Jacobi-resolve scratch (ORB_RESOLVE_JACOBI)
-  CallGraph projGraph;  // small orb_match_projection_local_batch calls (run_graphed)
   int resolveSchedule = ORB_RESOLVE_AUTO;  // orb_matcher_set_resolve
   int jacobiRounds = 6;
   // stereo / frame / BoW scratch
@@ -1499,7 +1452,7 @@ orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
   m->prof.names[2] = "k_proj_resolve";
   for (int i = 0; i < 3; ++i) m->prof.launchesPerCall[i] = 1;
   hipSetDevice(device);
-  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (create_own_stream(&m->stream) != hipSuccess) {
     delete m;
     return ORB_EDEVICE;
   }
@@ -1511,7 +1464,6 @@ void orb_matcher_destroy(orb_matcher_t* m) {
   if (!m) return;
   hipSetDevice(m->device);
   hipStreamSynchronize(m->stream);
-  m->projGraph.reset();
   DevBuf* bufs[] = {&m->dKeys, &m->dDesc, &m->dUr, &m->dLocked, &m->dNKeys, &m->dMps,
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
                     &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut, &m->dJac,
@@ -1587,7 +1539,6 @@ orb_status_t orb_match_projection_local_batch(
   const size_t jb = orb_k_proj_jacobi_bytes(kp_stride, mp_stride, n_problems, m->resolveSchedule);
   if (jb && (st = m->dJac.ensure(jb))) return st;
   StageProfiler& pf = m->prof;
-  auto enqueue = [&](hipStream_t s, bool) -> orb_status_t {
   std::vector<hipEvent_t>* ev = pf.begin_call();
   PROF_REC(ev, pf.t0(ev), s);
   PROF_REC(ev, pf.b(ev, 0), s);
@@ -1616,20 +1567,6 @@ orb_status_t orb_match_projection_local_batch(
   PROF_REC(ev, pf.e(ev, 2), s);
   PROF_REC(ev, pf.t1(ev), s);
   return ORB_OK;
-  };
-  if (n_problems > GRAPH_MAX_BATCH || pf.enabled) return enqueue(s, false);
-  std::vector<uintptr_t> key = {
-      (uintptr_t)n_problems, (uintptr_t)d_keys, (uintptr_t)d_desc, (uintptr_t)d_nkeys,
-      (uintptr_t)d_locked, (uintptr_t)kp_stride, (uintptr_t)d_mps, (uintptr_t)d_mp_desc,
-      (uintptr_t)d_nmps, (uintptr_t)mp_stride, (uintptr_t)d_kp_match, (uintptr_t)d_nmatches,
-      (uintptr_t)m->resolveSchedule, (uintptr_t)m->jacobiRounds, (uintptr_t)m->dCellStart.p,
-      (uintptr_t)m->dCellIdx.p, (uintptr_t)m->dTopk.p, (uintptr_t)m->dNcand.p,
-      (uintptr_t)m->dProjStage.p, (uintptr_t)m->dJac.p};
-  // the kernel parameters (bounds, scale factors, th, nnratio) by value
-  const size_t pw = (sizeof(P) + sizeof(uintptr_t) - 1) / sizeof(uintptr_t);
-  key.resize(key.size() + pw, 0);
-  memcpy(key.data() + key.size() - pw, &P, sizeof(P));
-  return run_graphed(m->projGraph, key, m->stream, s, enqueue);
 }
 
 orb_status_t orb_matcher_set_resolve(orb_matcher_t* m, int schedule, int jacobi_rounds) {
@@ -2801,7 +2738,7 @@ static orb_status_t vocab_new(int device, int k, int L, int scoring, int weighti
   V->device = device;
   V->k = k; V->L = L; V->scoring = scoring; V->weighting = weighting;
   hipSetDevice(device);
-  if (hipStreamCreateWithFlags(&V->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (create_own_stream(&V->stream) != hipSuccess) {
     delete V;
     return ORB_EDEVICE;
   }

@@ -460,11 +460,16 @@ def test_octree_12k_batch4_global_nodes(gpu, oracle):
 def test_host_pyramid_mirror(gpu, oracle):
     """orb_extractor_host_pyramid: the first request copies the call's levels
     once, later calls carry the copy in their graph; every level equals the
-    oracle.s pyramid on consecutive frames."""
+    oracle's pyramid on consecutive frames, and across frame-size changes
+    (the mirror and the staging are reallocated and the graph re-captured
+    while the mirror stays on)."""
     ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
-    for f in range(3):
-        img = gpu.synth_image(21, f, 1241, 376)
-        ext(img)
+    sizes = [(1241, 376)] * 3 + [(640, 480)] * 2 + [(1920, 1080), (1241, 376), (1241, 376)]
+    for f, (w, h) in enumerate(sizes):
+        img = gpu.synth_image(21, f, w, h)
+        k, d = ext(img)
+        kr, dr, _ = oracle.extract(img, 1000)
+        assert k.tobytes() == kr.tobytes() and d.tobytes() == dr.tobytes(), f
         ref = oracle.pyramid(img)
         for l in range(8):
             assert np.array_equal(ext.host_pyramid(l), ref[l]), (f, l)

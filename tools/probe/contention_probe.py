@@ -45,6 +45,25 @@ def pre_calls(orb, mode):
         h = orb.ORBextractor(2000, 1.2, 8, 20, 7)
         for im in imgs:
             h(im)
+    elif mode in ("raw3", "raw3keep", "raw3idle"):
+        # three HIP streams of the process's own (normal priority), each given a
+        # kernel unless idle, destroyed unless keep: is it the library or any stream?
+        import torch
+        hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        x = torch.zeros(1 << 16, device="cuda")
+        hs = []
+        for _ in range(3):
+            h = ctypes.c_void_p()
+            assert hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1)) == 0
+            hs.append(h)
+            if mode != "raw3idle":
+                with torch.cuda.stream(torch.cuda.ExternalStream(h.value)):
+                    x.add_(1.0)
+        torch.cuda.synchronize()
+        if mode != "raw3keep":
+            for h in hs:
+                hip.hipStreamDestroy(h)
+        pre_calls.keep = hs
     elif mode == "handles":
         hs = [orb.ORBextractor(2000, 1.2, 8, 20, 7) for _ in range(3)]
         del hs
