@@ -1077,13 +1077,19 @@ hipError_t orb_k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out
 }
 
 // k_grid_build4 (four waves) for frames with more keypoint slots than
-// GB4_MIN_SLOTS, the one-wave k_grid_build below that
-static bool grid4(int kpStride) { return kpStride > GB4_MIN_SLOTS && kpStride < 65536; }
+// GB4_MIN_SLOTS and for calls of a few frames (the one-wave build's serial
+// scatter is the latency of a one-frame call: 20 us of its 70 us
+// SearchByProjection, profiles/r05_latency.txt); the one-wave k_grid_build
+// for batches of small frames, where a wave per frame fills the chip
+#define GB4_FEW 16
+static bool grid4(int kpStride, int nproblems) {
+  return kpStride < 65536 && (kpStride > GB4_MIN_SLOTS || nproblems <= GB4_FEW);
+}
 
 hipError_t orb_k_grid_build(const orb_keypoint_t* keys, const int32_t* nkeys, int kpStride,
                             float minX, float minY, float invW, float invH, int32_t* cellStart,
                             int32_t* cellIdx, int nproblems, hipStream_t s) {
-  if (grid4(kpStride))
+  if (grid4(kpStride, nproblems))
     hipLaunchKernelGGL(k_grid_build4, dim3(nproblems), dim3(256), 0, s, keys, nkeys, kpStride, minX,
                        minY, invW, invH, cellStart, cellIdx, nullptr, nullptr, nullptr);
   else
@@ -1100,7 +1106,7 @@ hipError_t orb_k_grid_build_staged(const orb_keypoint_t* keys, const int32_t* nk
                                    int32_t* cellStart, int32_t* cellIdx, void* staged,
                                    int nproblems, hipStream_t s) {
   if (kpStride > GB_LDS_KEYS) return hipErrorNotSupported;
-  if (grid4(kpStride))
+  if (grid4(kpStride, nproblems))
     hipLaunchKernelGGL(k_grid_build4, dim3(nproblems), dim3(256), 0, s, keys, nkeys, kpStride, minX,
                        minY, invW, invH, cellStart, cellIdx, locked, uright, (uint4*)staged);
   else

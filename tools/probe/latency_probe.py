@@ -76,6 +76,26 @@ def main():
 
     out = {"tag": a.tag, "batch": B, "extract_ms": med(extract), "match_ms": med(match),
            "both_ms": med(lambda: (extract(), match()))}
+    # per-stage GPU time by the libraries' stage events (profile mode 1: the
+    # call's own launch shape; events add a little per stage)
+    ext.profile(1)
+    mt.profile(True)
+    for _ in range(100):
+        extract()
+        match()
+        s.synchronize()
+    stages = {}
+    for st in range(7):
+        name, ms, cnt = ext.profile_read(st)
+        if cnt:
+            stages[name] = ms / 100
+    for st in range(4):
+        name, ms, cnt = mt.profile_read(st)
+        if cnt:
+            stages[name] = ms / 100
+    ext.profile(0)
+    mt.profile(False)
+    out["stage_ms"] = stages
     host = orb.ORBextractor(NF, 1.2, 8, 20, 7)
     img0 = imgs[0]
     ts = []
