@@ -899,11 +899,26 @@ static int stream_prio(bool least) {
 #ifndef SIDE_CUMASK
 #define SIDE_CUMASK 1  // the side stream on an HSA queue of its own (a full-CU-mask stream)
 #endif
+static std::mutex g_sideMu;
+static hipStream_t g_side[64] = {};
+// The side streams are released by the process's exit handlers before the HIP
+// runtime's own teardown: a CU-masked stream left to that teardown crashed the
+// process at exit under rocprofv3 --kernel-trace (SIGSEGV in __cxa_finalize,
+// after the profiler's finalisation; profiles/r05_exit_crash.txt).
+static void release_side_streams() {
+  std::lock_guard<std::mutex> g(g_sideMu);
+  for (hipStream_t& st : g_side)
+    if (st) {
+      hipStreamDestroy(st);  // waits for the stream's work
+      st = nullptr;
+    }
+}
 static hipStream_t shared_side_stream(int device, int prio) {
-  static std::mutex mu;
-  static hipStream_t s[64] = {};
+  hipStream_t* s = g_side;
   if (device < 0 || device >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
+  std::lock_guard<std::mutex> g(g_sideMu);
+  static bool registered = false;
+  if (!registered) registered = std::atexit(release_side_streams) == 0;
   if (!s[device]) {
     hipError_t e;
     if (SIDE_CUMASK) {
@@ -919,7 +934,7 @@ static hipStream_t shared_side_stream(int device, int prio) {
     }
     if (e != hipSuccess) s[device] = nullptr;
   }
-  return s[device];  // process lifetime
+  return s[device];  // until exit
 }
 
 // A handle's own stream (single-frame calls, host-buffer matchers, readbacks,
