@@ -858,10 +858,16 @@ __host__ __device__ inline int fc_pitch(int C) {
 __host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
   return (maxRows * fc_pitch(maxCols) + 15) & ~15;  // 16-byte aligned strength map
 }
+#ifndef FC_LDS_PAD_TILES
+// unused byte tiles per wave: the LDS an LDS-DMA ring of that many further
+// cells would take (occupancy control, A/B only)
+#define FC_LDS_PAD_TILES 0
+#endif
 __host__ __device__ inline int fc_wave_bytes(int tileElems) {
   // byte tile + strengths + queue + corners (+ 64 rows x 64-bit NMS bitmap,
   // column-major path only)
-  return ((2 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + ((FC_ROWMAJOR && FC_TIGHT) ? 0 : 512)) + 15) & ~15;
+  return ((2 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + ((FC_ROWMAJOR && FC_TIGHT) ? 0 : 512) +
+           FC_LDS_PAD_TILES * tileElems) + 15) & ~15;
 }
 #define FC_CONST_PITCH (FC_TIGHT ? 48 : 56)  // the compile-time instance
 
@@ -2149,6 +2155,17 @@ struct DescWaveLds {
 #ifndef DESC_DBUF
 #define DESC_DBUF 0      // double-buffered window rows (A/B knob)
 #endif
+#ifndef DESC_GLDS
+// 1: window rows staged by LDS-DMA (buffer_load_dwordx4 ... lds, 264 16-byte
+// chunks per pair into a per-wave LDS buffer) and the next pair's DMA issued
+// as soon as this pair's rows are read back, so it overlaps IC_Angle, the row
+// pass and the sampling (A/B knob)
+#define DESC_GLDS 0
+#endif
+#define DESC_GLDS_CHUNKS 264
+#ifndef DESC_LDS_PAD
+#define DESC_LDS_PAD 0  // bytes of unused LDS per workgroup (occupancy control, A/B only)
+#endif  // 2 keypoints x 44 rows x 3 chunks of 16 bytes
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
@@ -2172,6 +2189,17 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // PPW == 0: ppwRt
   const int ppw = PPW ? PPW : ppwRt;
   __shared__ __attribute__((aligned(16))) DescWaveLds sm[4];
+#if DESC_LDS_PAD
+  // occupancy control for the DESC_GLDS A/B: the same LDS per workgroup
+  // without the DMA (never read; one store keeps it allocated)
+  __shared__ uint32_t sPad[DESC_LDS_PAD / 4];
+  if (threadIdx.x == 0) sPad[0] = 0u;
+#endif
+#if DESC_GLDS
+  // chunk q = 132 h + 3 r + k: keypoint h, window row r, 16-byte chunk k (5
+  // DMA instructions of 64 lanes; lanes past chunk 263 are masked off)
+  __shared__ __attribute__((aligned(16))) uint4 sStage[4][5 * 64];
+#endif
 #if DESC_LDS_TABLES
   // per workgroup: the rBRIEF pattern as floats (one ds_read_b128 per test
   // pair of points instead of a constant-memory load and four conversions),
@@ -2245,7 +2273,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   struct Pair {
     bool valid, active;
     int l, i, cx, cy;
-    uint32_t key;
+    uint32_t key, key0, key1;  // key0 / key1: the keypoints of half 0 / half 1
   };
   auto setup = [&](int j) {
     Pair P;
@@ -2262,6 +2290,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     const uint32_t k0 = __builtin_amdgcn_readlane(keyv, 2 * j);
     const uint32_t k1 = __builtin_amdgcn_readlane(keyv, 2 * j + 1);
     P.key = (half && P.active) ? k1 : k0;
+    P.key0 = k0;
+    P.key1 = i0 + 1 < nl ? k1 : k0;  // half 1 duplicates half 0 past the level's end
     P.cx = key_x(P.key);
     P.cy = key_y(P.key);
     return P;
@@ -2270,6 +2300,42 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // loads) from the 4-aligned byte at or below column cx-21
   uint32_t ra[12], rb[12], sha = 0, shb = 0;
   auto issue = [&](const Pair& P) {
+#if DESC_GLDS
+    {
+      const OrbLevelDesc& L = plan.lv[P.l];
+      const uint8_t* lvl;
+      int pitch;
+      if (P.l == 0) {
+        lvl = img0 + (long long)img * img0Pitch;
+        pitch = img0Stride;
+      } else {
+        lvl = arena + (long long)img * arenaPitch + L.arenaOff;
+        pitch = L.pitch;
+      }
+      const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
+      // the stage buffer's previous contents were read back (waited for)
+      // before this pair's DMA may overwrite them
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int q = 64 * i + lane;
+        if (q < DESC_GLDS_CHUNKS) {
+          const int kh = q >= DESC_GLDS_CHUNKS / 2;
+          const int qq = q - (kh ? DESC_GLDS_CHUNKS / 2 : 0);
+          const int r = (qq * 171) >> 9;  // qq / 3 for qq < 132
+          const int k = qq - 3 * r;
+          const uint32_t key = kh ? P.key1 : P.key0;
+          int y = key_y(key) - 21 + r;
+          y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
+          const uint32_t o = (uint32_t)(y * pitch + key_x(key) - 21) + im.sh;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              im.r, (__attribute__((address_space(3))) void*)&sStage[w][64 * i], 16,
+              (int)((o & ~3u) + 16 * k), 0, 0, 0);
+        }
+      }
+      return;
+    }
+#endif
 #if DESC_STUB >= 5
     sha = shb = (uint32_t)P.cx & 3u;
     return;
@@ -2340,10 +2406,46 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   if (cur.valid) issue(cur);
   for (int j = 0; j < ppw; ++j) {
     const Pair P = cur;
+#if DESC_GLDS
+    if (P.valid) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the pair's DMA has landed
+      if (second) {
+        const OrbLevelDesc& L = plan.lv[P.l];
+        const uint8_t* lvl = P.l == 0 ? img0 + (long long)img * img0Pitch
+                                      : arena + (long long)img * arenaPitch + L.arenaOff;
+        const int pitch = P.l == 0 ? img0Stride : L.pitch;
+        const uint32_t lsh = (uint32_t)((uintptr_t)lvl & 3);
+        auto read_row = [&](int r, uint32_t* d) {
+          int y = P.cy - 21 + r;
+          y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
+          const uint4* src = &sStage[w][half * (DESC_GLDS_CHUNKS / 2) + 3 * r];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const uint4 v = src[k];
+            d[4 * k] = v.x;
+            d[4 * k + 1] = v.y;
+            d[4 * k + 2] = v.z;
+            d[4 * k + 3] = v.w;
+          }
+          return ((uint32_t)(y * pitch + P.cx - 21) + lsh) & 3u;
+        };
+        sha = read_row(2 * hl, ra);
+        shb = read_row(2 * hl + 1, rb);
+        realign(ra, sha);
+        realign(rb, shb);
+      }
+    }
+    // the next pair's DMA goes out now, behind this pair's whole computation
+    if (j + 1 < ppw) {
+      cur = setup(j + 1);
+      if (cur.valid) issue(cur);
+    }
+#else
     if (P.valid && second) {
       realign(ra, sha);
       realign(rb, shb);
     }
+#endif
 #if DESC_DBUF
     // double-buffered window rows: the pair's realigned rows move to working
     // registers and the next pair's loads go out at once, so they overlap
@@ -2398,7 +2500,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
 #endif
     // (the rows stay in registers through the row pass: the next pair's loads
     // go out after it)
-    if (!DESC_DBUF && !P.valid && j + 1 < ppw) {
+    if (!DESC_DBUF && !DESC_GLDS && !P.valid && j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
@@ -2517,7 +2619,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       }
     }
 #endif
-    if (!DESC_DBUF && j + 1 < ppw) {
+    if (!DESC_DBUF && !DESC_GLDS && j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
