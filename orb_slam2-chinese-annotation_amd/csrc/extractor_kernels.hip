@@ -37,6 +37,12 @@
 #define PYR_IMAGES_PER_WG 16  // images per k_pyr_resize workgroup
 #endif
 #define PYR_TH 32
+#ifndef PYR_SMALL_WGS
+#define PYR_SMALL_WGS 0   // levels launching fewer workgroups than this ...
+#endif
+#ifndef PYR_SMALL_IPW
+#define PYR_SMALL_IPW 16  // ... take this many images per workgroup
+#endif
 // Staged source window (rows x dwords): >= the source rows a 32-row output
 // tile touches, multiple of 4, and >= the dwords of source row a 128-column
 // tile touches + 2 read-ahead.  Narrow: scale factors <= 1.25 (every ORB-SLAM2
@@ -143,7 +149,11 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   __shared__ __attribute__((aligned(16))) uint32_t tile[SROWS][SW];
   const int tid = threadIdx.x;
   const int tx = tid & 31, ty = tid >> 5;
-  const int x0 = blockIdx.x * PYR_TW, y0 = blockIdx.y * PYR_TH;
+  // XCD-contiguous tile order: a tile's neighbours (whose source windows
+  // share 128-byte lines with it) run on the same XCD and hit its L2
+  int bx, by, bz;
+  xcd_swizzle3(bx, by, bz);
+  const int x0 = bx * PYR_TW, y0 = by * PYR_TH;
   const int xs = x0 + 4 * tx;
   // this thread's weight tables, issued together with the source loads so the
   // workgroup pays one memory round trip before its compute
@@ -184,7 +194,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
     pf.issue(img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((sh - 1) * srcStride + sw)),
              ALIGNED, eoff);
   };
-  int z = blockIdx.z;
+  int z = bz;
   if (z >= nImg) return;
   issue(z);
   // Horizontal taps with v_perm + v_dot2: the thread's 4 columns read source
@@ -214,20 +224,11 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
       h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(W1, W0, sel[j])),
                                     wts[j], 0u, false);
   };
-  for (; z < nImg; z += gridDim.z) {
-    __syncthreads();  // the previous image's taps have read the window
-#if PYR_LOAD16
-    pf.commit(&tile[0][0], SW, nR, nStage, magic, ALIGNED);
-#else
-    pf.commit(&tile[0][0], SW, nR, nStage, magic);
-#endif
-    if (z + (int)gridDim.z < nImg) issue(z + gridDim.z);
-    __syncthreads();
-    if (xs >= dw) continue;
+  auto compute = [&](int zc) {
     // destination: arena level, pitch a multiple of 128 >= dw rounded to 4, so a
     // whole dword store at xs < dw stays inside the row (padding bytes unused)
     const __amdgpu_buffer_rsrc_t rd =
-        make_rsrc(dst + (long long)z * dstImgPitch, (uint32_t)(dh * dstStride));
+        make_rsrc(dst + (long long)zc * dstImgPitch, (uint32_t)(dh * dstStride));
 #pragma unroll
     for (int rr = 0; rr < PYR_TH / 8; ++rr) {
       const int y = y0 + (PYR_TH / 8) * ty + rr;
@@ -249,6 +250,18 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
       }
       buf_st32(rd, (uint32_t)(y * dstStride + xs), packed);
     }
+  };
+  for (; z < nImg; z += gridDim.z) {
+    __syncthreads();  // the previous image's taps have read the window
+#if PYR_LOAD16
+    pf.commit(&tile[0][0], SW, nR, nStage, magic, ALIGNED);
+#else
+    pf.commit(&tile[0][0], SW, nR, nStage, magic);
+#endif
+    if (z + (int)gridDim.z < nImg) issue(z + gridDim.z);
+    __syncthreads();
+    if (xs >= dw) continue;
+    compute(z);
   }
 }
 
@@ -2818,7 +2831,9 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   // each workgroup resizes one tile of PYR_IMAGES_PER_WG images (default
   // 16: with two extraction lanes 12 / 16 / 24 measured 323.8k / 322.3-324.4k /
   // 324.7k against 321.3-321.8k frames/s for 8, profiles/r03_lanes.txt)
-  constexpr int perWg = PYR_IMAGES_PER_WG;
+  const int tiles = ((dw + PYR_TW - 1) / PYR_TW) * ((dh + PYR_TH - 1) / PYR_TH);
+  const int perWg = tiles * ((nimg + PYR_IMAGES_PER_WG - 1) / PYR_IMAGES_PER_WG) < PYR_SMALL_WGS
+                        ? PYR_SMALL_IPW : PYR_IMAGES_PER_WG;
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, (nimg + perWg - 1) / perWg),
       block(256);
   // every image base and row start 4-aligned: one load per staged dword

@@ -265,4 +265,25 @@ __device__ __forceinline__ void xcd_swizzle(int& bx, int& by) {
   by = logical / gx;
   bx = logical - by * gx;
 }
+// The same over a 3-D grid (x fastest, then y, then z): XCD k runs one
+// contiguous range of (x, y, z).
+#ifndef ORB_XCD_SWIZZLE3
+#define ORB_XCD_SWIZZLE3 1
+#endif
+__device__ __forceinline__ void xcd_swizzle3(int& bx, int& by, int& bz) {
+  const int gx = gridDim.x, gxy = gx * gridDim.y, n = gxy * gridDim.z;
+  if (!ORB_XCD_SWIZZLE3) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    bz = blockIdx.z;
+    return;
+  }
+  const int L = blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z;
+  const int xcd = L & 7, pos = L >> 3, q = n >> 3, r = n & 7;
+  const int logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  bz = logical / gxy;
+  const int rem = logical - bz * gxy;
+  by = rem / gx;
+  bx = rem - by * gx;
+}
 
