@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--calls", type=int, default=300)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--timeline", type=int, default=0,
+                    help="only N extract+match calls 1 ms apart (for a kernel-trace timeline)")
     a = ap.parse_args()
     import torch
     orb = load_pkg()
@@ -63,6 +65,14 @@ def main():
         mt.search_by_projection_batch(B, k.data_ptr(), de.data_ptr(), n.data_ptr(), d_lk.data_ptr(),
                                       cap, d_mps.data_ptr(), d_mpd.data_ptr(), d_nm.data_ptr(), M,
                                       W, H, scale, 1.0, km.data_ptr(), nm.data_ptr(), s.cuda_stream)
+
+    if a.timeline:
+        for _ in range(a.timeline):
+            extract()
+            match()
+            s.synchronize()
+            time.sleep(0.001)
+        return
 
     def med(fn):
         ts = []
