@@ -326,9 +326,10 @@ _HIP = None
 _STREAMS = {}
 # HIP backs streams by a few HSA queues per priority level (GPU_MAX_HW_QUEUES,
 # 4 here), and two streams on one queue run in submission order.  The
-# extractor's side stream is low priority (its own pool); the extraction
-# stream is normal priority and the match and copy streams high priority, so
-# no two of the concurrently busy streams can share a queue
+# library's own streams are least priority and its side stream has an HSA
+# queue of its own (a CU-masked stream); the extraction streams are normal
+# priority and the match and copy streams high priority, so no two of the
+# concurrently busy streams can share a queue
 # (tools/archive/r03/c5_swap.py, profiles/r03_streams.txt)
 _STREAM_PRIO = {"extract": "normal", "match": "greatest", "h2d": "greatest", "d2h": "greatest"}
 _STREAM_PRIO.update({f"extract{i}": "normal" for i in range(1, 4)})
