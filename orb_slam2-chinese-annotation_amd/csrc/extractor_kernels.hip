@@ -1565,6 +1565,9 @@ __device__ __forceinline__ void oct_rank_by_count(unsigned long long* sortBuf, i
 
 #define OCT_MAX_PASSES 512
 #define OCT_REG_KEYS 8  // keys per thread held in registers (n <= 8 x 512), small batches
+#ifndef OCT_BATCH_THREADS
+#define OCT_BATCH_THREADS 256  // workgroup of the batch octree (A/B: 128)
+#endif
 #ifndef OCT_REG_THREADS
 #define OCT_REG_THREADS 512  // workgroup of the register-key octree (calls of <= 16 frames)
 #endif
@@ -1796,8 +1799,10 @@ __global__ __launch_bounds__(512) void k_octree(
         // (OCT_RANK_MAX / T candidates per thread: workgroups of 256 or 512)
         if (T >= OCT_RANK_MAX)
           oct_rank_by_count<1>(sortBuf, ncand, t, T);
-        else
+        else if (T >= 256)
           oct_rank_by_count<OCT_RANK_MAX / 256>(sortBuf, ncand, t, T);
+        else
+          oct_rank_by_count<OCT_RANK_MAX / 128>(sortBuf, ncand, t, T);
       } else {
         block_bitonic_desc(sortBuf, m2);
       }
@@ -2971,7 +2976,8 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
   // other lane's kernels (bench 317.0k / 316.6k vs 315.5k / 315.2k frames/s,
   // two interleaved pairs, profiles/r03_octree256.txt); 512 threads
   // was the old shape
-  constexpr int bthreads = 256;
+  constexpr int bthreads = OCT_BATCH_THREADS;
+  static_assert(OCT_BATCH_THREADS >= 128 && OCT_BATCH_THREADS % 64 == 0, "octree rank needs >= 128 threads");
   dim3 grid(nimg, levelEnd - levelBeg), block(reg ? OCT_REG_THREADS : bthreads);
 #define ORB_OCTREE_LAUNCH(R, G)                                                                 \
   hipLaunchKernelGGL((k_octree<R, G>), grid, block, lds, s, *plan, cellCount, cellKeys, gKeys,  \

@@ -67,7 +67,9 @@ struct OrbBandDesc {
   int16_t level, y0, y1, x0, x1, nCells;
   int32_t cellBeg;
 };
+#ifndef ORB_OCTREE_LDS_KB
 #define ORB_OCTREE_LDS_KB 52  // k_octree node tables + keys per workgroup (swept 24-64)
+#endif
 #define ORB_BAND_BYTES 6656  // elements (rows x LDS pitch) of one FAST band: f16 pixels + strengths; 5 workgroups per CU (swept 4-10 K)
 
 // One ORB_BLUR_TW x ORB_BLUR_TH output tile of the 7x7 Gaussian pass over level `level`.
