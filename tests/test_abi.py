@@ -105,3 +105,37 @@ def test_stereo_rejects_short_level_stride(orb):
     dp = np.zeros(1, np.float32)
     # validation happens before any device work (no GPU needed)
     assert L.orb_stereo_match(ctypes.c_void_p(1), ctypes.byref(s), orb._ptr(ur), orb._ptr(dp)) == orb.ORB_EINVAL
+
+
+def test_resolve_kernel_routing(orb):
+    """The resolve kernel orb_matcher_resolve_kernel reports (its host routing,
+    matcher_kernels.hip orb_k_proj_resolve_kernel) for the shapes the bench
+    and the tests use; host logic only, no GPU."""
+    L = orb.lib()
+    f = L.orb_k_proj_resolve_kernel
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int] * 4
+    AUTO, PREFIX, FP, JAC = 0, 1, 2, 3
+    W1, W4, W8, FPK, JACK = 1, 4, 8, 16, 32
+    cap = 1100  # keypoint slots of a 1241x376, 1000-feature frame (order of)
+    assert f(1024, cap, 5000, AUTO) == W1      # the headline's batches
+    assert f(256, cap, 5000, AUTO) == W1
+    assert f(32, cap, 5000, AUTO) == W4        # 9-127 problems
+    assert f(9, cap, 5000, AUTO) == W4
+    assert f(8, cap, 5000, AUTO) == FPK        # calls of <= 8 problems: fixed point
+    assert f(1, cap, 5000, AUTO) == FPK
+    assert f(16, 4400, 50000, AUTO) == FPK     # C5: large maps
+    assert f(16, 4400, 50000, PREFIX) == W8
+    assert f(1024, cap, 5000, PREFIX) == W1
+    assert f(4, cap, 5000, PREFIX) == W4
+    assert f(1024, cap, 5000, FP) == FPK
+    assert f(16, 4400, 50000, JAC) == JACK
+    # claims that do not fit in LDS (12 B per keypoint slot): prefix windows
+    assert f(1, 15000, 50000, AUTO) == W8
+    assert f(1, 15000, 50000, JAC) == W8
+    assert f(1, 15000, 5000, FP) == W4
+    jb = L.orb_k_proj_jacobi_bytes
+    jb.restype = ctypes.c_size_t
+    jb.argtypes = [ctypes.c_int] * 4
+    assert jb(cap, 5000, 1024, AUTO) == 0
+    assert jb(4400, 50000, 16, JAC) > 0
