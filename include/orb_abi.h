@@ -163,6 +163,11 @@ orb_status_t orb_extractor_pyramid_level(orb_extractor_t* h, int level, uint8_t*
  * keypoint copy.  ORB_EINVAL after a batch call. */
 orb_status_t orb_extractor_host_pyramid(orb_extractor_t* h, int level, const uint8_t** data,
                                         int* width, int* height, size_t* stride);
+/* Stops the per-call DMA of levels 1.. that orb_extractor_host_pyramid turned
+ * on (for a caller that no longer reads the mirror): later calls move no
+ * pyramid bytes until the next request, which again copies once and turns the
+ * per-call copy back on. */
+orb_status_t orb_extractor_host_pyramid_off(orb_extractor_t* h);
 /* The 7x7 Gaussian-blurred copy of level `level` of the first image of the
  * last call (the image computeDescriptors samples, src/ORBextractor.cc:1143-1145);
  * same conventions as orb_extractor_pyramid_level. */

@@ -107,6 +107,7 @@ def lib() -> ctypes.CDLL:
         "orb_extractor_pyramid_level": (i32, [vp, i32, vp, sz, vp, vp]),
         "orb_extractor_blurred_level": (i32, [vp, i32, vp, sz, vp, vp]),
         "orb_extractor_host_pyramid": (i32, [vp, i32, vp, vp, vp, vp]),
+        "orb_extractor_host_pyramid_off": (i32, [vp]),
         "orb_extractor_extract_batch": (i32, [vp, vp, i32, i32, i32, sz, sz, vp, vp, i32, vp, vp]),
         "orb_extractor_batch_level": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "orb_extractor_stream": (vp, [vp]),
@@ -305,6 +306,10 @@ class ORBextractor:
         buf = (ctypes.c_uint8 * (st.value * (h.value - 1) + w.value)).from_address(p.value)
         a = np.frombuffer(buf, np.uint8)
         return np.lib.stride_tricks.as_strided(a, (h.value, w.value), (st.value, 1)).copy()
+
+    def host_pyramid_off(self):
+        """Stop the per-call host mirror of levels 1.. (orb_extractor_host_pyramid_off)."""
+        _check(lib().orb_extractor_host_pyramid_off(self._h), "host_pyramid_off")
 
     @property
     def mvImagePyramid(self) -> list:

@@ -1273,6 +1273,16 @@ orb_status_t orb_extractor_host_pyramid(orb_extractor_t* h, int level, const uin
   return ORB_OK;
 }
 
+orb_status_t orb_extractor_host_pyramid_off(orb_extractor_t* h) {
+  if (!h) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  // the next single-frame call re-keys its graph without the pyramid DMA
+  // (pyrReadback is part of the graph key); the mirror buffer is kept
+  h->pyrReadback = false;
+  h->hPyrValid = false;
+  return ORB_OK;
+}
+
 orb_status_t orb_extractor_blurred_level(orb_extractor_t* h, int level, uint8_t* dst,
                                          size_t dst_stride, int* width, int* height) {
   if (!h) return ORB_EINVAL;

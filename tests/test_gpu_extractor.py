@@ -475,3 +475,13 @@ def test_host_pyramid_mirror(gpu, oracle):
             assert np.array_equal(ext.host_pyramid(l), ref[l]), (f, l)
     with pytest.raises(gpu.OrbError):
         ext.host_pyramid(8)
+    # switched off: calls move no pyramid; the next request copies once again
+    ext.host_pyramid_off()
+    for f in range(2):
+        img = gpu.synth_image(22, f, 1241, 376)
+        k, d = ext(img)
+        kr, dr, _ = oracle.extract(img, 1000)
+        assert k.tobytes() == kr.tobytes() and d.tobytes() == dr.tobytes(), f
+    ref = oracle.pyramid(img)
+    for l in range(8):
+        assert np.array_equal(ext.host_pyramid(l), ref[l]), ("off", l)
