@@ -978,6 +978,19 @@ __device__ __forceinline__ int fast_score_u8(const uint8_t* tile, int coff, int 
 // <= 96 -> 7; MI355X_MICROARCH "Residency")
 #define FC_WPE 7
 #endif
+#ifdef FC_STAMPS  // per-phase clock stamps of image 0's cells (tools/probe/fc_stamps.py), off by default
+__device__ unsigned long long g_fc_stamps[8192][8];
+extern "C" hipError_t orb_k_fc_stamps(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fc_stamps), sizeof(g_fc_stamps));
+}
+#define FCSTAMP(k)                                                                   \
+  do {                                                                               \
+    const unsigned long long tnow = __builtin_amdgcn_s_memtime();                    \
+    if (img == 0 && lane == 0 && ci < 8192) g_fc_stamps[ci][k] = tnow;               \
+  } while (0)
+#else
+#define FCSTAMP(k) do { } while (0)
+#endif
 template <int PT>
 #if FC_WPE > 0
 __global__ __launch_bounds__(64 * FC_WAVES) __attribute__((amdgpu_waves_per_eu(FC_WPE)))
@@ -1050,6 +1063,7 @@ void k_fast_cells(
   OrbCellDesc ncd = cells[ci];
   issue(ncd);
   for (int jc = 0; jc < FC_CPW && ci < cellEnd; ++jc) {
+  FCSTAMP(0);
   const OrbCellDesc cd = ncd;
   const int R = cd.y1 - cd.y0, C = cd.x1 - cd.x0;
   const long long slot = (long long)img * plan.ncells + ci;
@@ -1102,6 +1116,7 @@ void k_fast_cells(
               invW = __builtin_amdgcn_rcpf((float)iw);
   wave_lds_sync();
 
+  FCSTAMP(1);  // staged, strengths cleared, next cell's loads issued
   int nq = 0, nc = 0;  // wave-uniform queue / corner counts
   // score the queued candidates, list the corners (m > t)
   auto flush = [&](int t, bool fresh) {
@@ -1371,6 +1386,7 @@ void k_fast_cells(
   (void)compact;
 #endif
   fast_pass(ti, true);
+  FCSTAMP(2);
 #if FC_STUB >= 1
   int n = nc;
   (void)nms_emit;
@@ -1380,6 +1396,7 @@ void k_fast_cells(
   nms(ti);
   int n = compact();
 #endif
+  FCSTAMP(3);
   if (n == 0 && tm != ti) {
     // ---- phase B: no keypoint at iniThFAST -> minThFAST (:846-850)
     nc = 0;
@@ -1398,6 +1415,10 @@ void k_fast_cells(
   if (lane == 0) cellCount[slot] = sink == 0xFFFFFFFFu ? 1 : 0;
 #else
   if (lane == 0) cellCount[slot] = n;
+#endif
+  FCSTAMP(4);
+#ifdef FC_STAMPS
+  if (img == 0 && lane == 0 && ci < 8192) g_fc_stamps[ci][5] = (unsigned long long)jc;
 #endif
   ci = ciNext;
   wave_lds_sync();  // the next cell's staging overwrites the tile
