@@ -37,11 +37,12 @@
 #define PYR_IMAGES_PER_WG 16  // images per k_pyr_resize workgroup
 #endif
 #define PYR_TH 32
-#ifndef PYR_SMALL_WGS
-#define PYR_SMALL_WGS 0   // levels launching fewer workgroups than this ...
-#endif
-#ifndef PYR_SMALL_IPW
-#define PYR_SMALL_IPW 16  // ... take this many images per workgroup
+#ifndef PYR_TARGET_WGS
+// > 0: fewer images per workgroup below this many workgroups per level.  At
+// 2048, 16 C5 frames resize in 0.138 instead of 0.198 ms and C3 gains 2.5 %,
+// but C5's pipelined rate loses 5.5 % (the wider resize crowds the matcher's
+// 16-CU resolve) and the headline is unchanged (profiles/r05_resize_target.txt)
+#define PYR_TARGET_WGS 0
 #endif
 // Staged source window (rows x dwords): >= the source rows a 32-row output
 // tile touches, multiple of 4, and >= the dwords of source row a 128-column
@@ -2857,9 +2858,15 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   // each workgroup resizes one tile of PYR_IMAGES_PER_WG images (default
   // 16: with two extraction lanes 12 / 16 / 24 measured 323.8k / 322.3-324.4k /
   // 324.7k against 321.3-321.8k frames/s for 8, profiles/r03_lanes.txt)
+  // PYR_IMAGES_PER_WG images per workgroup; with PYR_TARGET_WGS > 0 fewer when
+  // the level would launch under that many workgroups (a workgroup walks its
+  // images one after another: C5's 16 1920x1080 frames are 510 workgroups of
+  // 16 images on level 1)
   const int tiles = ((dw + PYR_TW - 1) / PYR_TW) * ((dh + PYR_TH - 1) / PYR_TH);
-  const int perWg = tiles * ((nimg + PYR_IMAGES_PER_WG - 1) / PYR_IMAGES_PER_WG) < PYR_SMALL_WGS
-                        ? PYR_SMALL_IPW : PYR_IMAGES_PER_WG;
+  const int perWg =
+      PYR_TARGET_WGS > 0
+          ? std::max(1, std::min(PYR_IMAGES_PER_WG, (int)((long long)tiles * nimg / std::max(PYR_TARGET_WGS, 1))))
+          : PYR_IMAGES_PER_WG;
   dim3 grid((dw + PYR_TW - 1) / PYR_TW, (dh + PYR_TH - 1) / PYR_TH, (nimg + perWg - 1) / perWg),
       block(256);
   // every image base and row start 4-aligned: one load per staged dword

@@ -20,11 +20,12 @@ ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--calls", type=int, default=20)
 ap.add_argument("--width", type=int, default=1241)
 ap.add_argument("--height", type=int, default=376)
+ap.add_argument("--features", type=int, default=1000)
 a = ap.parse_args()
 W, H, B = a.width, a.height, a.batch
 imgs = np.stack([orb.synth_image(7, f, W, H) for f in range(16)])
 imgs = np.concatenate([imgs] * ((B + 15) // 16))[:B]
-ext = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+ext = orb.ORBextractor(a.features, 1.2, 8, 20, 7)
 cap = ext.capacity(W, H)
 d_img = torch.from_numpy(imgs).cuda()
 d_kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
