@@ -1203,6 +1203,9 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
 //  * k_proj_jacobi rounds over the whole chip, then k_proj_resolve_fp for any
 //    problem not settled (only on request: the rounds compete with a
 //    concurrent extraction for every CU, profiles/r04_c5_stages.txt).
+#ifndef RESOLVE_FP_T
+#define RESOLVE_FP_T 1024  // threads of k_proj_resolve_fp (1024-point windows: 1024 / T points per thread)
+#endif
 #define RESOLVE_FP_MIN_MAP 20000
 #define RESOLVE_FP_FEW 8
 #define RESOLVE_FP_LDS_MAX (160 * 1024 - 1024)
@@ -1240,7 +1243,7 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   if (kern == ORB_RESOLVE_KERNEL_FIXED_POINT || kern == ORB_RESOLVE_KERNEL_JACOBI) {
     const size_t ldsFp = (size_t)kpStride * 12;
     if (ldsFp > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)k_proj_resolve_fp<1024>,
+      hipError_t e = hipFuncSetAttribute((const void*)k_proj_resolve_fp<RESOLVE_FP_T, 1024 / RESOLVE_FP_T>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsFp);
       if (e != hipSuccess) return e;
     }
@@ -1261,7 +1264,8 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
       done = jacScratch + R;
       doneStride = js;
     }
-    hipLaunchKernelGGL(k_proj_resolve_fp<1024>, dim3(nproblems), dim3(1024), ldsFp, s, keys, desc,
+    hipLaunchKernelGGL((k_proj_resolve_fp<RESOLVE_FP_T, 1024 / RESOLVE_FP_T>), dim3(nproblems), dim3(RESOLVE_FP_T),
+                       ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
                        cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
     return hipGetLastError();
