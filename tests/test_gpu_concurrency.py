@@ -258,3 +258,48 @@ def test_batch_rate_with_extra_caller_streams(gpu):
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["spins"] > 0 and out["same"], out  # every caller stream ran; results unchanged
     assert out["busy"] > 0.85 * out["idle"], out
+
+
+_EXIT_CHILD = r"""
+import sys
+import numpy as np, torch
+sys.path.insert(0, ROOT); sys.path.insert(0, ROOT + '/tests')
+from conftest import load_pkg
+orb = load_pkg()
+W, H, B = 640, 480, 8   # B >= 4: the batch forks level 0's FAST onto the side stream
+imgs = np.stack([orb.synth_image(5, f, W, H) for f in range(B)])
+d = torch.from_numpy(imgs).cuda()
+ext = orb.ORBextractor(500, 1.2, 8, 20, 7)
+cap = ext.capacity(W, H)
+k = torch.zeros((B, cap, 7), dtype=torch.int32, device='cuda')
+de = torch.zeros((B, cap, 32), dtype=torch.uint8, device='cuda')
+n = torch.zeros(B, dtype=torch.int32, device='cuda')
+ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap, n.data_ptr())
+torch.cuda.synchronize()
+assert int(n.min()) > 0
+print('child done', flush=True)
+"""
+
+
+def test_clean_exit_under_kernel_trace(gpu, tmp_path):
+    """The shared side stream is a CU-masked stream; left to the HIP runtime's
+    own teardown it crashed the process at exit under rocprofv3 --kernel-trace
+    (SIGSEGV in __cxa_finalize, profiles/r05_exit_crash.txt).  The library now
+    releases it from an exit handler: a child that runs a side-stream batch
+    and exits under the kernel tracer must exit 0."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        pytest.skip("rocprofv3 not on PATH")
+    root = str(Path(__file__).resolve().parents[1])
+    env = dict(os.environ, TMPDIR="/tmp")
+    r = subprocess.run([prof, "--kernel-trace", "-d", str(tmp_path / "trace"), "-o", "run",
+                        "--output-format", "csv", "--", sys.executable, "-c",
+                        f"ROOT = {root!r}\n" + _EXIT_CHILD],
+                       capture_output=True, text=True, timeout=150, env=env, cwd="/tmp")
+    assert "child done" in r.stdout, r.stderr[-2000:]
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
