@@ -918,7 +918,10 @@ static hipStream_t shared_side_stream(int device, int prio) {
   if (device < 0 || device >= 64) return nullptr;
   std::lock_guard<std::mutex> g(g_sideMu);
   static bool registered = false;
-  if (!registered) registered = std::atexit(release_side_streams) == 0;
+#ifndef SIDE_RELEASE_AT_EXIT
+#define SIDE_RELEASE_AT_EXIT 1  // 0: leave the side streams to the runtime's teardown (the test's negative control)
+#endif
+  if (SIDE_RELEASE_AT_EXIT && !registered) registered = std::atexit(release_side_streams) == 0;
   if (!s[device]) {
     hipError_t e;
     if (SIDE_CUMASK) {
