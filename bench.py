@@ -406,6 +406,9 @@ def pipelined(torch, dev, extract, match, n_sets, steps, warmup, lanes=None, mat
 
 
 C3_SEED, C5_SEED = 0x4B495454 ^ 3, 5
+# buffer sets the C3 / C5 pipelines rotate (each with its own extractor and
+# matcher handles): a set is rewritten only after its previous match
+_SEC_SETS = int(os.environ.get("ORB_BENCH_SEC_SETS", "4"))
 
 
 def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
@@ -422,7 +425,7 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
     dl, dr = torch.from_numpy(il).to(dev), torch.from_numpy(ir).to(dev)
     z = lambda *sh, dt=torch.int32: torch.zeros(sh, dtype=dt, device=dev)
     sets = []
-    for _ in range(2):
+    for _ in range(_SEC_SETS):
         L = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
         R = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
         cap = L.capacity(W, H)
@@ -446,7 +449,7 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
                              st["nr"].data_ptr(), st["cap"], bf, fx, st["ur"].data_ptr(),
                              st["dp"].data_ptr(), st["sad"].data_ptr(), s)
 
-    sec = pipelined(torch, dev, extract, match, 2, steps, warmup)
+    sec = pipelined(torch, dev, extract, match, _SEC_SETS, steps, warmup)
     if min(int(torch.minimum(st["nl"], st["nr"]).min().item()) for st in sets) < 0:
         raise RuntimeError("C3: an extraction reported failure (negative count)")
     res = {"value": P / sec, "unit": "pairs/s", "pairs_per_step": P, "ms_per_step": sec * 1e3,
@@ -462,14 +465,16 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
     (orb_synth_local_map(seed + i, ...)), B problems (frames 0..B-1 of `seed`)
     per launch, pipelined as `pipelined`; also the matcher alone, serial on
     one stream.  Returns (result, state) with set 0's outputs for parity."""
+    nsets = _SEC_SETS
     ext = orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
-    exts = [ext, orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)]  # one per set (lane)
+    exts = [ext] + [orb.ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
+                    for _ in range(nsets - 1)]  # one per set
     scale = np.float32(ext.GetScaleFactors())
     cap = ext.capacity(W, H)
     d = torch.from_numpy(synth_images(orb, seed, list(range(B)), W, H, threads)).to(dev)
     z = lambda *sh, dt=torch.int32: torch.zeros(sh, dtype=dt, device=dev)
     sets = [dict(k=z(B, cap, 7), de=z(B, cap, 32, dt=torch.uint8), n=z(B), km=z(B, cap),
-                 nm=z(B)) for _ in range(2)]
+                 nm=z(B)) for _ in range(nsets)]
     s0 = torch.cuda.Stream(dev)
     ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, sets[0]["k"].data_ptr(),
                       sets[0]["de"].data_ptr(), cap, sets[0]["n"].data_ptr(), s0.cuda_stream)
@@ -489,7 +494,7 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
     d_nm = torch.full((B,), M, dtype=torch.int32, device=dev)
     # one matcher handle per buffer set: a handle's scratch serves one call at a
     # time, and two sets' matches may run at once on two streams
-    mts = [orb.ORBmatcher(0.8, device=dev.index) for _ in range(2)]
+    mts = [orb.ORBmatcher(0.8, device=dev.index) for _ in range(nsets)]
 
     def extract(j, s):
         st = sets[j]
@@ -503,8 +508,8 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
                                           d_mpd.data_ptr(), d_nm.data_ptr(), M, W, H, scale, 1.0,
                                           st["km"].data_ptr(), st["nm"].data_ptr(), s)
 
-    sec = pipelined(torch, dev, extract, match, 2, steps, warmup)
-    sec2 = pipelined(torch, dev, extract, match, 2, steps, warmup, match_lanes=2) \
+    sec = pipelined(torch, dev, extract, match, nsets, steps, warmup)
+    sec2 = pipelined(torch, dev, extract, match, nsets, steps, warmup, match_lanes=2) \
         if match_streams2 else None
     if min(int(st["n"].min().item()) for st in sets) < 0:
         raise RuntimeError("extract + match: an extraction reported failure (negative count)")
@@ -544,14 +549,15 @@ def proj_workload(orb, torch, dev, threads, W, H, NF, M, B, seed, steps=20, warm
            **({"two_match_streams": {
                "problems_per_s": B / sec2, "match_only_problems_per_s": B / msec2,
                "note": "each set's SearchByProjection on a match stream (and matcher handle) of "
-                       "its own, so one set's resolve runs beside the next set's candidate scan"}}
+                       "its own, so one set's resolve runs beside the next set's candidate scan; "
+                       "sensitive to which HSA queue the second stream lands on (profiles/r05_secsets.txt)"}}
               if match_streams2 else {}),
            "mean_matches": float(sets[0]["nm"].float().mean().item()),
            **({"serial_ms_per_call": serial * 1e3, "serial_frames_per_s": B / serial,
                "serial_calls": serial_calls} if serial else {}),
            "workload": f"{W}x{H}, {NF} feat, extraction + SearchByProjection vs {M:,} map points "
-                       f"(frames 0..{B - 1} of seed {seed}), {B} problems per launch, pipelined "
-                       "over two extraction lanes and a match stream"}
+                       f"(frames 0..{B - 1} of seed {seed}), {B} problems per launch, {nsets} buffer "
+                       "sets pipelined over two extraction lanes and a match stream"}
     return res, dict(scale=scale, kh=kh, dh=dh, nh=nh, mps=mps, mpd=mpd, lk=lk, set0=sets[0])
 
 
