@@ -875,11 +875,10 @@ orb_status_t orb_device_count(int* n) {
   return c > 0 ? ORB_OK : ORB_ENODEV;
 }
 
-// Side-stream priorities (A/B knobs): ORB_STREAM2_PRIO = least | normal |
-// greatest for the FAST side stream; ORB_CHAIN_STREAM=1 runs the resize chain
-// on a third stream at the greatest priority.
-// the side stream's priority: the least (least == true) or the normal stream
-// priority of the device (SIDE_PRIO: compile-time A/B, 0 least, 1 normal, 2 greatest)
+// Stream priorities: the least (least == true) or the normal stream priority of
+// the device; SIDE_PRIO (compile-time A/B: 0 least, 1 normal, 2 greatest) picks
+// the "least" one for the pooled side stream of a SIDE_CUMASK=0 build and for
+// the handles' own streams.
 #ifndef SIDE_PRIO
 #define SIDE_PRIO 0
 #endif
@@ -949,7 +948,8 @@ static hipStream_t shared_side_stream(int device, int prio) {
 // high-priority stream ran 2x slower beside busy normal-priority streams
 // after three idle normal streams had been created first, with or without
 // this library (tools/probe/contention_probe.py, profiles/r05_contention.txt).
-// The least priority keeps the library in the pool of its side stream.
+// The least priority keeps the library out of the pools the caller's streams
+// use (the side stream has a queue of its own, SIDE_CUMASK).
 #ifndef OWN_PRIO
 #define OWN_PRIO 0  // handles' own streams: 0 least priority, 1 normal (compile-time A/B)
 #endif
@@ -958,12 +958,13 @@ static hipError_t create_own_stream(hipStream_t* s) {
 }
 
 static bool create_side_streams(orb_extractor* h) {
-  // The side stream is low priority: HIP backs streams by a few HSA queues
-  // per priority level, and a side stream sharing the caller's (normal
-  // priority) queue runs in submission order with it, which serialises level
-  // 0's FAST with the resize chain.  Low rather than high: the chain on the
-  // caller's stream then wins the CUs the side FAST also wants (extraction
-  // 1.703 vs 1.727 ms per 512 frames; profiles/r03_streams.txt)
+  // The side stream must not share an HSA queue with the caller's stream: two
+  // streams on one queue run in submission order, which would serialise level
+  // 0's FAST with the resize chain.  It is a full-CU-mask stream (a queue of
+  // its own, round 5); a SIDE_CUMASK=0 build takes a least-priority pooled
+  // stream instead (round 3: the chain on the caller's stream then wins the
+  // CUs the side FAST also wants, extraction 1.703 vs 1.727 ms per 512
+  // frames; profiles/r03_streams.txt)
   h->stream2 = shared_side_stream(h->device, stream_prio(true));
   return h->stream2 != nullptr;
 }
