@@ -1618,8 +1618,8 @@ __global__ __launch_bounds__(512) void k_octree(
   // the keys stay in LDS then)
   // (GNODES is a template parameter so that the LDS build keeps ds_*
   // instructions: a pointer that may be either would compile to flat ones)
-  // (the slice is indexed by the absolute level: two launches over disjoint
-  // level ranges of one batch -- ORB_SIDE_TAIL -- run concurrently on two streams)
+  // (the slice is indexed by the absolute level, so launches over disjoint
+  // level ranges of one batch could run concurrently)
   unsigned char* p = GNODES ? gNodes + ((long long)img * plan.nlevels + l) * nodeStride : smem;
   unsigned long long* sortBuf = (unsigned long long*)p; p += (size_t)n2 * 8;
   OctNode* A = (OctNode*)p; p += (size_t)NC * sizeof(OctNode);
@@ -2898,7 +2898,7 @@ hipError_t orb_k_fast_band(const uint8_t* img0, long long img0Pitch, int img0Str
                            uint32_t* cellKeys, int32_t* cellCount, int32_t* errFlag, int nimg,
                            hipStream_t s) {
   const size_t lds = orb_k_fast_band_lds(plan->maxBandBytes);
-  // each workgroup takes ORB_FAST_BANDS_PER_WG bands (default 2; swept 1-8), prefetching the next
+  // each workgroup takes 2 bands (swept 1-8 in round 2), prefetching the next
   // (one band per workgroup for a frame or two per call: the grid is small and
   // the per-workgroup band chain is the latency)
   const int perWg = nimg <= 2 ? 1 : 2;
