@@ -452,7 +452,13 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
     sec = pipelined(torch, dev, extract, match, _SEC_SETS, steps, warmup)
     if min(int(torch.minimum(st["nl"], st["nr"]).min().item()) for st in sets) < 0:
         raise RuntimeError("C3: an extraction reported failure (negative count)")
+    # the two stages alone, one after another on one stream (set 0)
+    s0 = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s0):
+        esec = timed_loop(lambda: extract(0, s0.cuda_stream), max(5, steps // 4), 2, torch)
+        msec = timed_loop(lambda: match(0, s0.cuda_stream), max(5, steps // 4), 2, torch)
     res = {"value": P / sec, "unit": "pairs/s", "pairs_per_step": P, "ms_per_step": sec * 1e3,
+           "extraction_only_ms_per_step": esec * 1e3, "stereo_match_only_ms_per_step": msec * 1e3,
            "workload": f"1241x376 stereo pairs (frames 0..{P - 1} of seed {C3_SEED:#x}, left and "
                        "right views), 2000 feat/img, extraction x2 + ComputeStereoMatches, "
                        "pipelined over two extraction lanes and a match stream"}

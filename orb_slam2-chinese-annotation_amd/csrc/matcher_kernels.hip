@@ -1436,15 +1436,21 @@ __global__ __launch_bounds__(256) void k_stereo_match(
       // < 121 * 255 < 2^16, so two share a word through the wave reduction.
       const int xrb = (int)scaleduR0 - L - w;  // right patch column of shift -L
       const int cRv = lane < 2 * L + 1 ? (int)IR[(long long)(y0 + w) * sR + xrb + w + lane] : 0;
-      int acc[11];
+      uint32_t acc[11];
+      // |(l - cL) - (r - cR_k)| as one v_sad_u16 on values biased by 256
+      // (both in [1, 511]); the right byte and its shift's bias in one add
+      uint32_t rbias[11];
 #pragma unroll
-      for (int k = 0; k < 11; ++k) acc[k] = 0;
+      for (int k = 0; k < 11; ++k) {
+        acc[k] = 0u;
+        rbias[k] = (uint32_t)(256 - __builtin_amdgcn_readlane(cRv, k));
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int p = lane + 64 * q;
         if (p < 121) {
           const int yy = p / 11, xx = p - yy * 11;
-          const int a = (int)IL[(long long)(y0 + yy) * sL + xl0 + xx] - cL;
+          const uint32_t ab = (uint32_t)((int)IL[(long long)(y0 + yy) * sL + xl0 + xx] - cL + 256);
           const uint8_t* rrow = IR + (long long)(y0 + yy) * sR + xrb + xx;
           const uintptr_t ra = (uintptr_t)rrow;
           const uint32_t* rw = reinterpret_cast<const uint32_t*>(ra & ~(uintptr_t)3);
@@ -1457,15 +1463,15 @@ __global__ __launch_bounds__(256) void k_stereo_match(
           for (int k = 0; k < 3; ++k) bw[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], shb);
 #pragma unroll
           for (int k = 0; k < 11; ++k) {
-            const int b = (int)((bw[k >> 2] >> (8 * (k & 3))) & 0xFFu) - __builtin_amdgcn_readlane(cRv, k);
-            acc[k] += abs(a - b);
+            const uint32_t bb = ((bw[k >> 2] >> (8 * (k & 3))) & 0xFFu) + rbias[k];
+            acc[k] = __builtin_amdgcn_sad_u16(ab, bb, acc[k]);
           }
         }
       }
       int dists[11];
 #pragma unroll
       for (int k = 0; k < 11; k += 2) {
-        const int packed = acc[k] | (k + 1 < 11 ? acc[k + 1] << 16 : 0);
+        const int packed = (int)(acc[k] | (k + 1 < 11 ? acc[k + 1] << 16 : 0u));
         const int sum = wave_sum(packed);
         dists[k] = sum & 0xFFFF;
         if (k + 1 < 11) dists[k + 1] = (int)((uint32_t)sum >> 16);
