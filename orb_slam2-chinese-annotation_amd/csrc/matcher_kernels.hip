@@ -1507,6 +1507,168 @@ __global__ __launch_bounds__(256) void k_stereo_match(
   }
 }
 
+// Two left keypoints per wave (half-wave h = lanes 32h .. 32h+31 takes
+// keypoint 2w + h): the same steps as k_stereo_match, with the candidate
+// reduction, the right centres and the SAD sums kept inside each half.  The
+// kernel is a chain of dependent loads per keypoint (row band, candidates,
+// descriptors, then the patches), so its cost beside the extraction is the
+// wave slots it holds: two keypoints per wave halve them.
+__device__ __forceinline__ int stereo_half_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v += __builtin_amdgcn_ds_swizzle(v, 0x401F);                     // lane ^ 16
+  return v;
+}
+__global__ __launch_bounds__(256) void k_stereo_match2(
+    const orb_keypoint_t* __restrict__ lkeys, const uint8_t* __restrict__ ldesc,
+    const int32_t* __restrict__ nleft, const orb_keypoint_t* __restrict__ rkeys,
+    const uint8_t* __restrict__ rdesc, const int32_t* __restrict__ nright, int kpStride,
+    const StereoPairLevels* __restrict__ pyr, StereoParams P, float* __restrict__ uRight,
+    float* __restrict__ depth, int32_t* __restrict__ sad, const int32_t* __restrict__ rowStart,
+    const int32_t* __restrict__ rowIdx, int rowCap) {
+  const int pair = blockIdx.y, lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const int iL = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half;
+  const int NL = nleft[pair];
+  const bool live = iL < NL;
+  if (__ballot(live) == 0ull) return;  // (wave-uniform)
+  const size_t base = (size_t)pair * kpStride;
+  const orb_keypoint_t kpL = lkeys[base + (live ? iL : 0)];
+  float ur = -1.0f, dp = -1.0f;
+  int sadOut = -1;
+  const float mb = P.bf / P.fx;
+  const float minZ = mb, minD = 0.f, maxD = P.bf / minZ;
+  const int levelL = kpL.octave;
+  const float vL = kpL.y, uL = kpL.x;
+  const int row = (int)vL;  // vRowIndices[vL]: float -> size_t truncation
+  const float minU = uL - maxD, maxU = uL - minD;
+  int bestDist = 1 << 30, bestIdx = 1 << 30;
+  const bool scan = live && maxU >= 0 && row >= 0 && row < P.h[0];
+  if (scan) {
+    const ulonglong4 dL = load_desc(ldesc + (base + iL) * 32);
+    const int32_t* rs = rowStart + (size_t)pair * (P.h[0] + 1);
+    const int32_t* ri = rowIdx + (size_t)pair * rowCap;
+    const int jEnd = min(rs[row + 1], rowCap);
+    for (int j = rs[row] + hl; j < jEnd; j += 32) {
+      const int iR = ri[j];
+      const orb_keypoint_t kpR = rkeys[base + iR];
+      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+      const float uR = kpR.x;
+      if (!(uR >= minU && uR <= maxU)) continue;
+      const int dist = hamming256(dL, load_desc(rdesc + (base + iR) * 32));
+      if (dist < bestDist) { bestDist = dist; bestIdx = iR; }  // lane's iR ascend
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {  // inside the half
+    const int od = __shfl_xor(bestDist, o, 64), oi = __shfl_xor(bestIdx, o, 64);
+    if (od < bestDist || (od == bestDist && oi < bestIdx)) { bestDist = od; bestIdx = oi; }
+  }
+  const bool matched = scan && bestDist < 75;  // uniform within the half
+  float scaleduR0 = 0.f;
+  bool patch = false;
+  const int w = 5, L = 5;
+  const uint8_t* IL = nullptr;
+  const uint8_t* IR = nullptr;
+  int sL = 0, sR = 0, y0 = 0, xl0 = 0, xrb = 0;
+  if (matched) {
+    const float uR0 = rkeys[base + bestIdx].x;
+    const float sf = P.invScale[levelL];
+    scaleduR0 = round_half_away(uR0 * sf);
+    const float scaleduL = round_half_away(kpL.x * sf);
+    const float scaledvL = round_half_away(kpL.y * sf);
+    const float iniu = scaleduR0 + L - w;
+    const float endu = scaleduR0 + L + w + 1;
+    patch = !(iniu < 0 || endu >= P.w[levelL]);
+    IL = pyr[pair].L[levelL];
+    IR = pyr[pair].R[levelL];
+    sL = P.strideL[levelL];
+    sR = P.strideR[levelL];
+    y0 = (int)scaledvL - w;
+    xl0 = (int)scaleduL - w;
+    xrb = (int)scaleduR0 - L - w;  // right patch column of shift -L
+  }
+  if (__ballot(patch) != 0ull) {  // (wave-uniform: the cross-lane steps below need both halves)
+    const int cL = patch ? (int)IL[(long long)(y0 + w) * sL + xl0 + w] : 0;
+    // the half's lanes 0..10 load its shifts' right centres; every lane of
+    // the half takes them by a lane shuffle inside the half
+    const int cRv = (patch && hl < 2 * L + 1) ? (int)IR[(long long)(y0 + w) * sR + xrb + w + hl] : 0;
+    uint32_t acc[11], rbias[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+      acc[k] = 0u;
+      rbias[k] = (uint32_t)(256 - __shfl(cRv, (lane & 32) + k, 64));
+    }
+    if (patch) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int p = hl + 32 * q;
+        if (p < 121) {
+          const int yy = p / 11, xx = p - yy * 11;
+          const uint32_t ab = (uint32_t)((int)IL[(long long)(y0 + yy) * sL + xl0 + xx] - cL + 256);
+          const uint8_t* rrow = IR + (long long)(y0 + yy) * sR + xrb + xx;
+          const uintptr_t ra = (uintptr_t)rrow;
+          const uint32_t* rw = reinterpret_cast<const uint32_t*>(ra & ~(uintptr_t)3);
+          const uint32_t shb = (uint32_t)(ra & 3);
+          uint32_t wv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) wv[k] = rw[k];
+          uint32_t bw[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) bw[k] = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], shb);
+#pragma unroll
+          for (int k = 0; k < 11; ++k) {
+            const uint32_t bb = ((bw[k >> 2] >> (8 * (k & 3))) & 0xFFu) + rbias[k];
+            acc[k] = __builtin_amdgcn_sad_u16(ab, bb, acc[k]);
+          }
+        }
+      }
+    }
+    int dists[11];
+#pragma unroll
+    for (int k = 0; k < 11; k += 2) {
+      const int packed = (int)(acc[k] | (k + 1 < 11 ? acc[k + 1] << 16 : 0u));
+      const int sum = stereo_half_sum(packed);
+      dists[k] = sum & 0xFFFF;
+      if (k + 1 < 11) dists[k + 1] = (int)((uint32_t)sum >> 16);
+    }
+    if (patch) {
+      int bestSad = 2147483647, bestinc = 0;
+#pragma unroll
+      for (int inc = -L; inc <= L; ++inc)
+        if ((float)dists[inc + L] < (float)bestSad) { bestSad = dists[inc + L]; bestinc = inc; }
+      if (bestinc != -L && bestinc != L) {
+        const float dist1 = (float)dists[L + bestinc - 1], dist2 = (float)dists[L + bestinc],
+                    dist3 = (float)dists[L + bestinc + 1];
+        const float deltaR = __fdiv_rn(dist1 - dist3, 2.0f * (dist1 + dist3 - 2.0f * dist2));
+        if (!(deltaR < -1 || deltaR > 1)) {
+          float bestuR = P.scale[levelL] * ((float)scaleduR0 + (float)bestinc + deltaR);
+          float disparity = uL - bestuR;
+          if (disparity >= minD && disparity < maxD) {
+            if (disparity <= 0) {
+              disparity = 0.01f;
+              bestuR = (float)((double)uL - 0.01);
+            }
+            dp = __fdiv_rn(P.bf, disparity);
+            ur = bestuR;
+            sadOut = bestSad;
+          }
+        }
+      }
+    }
+  }
+  if (live && hl == 0) {
+    uRight[base + iL] = ur;
+    depth[base + iL] = dp;
+    sad[base + iL] = sadOut;
+  }
+}
+
+#ifndef STEREO_KPW
+#define STEREO_KPW 2  // left keypoints per wave of the stereo match (1: k_stereo_match)
+#endif
+
 // Median-based outlier rejection: k-th smallest SAD by bisection on the value
 // (k = V/2 of the V valid matches, == vDistIdx[size/2] after the sort), then
 // every match with SAD >= 1.5*1.4*median is reset to -1.  One block per pair.
@@ -1576,10 +1738,16 @@ extern "C" hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* l
                      kpStride, P, rowStart, rowIdx, (int)idxInts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_stereo_match, dim3((maxLeft + 3) / 4, npairs), dim3(256), 0, s, lkeys,
-                     ldesc, nleft, rkeys, rdesc, nright, kpStride,
-                     (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
-                     (int)idxInts);
+  if (STEREO_KPW == 2)
+    hipLaunchKernelGGL(k_stereo_match2, dim3((maxLeft + 7) / 8, npairs), dim3(256), 0, s, lkeys,
+                       ldesc, nleft, rkeys, rdesc, nright, kpStride,
+                       (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
+                       (int)idxInts);
+  else
+    hipLaunchKernelGGL(k_stereo_match, dim3((maxLeft + 3) / 4, npairs), dim3(256), 0, s, lkeys,
+                       ldesc, nleft, rkeys, rdesc, nright, kpStride,
+                       (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
+                       (int)idxInts);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_stereo_prune, dim3(npairs), dim3(256), 0, s, nleft, kpStride, uRight,
