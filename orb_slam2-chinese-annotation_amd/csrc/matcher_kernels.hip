@@ -1507,20 +1507,26 @@ __global__ __launch_bounds__(256) void k_stereo_match(
   }
 }
 
-// Two left keypoints per wave (half-wave h = lanes 32h .. 32h+31 takes
-// keypoint 2w + h): the same steps as k_stereo_match, with the candidate
-// reduction, the right centres and the SAD sums kept inside each half.  The
-// kernel is a chain of dependent loads per keypoint (row band, candidates,
-// descriptors, then the patches), so its cost beside the extraction is the
-// wave slots it holds: two keypoints per wave halve them.
-__device__ __forceinline__ int stereo_half_sum(int v) {
+// 64 / G left keypoints per wave (lane group h = lanes G h .. G h + G - 1
+// takes keypoint (64 / G) w + h): the same steps as k_stereo_match, with the
+// candidate reduction, the right centres and the SAD sums kept inside each
+// group.  The kernel is a chain of dependent loads per keypoint (row band,
+// candidates, descriptors, then the patches), so its cost beside the
+// extraction is the wave slots it holds: C3's stereo match 0.535 ms per 256
+// pairs with one keypoint per wave, 0.445 with two, 0.412 with four
+// (profiles/r05_stereo.txt); G = 16 is the smallest group that holds the 11
+// shifts' right centres.
+// sum over the G-lane group (G = 32 or 16) a lane belongs to
+template <int G>
+__device__ __forceinline__ int stereo_group_sum(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
   v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
   v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
   v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
-  v += __builtin_amdgcn_ds_swizzle(v, 0x401F);                     // lane ^ 16
+  if (G == 32) v += __builtin_amdgcn_ds_swizzle(v, 0x401F);        // lane ^ 16
   return v;
 }
+template <int G>
 __global__ __launch_bounds__(256) void k_stereo_match2(
     const orb_keypoint_t* __restrict__ lkeys, const uint8_t* __restrict__ ldesc,
     const int32_t* __restrict__ nleft, const orb_keypoint_t* __restrict__ rkeys,
@@ -1528,8 +1534,9 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
     const StereoPairLevels* __restrict__ pyr, StereoParams P, float* __restrict__ uRight,
     float* __restrict__ depth, int32_t* __restrict__ sad, const int32_t* __restrict__ rowStart,
     const int32_t* __restrict__ rowIdx, int rowCap) {
-  const int pair = blockIdx.y, lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
-  const int iL = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half;
+  constexpr int KPW = 64 / G;  // keypoints per wave
+  const int pair = blockIdx.y, lane = threadIdx.x & 63, half = lane / G, hl = lane & (G - 1);
+  const int iL = (blockIdx.x * 4 + (threadIdx.x >> 6)) * KPW + half;
   const int NL = nleft[pair];
   const bool live = iL < NL;
   if (__ballot(live) == 0ull) return;  // (wave-uniform)
@@ -1550,7 +1557,7 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
     const int32_t* rs = rowStart + (size_t)pair * (P.h[0] + 1);
     const int32_t* ri = rowIdx + (size_t)pair * rowCap;
     const int jEnd = min(rs[row + 1], rowCap);
-    for (int j = rs[row] + hl; j < jEnd; j += 32) {
+    for (int j = rs[row] + hl; j < jEnd; j += G) {
       const int iR = ri[j];
       const orb_keypoint_t kpR = rkeys[base + iR];
       if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
@@ -1561,7 +1568,7 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
     }
   }
 #pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {  // inside the half
+  for (int o = G / 2; o > 0; o >>= 1) {  // inside the group
     const int od = __shfl_xor(bestDist, o, 64), oi = __shfl_xor(bestIdx, o, 64);
     if (od < bestDist || (od == bestDist && oi < bestIdx)) { bestDist = od; bestIdx = oi; }
   }
@@ -1598,12 +1605,12 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
 #pragma unroll
     for (int k = 0; k < 11; ++k) {
       acc[k] = 0u;
-      rbias[k] = (uint32_t)(256 - __shfl(cRv, (lane & 32) + k, 64));
+      rbias[k] = (uint32_t)(256 - __shfl(cRv, (lane & ~(G - 1)) + k, 64));
     }
     if (patch) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int p = hl + 32 * q;
+      for (int q = 0; q < (121 + G - 1) / G; ++q) {
+        const int p = hl + G * q;
         if (p < 121) {
           const int yy = p / 11, xx = p - yy * 11;
           const uint32_t ab = (uint32_t)((int)IL[(long long)(y0 + yy) * sL + xl0 + xx] - cL + 256);
@@ -1629,7 +1636,7 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
 #pragma unroll
     for (int k = 0; k < 11; k += 2) {
       const int packed = (int)(acc[k] | (k + 1 < 11 ? acc[k + 1] << 16 : 0u));
-      const int sum = stereo_half_sum(packed);
+      const int sum = stereo_group_sum<G>(packed);
       dists[k] = sum & 0xFFFF;
       if (k + 1 < 11) dists[k + 1] = (int)((uint32_t)sum >> 16);
     }
@@ -1666,7 +1673,7 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
 }
 
 #ifndef STEREO_KPW
-#define STEREO_KPW 2  // left keypoints per wave of the stereo match (1: k_stereo_match)
+#define STEREO_KPW 4  // left keypoints per wave of the stereo match: 4 (16-lane groups), 2, or 1 (k_stereo_match)
 #endif
 
 // Median-based outlier rejection: k-th smallest SAD by bisection on the value
@@ -1738,8 +1745,13 @@ extern "C" hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* l
                      kpStride, P, rowStart, rowIdx, (int)idxInts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (STEREO_KPW == 2)
-    hipLaunchKernelGGL(k_stereo_match2, dim3((maxLeft + 7) / 8, npairs), dim3(256), 0, s, lkeys,
+  if (STEREO_KPW == 4)
+    hipLaunchKernelGGL(k_stereo_match2<16>, dim3((maxLeft + 15) / 16, npairs), dim3(256), 0, s, lkeys,
+                       ldesc, nleft, rkeys, rdesc, nright, kpStride,
+                       (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
+                       (int)idxInts);
+  else if (STEREO_KPW == 2)
+    hipLaunchKernelGGL(k_stereo_match2<32>, dim3((maxLeft + 7) / 8, npairs), dim3(256), 0, s, lkeys,
                        ldesc, nleft, rkeys, rdesc, nright, kpStride,
                        (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
                        (int)idxInts);
