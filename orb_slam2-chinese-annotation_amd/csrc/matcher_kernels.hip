@@ -1127,6 +1127,9 @@ int orb_k_grid_stage_max(void) { return GB_LDS_KEYS; }
 #ifndef PROJ_PPT_LARGE
 #define PROJ_PPT_LARGE 1
 #endif
+#ifndef PROJ_PPT_SMALL
+#define PROJ_PPT_SMALL 1  // map points per thread of the candidate scan for maps under PROJ_LARGE_MAP
+#endif
 // large problems (C5: 4,000 keypoints staged = 64 KB of LDS per workgroup,
 // 50,000 points) take 1024-point workgroups: half the staging per point
 #define PROJ_LARGE_MAP 20000
@@ -1155,8 +1158,10 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
     grid = dim3((mpMax + 1024 * (direct ? 1 : ppt) - 1) / (1024 * (direct ? 1 : ppt)), nproblems);
     wg = 1024;
   } else {
-    fn = direct ? (const void*)k_proj_candidates<PROJ_WG, true> : (const void*)k_proj_candidates<PROJ_WG>;
-    grid = dim3((mpMax + PROJ_WG - 1) / PROJ_WG, nproblems);
+    fn = direct ? (const void*)k_proj_candidates<PROJ_WG, true>
+                : (const void*)k_proj_candidates<PROJ_WG, false, PROJ_PPT_SMALL>;
+    const int per = PROJ_WG * (direct ? 1 : PROJ_PPT_SMALL);
+    grid = dim3((mpMax + per - 1) / per, nproblems);
     wg = PROJ_WG;
   }
   if (lds > 65536 - (GRID_CELLS + 1) * 4 - 64) {  // with the static grid table
@@ -1177,9 +1182,9 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
                        locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, sg,
                        stageCap, P, topk, ncand);
   else
-    hipLaunchKernelGGL(k_proj_candidates<PROJ_WG>, grid, dim3(wg), lds, s, keys, desc, uright, locked,
-                       kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, sg, stageCap,
-                       P, topk, ncand);
+    hipLaunchKernelGGL((k_proj_candidates<PROJ_WG, false, PROJ_PPT_SMALL>), grid, dim3(wg), lds, s, keys,
+                       desc, uright, locked, kpStride, nkeys, mps, mpDesc, nmps, mpStride, cellStart,
+                       cellIdx, sg, stageCap, P, topk, ncand);
   return hipGetLastError();
 }
 
