@@ -1363,13 +1363,22 @@ __global__ __launch_bounds__(1024) void k_stereo_rows(const orb_keypoint_t* __re
   int32_t* rs = rowStart + (size_t)pair * (H + 1);
   for (int i = t; i <= H; i += T) rs[i] = cnt[i];
   __syncthreads();
-  int32_t* ri = rowIdx + (size_t)pair * rowCap;
+  // entry j of the pair's row lists: iR | octave << 24, and the keypoint's x
+  // in the parallel float array rx (the match's candidate filter then needs
+  // no load of the keypoint record)
+  int32_t* ri = rowIdx + (size_t)pair * 2 * rowCap;
+  float* rx = reinterpret_cast<float*>(ri + rowCap);
   for (int iR = t; iR < NR; iR += T) {
+    const orb_keypoint_t kp = K[iR];
     int lo, hi;
-    band(K[iR], &lo, &hi);
+    band(kp, &lo, &hi);
+    const int e = iR | (kp.octave << 24);
     for (int yi = lo; yi <= hi; ++yi) {
       const int pos = atomicAdd(&cnt[yi], 1);
-      if (pos < rowCap) ri[pos] = iR;
+      if (pos < rowCap) {
+        ri[pos] = e;
+        rx[pos] = kp.x;
+      }
     }
   }
 }
@@ -1396,31 +1405,34 @@ __global__ __launch_bounds__(256) void k_stereo_match(
   const int row = (int)vL;  // vRowIndices[vL]: float -> size_t truncation
   const float minU = uL - maxD, maxU = uL - minD;
   int bestDist = 1 << 30, bestIdx = 1 << 30;
+  float bestX = 0.f;
   (void)NR;
   if (maxU >= 0 && row >= 0 && row < P.h[0]) {
     const ulonglong4 dL = load_desc(ldesc + (base + iL) * 32);
     // vCandidates = vRowIndices[vL]: the right keypoints whose band holds the row
     const int32_t* rs = rowStart + (size_t)pair * (P.h[0] + 1);
-    const int32_t* ri = rowIdx + (size_t)pair * rowCap;
+    const int32_t* ri = rowIdx + (size_t)pair * 2 * rowCap;
+    const float* rx = reinterpret_cast<const float*>(ri + rowCap);
     const int jEnd = min(rs[row + 1], rowCap);
     for (int j = rs[row] + lane; j < jEnd; j += 64) {
-      const int iR = ri[j];
-      const orb_keypoint_t kpR = rkeys[base + iR];
-      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-      const float uR = kpR.x;
+      const int e = ri[j];
+      const float uR = rx[j];
+      const int iR = e & 0xFFFFFF, octR = e >> 24;
+      if (octR < levelL - 1 || octR > levelL + 1) continue;
       if (!(uR >= minU && uR <= maxU)) continue;
       const int dist = hamming256(dL, load_desc(rdesc + (base + iR) * 32));
-      if (dist < bestDist) { bestDist = dist; bestIdx = iR; }  // lane's iR ascend
+      if (dist < bestDist) { bestDist = dist; bestIdx = iR; bestX = uR; }  // lane's iR ascend
     }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const int od = __shfl_xor(bestDist, o, 64), oi = __shfl_xor(bestIdx, o, 64);
-    if (od < bestDist || (od == bestDist && oi < bestIdx)) { bestDist = od; bestIdx = oi; }
+    const float ox = __shfl_xor(bestX, o, 64);
+    if (od < bestDist || (od == bestDist && oi < bestIdx)) { bestDist = od; bestIdx = oi; bestX = ox; }
   }
   // bestDist starts at TH_HIGH=100 in the reference; accept below (100+50)/2
   if (maxU >= 0 && bestDist < 75) {
-    const float uR0 = rkeys[base + bestIdx].x;
+    const float uR0 = bestX;
     const float sf = P.invScale[levelL];
     const float scaleduL = round_half_away(kpL.x * sf);
     const float scaledvL = round_half_away(kpL.y * sf);
@@ -1556,26 +1568,29 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
   const int row = (int)vL;  // vRowIndices[vL]: float -> size_t truncation
   const float minU = uL - maxD, maxU = uL - minD;
   int bestDist = 1 << 30, bestIdx = 1 << 30;
+  float bestX = 0.f;  // the best candidate's x (from the row list)
   const bool scan = live && maxU >= 0 && row >= 0 && row < P.h[0];
   if (scan) {
     const ulonglong4 dL = load_desc(ldesc + (base + iL) * 32);
     const int32_t* rs = rowStart + (size_t)pair * (P.h[0] + 1);
-    const int32_t* ri = rowIdx + (size_t)pair * rowCap;
+    const int32_t* ri = rowIdx + (size_t)pair * 2 * rowCap;
+    const float* rx = reinterpret_cast<const float*>(ri + rowCap);
     const int jEnd = min(rs[row + 1], rowCap);
     for (int j = rs[row] + hl; j < jEnd; j += G) {
-      const int iR = ri[j];
-      const orb_keypoint_t kpR = rkeys[base + iR];
-      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-      const float uR = kpR.x;
+      const int e = ri[j];
+      const float uR = rx[j];
+      const int iR = e & 0xFFFFFF, octR = e >> 24;
+      if (octR < levelL - 1 || octR > levelL + 1) continue;
       if (!(uR >= minU && uR <= maxU)) continue;
       const int dist = hamming256(dL, load_desc(rdesc + (base + iR) * 32));
-      if (dist < bestDist) { bestDist = dist; bestIdx = iR; }  // lane's iR ascend
+      if (dist < bestDist) { bestDist = dist; bestIdx = iR; bestX = uR; }  // lane's iR ascend
     }
   }
 #pragma unroll
   for (int o = G / 2; o > 0; o >>= 1) {  // inside the group
     const int od = __shfl_xor(bestDist, o, 64), oi = __shfl_xor(bestIdx, o, 64);
-    if (od < bestDist || (od == bestDist && oi < bestIdx)) { bestDist = od; bestIdx = oi; }
+    const float ox = __shfl_xor(bestX, o, 64);
+    if (od < bestDist || (od == bestDist && oi < bestIdx)) { bestDist = od; bestIdx = oi; bestX = ox; }
   }
   const bool matched = scan && bestDist < 75;  // uniform within the half
   float scaleduR0 = 0.f;
@@ -1585,7 +1600,7 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
   const uint8_t* IR = nullptr;
   int sL = 0, sR = 0, y0 = 0, xl0 = 0, xrb = 0;
   if (matched) {
-    const float uR0 = rkeys[base + bestIdx].x;
+    const float uR0 = bestX;
     const float sf = P.invScale[levelL];
     scaleduR0 = round_half_away(uR0 * sf);
     const float scaleduL = round_half_away(kpL.x * sf);
@@ -1731,7 +1746,8 @@ extern "C" void orb_k_stereo_scratch(const void* params, int kpStride, size_t* s
   float smax = 1.f;
   for (int l = 0; l < P.nLevels; ++l) smax = std::max(smax, P.scale[l]);
   *startInts = (size_t)P.h[0] + 1;
-  *idxInts = (size_t)kpStride * (size_t)(std::ceil(4.0 * smax) + 3.0);
+  // entries (iR | octave << 24) and their keypoints' x, two arrays
+  *idxInts = 2 * (size_t)kpStride * (size_t)(std::ceil(4.0 * smax) + 3.0);
 }
 
 extern "C" hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc,
@@ -1747,24 +1763,24 @@ extern "C" hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* l
   const size_t rowsLds = ((size_t)P.h[0] + 1) * sizeof(int);
   if (rowsLds > 64 * 1024) return hipErrorInvalidValue;  // images up to 16k rows
   hipLaunchKernelGGL(k_stereo_rows, dim3(npairs), dim3(1024), rowsLds, s, rkeys, nright,
-                     kpStride, P, rowStart, rowIdx, (int)idxInts);
+                     kpStride, P, rowStart, rowIdx, (int)(idxInts / 2));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (STEREO_KPW == 4)
     hipLaunchKernelGGL(k_stereo_match2<16>, dim3((maxLeft + 15) / 16, npairs), dim3(256), 0, s, lkeys,
                        ldesc, nleft, rkeys, rdesc, nright, kpStride,
                        (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
-                       (int)idxInts);
+                       (int)(idxInts / 2));
   else if (STEREO_KPW == 2)
     hipLaunchKernelGGL(k_stereo_match2<32>, dim3((maxLeft + 7) / 8, npairs), dim3(256), 0, s, lkeys,
                        ldesc, nleft, rkeys, rdesc, nright, kpStride,
                        (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
-                       (int)idxInts);
+                       (int)(idxInts / 2));
   else
     hipLaunchKernelGGL(k_stereo_match, dim3((maxLeft + 3) / 4, npairs), dim3(256), 0, s, lkeys,
                        ldesc, nleft, rkeys, rdesc, nright, kpStride,
                        (const StereoPairLevels*)pyr, P, uRight, depth, sad, rowStart, rowIdx,
-                       (int)idxInts);
+                       (int)(idxInts / 2));
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_stereo_prune, dim3(npairs), dim3(256), 0, s, nleft, kpStride, uRight,
