@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--calls", type=int, default=300)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--resolve", type=int, default=0, help="matcher resolve schedule (ORB_RESOLVE_*)")
     ap.add_argument("--timeline", type=int, default=0,
                     help="only N extract+match calls 1 ms apart (for a kernel-trace timeline)")
     a = ap.parse_args()
@@ -56,6 +57,7 @@ def main():
     km = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
     nm = torch.zeros(B, dtype=torch.int32, device="cuda")
     mt = orb.ORBmatcher(0.8)
+    mt.set_resolve(a.resolve)
 
     def extract():
         ext.extract_batch(d.data_ptr(), B, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
@@ -84,7 +86,7 @@ def main():
                 ts.append(time.perf_counter() - t0)
         return float(np.median(ts)) * 1e3
 
-    out = {"tag": a.tag, "batch": B, "extract_ms": med(extract), "match_ms": med(match),
+    out = {"tag": a.tag, "batch": B, "resolve": a.resolve, "extract_ms": med(extract), "match_ms": med(match),
            "both_ms": med(lambda: (extract(), match()))}
     # per-stage GPU time by the libraries' stage events (profile mode 1: the
     # call's own launch shape; events add a little per stage)
