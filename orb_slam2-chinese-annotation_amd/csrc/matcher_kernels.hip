@@ -1421,7 +1421,8 @@ __global__ __launch_bounds__(256) void k_stereo_match(
       if (octR < levelL - 1 || octR > levelL + 1) continue;
       if (!(uR >= minU && uR <= maxU)) continue;
       const int dist = hamming256(dL, load_desc(rdesc + (base + iR) * 32));
-      if (dist < bestDist) { bestDist = dist; bestIdx = iR; bestX = uR; }  // lane's iR ascend
+      // (distance, iR) order: a row list holds its entries in no particular order
+      if (dist < bestDist || (dist == bestDist && iR < bestIdx)) { bestDist = dist; bestIdx = iR; bestX = uR; }
     }
   }
 #pragma unroll
@@ -1583,7 +1584,8 @@ __global__ __launch_bounds__(256) void k_stereo_match2(
       if (octR < levelL - 1 || octR > levelL + 1) continue;
       if (!(uR >= minU && uR <= maxU)) continue;
       const int dist = hamming256(dL, load_desc(rdesc + (base + iR) * 32));
-      if (dist < bestDist) { bestDist = dist; bestIdx = iR; bestX = uR; }  // lane's iR ascend
+      // (distance, iR) order: a row list holds its entries in no particular order
+      if (dist < bestDist || (dist == bestDist && iR < bestIdx)) { bestDist = dist; bestIdx = iR; bestX = uR; }
     }
   }
 #pragma unroll

@@ -22,6 +22,37 @@ def test_stereo_matches(gpu, oracle, seed):
     assert dp.tobytes() == dp_ref.tobytes()
 
 
+def test_stereo_distance_ties(gpu, oracle):
+    """Every right keypoint twice: a copy 3 px to the right with the same
+    descriptor and the SMALLER index, then the original.  Each candidate's
+    distance ties with its copy's, and the reference's first minimum in
+    ascending iR picks the copy (src/Frame.cc:584-607), whose x moves the SAD
+    search.  The device row lists hold the two in arbitrary order, so this
+    pins the (distance, iR) order inside a lane as well as across lanes."""
+    sp = scenarios.stereo_pair(oracle, 3)
+    kr, dr = sp["kr"], sp["dr"]
+    moved = kr.copy()
+    moved["x"] = (moved["x"] + np.float32(3.0)).astype(np.float32)
+    # blocks of 64: the copies, then their originals, so the two of a tie
+    # are listed by different waves of the same round of the list builder
+    n = len(kr) // 64 * 64
+    parts_k, parts_d = [], []
+    for b in range(0, n, 64):
+        parts_k += [moved[b:b + 64], kr[b:b + 64]]
+        parts_d += [dr[b:b + 64], dr[b:b + 64]]
+    kr2 = np.concatenate(parts_k)
+    dr2 = np.concatenate(parts_d)
+    args = (sp["kl"], sp["dl"], sp["scale"], kr2, dr2, sp["lpyr"], sp["rpyr"],
+            sp["inv"], scenarios.BF, scenarios.FX, sp["w"], sp["h"])
+    ur_ref, dp_ref = oracle.stereo_match(*args)
+    F = gpu.Frame(sp["kl"], sp["dl"], sp["scale"], sp["w"], sp["h"])
+    ur, dp = gpu.ORBmatcher().ComputeStereoMatches(F, kr2, dr2, sp["lpyr"], sp["rpyr"],
+                                                   sp["inv"], scenarios.BF, scenarios.FX)
+    assert (ur_ref > 0).sum() > 50
+    assert ur.tobytes() == ur_ref.tobytes(), np.nonzero(ur != ur_ref)[0][:10]
+    assert dp.tobytes() == dp_ref.tobytes()
+
+
 def test_stereo_batch_from_extractors(gpu, oracle):
     """C3 path: both images of each pair through extract_batch, stereo on device."""
     torch = pytest.importorskip("torch")
