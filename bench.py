@@ -16,7 +16,9 @@ overlaps the next launches' extraction (every launch does all of its work; the
 timed region ends with a device synchronize).
 
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant
-kernel, HIP-event timed over the timed region; HBM bytes per SURVEY §8(d) as
+kernel, HIP-event timed alone after the timed region, and pipelined in a
+profiled pass of the same launches after it -- no event sits inside the timed
+region; HBM bytes per SURVEY §8(d) as
 the primary fraction, VALU issue beside it), `host_input` (the same pipeline
 fed from pinned host memory: H2D of every frame and D2H of every result, the
 drop-in's PCIe-inclusive rate, never `value`), `parity_sample` (8 frames of
@@ -327,11 +329,14 @@ _STREAMS = {}
 # HIP backs streams by a few HSA queues per priority level (GPU_MAX_HW_QUEUES,
 # 4 here), and two streams on one queue run in submission order.  The
 # library's own streams are least priority and its side stream has an HSA
-# queue of its own (a CU-masked stream); the extraction streams are normal
-# priority and the match and copy streams high priority, so no two of the
-# concurrently busy streams can share a queue
-# (tools/archive/r03/c5_swap.py, profiles/r03_streams.txt)
-_STREAM_PRIO = {"extract": "normal", "match": "greatest", "h2d": "greatest", "d2h": "greatest"}
+# queue of its own (a CU-masked stream); the extraction streams and the
+# headline's match stream are normal priority, C5's second match stream and
+# the copy streams high priority (tools/archive/r03/c5_swap.py,
+# profiles/r03_streams.txt).  The headline's match stream at the greatest
+# priority ran 315-321k frames/s against 333-334k at normal once the stage
+# events left the timed region: the events had been pacing it
+# (profiles/r05_markers.txt)
+_STREAM_PRIO = {"extract": "normal", "match": "normal", "h2d": "greatest", "d2h": "greatest"}
 _STREAM_PRIO.update({f"extract{i}": "normal" for i in range(1, 4)})
 _STREAM_PRIO.update({f"match{i}": "greatest" for i in range(1, 4)})
 
@@ -851,6 +856,12 @@ def main():
     ap.add_argument("--cpu-max-frames", type=int, default=400)
     ap.add_argument("--iso-launches", type=int, default=8,
                     help="extract + match calls timed with every kernel alone (kernel table)")
+    ap.add_argument("--bounded", action="store_true",
+                    help="the host queues a buffer set's next launch only once its previous one is "
+                         "matched (at most one launch per set in flight)")
+    ap.add_argument("--timed-events", choices=("off", "ext", "match", "both"), default="off",
+                    help="record the per-stage HIP events inside the timed region (A/B; default: "
+                         "in a profiled pipelined pass after it)")
     ap.add_argument("--cpu-all-seconds", type=float, default=8.0,
                     help="wall-clock sample of the all-cores oracle rate (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -984,6 +995,10 @@ def main():
         mt = matchers[ln] if inlane else matcher
         cnt = step_counts[(g // NB) % 2][b * B:(b + 1) * B]
         st["cnt"] = cnt
+        if g >= NS and args.bounded:
+            # the host waits for set j's previous launch (g - NS) to be matched
+            # before it queues the next use of the set: at most NS launches in flight
+            matched[j].synchronize()
         if g >= NS and not inlane:
             es.wait_event(matched[j])
         exts[ln].extract_batch(d_img.data_ptr() + b * B * frame_bytes, B, W, H, W, frame_bytes,
@@ -1016,8 +1031,13 @@ def main():
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    ext.profile(True)
-    matcher.profile(True)
+    # stage events (the pipelined kernel table) go in a profiled pass after the
+    # timed region, so no event record sits between the timed kernels
+    # (--timed-events: inside it, the round-4 / round-5 layout)
+    if args.timed_events in ("ext", "both"):
+        ext.profile(True)
+    if args.timed_events in ("match", "both"):
+        matcher.profile(True)
     t0 = time.perf_counter()
     g_first = g
     for k in range(args.steps):
@@ -1053,7 +1073,21 @@ def main():
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         gather_ok = bool(ok.item())
 
-    # per-kernel HIP-event times over the timed region, each on its own stream.
+    if args.timed_events != "both":
+        # the profiled pipelined pass: the same launches, stage events on
+        prof_steps = max(2, min(args.steps, 6))
+        ext.profile(False)  # (drops whatever the timed region recorded)
+        matcher.profile(False)
+        ext.profile(True)
+        matcher.profile(True)
+        g_first = g
+        for k in range(prof_steps):
+            for _ in range(NB):
+                launch(g)
+                g += 1
+        torch.cuda.synchronize()
+    # per-kernel HIP-event times over the timed region (or the profiled pass
+    # after it), each on its own stream.
     # The extract stream is the critical path (the matcher stream runs in its
     # shadow, so matcher kernel times include time-sharing with the next
     # launch's extraction): the roofline kernel is the longest extraction kernel.
@@ -1126,7 +1160,8 @@ def main():
                           f"{B} frames / {t['launches_per_call']:g} launch(es) per call",
             "timing": f"HIP events around each launch, kernels run one after another on one "
                       f"stream ({iso_calls} calls after the timed region); "
-                      "`ms_per_launch_pipelined` is the same kernel inside the timed pipeline "
+                      "`ms_per_launch_pipelined` is the same kernel in a profiled pass of the timed pipeline's "
+                      "launches after the timed region "
                       "(time-shared with the other lane and the matcher)"}
     if valu is not None:
         rate = valu["valu_instr_per_launch"] / (dom_ms_per_launch * 1e-3) / 1e9
@@ -1143,7 +1178,7 @@ def main():
                           "passes)" if traffic_src else None,
         "ms_per_launch": dom_ms_per_launch,
         "ms_per_launch_pipelined": t.get("ms_per_launch_pipelined"),
-        # the same bytes over the kernel's time inside the timed pipeline
+        # the same bytes over the kernel's time inside the pipeline (profiled pass)
         # (time-shared with the other lane and the matcher)
         "frac_pipelined": (dom_bytes / (t["ms_per_launch_pipelined"] * 1e-3) / 1e9 / HBM_PEAK_GBS
                            if t.get("ms_per_launch_pipelined") else None),
