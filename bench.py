@@ -329,16 +329,16 @@ _STREAMS = {}
 # HIP backs streams by a few HSA queues per priority level (GPU_MAX_HW_QUEUES,
 # 4 here), and two streams on one queue run in submission order.  The
 # library's own streams are least priority and its side stream has an HSA
-# queue of its own (a CU-masked stream); the extraction streams and the
-# headline's match stream are normal priority, C5's second match stream and
-# the copy streams high priority (tools/archive/r03/c5_swap.py,
-# profiles/r03_streams.txt).  The headline's match stream at the greatest
-# priority ran 315-321k frames/s against 333-334k at normal once the stage
-# events left the timed region: the events had been pacing it
-# (profiles/r05_markers.txt)
+# queue of its own (a CU-masked stream); the extraction and match streams are
+# normal priority, the copy streams high priority (tools/archive/r03/c5_swap.py,
+# profiles/r03_streams.txt).  The match streams at the greatest priority ran
+# the headline at 315-321k frames/s against 333-334k at normal once the stage
+# events left the timed region (the events had been pacing the match stream),
+# and C5's two-stream pipeline at 47-48k problems/s against 56-57k with its
+# second match stream at normal too (profiles/r05_markers.txt)
 _STREAM_PRIO = {"extract": "normal", "match": "normal", "h2d": "greatest", "d2h": "greatest"}
 _STREAM_PRIO.update({f"extract{i}": "normal" for i in range(1, 4)})
-_STREAM_PRIO.update({f"match{i}": "greatest" for i in range(1, 4)})
+_STREAM_PRIO.update({f"match{i}": "normal" for i in range(1, 4)})
 
 
 def _hip(torch):
