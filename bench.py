@@ -438,7 +438,8 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
                          nl=z(P), kr=z(P, cap, 7), dr=z(P, cap, 32, dt=torch.uint8), nr=z(P),
                          ur=z(P, cap, dt=torch.float32), dp=z(P, cap, dt=torch.float32),
                          sad=z(P, cap)))
-    m = orb.ORBmatcher(device=dev.index)
+    # a matcher handle per set: a handle's stereo scratch serves one call at a time
+    mts = [orb.ORBmatcher(device=dev.index) for _ in range(len(sets))]
 
     def extract(j, s):
         st = sets[j]
@@ -449,12 +450,13 @@ def c3_workload(orb, torch, dev, threads, steps=20, warmup=3, pairs=256):
 
     def match(j, s):
         st = sets[j]
-        m.stereo_match_batch(P, st["L"], st["R"], st["kl"].data_ptr(), st["dl"].data_ptr(),
+        mts[j].stereo_match_batch(P, st["L"], st["R"], st["kl"].data_ptr(), st["dl"].data_ptr(),
                              st["nl"].data_ptr(), st["kr"].data_ptr(), st["dr"].data_ptr(),
                              st["nr"].data_ptr(), st["cap"], bf, fx, st["ur"].data_ptr(),
                              st["dp"].data_ptr(), st["sad"].data_ptr(), s)
 
-    sec = pipelined(torch, dev, extract, match, _SEC_SETS, steps, warmup)
+    sec = pipelined(torch, dev, extract, match, _SEC_SETS, steps, warmup,
+                    match_lanes=int(os.environ.get("ORB_BENCH_C3_MATCH_LANES", "1")))
     if min(int(torch.minimum(st["nl"], st["nr"]).min().item()) for st in sets) < 0:
         raise RuntimeError("C3: an extraction reported failure (negative count)")
     # the two stages alone, one after another on one stream (set 0)
