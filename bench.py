@@ -366,7 +366,17 @@ def new_stream(torch, dev, key):
         hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest))
         name = os.environ.get("ORB_BENCH_PRIO_" + key.upper(), _STREAM_PRIO[key])
         prio = {"normal": 0, "least": least.value, "greatest": greatest.value}[name]
-        rc = hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(1), ctypes.c_int(prio))
+        ncu = int(os.environ.get("ORB_BENCH_CUS_" + key.upper(), "0"))  # A/B: a CU-masked stream
+        if ncu > 0:
+            total = torch.cuda.get_device_properties(dev).multi_processor_count
+            step = max(1, total // ncu)
+            words = [0] * ((total + 31) // 32)
+            for c in range(0, total, step):
+                words[c >> 5] |= 1 << (c & 31)
+            arr = (ctypes.c_uint32 * len(words))(*words)
+            rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), arr)
+        else:
+            rc = hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(1), ctypes.c_int(prio))
     if rc != 0:
         raise RuntimeError(f"HIP stream creation failed ({rc})")
     _STREAMS[key] = torch.cuda.ExternalStream(h.value, device=dev)  # kept for the process's lifetime
