@@ -1155,6 +1155,11 @@ def main():
     # among the kernels SURVEY §8(d) assigns algorithmic bytes
     dom = max((k for k in table if table[k]["alg_bytes_per_launch"] > 0),
               key=lambda k: table[k]["ms_per_call_isolated"])
+    # (and the longest kernel of all, with the kernels left out for having no
+    # §8(d) bytes, so a byte-less bottleneck cannot drop out silently)
+    longest = max(table, key=lambda k: table[k]["ms_per_call_isolated"])
+    no_bytes = {k: table[k]["ms_per_call_isolated"] for k in table
+                if not table[k]["alg_bytes_per_launch"] > 0}
     t = table[dom]
     dom_ms_per_launch = t["ms_per_launch_isolated"]
     dom_bytes = t["alg_bytes_per_launch"]
@@ -1194,9 +1199,15 @@ def main():
         # (time-shared with the other lane and the matcher)
         "frac_pipelined": (dom_bytes / (t["ms_per_launch_pipelined"] * 1e-3) / 1e9 / HBM_PEAK_GBS
                            if t.get("ms_per_launch_pipelined") else None),
-        "binding_limit": "memory latency per wave (HBM bandwidth is the roof the contract "
-                         "prices against; the kernel moves ~1.07x its algorithmic bytes and "
-                         "issues VALU at `valu.frac` of peak: DESIGN.md §4)",
+        # `bound` names the roofline the contract prices against (HBM: no MFMA
+        # work on this path); `limiter` is what holds the kernel below it
+        "limiter": "latency",
+        "binding_limit": "memory latency per wave, not HBM bandwidth: the kernel moves ~1.07x its "
+                         "algorithmic bytes at `frac` of the HBM roof and issues VALU at "
+                         "`valu.frac` of peak (DESIGN.md §4)",
+        "longest_kernel_isolated": {"kernel": longest,
+                                    "ms_per_call": table[longest]["ms_per_call_isolated"]},
+        "kernels_without_alg_bytes": no_bytes,
     })
     host = None
     if args.host_frames > 0:

@@ -120,8 +120,9 @@ typedef struct orb_matcher orb_matcher_t;
  *     nodes.  Exceeding any of them is not reachable with keys the FAST stage
  *     emits; if it happened the image fails as a whole: orb_extractor_extract
  *     returns ORB_EDEVICE and the batch form writes d_counts[i] = ORB_EDEVICE
- *     (negative).  ORB_OCTREE_MAX_PASSES (environment, test hook) lowers the
- *     pass bound to drive that path (tests/test_gpu_extractor.py). */
+ *     (negative).  A test-only build of the library with the pass bound
+ *     lowered drives that path (tests/test_gpu_extractor.py); the product
+ *     reads no environment variable that changes results. */
 orb_status_t orb_extractor_create(int nfeatures, float scale_factor, int nlevels,
                                   int ini_th_fast, int min_th_fast, int device,
                                   orb_extractor_t** out);

@@ -391,12 +391,6 @@ __device__ __forceinline__ uint32_t pretest_pair(uint32_t v, uint32_t q0, uint32
 #endif
 }
 
-#ifdef ORB_FAST_STAMPS  // phase timing probe (tools/probe/fast_stamps.py), off by default
-__device__ unsigned long long g_fast_stamps[4096][8];
-#define FSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.y == 0 && b < 4096) g_fast_stamps[b][k] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define FSTAMP(k) do { } while (0)
-#endif
 __global__ __launch_bounds__(256) void k_fast_band(
     const uint8_t* __restrict__ img0, long long img0Pitch, int img0Stride,
     const uint8_t* __restrict__ arena, long long arenaPitch, OrbPlanDesc plan,
@@ -465,7 +459,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
   OrbBandDesc nbd = bands[b];
   issue(nbd);
   for (; b < nBands; b += gridDim.x) {
-  FSTAMP(0);
   const OrbBandDesc bd = nbd;
   const OrbCellDesc myCell = pcell;
   const int R = bd.y1 - bd.y0, C = bd.x1 - bd.x0;
@@ -500,7 +493,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
   const int nK = (iw + 7) >> 3;  // 8-pixel groups per interior row
   const int nBitWords = (ni >> 5) + 3;
   // cell windows of the band (<= 64 cells, host-checked)
-  FSTAMP(1);
   int cx0 = 0, ww = 0;
   if (tid < bd.nCells) {
     cx0 = myCell.x0 - bd.x0;
@@ -719,12 +711,9 @@ __global__ __launch_bounds__(256) void k_fast_band(
   };
 
   // ---- phase A: every cell at iniThFAST
-  FSTAMP(2);
   fast_pass(ti, std::false_type{});
-  FSTAMP(3);
   nms_pass(ti, bitsIni, false);
   __syncthreads();
-  FSTAMP(4);
   for (int ci = wave; ci < bd.nCells; ci += nw) {
     const int n = compact(ci, bitsIni);
     if (lane == 0) {
@@ -734,8 +723,7 @@ __global__ __launch_bounds__(256) void k_fast_band(
   }
   if (tid == 0) cCount = 0;
   __syncthreads();
-  FSTAMP(5);
-  if ((fbMask[0] | fbMask[1]) == 0) { FSTAMP(6); continue; }  // LDS free: barrier above
+  if ((fbMask[0] | fbMask[1]) == 0) { continue; }  // LDS free: barrier above
   // ---- phase B: cells without an iniThFAST keypoint, at minThFAST, over the
   // group columns that touch one (wave 0 lists them in order with ballots).
   // Column flags fbCol[x] (x < 8 nK) = column x lies in a fallback cell: the
@@ -773,7 +761,6 @@ __global__ __launch_bounds__(256) void k_fast_band(
     const int n = compact(ci, bitsMin);
     if (lane == 0) cellCount[slot0 + ci] = n;
   }
-  FSTAMP(7);
   __syncthreads();  // the next band's pixels overwrite LDS
   }  // band loop
 }
@@ -841,19 +828,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef FC_PERM
 #define FC_PERM (!FC_ROWMAJOR)  // pretest lane -> pixel-group permutation (LDS banking)
 #endif
-// Attribution builds (tools/r04/fast_attr.sh; results WRONG, never shipped):
-// FC_STUB = k drops the last k phases of the cell pipeline, each build keeping
-// the work before it alive through a sink, so the differences between
-// successive builds give each phase's time and instruction counts:
-//   1 NMS + key emit, 2 + arc-strength scoring / corner list,
-//   3 + candidate queue append (scan, per-lane loop), 4 + compass pretest,
-//   5 + LDS staging stores (the global loads stay, XOR-ed into the sink).
-// Stubbed builds write a count of 0 (the octree and descriptors then idle).
-// Phase B (minThFAST) still runs where the real kernel would run it while the
-// corner count is known (FC_STUB 1); from FC_STUB 2 on it follows the queue.
-#ifndef FC_STUB
-#define FC_STUB 0
-#endif
+// Attribution builds (phase stubs, per-phase clock stamps; results wrong,
+// never shipped) are patches against this file: tools/attribution/.
 
 // LDS row pitch (bytes) of a cell ROI C pixels wide: byte 5 is ROI column 0,
 // byte 8 interior column 0 (ROI column 3); groups of 8 interior pixels read
@@ -872,16 +848,11 @@ __host__ __device__ inline int fc_pitch(int C) {
 __host__ __device__ inline int fc_tile_elems(int maxRows, int maxCols) {
   return (maxRows * fc_pitch(maxCols) + 15) & ~15;  // 16-byte aligned strength map
 }
-#ifndef FC_LDS_PAD_TILES
-// unused byte tiles per wave: the LDS an LDS-DMA ring of that many further
-// cells would take (occupancy control, A/B only)
-#define FC_LDS_PAD_TILES 0
-#endif
 __host__ __device__ inline int fc_wave_bytes(int tileElems) {
   // byte tile + strengths + queue + corners (+ 64 rows x 64-bit NMS bitmap,
   // column-major path only)
-  return ((2 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + ((FC_ROWMAJOR && FC_TIGHT) ? 0 : 512) +
-           FC_LDS_PAD_TILES * tileElems) + 15) & ~15;
+  return ((2 * tileElems + 2 * FC_QCAP + 2 * FC_CCAP + ((FC_ROWMAJOR && FC_TIGHT) ? 0 : 512)) + 15) &
+         ~15;
 }
 #define FC_CONST_PITCH (FC_TIGHT ? 48 : 56)  // the compile-time instance
 
@@ -979,19 +950,6 @@ __device__ __forceinline__ int fast_score_u8(const uint8_t* tile, int coff, int 
 // <= 96 -> 7; MI355X_MICROARCH "Residency")
 #define FC_WPE 7
 #endif
-#ifdef FC_STAMPS  // per-phase clock stamps of image 0's cells (tools/probe/fc_stamps.py), off by default
-__device__ unsigned long long g_fc_stamps[8192][8];
-extern "C" hipError_t orb_k_fc_stamps(void* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fc_stamps), sizeof(g_fc_stamps));
-}
-#define FCSTAMP(k)                                                                   \
-  do {                                                                               \
-    const unsigned long long tnow = __builtin_amdgcn_s_memtime();                    \
-    if (img == 0 && lane == 0 && ci < 8192) g_fc_stamps[ci][k] = tnow;               \
-  } while (0)
-#else
-#define FCSTAMP(k) do { } while (0)
-#endif
 template <int PT>
 #if FC_WPE > 0
 __global__ __launch_bounds__(64 * FC_WAVES) __attribute__((amdgpu_waves_per_eu(FC_WPE)))
@@ -1058,24 +1016,17 @@ void k_fast_cells(
       raw[4 * k + 3] = (uint32_t)v[3];
     }
   };
-  [[maybe_unused]] uint32_t sink = 0;
   int ci = cell_of(0);
   if (ci >= cellEnd) return;
   OrbCellDesc ncd = cells[ci];
   issue(ncd);
   for (int jc = 0; jc < FC_CPW && ci < cellEnd; ++jc) {
-  FCSTAMP(0);
   const OrbCellDesc cd = ncd;
   const int R = cd.y1 - cd.y0, C = cd.x1 - cd.x0;
   const long long slot = (long long)img * plan.ncells + ci;
   const bool tiny = R < 7 || C < 7;
   const int P = PT ? PT : fc_pitch(C);
-#if FC_STUB >= 5
-  for (int k = 0; k < 16; ++k) sink ^= raw[k];
-  if (false) {
-#else
   if (!tiny && lane < R) {
-#endif
     const int nS = P >> 2;  // dwords per row (<= 14, host-checked): the row, no further
     uint2* dst = reinterpret_cast<uint2*>(tile + lane * P);
 #pragma unroll
@@ -1117,15 +1068,9 @@ void k_fast_cells(
               invW = __builtin_amdgcn_rcpf((float)iw);
   wave_lds_sync();
 
-  FCSTAMP(1);  // staged, strengths cleared, next cell's loads issued
   int nq = 0, nc = 0;  // wave-uniform queue / corner counts
   // score the queued candidates, list the corners (m > t)
   auto flush = [&](int t, bool fresh) {
-#if FC_STUB >= 2
-    nc += nq;  // stand-in corner count: every queued candidate
-    nq = 0;
-    return;
-#endif
     for (int j0 = 0; j0 < nq; j0 += 64) {
       const int j = j0 + lane;
       bool corner = false;
@@ -1188,12 +1133,7 @@ void k_fast_cells(
       const bool valid = g0 + pl < nG;
       const bool last = k == nK - 1;
       const int o = valid ? off : 3 * P + 8;  // invalid lanes read group 0 (masked below)
-#if FC_STUB >= 4
-      sink ^= (uint32_t)o;
-      if (false) {
-#else
       {
-#endif
       // bytes o-8 .. o+15 of the row, and o .. o+7 three rows down / up
       const uint2* rw = reinterpret_cast<const uint2*>(tile + o);
       const uint2 A = rw[-1], B = rw[0], Cc = rw[1];
@@ -1233,10 +1173,6 @@ void k_fast_cells(
       const uint32_t fails = ((X >> 7) & 0x01010101u) | ((Y >> 3) & 0x10101010u);
       uint32_t mk = ~((fails * 0x01020408u) >> 24) &
                     (valid ? (last ? (1u << nvLast) - 1u : 0xFFu) : 0u);
-#if FC_STUB >= 3
-      sink ^= mk;
-      nq += __builtin_amdgcn_readfirstlane(mk) & 1;  // (a wave-uniform stand-in count)
-#else
       const int cnt = __builtin_popcount(mk);
       int incl = wave_incl_scan(cnt);
       // opaque: otherwise hipcc forms incl - cnt from the scan's partial DPP
@@ -1249,7 +1185,6 @@ void k_fast_cells(
         queue[pos++] = (uint16_t)(off + j);
       }
       nq += __builtin_amdgcn_readlane(incl, 63);
-#endif  // FC_STUB >= 3
 #else
       // pixel j of a valid lane is interior when j < nvLast or the group is not a row's last
       const unsigned long long vm = __ballot(valid), vIn = __ballot(valid && !last);
@@ -1264,7 +1199,7 @@ void k_fast_cells(
         nq += __popcll(bj);
       }
 #endif
-      }  // pretest (FC_STUB < 4)
+      }  // pretest
       k += kInc;
       off += dOff;
       if (k >= nK) {
@@ -1387,50 +1322,29 @@ void k_fast_cells(
   (void)compact;
 #endif
   fast_pass(ti, true);
-  FCSTAMP(2);
-#if FC_STUB >= 1
-  int n = nc;
-  (void)nms_emit;
-#elif FC_ROWMAJOR
+#if FC_ROWMAJOR
   int n = nms_emit(ti);
 #else
   nms(ti);
   int n = compact();
 #endif
-  FCSTAMP(3);
   if (n == 0 && tm != ti) {
     // ---- phase B: no keypoint at iniThFAST -> minThFAST (:846-850)
     nc = 0;
     fast_pass(tm, false);
-#if FC_STUB >= 1
-    n = nc;
-#elif FC_ROWMAJOR
+#if FC_ROWMAJOR
     n = nms_emit(tm);
 #else
     nms(tm);
     n = compact();
 #endif
   }
-#if FC_STUB >= 1
-  sink ^= (uint32_t)n;
-  if (lane == 0) cellCount[slot] = sink == 0xFFFFFFFFu ? 1 : 0;
-#else
   if (lane == 0) cellCount[slot] = n;
-#endif
-  FCSTAMP(4);
-#ifdef FC_STAMPS
-  if (img == 0 && lane == 0 && ci < 8192) g_fc_stamps[ci][5] = (unsigned long long)jc;
-#endif
   ci = ciNext;
   wave_lds_sync();  // the next cell's staging overwrites the tile
   }  // cell loop
 }
 
-#ifdef ORB_FAST_STAMPS
-extern "C" hipError_t orb_k_fast_stamps(void* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fast_stamps), sizeof(g_fast_stamps));
-}
-#endif
 
 // ================================================================ k_octree
 // ExtractorNode::DivideNode + ORBextractor::DistributeOctTree
@@ -2170,12 +2084,6 @@ struct DescWaveLds {
 #else
 #define DESC_LAUNCH_BOUNDS __launch_bounds__(256)
 #endif
-#ifndef DESC_MFMA_ROWS
-// 1: row pass on the matrix cores (v_mfma_i32_16x16x64_i8). Bit-exact but
-// slower: orient 0.495 vs 0.422 ms per 512 frames (124 vs 97 VGPRs, 35 KB LDS
-// per workgroup; profiles/r03_orient_mfma.txt), so the VALU dot4 pass stays.
-#define DESC_MFMA_ROWS 0
-#endif
 #ifndef DESC_LDS_TABLES
 #define DESC_LDS_TABLES 1  // rBRIEF pattern floats and column weights in LDS (k_orient_desc)
 #endif
@@ -2185,37 +2093,12 @@ struct DescWaveLds {
 #ifndef DESC_ROW37
 #define DESC_ROW37 1     // row pass stops at column 36, the last one a sample reaches
 #endif
-#ifndef DESC_PK_ROT
-// rBRIEF point rotation + rounding adder as packed f32 (v_pk_mul / v_pk_add:
-// the same IEEE operations per component).  A/B knob: its first build took
-// the x coordinate from the y one (a clang lowering of bit_cast on a vector
-// component); the 0.829 -> 0.779 ms it measured was that bug
-#define DESC_PK_ROT 0
-#endif
-#ifndef DESC_DBUF
-#define DESC_DBUF 0      // double-buffered window rows (A/B knob)
-#endif
-#ifndef DESC_GLDS
-// 1: window rows staged by LDS-DMA (buffer_load_dwordx4 ... lds, 264 16-byte
-// chunks per pair into a per-wave LDS buffer) and the next pair's DMA issued
-// as soon as this pair's rows are read back, so it overlaps IC_Angle, the row
-// pass and the sampling (A/B knob)
-#define DESC_GLDS 0
-#endif
-#define DESC_GLDS_CHUNKS 264
-#ifndef DESC_LDS_PAD
-#define DESC_LDS_PAD 0  // bytes of unused LDS per workgroup (occupancy control, A/B only)
-#endif  // 2 keypoints x 44 rows x 3 chunks of 16 bytes
 #ifndef DESC_SMALL_CT
 #define DESC_SMALL_CT 1   // one-pair calls take k_orient_desc<1> (compile-time count), else <0>
 #endif
-// Attribution builds (tools/r04/orient_attr; results WRONG, never shipped):
-// DESC_STUB = k drops the last k phases of a pair, the work before it kept
-// alive through a sink: 1 rBRIEF sampling, 2 + row pass (row-sum stores),
-// 3 + IC_Angle moments, 4 + fastAtan2 / pinned sincos, 5 + window loads.
-#ifndef DESC_STUB
-#define DESC_STUB 0
-#endif
+// Attribution builds (phase stubs) and the measured-slower variants (LDS-DMA
+// window staging, double-buffered rows, MFMA row pass, packed rotation) are
+// patches against this file: tools/attribution/.
 
 template <int PPW>
 __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
@@ -2229,17 +2112,6 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // PPW == 0: ppwRt
   const int ppw = PPW ? PPW : ppwRt;
   __shared__ __attribute__((aligned(16))) DescWaveLds sm[4];
-#if DESC_LDS_PAD
-  // occupancy control for the DESC_GLDS A/B: the same LDS per workgroup
-  // without the DMA (never read; one store keeps it allocated)
-  __shared__ uint32_t sPad[DESC_LDS_PAD / 4];
-  if (threadIdx.x == 0) sPad[0] = 0u;
-#endif
-#if DESC_GLDS
-  // chunk q = 132 h + 3 r + k: keypoint h, window row r, 16-byte chunk k (5
-  // DMA instructions of 64 lanes; lanes past chunk 263 are masked off)
-  __shared__ __attribute__((aligned(16))) uint4 sStage[4][5 * 64];
-#endif
 #if DESC_LDS_TABLES
   // per workgroup: the rBRIEF pattern as floats (one ds_read_b128 per test
   // pair of points instead of a constant-memory load and four conversions),
@@ -2247,26 +2119,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // sample instead of four selects)
   __shared__ __attribute__((aligned(16))) float4 sPat[ORB_PATTERN_POINTS / 2];
   __shared__ __attribute__((aligned(16))) uint4 sW[2];
-#if DESC_MFMA_ROWS
-  // row pass as a product on the matrix cores: rows x bytes (signed, x - 128)
-  // times the 64 x 48 Toeplitz matrix of the 7 taps (column c takes bytes
-  // c..c+6); sB[n][lane] = lane's B fragment of column tile n
-  __shared__ __attribute__((aligned(16))) uint4 sB[3][64];
-#endif
   {
     const int t = threadIdx.x;  // 256 threads, 256 tests
-#if DESC_MFMA_ROWS
-    if (t < 192) {
-      const int n = t >> 6, l = t & 63, c = 16 * n + (l & 15);
-      const uint32_t taps[7] = {18, 34, 49, 55, 49, 34, 18};
-      uint32_t wd[4] = {0u, 0u, 0u, 0u};
-      for (int j = 0; j < 16; ++j) {
-        const int d = 16 * (l >> 4) + j - c;  // byte b = 16 (l >> 4) + j of column c
-        if (d >= 0 && d <= 6) wd[j >> 2] |= taps[d] << (8 * (j & 3));
-      }
-      sB[n][l] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-    }
-#endif
     sPat[t] = make_float4((float)c_pattern[4 * t], (float)c_pattern[4 * t + 1],
                           (float)c_pattern[4 * t + 2], (float)c_pattern[4 * t + 3]);
     if (t < 2)  // even rows: (18,34) (49,55) (49,34) (18,0); odd: (0,18) (34,49) (55,49) (34,18)
@@ -2340,46 +2194,6 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   // loads) from the 4-aligned byte at or below column cx-21
   uint32_t ra[12], rb[12], sha = 0, shb = 0;
   auto issue = [&](const Pair& P) {
-#if DESC_GLDS
-    {
-      const OrbLevelDesc& L = plan.lv[P.l];
-      const uint8_t* lvl;
-      int pitch;
-      if (P.l == 0) {
-        lvl = img0 + (long long)img * img0Pitch;
-        pitch = img0Stride;
-      } else {
-        lvl = arena + (long long)img * arenaPitch + L.arenaOff;
-        pitch = L.pitch;
-      }
-      const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
-      // the stage buffer's previous contents were read back (waited for)
-      // before this pair's DMA may overwrite them
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const int q = 64 * i + lane;
-        if (q < DESC_GLDS_CHUNKS) {
-          const int kh = q >= DESC_GLDS_CHUNKS / 2;
-          const int qq = q - (kh ? DESC_GLDS_CHUNKS / 2 : 0);
-          const int r = (qq * 171) >> 9;  // qq / 3 for qq < 132
-          const int k = qq - 3 * r;
-          const uint32_t key = kh ? P.key1 : P.key0;
-          int y = key_y(key) - 21 + r;
-          y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
-          const uint32_t o = (uint32_t)(y * pitch + key_x(key) - 21) + im.sh;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              im.r, (__attribute__((address_space(3))) void*)&sStage[w][64 * i], 16,
-              (int)((o & ~3u) + 16 * k), 0, 0, 0);
-        }
-      }
-      return;
-    }
-#endif
-#if DESC_STUB >= 5
-    sha = shb = (uint32_t)P.cx & 3u;
-    return;
-#endif
     const OrbLevelDesc& L = plan.lv[P.l];
     const uint8_t* lvl;
     int pitch;
@@ -2446,67 +2260,12 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   if (cur.valid) issue(cur);
   for (int j = 0; j < ppw; ++j) {
     const Pair P = cur;
-#if DESC_GLDS
-    if (P.valid) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the pair's DMA has landed
-      if (second) {
-        const OrbLevelDesc& L = plan.lv[P.l];
-        const uint8_t* lvl = P.l == 0 ? img0 + (long long)img * img0Pitch
-                                      : arena + (long long)img * arenaPitch + L.arenaOff;
-        const int pitch = P.l == 0 ? img0Stride : L.pitch;
-        const uint32_t lsh = (uint32_t)((uintptr_t)lvl & 3);
-        auto read_row = [&](int r, uint32_t* d) {
-          int y = P.cy - 21 + r;
-          y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
-          const uint4* src = &sStage[w][half * (DESC_GLDS_CHUNKS / 2) + 3 * r];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            const uint4 v = src[k];
-            d[4 * k] = v.x;
-            d[4 * k + 1] = v.y;
-            d[4 * k + 2] = v.z;
-            d[4 * k + 3] = v.w;
-          }
-          return ((uint32_t)(y * pitch + P.cx - 21) + lsh) & 3u;
-        };
-        sha = read_row(2 * hl, ra);
-        shb = read_row(2 * hl + 1, rb);
-        realign(ra, sha);
-        realign(rb, shb);
-      }
-    }
-    // the next pair's DMA goes out now, behind this pair's whole computation
-    if (j + 1 < ppw) {
-      cur = setup(j + 1);
-      if (cur.valid) issue(cur);
-    }
-#else
     if (P.valid && second) {
       realign(ra, sha);
       realign(rb, shb);
     }
-#endif
-#if DESC_DBUF
-    // double-buffered window rows: the pair's realigned rows move to working
-    // registers and the next pair's loads go out at once, so they overlap
-    // IC_Angle, the row pass and the sampling (24 more VGPRs: still 4 waves
-    // per SIMD, the occupancy the kernel already has)
-    uint32_t wa[12], wb[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-      wa[k] = ra[k];
-      wb[k] = rb[k];
-    }
-    if (j + 1 < ppw) {
-      cur = setup(j + 1);
-      if (cur.valid) issue(cur);
-    }
-#define RA wa
-#define RB wb
-#else
 #define RA ra
 #define RB rb
-#endif
     // ---- IC_Angle from the rows in registers: row v = ri - 15 is staged row
     // ri + 6; columns u = -16..15 are staged bytes 5..36 (dwords 1..9 shifted
     // by one byte; reading dwords 1..9 as loaded under byte-shifted masks
@@ -2525,22 +2284,13 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       m10 += (int)rm - 16 * (int)rs;
       m01 += (ri - 15) * (int)rs;
     };
-#if DESC_STUB >= 3
-    {
-      uint32_t x = 0;
-      for (int k = 0; k < 12; ++k) x ^= RA[k] ^ RB[k];
-      m01 = (int)(x & 0xFF);
-      m10 = (int)((x >> 8) & 0xFF) + 1;
-    }
-#else
     if (P.valid && second) {
       if (2 * hl >= 6 && 2 * hl <= 36) ic_row(RA, mka, 2 * hl - 6);
       if (2 * hl + 1 >= 6 && 2 * hl + 1 <= 36) ic_row(RB, mkb, 2 * hl + 1 - 6);
     }
-#endif
     // (the rows stay in registers through the row pass: the next pair's loads
     // go out after it)
-    if (!DESC_DBUF && !DESC_GLDS && !P.valid && j + 1 < ppw) {
+    if (!P.valid && j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
@@ -2576,59 +2326,8 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       wave_lds_sync();
     }
     // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
-#if DESC_MFMA_ROWS
-    // On the matrix cores: each half-wave stages its keypoint's 44 rows as
-    // signed bytes (x - 128) at a 64-byte pitch in that keypoint's row-sum
-    // area; per keypoint, the 3 row tiles (A fragments) are read, then 3 x 3
-    // v_mfma_i32_16x16x64_i8 against the Toeplitz column tiles, each result
-    // biased by 128 * 257 (the taps' sum) and packed into the row-sum pairs,
-    // overwriting the staging (every fragment is in registers by then).
-    // Bytes 48..63 and rows 44..47 of the staging are never written: they only
-    // reach the padding columns 40..47 and rows 44..47, which are not stored.
-    if (second) {
-      uint4* st0 = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(&rsp[0][0]) + 128 * hl);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        st0[q] = make_uint4(RA[4 * q] ^ 0x80808080u, RA[4 * q + 1] ^ 0x80808080u,
-                            RA[4 * q + 2] ^ 0x80808080u, RA[4 * q + 3] ^ 0x80808080u);
-        st0[4 + q] = make_uint4(RB[4 * q] ^ 0x80808080u, RB[4 * q + 1] ^ 0x80808080u,
-                                RB[4 * q + 2] ^ 0x80808080u, RB[4 * q + 3] ^ 0x80808080u);
-      }
-    }
-    wave_lds_sync();
-    {
-      typedef int v4i __attribute__((ext_vector_type(4)));
-      const int lr = lane & 15, lq = lane >> 4;
-#pragma unroll
-      for (int kp = 0; kp < 2; ++kp) {
-        uint32_t* area = &sm[w].rsp[kp][0][0];
-        const uint8_t* stg = reinterpret_cast<const uint8_t*>(area);
-        v4i a[3];
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-          a[m] = *reinterpret_cast<const v4i*>(stg + (16 * m + lr) * 64 + 16 * lq);
-#pragma unroll
-        for (int n = 0; n < 3; ++n) {
-          const v4i bf = __builtin_bit_cast(v4i, sB[n][lane]);
-#pragma unroll
-          for (int m = 0; m < 3; ++m) {
-            // C = the bias 128 * (18 + 34 + 49 + 55 + 49 + 34 + 18) = 32896
-            const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[m], bf, (v4i){32896, 32896, 32896, 32896},
-                                                                  0, 0, 0);
-            const int c = 16 * n + lr, r0 = 16 * m + 4 * lq;  // D: column lr, rows r0 .. r0 + 3
-            if ((n < 2 || c < 40) && (m < 2 || r0 < 44)) {
-              area[(r0 >> 1) * DESC_RS_DW + c] =
-                  __builtin_amdgcn_perm((uint32_t)acc[1], (uint32_t)acc[0], 0x05040100u);
-              area[((r0 >> 1) + 1) * DESC_RS_DW + c] =
-                  __builtin_amdgcn_perm((uint32_t)acc[3], (uint32_t)acc[2], 0x05040100u);
-            }
-          }
-        }
-      }
-    }
-#else
     // ---- row pass: row-sum column c of staged row r = sum_i k_i * byte(r, c + i)
-    if (second && !(DESC_STUB >= 2)) {  // the lane's row pair from registers, group by group
+    if (second) {  // the lane's row pair from registers, group by group
       // (samples reach columns 0..36 only: |rotated pattern point| <= 18.4,
       // so the last group computes column 36 alone)
 #pragma unroll
@@ -2658,35 +2357,25 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
                        pk(o[0][3], o[1][3]));
       }
     }
-#endif
-    if (!DESC_DBUF && !DESC_GLDS && j + 1 < ppw) {
+    if (j + 1 < ppw) {
       cur = setup(j + 1);
       if (cur.valid) issue(cur);
     }
     m01 = half_sum(m01);
     m10 = half_sum(m10);
-#if DESC_STUB >= 4
-    const float angle = (float)(m01 & 7);
-#else
     const float angle = fast_atan2_deg((float)m01, (float)m10);
-#endif
     wave_lds_sync();
     // ---- rBRIEF sampling the blur directly: blurred pixel (ry, rx) of the
     // patch = column pass of row-sum rows 18+ry .. 24+ry at column 18+rx,
     // i.e. the four pairs (18+ry)/2 .. +3 with the parity's weights
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float a, b;
-#if DESC_STUB >= 4
-    a = angle;
-    b = angle * 0.5f;
-#else
     {
       float sn, cs;
       pinned_sincos(angle * factorPI, &sn, &cs);
       a = cs;
       b = sn;
     }
-#endif
     const uint32_t wE[4] = {__builtin_bit_cast(uint32_t, E0), __builtin_bit_cast(uint32_t, E1),
                             __builtin_bit_cast(uint32_t, E2), __builtin_bit_cast(uint32_t, E3)};
     const uint32_t wO[4] = {__builtin_bit_cast(uint32_t, O0), __builtin_bit_cast(uint32_t, O1),
@@ -2744,11 +2433,6 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     };
 #endif
     unsigned long long words[8];
-#if DESC_STUB >= 1
-#pragma unroll
-    for (int kq = 0; kq < 8; ++kq) words[kq] = __ballot(((int)(a * 8.f) ^ kq) & 1);
-    if (false)
-#endif
 #pragma unroll
     for (int kq = 0; kq < 8; ++kq) {
       const int test = hl + 32 * kq;
@@ -2759,22 +2443,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       const float px0 = (float)c_pattern[4 * test], py0 = (float)c_pattern[4 * test + 1];
       const float px1 = (float)c_pattern[4 * test + 2], py1 = (float)c_pattern[4 * test + 3];
 #endif
-#if DESC_LDS_TABLES && DESC_MAGIC_ROUND && DESC_PK_ROT
-      // both coordinates of a point in one packed-f32 chain: {px b, px a} +
-      // {py a, -(py b)}, then + the adder (IEEE per component, no contraction:
-      // the same floats as the scalar expressions)
-      typedef float f2 __attribute__((ext_vector_type(2)));
-      const f2 ba = {b, a}, ab = {a, b}, mg = {12582912.0f, 12582912.0f};
-      f2 q0 = (f2){py0, py0} * ab, q1 = (f2){py1, py1} * ab;
-      q0.y = -q0.y;
-      q1.y = -q1.y;
-      const f2 r0 = ((f2){px0, px0} * ba + q0) + mg, r1 = ((f2){px1, px1} * ba + q1) + mg;
-      // (components into scalars first: ROCm 7.2 clang lowers
-      // __builtin_bit_cast(int, v.y) of an ext_vector component to element 0)
-      const float y0 = r0.x, x0 = r0.y, y1 = r1.x, x1 = r1.y;
-      const int v0 = blurred(__builtin_bit_cast(int, y0), __builtin_bit_cast(int, x0));
-      const int v1 = blurred(__builtin_bit_cast(int, y1), __builtin_bit_cast(int, x1));
-#elif DESC_MAGIC_ROUND
+#if DESC_MAGIC_ROUND
       const int v0 = blurred(__builtin_bit_cast(int, (px0 * b + py0 * a) + 12582912.0f),
                              __builtin_bit_cast(int, (px0 * a - py0 * b) + 12582912.0f));
       const int v1 = blurred(__builtin_bit_cast(int, (px1 * b + py1 * a) + 12582912.0f),
@@ -2994,11 +2663,15 @@ hipError_t orb_k_octree(const OrbPlanDesc* plan, const int32_t* cellCount,
   }
   // The pass bound is never reached with the reference's own bounds (a pass
   // halves every divided node; distinct keys separate in ~12 passes, the
-  // final phase adds a few).  ORB_OCTREE_MAX_PASSES lowers it: a test hook
-  // that drives the failed-image path (negative count, ORB_EDEVICE).
-  static const int maxPasses = getenv("ORB_OCTREE_MAX_PASSES")
-                                   ? std::max(1, std::min(OCT_MAX_PASSES, atoi(getenv("ORB_OCTREE_MAX_PASSES"))))
-                                   : OCT_MAX_PASSES;
+  // final phase adds a few).  The test build lib/variants/octree_passes2.so
+  // (make testhook: -DORB_OCTREE_TEST_PASSES=2) lowers it to drive the
+  // failed-image path (negative count, ORB_EDEVICE); the product has no hook.
+#ifdef ORB_OCTREE_TEST_PASSES
+  constexpr int maxPasses = ORB_OCTREE_TEST_PASSES;
+  static_assert(ORB_OCTREE_TEST_PASSES >= 1 && ORB_OCTREE_TEST_PASSES <= OCT_MAX_PASSES, "pass bound");
+#else
+  constexpr int maxPasses = OCT_MAX_PASSES;
+#endif
   // Batches take 256-thread workgroups: the octree alone is slower (0.150 vs
   // 0.132 ms per 512 frames) but the smaller workgroups fit better beside the
   // other lane's kernels (bench 317.0k / 316.6k vs 315.5k / 315.2k frames/s,

@@ -1261,7 +1261,8 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
       const int initN = std::max(3 * kpStride, R + 1);
       hipLaunchKernelGGL(k_proj_jacobi_init, dim3((initN + JAC_T - 1) / JAC_T, nproblems), dim3(JAC_T),
                          0, s, jacScratch, js, kpStride, R, nkeys, kpMatch, nmatches);
-      const dim3 g((mpStride + JAC_T * JAC_PPT - 1) / (JAC_T * JAC_PPT), nproblems);
+      // (an empty map stride still launches one workgroup per problem: a grid of x = 0 is invalid)
+      const dim3 g((std::max(mpStride, 1) + JAC_T * JAC_PPT - 1) / (JAC_T * JAC_PPT), nproblems);
       for (int r = 0; r <= R; ++r)
         hipLaunchKernelGGL(k_proj_jacobi<JAC_PPT>, g, dim3(JAC_T), 0, s, keys, desc, uright, locked,
                            kpStride, mps, mpDesc, nmps, mpStride, cellStart, cellIdx, P, topk, ncand,

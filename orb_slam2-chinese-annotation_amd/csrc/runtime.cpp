@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <shared_mutex>
 #include <cmath>
 #include <vector>
 
@@ -183,6 +184,49 @@ namespace {
 
 static inline int cvRoundF(float v) { return (int)lrintf(v); }
 static inline short satShort(int v) { return (short)std::min(std::max(v, -32768), 32767); }
+
+static bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
+}
+
+// Call order on one handle.  Every call reuses the handle's device scratch
+// (the extractor's arena, cell keys and octree tables; the matcher's grid,
+// candidate lists and claim buffers), and a batch call runs asynchronously on
+// whatever stream its caller passes, so a call on a stream other than the
+// previous call's makes its stream wait for that call first (on the device, no
+// host synchronisation), and every call records where it ended.  The reference
+// has the same rule in host form: an ORBextractor is not reentrant
+// (include/ORBextractor.h:85), a Frame drives two instances concurrently
+// (src/Frame.cc:81-84).  A stream being captured into a graph is left to the
+// caller's ordering of the graph's launches.  (Growing a scratch buffer is
+// safe on its own: hipFree synchronises the device.)
+#ifndef ORB_CALL_ORDER
+#define ORB_CALL_ORDER 1  // 0: no cross-stream waits (the ordering test's negative control only)
+#endif
+static inline bool must_wait(hipStream_t last, hipStream_t s) {
+  return ORB_CALL_ORDER && last && last != s;
+}
+struct CallOrder {
+  hipEvent_t ev;
+  hipStream_t* last;
+  hipStream_t s;
+  bool capture;
+  orb_status_t status = ORB_OK;
+  CallOrder(hipEvent_t e, hipStream_t* l, hipStream_t st)
+      : ev(e), last(l), s(st), capture(stream_capturing(st)) {
+    if (!capture && must_wait(*last, s) && hipStreamWaitEvent(s, ev, 0) != hipSuccess)
+      status = ORB_EDEVICE;
+  }
+  // the call synchronised its stream: nothing of it is pending any more
+  void settled() {
+    if (!capture) *last = nullptr;
+    capture = true;
+  }
+  ~CallOrder() {
+    if (!capture && hipEventRecord(ev, s) == hipSuccess) *last = s;
+  }
+};
 
 // Growable device buffer.
 struct DevBuf {
@@ -355,6 +399,7 @@ struct orb_extractor {
   hipEvent_t evL0Fork = nullptr, evL0Join = nullptr;  // level-0 FAST beside the resize chain
   hipEvent_t evLvl = nullptr;  // the resize chain has written level FAST_SIDE_LEVELS
   hipEvent_t evBatch = nullptr;  // recorded at the end of every run_batch on its stream
+  hipStream_t lastStream = nullptr;  // the stream evBatch was last recorded on (null: none pending)
   bool ownStream = false;
   std::mutex mu;
 
@@ -656,6 +701,9 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (ldsNodes + (size_t)ldsKeyCap * 6 > 160 * 1024) return ORB_EINVAL;
 
   hipSetDevice(h->device);
+  // the tables below are read by the previous call's kernels, which may still
+  // run on another stream (CallOrder): the uploads wait for that call
+  if (must_wait(h->lastStream, h->stream)) HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));
   orb_status_t st = h->dCells.ensure(cells.size() * sizeof(OrbCellDesc));
   if (st) return st;
   st = h->dRtab.ensure(std::max<size_t>(rtab.size(), 1) * 4);
@@ -674,6 +722,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
     HIP_TRY(hipMemcpyAsync(h->dRtab.p, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice,
                            h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  h->lastStream = nullptr;  // the previous call has finished (waited for above)
   h->plan = P;
   h->cells.swap(cells);
   h->arenaBytes = (arena + 255) & ~255LL;
@@ -709,6 +758,12 @@ static orb_status_t ensure_batch(orb_extractor* h, int B) {
 }
 
 static int stream_prio(bool least);
+// The shared side streams (shared_side_stream below) are destroyed by an exit
+// handler; run_batch holds g_sideUse shared while it enqueues, and a call that
+// starts after the release fails with ORB_EDEVICE instead of launching on a
+// destroyed stream (e.g. from a thread still running at exit).
+static std::shared_mutex g_sideUse;
+static bool g_sideReleased = false;
 
 // Schedule constants of run_batch (compile-time A/B: tools/build_variant.sh)
 #ifndef FAST_CELLS_MIN_BATCH
@@ -737,10 +792,12 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   // the side stream: the device's shared one, or -- while the caller's stream
   // is being captured into a graph -- a stream of this handle's own, so a
   // capture never pulls another handle's side work into its graph
+  std::shared_lock<std::shared_mutex> sideUse(g_sideUse);
+  if (g_sideReleased) return ORB_EDEVICE;  // process exit has begun
   hipStream_t side = h->stream2;
+  capturing = capturing || stream_capturing(s);
   {
-    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone) {
+    if (capturing) {
       if (!h->privSide &&
           hipStreamCreateWithPriority(&h->privSide, hipStreamNonBlocking, stream_prio(true)) != hipSuccess) {
         h->privSide = nullptr;
@@ -844,7 +901,10 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                             P.nlevels, s));
   PROF_REC(ev, pf.e(ev, 4), s);
   PROF_REC(ev, pf.t1(ev), s);
-  if (!capturing) HIP_TRY(hipEventRecord(h->evBatch, s));  // readbacks on the handle stream wait for it
+  if (!capturing) {  // readbacks and the next call on another stream wait for it (CallOrder)
+    HIP_TRY(hipEventRecord(h->evBatch, s));
+    h->lastStream = s;
+  }
   h->lastImg0 = d_images;
   h->lastImg0Pitch = imgPitch;
   h->lastImg0Stride = (int)stride;
@@ -905,7 +965,9 @@ static hipStream_t g_side[64] = {};
 // process at exit under rocprofv3 --kernel-trace (SIGSEGV in __cxa_finalize,
 // after the profiler's finalisation; profiles/r05_exit_crash.txt).
 static void release_side_streams() {
+  std::unique_lock<std::shared_mutex> u(g_sideUse);  // no run_batch is enqueueing
   std::lock_guard<std::mutex> g(g_sideMu);
+  g_sideReleased = true;
   for (hipStream_t& st : g_side)
     if (st) {
       hipStreamDestroy(st);  // waits for the stream's work
@@ -928,9 +990,11 @@ static hipStream_t shared_side_stream(int device, int prio) {
       // pooled one: a mask of every CU of the device
       hipDeviceProp_t prop;
       e = hipGetDeviceProperties(&prop, device);
-      std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
-      for (int c = 0; c < prop.multiProcessorCount; ++c) mask[c >> 5] |= 1u << (c & 31);
-      if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&s[device], (uint32_t)mask.size(), mask.data());
+      if (e == hipSuccess) {
+        std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+        for (int c = 0; c < prop.multiProcessorCount; ++c) mask[c >> 5] |= 1u << (c & 31);
+        e = hipExtStreamCreateWithCUMask(&s[device], (uint32_t)mask.size(), mask.data());
+      }
     } else {
       e = hipStreamCreateWithPriority(&s[device], hipStreamNonBlocking, prio);
     }
@@ -1029,6 +1093,7 @@ void orb_extractor_destroy(orb_extractor_t* h) {
   if (!h) return;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->lastStream) hipEventSynchronize(h->evBatch);  // a batch call on a caller's stream
   DevBuf* bufs[] = {&h->dCells, &h->dRtab, &h->dTiles, &h->dBlur, &h->dArena, &h->dCellKeys, &h->dCellCount, &h->dOctNodes,
                     &h->dGKeys, &h->dGNid, &h->dOutKeys, &h->dOutCount, &h->dErr,
                     &h->dImg, &h->dOne};
@@ -1091,6 +1156,10 @@ orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_im
   if (capacity < h->plan.slotsPerImage) return ORB_ECAPACITY;
   if ((st = ensure_batch(h, n_images))) return st;
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  // the previous call may still run on another stream: its scratch is this
+  // call's scratch (CallOrder)
+  if (must_wait(h->lastStream, s) && !stream_capturing(s))
+    HIP_TRY(hipStreamWaitEvent(s, h->evBatch, 0));
   st = run_batch(h, d_images, n_images, stride, image_pitch, d_keypoints, d_descriptors, capacity,
                  d_counts, s);
   if (st) return st;
@@ -1122,6 +1191,8 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   if ((st = h->hOut.ensure(outBytes))) return st;
   if (h->pyrReadback && (st = h->hPyr.ensure((size_t)std::max<long long>(h->arenaBytes, 1)))) return st;
   h->hPyrValid = false;
+  // a batch call may still run on a caller's stream (CallOrder)
+  if (must_wait(h->lastStream, h->stream)) HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));
   // image -> pinned staging at the device row pitch
   for (int y = 0; y < height; ++y)
     memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
@@ -1177,6 +1248,7 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     h->lastImg0Stride = (int)dstride;
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
+  h->lastStream = nullptr;  // nothing of this handle is pending
   h->oneCap = cap;
   h->lastSingle = true;
   h->hPyrValid = h->pyrReadback;
@@ -1418,6 +1490,8 @@ struct InitParamsHost {  // mirrors InitParams in mapping_kernels.hip
 struct orb_matcher {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipEvent_t evLast = nullptr;        // recorded where the last call ended (CallOrder)
+  hipStream_t lastStream = nullptr;   // its stream (null: nothing pending)
   std::mutex mu;
   // profiling: stages k_grid_build, k_proj_candidates + k_proj_resolve
   StageProfiler prof;
@@ -1485,6 +1559,11 @@ orb_status_t orb_matcher_create(int device, orb_matcher_t** out) {
     delete m;
     return ORB_EDEVICE;
   }
+  if (hipEventCreateWithFlags(&m->evLast, hipEventDisableTiming) != hipSuccess) {
+    hipStreamDestroy(m->stream);
+    delete m;
+    return ORB_EDEVICE;
+  }
   *out = m;
   return ORB_OK;
 }
@@ -1493,6 +1572,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
   if (!m) return;
   hipSetDevice(m->device);
   hipStreamSynchronize(m->stream);
+  if (m->lastStream) hipEventSynchronize(m->evLast);  // a batch call on a caller's stream
   DevBuf* bufs[] = {&m->dKeys, &m->dDesc, &m->dUr, &m->dLocked, &m->dNKeys, &m->dMps,
                     &m->dMpDesc, &m->dNMps, &m->dCellStart, &m->dCellIdx, &m->dTopk,
                     &m->dNcand, &m->dKpMatch, &m->dNMatch, &m->dA, &m->dB, &m->dOut, &m->dJac,
@@ -1511,6 +1591,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
   for (DevBuf& b : m->sx) b.release();
   m->prof.destroy();
   hipStreamDestroy(m->stream);
+  hipEventDestroy(m->evLast);
   delete m;
 }
 
@@ -1555,6 +1636,8 @@ orb_status_t orb_match_projection_local_batch(
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   const ProjParamsHost P =
       proj_params(min_x, max_x, min_y, max_y, n_levels, scale_factors, th, nnratio);
   orb_status_t st;
@@ -1662,6 +1745,8 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   if ((st = m->dTopk.ensure((size_t)std::max(M, 1) * 16))) return st;
   if ((st = m->dNcand.ensure((size_t)std::max(M, 1) * 4))) return st;
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   // every input in one pinned block, one DMA in (six pageable copies each
   // staged by the runtime cost more than the kernels): [nk, nm | keys |
   // descriptors | uR | locked | tracks | map-point descriptors], 16-B aligned
@@ -1727,6 +1812,7 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   // one DMA out (count, then the matches) into pinned memory
   HIP_TRY(hipMemcpyAsync(m->hOutM.p, m->dKpMatch.p, (size_t)N * 4 + 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  order.settled();
   memcpy(kp_match, m->hOutM.p, (size_t)N * 4);
   memcpy(nmatches, m->hOutM.as<uint8_t>() + (size_t)N * 4, 4);
   return ORB_OK;
@@ -1752,6 +1838,8 @@ orb_status_t orb_frustum(orb_matcher_t* m, int n_mp, const orb_map_point_t* mps,
   if ((st = m->dNInView.ensure(16))) return st;
   if ((st = m->dNMps.ensure(16))) return st;
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   HIP_TRY(hipMemcpyAsync(m->dMapPts.p, mps, (size_t)n_mp * sizeof(orb_map_point_t),
                          hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(m->dPose.p, pose, sizeof(orb_pose_t), hipMemcpyHostToDevice, s));
@@ -1828,6 +1916,8 @@ orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in, fl
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   const int stride = std::max(NL, std::max(NR, 1));
   orb_status_t st;
   if ((st = upload(m->dKeys, F->keys, (size_t)NL * sizeof(orb_keypoint_t), s))) return st;
@@ -1906,6 +1996,8 @@ orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   StereoParamsHost P;
   memset(&P, 0, sizeof(P));
   P.nLevels = L;
@@ -1976,6 +2068,8 @@ orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   HIP_TRY(hipStreamWaitEvent(s, left_ext->evBatch, 0));
   HIP_TRY(hipStreamWaitEvent(s, right_ext->evBatch, 0));
   StereoParamsHost P;
@@ -2054,6 +2148,8 @@ orb_status_t orb_match_projection_frame(orb_matcher_t* m, const orb_frame_t* C,
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   const int N = C->n, M = n_last;
   orb_status_t st;
   if ((st = upload(m->dKeys, C->keys, (size_t)N * sizeof(orb_keypoint_t), s))) return st;
@@ -2116,6 +2212,8 @@ orb_status_t orb_match_bow(orb_matcher_t* m, int n_kf, const uint8_t* kf_desc,
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   orb_status_t st;
   if ((st = upload(m->dBowA, kf_desc, (size_t)n_kf * 32, s))) return st;
   if ((st = upload(m->dBowB, kf_angle, (size_t)n_kf * 4, s))) return st;
@@ -2208,6 +2306,8 @@ orb_status_t orb_search_for_initialization(orb_matcher_t* m, const orb_frame_t* 
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   orb_status_t st;
   if ((st = upload(m->dK1, f1->keys, (size_t)N1 * sizeof(orb_keypoint_t), s))) return st;
   if ((st = upload(m->dD1, f1->descriptors, (size_t)N1 * 32, s))) return st;
@@ -2247,6 +2347,8 @@ orb_status_t orb_search_for_initialization_batch(
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   return search_init_device(m, n_problems, d_keys1, d_desc1, d_n1, d_keys2, d_desc2, d_n2,
                             kp_stride, min_x, max_x, min_y, max_y, window_size, nnratio,
                             check_orientation, d_prev_matched, d_matches12, d_nmatches, s);
@@ -2266,6 +2368,8 @@ orb_status_t orb_distinctive_descriptors(orb_matcher_t* m, int n_mp, const int32
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   orb_status_t st;
   if ((st = upload(m->dOffs, obs_offs, (size_t)(n_mp + 1) * 4, s))) return st;
   if ((st = upload(m->dObsDesc, obs_desc, nobs * 32, s))) return st;
@@ -2442,6 +2546,8 @@ orb_status_t orb_search_by_projection_reloc(orb_matcher_t* m, const orb_frame_t*
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   if ((st = pp_frame(m, frame, P, 0, s))) return st;
   return pp_run(m, 0, P, 0, frame, kp_locked, n_mp, mps, nullptr, nullptr, mp_desc,
                 check_orientation ? kf_angle : nullptr, nullptr, kp_match, nmatches, s);
@@ -2463,6 +2569,8 @@ orb_status_t orb_search_by_projection_sim3(orb_matcher_t* m, const orb_frame_t* 
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   if ((st = pp_frame(m, kf, P, 0, s))) return st;
   return pp_run(m, 1, P, 0, kf, nullptr, n_mp, mps, nullptr, nullptr, mp_desc, nullptr, nullptr,
                 kp_matched, nmatches, s);
@@ -2488,6 +2596,8 @@ orb_status_t orb_fuse(orb_matcher_t* m, const orb_frame_t* kf, const float* inv_
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   if ((st = pp_frame(m, kf, P, 0, s))) return st;
   return pp_run(m, 2, P, 0, kf, nullptr, n_mp, mps, nullptr, nullptr, mp_desc, nullptr,
                 fuse_idx, nullptr, n_fuse, s);
@@ -2509,6 +2619,8 @@ orb_status_t orb_fuse_sim3(orb_matcher_t* m, const orb_frame_t* kf, const float*
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   if ((st = pp_frame(m, kf, P, 0, s))) return st;
   return pp_run(m, 3, P, 0, kf, nullptr, n_mp, mps, nullptr, nullptr, mp_desc, nullptr,
                 fuse_idx, nullptr, n_fuse, s);
@@ -2548,6 +2660,8 @@ orb_status_t orb_search_by_sim3(orb_matcher_t* m, const orb_frame_t* kf1, const 
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   if ((st = pp_frame(m, kf2, P1, 0, s))) return st;
   if ((st = pp_frame(m, kf1, P2, 4, s))) return st;
   if ((st = m->sx[21].ensure((size_t)kf1->n * 4))) return st;
@@ -2591,6 +2705,8 @@ orb_status_t orb_match_bow_kf(orb_matcher_t* m, int n1, const uint8_t* desc1,
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   orb_status_t st;
   DevBuf* b = m->sx;
   if ((st = upload(b[0], desc1, (size_t)n1 * 32, s))) return st;
@@ -2659,6 +2775,8 @@ orb_status_t orb_search_for_triangulation(
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   orb_status_t st;
   DevBuf* b = m->sx;
   const int n1 = kf1->n, n2 = kf2->n;
@@ -3017,6 +3135,8 @@ orb_status_t orb_undistort_points(orb_matcher_t* m, int n, const float* xy, cons
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   if ((st = upload(m->dA, xy, (size_t)n * 8, s)) || (st = m->dB.ensure((size_t)n * 8))) return st;
   HIP_TRY(orb_k_undistort_points(&P, n, m->dA.as<float>(), m->dB.as<float>(), s));
   HIP_TRY(hipMemcpyAsync(out_xy, m->dB.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
@@ -3039,6 +3159,8 @@ orb_status_t orb_undistort_keypoints(orb_matcher_t* m, int n, const orb_keypoint
   std::lock_guard<std::mutex> g(m->mu);
   hipSetDevice(m->device);
   hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
   const size_t bytes = (size_t)n * sizeof(orb_keypoint_t);
   if ((st = upload(m->dA, keys, bytes, s)) || (st = m->dB.ensure(bytes))) return st;
   HIP_TRY(orb_k_undistort_keys(&P, 1, nullptr, n, n, m->dA.p, m->dB.p, 0, s));

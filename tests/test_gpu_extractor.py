@@ -394,7 +394,8 @@ def test_octree_pass_bound_fails_cleanly(gpu):
     """An octree that hits its pass bound fails the image as a whole: the
     single-frame call raises ORB_EDEVICE, the batch form reports a negative
     count, and the handle keeps working afterwards (the bound lowered through
-    the ORB_OCTREE_MAX_PASSES test hook, in a child process)."""
+    test build lib/variants/octree_passes2.so, `make testhook`, in a child
+    process: the product library has no hook)."""
     import subprocess
     import sys
     from pathlib import Path
@@ -421,7 +422,9 @@ torch.cuda.synchronize()
 print('batch:', n.tolist())
 """
     import os
-    env = dict(os.environ, ORB_OCTREE_MAX_PASSES="2")
+    variant = root / "orb_slam2-chinese-annotation_amd" / "lib" / "variants" / "octree_passes2.so"
+    assert variant.exists(), "build the test variant first (make -C orb_slam2-chinese-annotation_amd testhook)"
+    env = dict(os.environ, ORB_AMD_LIB=str(variant))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
                        env=env)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -210,6 +210,33 @@ def test_search_by_projection_resolve_schedules(gpu, oracle, name, schedule, rou
             assert np.array_equal(km, km_ref), (w, i, np.nonzero(km != km_ref)[0][:10])
 
 
+@pytest.mark.parametrize("schedule", [0, 1, 2, 3])
+def test_search_by_projection_batch_empty_map_stride(gpu, oracle, schedule):
+    """mp_stride = 0 (no map point in any problem) under every schedule: no
+    match, every keypoint -1 (the Jacobi rounds' grid is clamped to one
+    workgroup per problem instead of an invalid x = 0)."""
+    torch = pytest.importorskip("torch")
+    w, h = 640, 480
+    k, d, scale = _frame(gpu, oracle, w, h, 1000, 2)
+    P, cap = 3, len(k)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).cuda()
+    dk = t(np.stack([k] * P))
+    dd = t(np.stack([d] * P))
+    dn = torch.full((P,), len(k), dtype=torch.int32, device="cuda")
+    dnm = torch.zeros(P, dtype=torch.int32, device="cuda")
+    dummy = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    km = torch.full((P, cap), -7, dtype=torch.int32, device="cuda")
+    nm = torch.full((P,), -7, dtype=torch.int32, device="cuda")
+    m = gpu.ORBmatcher(0.8)
+    m.set_resolve(schedule, 6)
+    m.search_by_projection_batch(P, dk.data_ptr(), dd.data_ptr(), dn.data_ptr(), 0, cap,
+                                 dummy.data_ptr(), dummy.data_ptr(), dnm.data_ptr(), 0, w, h,
+                                 scale, 1.0, km.data_ptr(), nm.data_ptr())
+    torch.cuda.synchronize()
+    assert (nm.cpu().numpy() == 0).all()
+    assert (km.cpu().numpy() == -1).all()
+
+
 def test_resolve_schedule_rejects_bad_values(gpu):
     m = gpu.ORBmatcher(0.8)
     for sched, r in ((4, 6), (-1, 6), (3, 0), (3, 49)):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase clock counts of k_fast_cells (needs the FC_STAMPS build:
-tools/build_variant.sh fcst -DFC_STAMPS, run with ORB_AMD_LIB=.../fcst.so).
+tools/attribution/build.sh fcst -DFC_STAMPS, run with ORB_AMD_LIB=.../fcst.so).
 Image 0's cells of the last B-frame batch call, s_memtime by lane 0 of each
 cell's wave: stage (staging, strength clear, next loads issued, setup), fastA
 (pretest, queue, scoring at iniThFAST), nmsA (NMS and key emit), phaseB
