@@ -66,11 +66,17 @@ def level_sizes(w, h, scale, nlevels):
     return out
 
 
-def algorithmic_bytes(w, h, scale, nlevels, n_kp, n_mp):
-    """Per-frame algorithmic HBM bytes of each kernel."""
+def algorithmic_bytes(w, h, scale, nlevels, n_kp, n_mp, resize_launches=None):
+    """Per-frame algorithmic HBM bytes of each kernel.
+    resize_launches: launches per call of the pyramid stage; when the planner
+    paired the levels (k_pyr_resize2 builds l and l + 1 from l - 1, pairs from
+    level 1), level l of a pair is written and never read back."""
     sizes = level_sizes(w, h, scale, nlevels)
     P = [a * b for a, b in sizes]
     pyr = sum(P[l - 1] + P[l] for l in range(1, nlevels))  # read level l-1, write level l
+    pairs = [(l, l + 1 < nlevels) for l in range(1, nlevels, 2)]
+    if resize_launches is not None and resize_launches == len(pairs) < nlevels - 1:
+        pyr = sum(P[l - 1] + P[l] + (P[l + 1] if two else 0) for l, two in pairs)
     fast = sum(P)                                          # read every level once
     desc = 60 * n_kp                                       # 28 B keypoint + 32 B descriptor
     match = 60 * n_mp + 48 * n_kp + 24576                  # SURVEY §8(d) B_lm
@@ -1132,7 +1138,8 @@ def main():
     matcher.profile(False)
     n_kp = float(cnt_h.mean())
     nmatch = float(sets[0]["nmatch"].float().mean().item())
-    alg = algorithmic_bytes(W, H, scale, 8, n_kp, M)
+    rl = kern.get("k_pyr_resize", (0, 0))[1] / max(n_prof, 1)
+    alg = algorithmic_bytes(W, H, scale, 8, n_kp, M, resize_launches=round(rl) if rl else None)
     # every kernel alone (one stream, every stage after the previous one, no
     # side stream): kernel-only launch times for the roofline and the per-kernel
     # table; the pipelined HIP-event times above stay beside them

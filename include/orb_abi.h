@@ -5,6 +5,21 @@
  * OpenCV, no torch, no HIP types in any signature (streams are passed as
  * `void*`, a hipStream_t, NULL = the handle's own stream).
  *
+ * Streams and call order.  A handle's calls are serialised on the host (a
+ * mutex per handle) and on the device: every call reuses the handle's device
+ * scratch, so a call issued on a different stream from the previous call on
+ * the same handle first makes its stream wait for that call (an event wait,
+ * no host synchronisation), and a frame-size change, which rewrites the
+ * extractor's plan tables, waits on the host for the previous call.  One
+ * handle may therefore be driven from any mix of streams (the reference's
+ * ORBextractor is not reentrant at all, include/ORBextractor.h:85).  The
+ * caller still orders its own data: a batch call's inputs must be ready on
+ * the stream passed, and its outputs are ready on that stream only.  Calls
+ * issued on a stream being captured into a graph record no event; the caller
+ * orders the graph's launches.  The extractor's batch calls also use one
+ * device-wide side stream that HIP creates blocking, so work on the legacy
+ * null stream waits for its FAST kernels in flight (INTEGRATION.md "Streams").
+ *
  * Reference interfaces each entry point replaces (paths relative to the
  * reference tree, yg838457845/ORB_SLAM2-Chinese-annotation):
  *

@@ -266,6 +266,190 @@ __global__ __launch_bounds__(256) void k_pyr_resize(
   }
 }
 
+// ========================================================== k_pyr_resize2
+// Two pyramid levels per launch: level l + 1 (the output tile, 128 x 32, as
+// k_pyr_resize) from level l, and level l from level l - 1, in one workgroup.
+// The workgroup computes the region R1 of level l that its output tile's taps
+// read (plus the level-l pixels it owns, below) into LDS from the level l - 1
+// window S0, writes the level-l pixels it owns to the arena, and computes its
+// level-(l+1) tile from R1 without a global round trip.  Ownership partitions
+// level l: tile (bx, by) owns columns [X0(bx), X0(bx + 1)) with X0(b) the
+// 4-aligned first source column of output column 128 b (X0(0) = 0, the last
+// tile to the level's width), rows likewise; R1 covers both the owned range
+// and the taps, so a level-l pixel next to a tile edge is computed twice from
+// the same integer expressions (identical bytes) and stored once.  Every level-l
+// pixel is the OpenCV INTER_LINEAR value of k_pyr_resize (SURVEY.md Appendix
+// A.2), so the pyramid is bit-identical; the launch replaces two dependent
+// launches and level l is never read back from HBM.  The planner enables it
+// for a pair of narrow levels whose every tile fits the windows below
+// (orb_plan: lv[l].resize2).
+#define PYR2_S0R 56   // level l-1 window rows
+#define PYR2_S0W 56   // level l-1 window dwords per row (incl. 2 read-ahead)
+#define PYR2_R1R PYR_SROWS  // level-l region rows (the narrow source window)
+#define PYR2_R1W PYR_SW     // level-l region dwords per row (incl. 2 read-ahead)
+#define PYR2_TAB 176        // level-l columns of the region's x tables (>= 4 x PYR2_R1W)
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_pyr_resize2(
+    const uint8_t* __restrict__ src, long long srcImgPitch, int srcStride, int w0, int h0,
+    uint8_t* __restrict__ mid, long long midImgPitch, int midStride, int w1, int h1,
+    const int* __restrict__ xo1, const int* __restrict__ al1, const int* __restrict__ yo1,
+    const int* __restrict__ be1, uint8_t* __restrict__ dst, long long dstImgPitch, int dstStride,
+    int w2, int h2, const int* __restrict__ xo2, const int* __restrict__ al2,
+    const int* __restrict__ yo2, const int* __restrict__ be2, int nImg) {
+  __shared__ __attribute__((aligned(16))) uint32_t s0[PYR2_S0R][PYR2_S0W];
+  __shared__ __attribute__((aligned(16))) uint32_t r1[PYR2_R1R][PYR2_R1W];
+  __shared__ __attribute__((aligned(16))) int sXo[PYR2_TAB], sAl[PYR2_TAB];
+  __shared__ int sYo[PYR2_R1R], sBe[PYR2_R1R];
+  const int tid = threadIdx.x;
+  const int tx = tid & 31, ty = tid >> 5;
+  int bx, by, bz;
+  xcd_swizzle3(bx, by, bz);
+  const int x0 = bx * PYR_TW, y0 = by * PYR_TH;
+  const int xs = x0 + 4 * tx;
+  // ---- level l+1 taps of this thread (as k_pyr_resize)
+  int xo[4], al[4], yo[PYR_TH / 8], be[PYR_TH / 8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int dx = min(xs + j, w2 - 1);
+    xo[j] = xo2[dx];
+    al[j] = al2[dx];
+  }
+#pragma unroll
+  for (int rr = 0; rr < PYR_TH / 8; ++rr) {
+    const int y = min(y0 + (PYR_TH / 8) * ty + rr, h2 - 1);
+    yo[rr] = yo2[y];
+    be[rr] = be2[y];
+  }
+  // ---- R1: level-l columns [X0, X1e), rows [Y0, Y1e); owned [X0, ownX) x [Y0, ownY)
+  const int xl = min(x0 + PYR_TW - 1, w2 - 1), yl = min(y0 + PYR_TH - 1, h2 - 1);
+  const int X0 = x0 == 0 ? 0 : (xo2[x0] & ~3);
+  const int ownX = x0 + PYR_TW >= w2 ? w1 : (xo2[x0 + PYR_TW] & ~3);
+  const int X1e = max(min(xo2[xl] + 1, w1 - 1) + 1, ownX);
+  const int Y0 = y0 == 0 ? 0 : min(max(yo2[y0], 0), h1 - 1);
+  const int ownY = y0 + PYR_TH >= h2 ? h1 : min(max(yo2[y0 + PYR_TH], 0), h1 - 1);
+  const int Y1e = max(min(max(yo2[yl] + 1, 0), h1 - 1) + 1, ownY);
+  const int nG1 = (X1e - X0 + 3) >> 2, nR1 = Y1e - Y0;
+  // ---- S0: the level l-1 window R1's taps read
+  const int c0a = xo1[X0], c0b = min(xo1[min(X0 + 4 * nG1 - 1, w1 - 1)] + 1, w0 - 1);
+  const int colBase0 = c0a & ~3;
+  const int r0a = min(max(yo1[Y0], 0), h0 - 1), r0b = min(max(yo1[Y1e - 1] + 1, 0), h0 - 1);
+  const int nW0 = ((c0b - colBase0) >> 2) + 1, nR0 = r0b - r0a + 1;
+  // R1's tables in LDS (read per item below)
+  for (int i = tid; i < 4 * nG1; i += 256) {
+    const int dx = min(X0 + i, w1 - 1);
+    sXo[i] = xo1[dx];
+    sAl[i] = al1[dx];
+  }
+  if (tid < nR1) {  // both source rows of level-l row Y0 + tid, relative to r0a
+    const int yy = yo1[Y0 + tid];
+    sYo[tid] = (min(max(yy, 0), h0 - 1) - r0a) | ((min(max(yy + 1, 0), h0 - 1) - r0a) << 16);
+    sBe[tid] = be1[Y0 + tid];
+  }
+  const int nStage = (nW0 + 3) >> 2;
+  const uint32_t magic = div_magic(nStage);
+  constexpr int NQ = (PYR2_S0R * (PYR2_S0W / 4) + 255) / 256;
+  TilePrefetch16<NQ> pf;
+  uint32_t eoff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint32_t i = (uint32_t)min(q * 256 + tid, nR0 * nStage - 1);
+    const uint32_t r = __umulhi(i << 1, magic), c = i - r * (uint32_t)nStage;
+    eoff[q] = (r0a + r) * (uint32_t)srcStride + (uint32_t)colBase0 + 16 * c;
+  }
+  auto issue = [&](int z) {
+    pf.issue(img_rsrc(src + (long long)z * srcImgPitch, (uint32_t)((h0 - 1) * srcStride + w0)),
+             ALIGNED, eoff);
+  };
+  int z = bz;
+  if (z >= nImg) return;
+  issue(z);
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  // one 4-column group of 2 source rows -> 4 horizontal sums (as k_pyr_resize's hrow)
+  auto hsum = [](const uint32_t* R, int sh, const uint32_t* sel, const u16x2* wts, uint32_t* h) {
+    const uint32_t w0_ = R[0], w1_ = R[1], w2_ = R[2];
+    const uint32_t W0 = __builtin_amdgcn_alignbyte(w1_, w0_, sh);
+    const uint32_t W1 = __builtin_amdgcn_alignbyte(w2_, w1_, sh);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(W1, W0, sel[j])),
+                                    wts[j], 0u, false);
+  };
+  auto vsum = [](const uint32_t* ha, const uint32_t* hb, uint32_t b) {
+    const uint32_t b0 = b & 0xFFFFu, b1 = b >> 16;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int v = min((int)((__umul24(ha[j], b0) + __umul24(hb[j], b1) + (1u << 21)) >> 22), 255);
+      __asm__ volatile("" : "+v"(v));  // see k_pyr_resize
+      packed |= (uint32_t)v << (8 * j);
+    }
+    return packed;
+  };
+  // level l+1 taps from R1 (relative to X0 / Y0)
+  const int rel0 = xo[0] - X0;
+  const int k0 = rel0 >> 2, sh0 = rel0 & 3;
+  uint32_t sel[4];
+  u16x2 wts[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t bj = (uint32_t)(xo[j] - xo[0]);
+    sel[j] = bj | (0x0Cu << 8) | ((bj + 1) << 16) | (0x0Cu << 24);
+    wts[j] = __builtin_bit_cast(u16x2, (uint32_t)al[j]);
+  }
+  const int nItems = nR1 * nG1;
+  const uint32_t gMagic = div_magic(nG1);
+  for (; z < nImg; z += gridDim.z) {
+    __syncthreads();  // the previous image's R1 reads are done (and the tables on the first pass)
+    pf.commit(&s0[0][0], PYR2_S0W, nR0, nStage, magic, ALIGNED);
+    if (z + (int)gridDim.z < nImg) issue(z + gridDim.z);
+    __syncthreads();
+    // ---- R1 (level l) from S0, owned groups to the arena
+    {
+      const __amdgpu_buffer_rsrc_t rm =
+          make_rsrc(mid + (long long)z * midImgPitch, (uint32_t)(h1 * midStride));
+      for (int i = tid; i < nItems; i += 256) {
+        const int r = (int)__umulhi((uint32_t)i << 1, gMagic), g = i - r * nG1;
+        const int4 xq = *reinterpret_cast<const int4*>(&sXo[4 * g]);
+        const int4 aq = *reinterpret_cast<const int4*>(&sAl[4 * g]);
+        const int xa[4] = {xq.x, xq.y, xq.z, xq.w}, aa[4] = {aq.x, aq.y, aq.z, aq.w};
+        const int rl = xa[0] - colBase0;
+        uint32_t s1[4];
+        u16x2 w1v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t bj = (uint32_t)(xa[j] - xa[0]);
+          s1[j] = bj | (0x0Cu << 8) | ((bj + 1) << 16) | (0x0Cu << 24);
+          w1v[j] = __builtin_bit_cast(u16x2, (uint32_t)aa[j]);
+        }
+        const int sy = sYo[r] & 0xFFFF, sy1 = sYo[r] >> 16;
+        uint32_t ha[4], hb[4];
+        hsum(&s0[sy][rl >> 2], rl & 3, s1, w1v, ha);
+        hsum(&s0[sy1][rl >> 2], rl & 3, s1, w1v, hb);
+        const uint32_t v = vsum(ha, hb, (uint32_t)sBe[r]);
+        r1[r][g] = v;
+        if (Y0 + r < ownY && X0 + 4 * g < ownX)
+          buf_st32(rm, (uint32_t)((Y0 + r) * midStride + X0 + 4 * g), v);
+      }
+    }
+    __syncthreads();
+    // ---- level l+1 tile from R1
+    if (xs < w2) {
+      const __amdgpu_buffer_rsrc_t rd =
+          make_rsrc(dst + (long long)z * dstImgPitch, (uint32_t)(h2 * dstStride));
+#pragma unroll
+      for (int rr = 0; rr < PYR_TH / 8; ++rr) {
+        const int y = y0 + (PYR_TH / 8) * ty + rr;
+        if (y >= h2) break;
+        uint32_t ha[4], hb[4];
+        hsum(&r1[min(max(yo[rr], 0), h1 - 1) - Y0][k0], sh0, sel, wts, ha);
+        hsum(&r1[min(max(yo[rr] + 1, 0), h1 - 1) - Y0][k0], sh0, sel, wts, hb);
+        buf_st32(rd, (uint32_t)(y * dstStride + xs), vsum(ha, hb, (uint32_t)be[rr]));
+      }
+    }
+  }
+}
+
 // ============================================================ k_fast_band
 // FAST arc strength at the pixel `c` points to (LDS band of biased f16 pixels,
 // row pitch `p` elements): m = max(best dark 9-arc, best bright 9-arc), where
@@ -1344,7 +1528,6 @@ void k_fast_cells(
   wave_lds_sync();  // the next cell's staging overwrites the tile
   }  // cell loop
 }
-
 
 // ================================================================ k_octree
 // ExtractorNode::DivideNode + ORBextractor::DistributeOctTree
@@ -2550,6 +2733,69 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
   else ORB_RESIZE_LAUNCH(false, PYR_SROWS_WIDE, PYR_SW_WIDE);
 #undef ORB_RESIZE_LAUNCH
   return hipGetLastError();
+}
+
+// Levels l and l + 1 in one launch (k_pyr_resize2): src = level l - 1, mid =
+// level l, dst = level l + 1, each with its own tables (l from l - 1, l + 1
+// from l).  The planner has checked every tile against the kernel's windows
+// (orb_k_pyr_resize2_fits).
+hipError_t orb_k_pyr_resize2(const uint8_t* src, long long srcImgPitch, int srcStride, int w0,
+                             int h0, uint8_t* mid, long long midImgPitch, int midStride, int w1,
+                             int h1, const int* xo1, const void* al1, const int* yo1,
+                             const void* be1, uint8_t* dst, long long dstImgPitch, int dstStride,
+                             int w2, int h2, const int* xo2, const void* al2, const int* yo2,
+                             const void* be2, int nimg, hipStream_t s) {
+  const dim3 grid((w2 + PYR_TW - 1) / PYR_TW, (h2 + PYR_TH - 1) / PYR_TH,
+                  (nimg + PYR_IMAGES_PER_WG - 1) / PYR_IMAGES_PER_WG),
+      block(256);
+  const bool aligned = (srcStride & 3) == 0 && (((uintptr_t)src) & 3) == 0 && (srcImgPitch & 3) == 0;
+  if (aligned)
+    hipLaunchKernelGGL(k_pyr_resize2<true>, grid, block, 0, s, src, srcImgPitch, srcStride, w0, h0,
+                       mid, midImgPitch, midStride, w1, h1, xo1, (const int*)al1, yo1,
+                       (const int*)be1, dst, dstImgPitch, dstStride, w2, h2, xo2, (const int*)al2,
+                       yo2, (const int*)be2, nimg);
+  else
+    hipLaunchKernelGGL(k_pyr_resize2<false>, grid, block, 0, s, src, srcImgPitch, srcStride, w0, h0,
+                       mid, midImgPitch, midStride, w1, h1, xo1, (const int*)al1, yo1,
+                       (const int*)be1, dst, dstImgPitch, dstStride, w2, h2, xo2, (const int*)al2,
+                       yo2, (const int*)be2, nimg);
+  return hipGetLastError();
+}
+
+// Whether every tile of the level pair fits k_pyr_resize2's windows: the
+// level-l region (rows, dwords + 2 read-ahead) within PYR2_R1R x PYR2_R1W, the
+// level l-1 window within PYR2_S0R x PYR2_S0W (with each group's read-ahead).
+// Tables as the planner builds them (x: xofs, y: yofs per level).
+int orb_k_pyr_resize2_fits(int w0, int h0, int w1, int h1, const int* xo1, const int* yo1, int w2,
+                           int h2, const int* xo2, const int* yo2) {
+  for (int x0 = 0; x0 < w2; x0 += PYR_TW) {
+    const int xl = std::min(x0 + PYR_TW - 1, w2 - 1), xt = std::min(x0 + PYR_TW - 4, w2 - 1);
+    const int X0 = x0 == 0 ? 0 : (xo2[x0] & ~3);
+    const int ownX = x0 + PYR_TW >= w2 ? w1 : (xo2[x0 + PYR_TW] & ~3);
+    const int X1e = std::max(std::min(xo2[xl] + 1, w1 - 1) + 1, ownX);
+    const int nG1 = (X1e - X0 + 3) >> 2;
+    if (X0 < 0 || ownX < X0 || 4 * nG1 > PYR2_TAB || nG1 > PYR2_R1W) return 0;
+    if (((xo2[xt] - X0) >> 2) + 2 >= PYR2_R1W) return 0;  // level l+1 read-ahead
+    const int c0a = xo1[X0], c0b = std::min(xo1[std::min(X0 + 4 * nG1 - 1, w1 - 1)] + 1, w0 - 1);
+    const int colBase0 = c0a & ~3, nW0 = ((c0b - colBase0) >> 2) + 1;
+    if (4 * ((nW0 + 3) >> 2) > PYR2_S0W) return 0;
+    for (int g = 0; g < nG1; ++g) {
+      const int xa = std::min(X0 + 4 * g, w1 - 1);
+      if (xo1[std::min(xa + 3, w1 - 1)] - xo1[xa] > 6) return 0;  // 8 source bytes per group
+      if (((xo1[xa] - colBase0) >> 2) + 2 >= PYR2_S0W) return 0;
+    }
+  }
+  for (int y0 = 0; y0 < h2; y0 += PYR_TH) {
+    const int yl = std::min(y0 + PYR_TH - 1, h2 - 1);
+    const int Y0 = y0 == 0 ? 0 : std::min(std::max(yo2[y0], 0), h1 - 1);
+    const int ownY = y0 + PYR_TH >= h2 ? h1 : std::min(std::max(yo2[y0 + PYR_TH], 0), h1 - 1);
+    const int Y1e = std::max(std::min(std::max(yo2[yl] + 1, 0), h1 - 1) + 1, ownY);
+    if (ownY < Y0 || Y1e - Y0 > PYR2_R1R) return 0;
+    const int r0a = std::min(std::max(yo1[Y0], 0), h0 - 1);
+    const int r0b = std::min(std::max(yo1[Y1e - 1] + 1, 0), h0 - 1);
+    if (r0b - r0a + 1 > PYR2_S0R) return 0;
+  }
+  return 1;
 }
 
 // Dynamic LDS of k_fast_band for bands of up to `bandElems` elements (rows x

@@ -33,6 +33,7 @@ struct OrbLevelDesc {
   int resizeMode;    // ORB_RESIZE_NARROW / _WIDE / _GENERIC: k_pyr_resize variant for this level
   int tileBeg;       // first blur tile of this level
   int cellMaxRows, cellMaxCols;  // largest cell ROI of this level (k_fast_cells LDS per launch)
+  int resize2;       // 1: levels l and l + 1 are built by one k_pyr_resize2 launch (from l - 1)
 };
 
 #define ORB_RESIZE_NARROW 0   // 44 x 44-dword source windows (downscale <= 1.25)

@@ -32,6 +32,15 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
 size_t orb_k_fast_band_lds(int bandElems);
 size_t orb_k_fast_cells_lds(int maxRows, int maxCols);
 bool orb_k_fast_cells_fits(const OrbPlanDesc* plan);
+
+hipError_t orb_k_pyr_resize2(const uint8_t* src, long long srcImgPitch, int srcStride, int w0,
+                             int h0, uint8_t* mid, long long midImgPitch, int midStride, int w1,
+                             int h1, const int* xo1, const void* al1, const int* yo1,
+                             const void* be1, uint8_t* dst, long long dstImgPitch, int dstStride,
+                             int w2, int h2, const int* xo2, const void* al2, const int* yo2,
+                             const void* be2, int nimg, hipStream_t s);
+int orb_k_pyr_resize2_fits(int w0, int h0, int w1, int h1, const int* xo1, const int* yo1, int w2,
+                           int h2, const int* xo2, const int* yo2);
 hipError_t orb_k_fast_cells(const uint8_t* img0, long long img0Pitch, int img0Stride,
                             const uint8_t* arena, long long arenaPitch, const OrbPlanDesc* plan,
                             const OrbCellDesc* cells, uint32_t* cellKeys, int32_t* cellCount,
@@ -485,6 +494,9 @@ static void compute_tables(orb_extractor* h) {
 
 // Build the plan for a W x H input (level sizes, resize tables, FAST cells,
 // octree roots, output slots) and upload its tables.
+#ifndef PYR_FUSE2
+#define PYR_FUSE2 1  // level pairs in one k_pyr_resize2 launch where they fit (0: one launch per level)
+#endif
 static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (h->planW == W && h->planH == H) return ORB_OK;
   const int L = h->nlevels;
@@ -676,6 +688,24 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
                                                   : ORB_RESIZE_GENERIC;
     }
   }
+  // Pairs of levels built by one launch (k_pyr_resize2: level l + 1 from a
+  // level-l region the workgroup computes in LDS from level l - 1): greedily
+  // from level 1, where both levels take the narrow tiles and every tile of
+  // the pair fits the kernel's windows (every ORB-SLAM2 configuration: 1+2,
+  // 3+4, 5+6, then 7 alone); other levels keep one launch each
+  int nResize = 0;
+  for (int l = 1; l < L;) {
+    OrbLevelDesc& d = P.lv[l];
+    d.resize2 = 0;
+    if (PYR_FUSE2 && l + 1 < L && d.resizeMode == ORB_RESIZE_NARROW &&
+        P.lv[l + 1].resizeMode == ORB_RESIZE_NARROW) {
+      const OrbLevelDesc& e = P.lv[l + 1];
+      d.resize2 = orb_k_pyr_resize2_fits(P.lv[l - 1].w, P.lv[l - 1].h, d.w, d.h, &rtab[d.rtabX],
+                                         &rtab[d.rtabY], e.w, e.h, &rtab[e.rtabX], &rtab[e.rtabY]);
+    }
+    l += d.resize2 ? 2 : 1;
+    ++nResize;
+  }
   // k_fast_band: one band = at least one cell; its pixels and scores + the
   // candidate queue must fit the 64 KiB a workgroup may allocate
   if (orb_k_fast_band_lds(maxBandBytes) > 64 * 1024) return ORB_EINVAL;
@@ -733,6 +763,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   h->octNodeBytes = octGlobal ? (long long)((nodeBytes + 255) & ~(size_t)255) : 0;
   h->planW = W;
   h->planH = H;
+  h->prof.launchesPerCall[0] = nResize;
   h->batchCap = 0;  // scratch layout depends on the plan
   return ORB_OK;
 }
@@ -818,6 +849,12 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   // single stream give the lower latency)
   const bool useBands = B < FAST_CELLS_MIN_BATCH || !orb_k_fast_cells_fits(&P);
   pf.names[2] = useBands ? "k_fast_band" : "k_fast_cells";
+  // k_fast_cells over the cells [cb, ce) (whole levels) on stream st
+  auto fast = [&](int cb, int ce, hipStream_t st) -> hipError_t {
+    return orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
+                            h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
+                            h->dCellCount.as<int32_t>(), h->dErr.as<int32_t>(), cb, ce, B, st);
+  };
   // Level 0 is the caller's image: its FAST cells need no pyramid, so they run
   // on the side stream beside the latency-bound resize chain (fork / join by
   // events, graph-capturable).  Levels 1..sideLevels follow on the side stream
@@ -831,14 +868,11 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   const bool l0Side = !useBands && !FAST_L0_INLINE && !(ev && pf.serial) && l0End > 0 && P.nlevels > 1;
   const int sideLevels = l0Side ? std::min(FAST_SIDE_LEVELS, P.nlevels - 1) : 0;
   const int sideEnd = sideLevels > 0 ? P.lv[sideLevels].cellEnd : l0End;
-  int32_t* fastErr = h->dErr.as<int32_t>();
   if (l0Side) {
     HIP_TRY(hipEventRecord(h->evL0Fork, s));
     HIP_TRY(hipStreamWaitEvent(side, h->evL0Fork, 0));
     PROF_REC(ev, pf.b(ev, 5), side);
-    HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                             h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), fastErr, 0, l0End, B, side));
+    HIP_TRY(fast(0, l0End, side));
     PROF_REC(ev, pf.e(ev, 5), side);
     if (sideLevels == 0) HIP_TRY(hipEventRecord(h->evL0Join, side));
   } else if (ev) {
@@ -854,17 +888,26 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
     const uint8_t* src = l == 1 ? d_images : arena + sd.arenaOff;
     const long long srcPitch = l == 1 ? (long long)imgPitch : ap;
     const int srcStride = l == 1 ? (int)stride : sd.pitch;
-    HIP_TRY(orb_k_pyr_resize(src, srcPitch, srcStride, sd.w, sd.h, arena + d.arenaOff, ap, d.pitch, d.w,
-                             d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
-                             rt + d.rtabY + d.h, d.resizeMode, B, s));
-    if (l == sideLevels) {
+    const int top = d.resize2 ? l + 1 : l;  // last level this launch writes
+    if (d.resize2) {
+      const OrbLevelDesc& e = P.lv[l + 1];
+      HIP_TRY(orb_k_pyr_resize2(src, srcPitch, srcStride, sd.w, sd.h, arena + d.arenaOff, ap, d.pitch,
+                                d.w, d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
+                                rt + d.rtabY + d.h, arena + e.arenaOff, ap, e.pitch, e.w, e.h,
+                                rt + e.rtabX, rt + e.rtabX + e.w, rt + e.rtabY, rt + e.rtabY + e.h,
+                                B, s));
+    } else {
+      HIP_TRY(orb_k_pyr_resize(src, srcPitch, srcStride, sd.w, sd.h, arena + d.arenaOff, ap, d.pitch,
+                               d.w, d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
+                               rt + d.rtabY + d.h, d.resizeMode, B, s));
+    }
+    l = top;
+    if (l >= sideLevels && l - (d.resize2 ? 1 : 0) <= sideLevels) {  // this launch wrote level sideLevels
       if (sideEnd > l0End) {
         HIP_TRY(hipEventRecord(h->evLvl, s));
         HIP_TRY(hipStreamWaitEvent(side, h->evLvl, 0));
         PROF_REC(ev, pf.b(ev, 5, 1), side);
-        HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                                 h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                                 h->dCellCount.as<int32_t>(), fastErr, l0End, sideEnd, B, side));
+        HIP_TRY(fast(l0End, sideEnd, side));
         PROF_REC(ev, pf.e(ev, 5, 1), side);
         if (ev) pf.segments(5, 2);
       }
@@ -879,10 +922,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                             h->dCellKeys.as<uint32_t>(), h->dCellCount.as<int32_t>(),
                             h->dErr.as<int32_t>(), B, s));
   else
-    HIP_TRY(orb_k_fast_cells(d_images, (long long)imgPitch, (int)stride, arena, ap, &P,
-                             h->dCells.as<OrbCellDesc>(), h->dCellKeys.as<uint32_t>(),
-                             h->dCellCount.as<int32_t>(), fastErr, l0Side ? sideEnd : 0, P.ncells,
-                             B, s));
+    HIP_TRY(fast(l0Side ? sideEnd : 0, P.ncells, s));
   PROF_REC(ev, pf.e(ev, 2), s);
   // (level 0's octree on the side stream as well measured no gain: the octree's
   // time is its per-workgroup pass latency, not level 0's size)

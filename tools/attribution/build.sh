@@ -10,6 +10,8 @@
 #   DESC_STUB=1..5    k_orient_desc phase stubs (results wrong)
 #   DESC_GLDS, DESC_LDS_PAD, DESC_DBUF, DESC_MFMA_ROWS, DESC_PK_ROT,
 #   FC_LDS_PAD_TILES  measured-slower k_orient_desc / k_fast_cells variants
+# PATCHES=fast_runs.patch instead restores k_fast_runs (round 6: FAST over runs
+# of ORB_FAST_RUN_CELLS cells per wave; measured slower).
 # Select the build with ORB_AMD_LIB=<path>.  variants.patch is the diff from
 # the product file to the round-5 source that held these blocks inline
 # (regenerate: tools/unifdef.py resolves them, see its docstring).
@@ -23,6 +25,8 @@ mkdir -p "$W/pkg"
 cp -r "$PKG/csrc" "$W/pkg/csrc"
 cp "$PKG/Makefile" "$W/pkg/Makefile"
 ln -s "$R/include" "$W/include"
-patch -s -d "$W/pkg" -p1 < "$R/tools/attribution/variants.patch"
+for p in ${PATCHES:-variants.patch}; do  # e.g. PATCHES=fast_runs.patch
+  patch -s -d "$W/pkg" -p1 < "$R/tools/attribution/$p"
+done
 make -s -j8 -C "$W/pkg" BUILD=build LIBOUT="$PKG/lib/variants/$NAME.so" EXTRA_HIPFLAGS="$FLAGS"
 echo "$PKG/lib/variants/$NAME.so"
