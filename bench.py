@@ -899,6 +899,10 @@ def main():
                     help="extraction lanes: extractor handles on streams of their own, "
                          "taking launches round-robin (1 / 2 / 3 / 4 lanes: 307k / 315k / "
                          "305k / 296k frames/s, profiles/r03_lanes.txt)")
+    ap.add_argument("--match-streams", type=int,
+                    default=int(os.environ.get("ORB_BENCH_MATCH_STREAMS", "1")),
+                    help="match streams (each with a matcher handle of its own) taking the "
+                         "launches' SearchByProjection round-robin")
     ap.add_argument("--lane-match", default=os.environ.get("ORB_BENCH_LANE_MATCH", "stream"),
                     choices=["stream", "inlane"],
                     help="matcher on one match stream, or on each lane's own stream after "
@@ -947,12 +951,14 @@ def main():
     ext_streams = [new_stream(torch, dev, "extract" if i == 0 else f"extract{i}") for i in range(L)]
     ext_stream = ext_streams[0]
     match_stream = new_stream(torch, dev, "match")
+    MSN = max(1, args.match_streams)
     # every stream the run uses, created up front in one order (HIP maps a new
     # stream onto the least-used HSA queue of its priority, so the mapping
     # depends on creation order; profiles/r05_secsets.txt)
     for key in ("match1", "h2d", "d2h"):
         new_stream(torch, dev, key)
     exts = [ext] + [orb.ORBextractor(NF, 1.2, 8, 20, 7, device=local) for _ in range(L - 1)]
+    match_streams = [match_stream] + [new_stream(torch, dev, f"match{i}") for i in range(1, MSN)]
     torch.cuda.set_stream(ext_stream)
     d_img = torch.from_numpy(imgs).to(dev)
     NS = 2 * L  # buffer sets: launch g writes set g % NS
@@ -1002,15 +1008,16 @@ def main():
     del mpd_all, lock_all
     matcher = orb.ORBmatcher(0.8, device=local)
     inlane = args.lane_match == "inlane"
-    matchers = [matcher] + [orb.ORBmatcher(0.8, device=local) for _ in range(L - 1 if inlane else 0)]
+    matchers = [matcher] + [orb.ORBmatcher(0.8, device=local)
+                            for _ in range(L - 1 if inlane else MSN - 1)]
     torch.cuda.synchronize()
 
     def launch(g):
         j, b, ln = g % NS, g % NB, g % L
         st = sets[j]
         es = ext_streams[ln]
-        ms = es if inlane else match_stream
-        mt = matchers[ln] if inlane else matcher
+        ms = es if inlane else match_streams[g % MSN]
+        mt = matchers[ln] if inlane else matchers[g % MSN]
         cnt = step_counts[(g // NB) % 2][b * B:(b + 1) * B]
         st["cnt"] = cnt
         if g >= NS and args.bounded:
@@ -1036,6 +1043,8 @@ def main():
             # every lane's launches of the step are done before the gather
             for o in range(1, L if inlane else 1):
                 matched[(j - o) % NS].record(ext_streams[(ln - o) % L])
+                ms.wait_event(matched[(j - o) % NS])
+            for o in range(1, 1 if inlane else MSN):  # the other match streams' last launches
                 ms.wait_event(matched[(j - o) % NS])
             with torch.cuda.stream(ms):
                 gather_counts(dist, step_counts[k], gathered[k])
@@ -1247,7 +1256,9 @@ def main():
             "distinct_frames_per_gpu": D,
             "frames_per_launch": B,
             "extraction_lanes": f"{L} extractor handle(s) on {L} stream(s), launches "
-                                "round-robin; SearchByProjection on one match stream",
+                                "round-robin; SearchByProjection on " +
+                                ("one match stream" if MSN == 1 else
+                                 f"{MSN} match streams (a matcher handle each), launches round-robin"),
             "timed_region_s": elapsed,
             "inputs": "frames resident in HBM before the timed region (device-resident rate; "
                       "the PCIe-inclusive drop-in rate is `host_input`)",

@@ -177,6 +177,20 @@ def lib() -> ctypes.CDLL:
     return L
 
 
+_HIP_RT = None
+
+
+def _hip_runtime() -> ctypes.CDLL:
+    """The HIP runtime this process already uses: liborb_amd.so's dependency,
+    looked up by its SONAME, so the loaded copy (torch's, when torch came
+    first) is returned rather than a second runtime."""
+    global _HIP_RT
+    if _HIP_RT is None:
+        lib()
+        _HIP_RT = ctypes.CDLL("libamdhip64.so.7")
+    return _HIP_RT
+
+
 def _check(status: int, what: str) -> int:
     if status not in (ORB_OK,):
         raise OrbError(status, what)
@@ -351,6 +365,22 @@ class ORBextractor:
 
     def stream(self) -> int:
         return lib().orb_extractor_stream(self._h) or 0
+
+    def batch_level(self, image: int, level: int) -> np.ndarray:
+        """Host copy of pyramid level `level` of batch image `image` after
+        extract_batch (orb_extractor_batch_level's device view, copied with the
+        process's HIP runtime; call after the batch's stream is synchronised)."""
+        p, w, h, st = ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
+        _check(lib().orb_extractor_batch_level(self._h, image, level, ctypes.byref(p), ctypes.byref(w),
+                                               ctypes.byref(h), ctypes.byref(st)),
+               "orb_extractor_batch_level")
+        out = np.zeros((h.value, w.value), np.uint8)
+        hip = _hip_runtime()
+        rc = hip.hipMemcpy2D(ctypes.c_void_p(out.ctypes.data), ctypes.c_size_t(w.value), p, st,
+                             ctypes.c_size_t(w.value), ctypes.c_size_t(h.value), ctypes.c_int(2))
+        if rc != 0:
+            raise OrbError(ORB_EDEVICE, f"hipMemcpy2D -> {rc}")
+        return out
 
     def profile(self, enable: bool = True):
         _check(lib().orb_extractor_profile(self._h, int(enable)), "profile")

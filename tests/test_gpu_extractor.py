@@ -62,6 +62,45 @@ def test_pyramid_bit_exact(gpu, oracle, w, h):
         assert np.array_equal(a, b), f"level {l}: {(a != b).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("w,h,sf,nl,launches", [
+    (1241, 376, 1.2, 8, 4),    # pairs 1+2, 3+4, 5+6, then 7: k_pyr_resize2 x 3 + k_pyr_resize
+    (640, 480, 1.2, 9, 4),     # 1+2, 3+4, 5+6, 7+8
+    (1920, 1080, 1.1, 12, 6),  # narrow downscales, 11 levels in 6 launches
+    (1241, 376, 1.5, 8, 7),    # wide tiles (downscale > 1.25): one launch per level
+    (997, 613, 1.2, 7, 3),     # odd sizes: 1+2, 3+4, 5+6
+    (1003, 333, 1.22, 8, 4),   # odd sizes, a non-ORB-SLAM2 scale factor
+    (997, 613, 1.25, 6, 5)])   # downscales just past 1.25 (levels 1-4 wide, one launch each), 5
+def test_pyramid_level_pairs_batch(gpu, oracle, w, h, sf, nl, launches):
+    """The batch path's pyramid through the paired-level resize (k_pyr_resize2:
+    level l + 1 from a level-l region the workgroup builds in LDS, each level-l
+    pixel stored by exactly one workgroup; src/ORBextractor.cc:1172-1207) is
+    bit-identical to the oracle's level-by-level resize, for every image of a
+    batch; the stage's launch count pins which levels were paired."""
+    torch = pytest.importorskip("torch")
+    B = 5
+    imgs = np.stack([gpu.synth_image(21, f, w, h) for f in range(B)])
+    ext = gpu.ORBextractor(1000, sf, nl, 20, 7)
+    cap = ext.capacity(w, h)
+    d_img = torch.from_numpy(imgs).cuda()
+    d_k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    d_d = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ext.profile(True)
+    ext.extract_batch(d_img.data_ptr(), B, w, h, w, w * h, d_k.data_ptr(), d_d.data_ptr(), cap,
+                      d_n.data_ptr())
+    torch.cuda.synchronize()
+    name, _, n = ext.profile_read(0)
+    ext.profile(False)
+    assert name == "k_pyr_resize" and n == launches, (name, n)
+    for i in (0, B - 1):
+        ref = oracle.pyramid(imgs[i], sf, nl)
+        for l in range(1, nl):
+            got = ext.batch_level(i, l)
+            assert got.shape == ref[l].shape, (i, l)
+            assert np.array_equal(got, ref[l]), f"image {i} level {l}: {(got != ref[l]).sum()} px differ"
+
+
 @pytest.mark.parametrize("w,h", [(640, 480), (1241, 376), (1920, 1080), (403, 301)])
 def test_blurred_levels_bit_exact(gpu, oracle, w, h):
     """GaussianBlur(7x7, sigma 2, REFLECT_101) of every level (src/ORBextractor.cc:1143-1145)."""
