@@ -327,6 +327,32 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* fra
                                         float th, float nnratio, int32_t* kp_match,
                                         int32_t* nmatches);
 
+/* Zero-copy form of orb_match_projection_local, for a caller that flattens its
+ * Frame and MapPoints anyway (the reference-typed drop-in's SearchByProjection,
+ * integration/ORBmatcher.cc): _stage returns pointers into the handle's pinned
+ * input block laid out for n_keys keypoints and n_mp map points, the caller
+ * writes keys, descriptors, the map-point tracks and descriptors there (and
+ * u_right / kp_locked when it passes stereo / locked), and _staged runs the
+ * match on them: one DMA in, no library-side copy.  `frame` supplies n (==
+ * n_keys), the bounds, levels and scale factors; its keys / descriptors /
+ * u_right pointers are not read.  The pointers are valid until the next call
+ * on this handle; the pair must not interleave with other calls on it (one
+ * handle per thread, as the reference's per-call-site ORBmatcher objects). */
+typedef struct orb_local_stage {
+  orb_keypoint_t* keys;        /* n_keys */
+  uint8_t* descriptors;        /* n_keys x 32 */
+  float* u_right;              /* n_keys (read only with stereo != 0) */
+  uint8_t* kp_locked;          /* n_keys (read only with locked != 0) */
+  orb_mp_track_t* mps;         /* n_mp */
+  uint8_t* mp_desc;            /* n_mp x 32 */
+} orb_local_stage_t;
+orb_status_t orb_match_projection_local_stage(orb_matcher_t* m, int n_keys, int n_mp,
+                                              orb_local_stage_t* out);
+orb_status_t orb_match_projection_local_staged(orb_matcher_t* m, const orb_frame_t* frame,
+                                               int n_mp, int stereo, int locked, float th,
+                                               float nnratio, int32_t* kp_match,
+                                               int32_t* nmatches);
+
 /* Device-batched form: P independent (frame, local map) problems.
  * Problem p: keypoints d_keys + p*kp_stride (count d_nkeys[p]), descriptors
  * d_desc + p*kp_stride*32, locks d_locked + p*kp_stride (may be NULL),

@@ -185,11 +185,21 @@ ORBmatcher::ORBmatcher(float nnratio, bool checkOri) : mfNNratio(nnratio), mbChe
 // src/ORBmatcher.cc:47-133 (Tracking::SearchLocalPoints after the isInFrustum pass)
 int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, const float th) {
   const int N = F.N, M = (int)vpMapPoints.size();
-  vector<orb_mp_track_t> trk(M);
-  vector<uint8_t> mpDesc((size_t)M * 32);
+  if (N == 0) return 0;
+  // the frame and every map point flattened straight into the handle's pinned
+  // input block (orb_match_projection_local_stage: one DMA in, no library-side
+  // copy, no per-call heap buffers)
+  orb_local_stage_t S;
+  check(orb_match_projection_local_stage(gpu(), N, M, &S), "SearchByProjection(F, vpMapPoints) stage");
+  memcpy(S.keys, F.mvKeysUn.data(), (size_t)N * sizeof(orb_keypoint_t));
+  memcpy(S.descriptors, F.mDescriptors.ptr<uint8_t>(), (size_t)N * 32);
+  const bool stereo = !F.mvuRight.empty();
+  if (stereo) memcpy(S.u_right, F.mvuRight.data(), (size_t)N * 4);
+  for (int i = 0; i < N; ++i)  // a claim by a point with observations locks the keypoint (:90-93)
+    S.kp_locked[i] = F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0;
   for (int i = 0; i < M; ++i) {
     MapPoint* p = vpMapPoints[i];
-    orb_mp_track_t& t = trk[i];
+    orb_mp_track_t& t = S.mps[i];
     t.proj_x = p->mTrackProjX;
     t.proj_y = p->mTrackProjY;
     t.proj_xr = p->mTrackProjXR;
@@ -197,17 +207,17 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
     t.level = p->mnTrackScaleLevel;
     t.in_view = p->mbTrackInView ? 1 : 0;
     t.bad = p->isBad() ? 1 : 0;
-    t.has_obs = p->Observations() > 0 ? 1 : 0;  // a claim by it locks the keypoint (:90-93)
+    t.has_obs = p->Observations() > 0 ? 1 : 0;
     t._pad = 0;
-    if (t.in_view && !t.bad) copy_descriptor(p, &mpDesc[(size_t)i * 32]);
+    // (a point skipped by :57-61 is never read: its descriptor is not copied)
+    if (t.in_view && !t.bad) copy_descriptor(p, S.mp_desc + (size_t)i * 32);
   }
-  vector<uint8_t> locked(N);
-  for (int i = 0; i < N; ++i) locked[i] = F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0;
   const orb_frame_t f = frame_view(F);
-  vector<int32_t> kpMatch(N);
+  thread_local vector<int32_t> kpMatch;
+  kpMatch.resize(N);
   int32_t nmatches = 0;
-  check(orb_match_projection_local(gpu(), &f, locked.data(), M, trk.data(), mpDesc.data(), th,
-                                   mfNNratio, kpMatch.data(), &nmatches),
+  check(orb_match_projection_local_staged(gpu(), &f, M, stereo ? 1 : 0, 1, th, mfNNratio,
+                                          kpMatch.data(), &nmatches),
         "SearchByProjection(F, vpMapPoints)");
   for (int i = 0; i < N; ++i)
     if (kpMatch[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[kpMatch[i]];  // :127

@@ -110,6 +110,8 @@ def lib() -> ctypes.CDLL:
         "orb_extractor_host_pyramid_off": (i32, [vp]),
         "orb_extractor_extract_batch": (i32, [vp, vp, i32, i32, i32, sz, sz, vp, vp, i32, vp, vp]),
         "orb_extractor_batch_level": (i32, [vp, i32, i32, vp, vp, vp, vp]),
+        "orb_match_projection_local_stage": (i32, [vp, i32, i32, vp]),
+        "orb_match_projection_local_staged": (i32, [vp, vp, i32, i32, i32, f32, f32, vp, vp]),
         "orb_extractor_stream": (vp, [vp]),
         "orb_extractor_profile": (i32, [vp, i32]),
         "orb_extractor_profile_read": (i32, [vp, i32, vp, vp, vp]),
@@ -420,6 +422,12 @@ class Frame:
         return f
 
 
+class _LocalStage(ctypes.Structure):  # orb_local_stage_t
+    _fields_ = [("keys", ctypes.c_void_p), ("descriptors", ctypes.c_void_p),
+                ("u_right", ctypes.c_void_p), ("kp_locked", ctypes.c_void_p),
+                ("mps", ctypes.c_void_p), ("mp_desc", ctypes.c_void_p)]
+
+
 class _StereoInput(ctypes.Structure):
     _fields_ = [
         ("left", ctypes.c_void_p), ("n_right", ctypes.c_int32), ("right_keys", ctypes.c_void_p),
@@ -530,6 +538,41 @@ class ORBmatcher:
             self._h, ctypes.byref(f), _ptr(locked) if locked is not None else None, len(mps),
             _ptr(mps) if len(mps) else None, _ptr(mp_desc) if len(mps) else None, th,
             self.mfNNratio, _ptr(kp_match), ctypes.byref(nm)), "SearchByProjection")
+        return nm.value, kp_match
+
+    def SearchByProjectionStaged(self, F: Frame, mps: np.ndarray, mp_desc: np.ndarray, th: float,
+                                 kp_locked: np.ndarray | None = None):
+        """SearchByProjection through the zero-copy pair
+        orb_match_projection_local_stage / _staged: the inputs are written
+        straight into the handle's pinned block (as the C++ drop-in does)."""
+        mps = np.ascontiguousarray(mps, MP_TRACK_DTYPE)
+        mp_desc = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        n, M = F.N, len(mps)
+        if n == 0:
+            return 0, np.zeros(0, np.int32)
+        st = _LocalStage()
+        _check(lib().orb_match_projection_local_stage(self._h, n, M, ctypes.byref(st)), "stage")
+
+        def view(ptr, dtype, count):
+            nbytes = count * np.dtype(dtype).itemsize
+            buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(ptr)
+            return np.frombuffer(buf, np.uint8, nbytes).view(dtype)
+        view(st.keys, KEYPOINT_DTYPE, n)[:] = F.mvKeysUn
+        view(st.descriptors, np.uint8, n * 32)[:] = F.mDescriptors.reshape(-1)
+        stereo = F.mvuRight is not None
+        if stereo:
+            view(st.u_right, np.float32, n)[:] = F.mvuRight
+        if kp_locked is not None:
+            view(st.kp_locked, np.uint8, n)[:] = kp_locked
+        if M:
+            view(st.mps, MP_TRACK_DTYPE, M)[:] = mps
+            view(st.mp_desc, np.uint8, M * 32)[:] = mp_desc.reshape(-1)
+        kp_match = np.full(n, -1, np.int32)
+        nm = ctypes.c_int32(0)
+        f = F._c()
+        _check(lib().orb_match_projection_local_staged(
+            self._h, ctypes.byref(f), M, int(stereo), int(kp_locked is not None), th, self.mfNNratio,
+            _ptr(kp_match), ctypes.byref(nm)), "SearchByProjectionStaged")
         return nm.value, kp_match
 
 

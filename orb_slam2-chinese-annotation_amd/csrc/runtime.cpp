@@ -1538,6 +1538,7 @@ struct orb_matcher {
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
   DevBuf dJac;  // Jacobi-resolve scratch (ORB_RESOLVE_JACOBI)
+  int stagedN = -1, stagedM = -1;  // orb_match_projection_local_stage's layout
   int resolveSchedule = ORB_RESOLVE_AUTO;  // orb_matcher_set_resolve
   int jacobiRounds = 6;
   // stereo / frame / BoW scratch
@@ -1762,21 +1763,48 @@ orb_status_t orb_matcher_profile_read(orb_matcher_t* m, int stage, double* total
   return ORB_OK;
 }
 
-orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
-                                        const uint8_t* kp_locked, int n_mp,
-                                        const orb_mp_track_t* mps, const uint8_t* mp_desc,
-                                        float th, float nnratio, int32_t* kp_match,
-                                        int32_t* nmatches) {
-  if (!m || !F || n_mp < 0 || (n_mp > 0 && (!mps || !mp_desc)) || !kp_match || !nmatches)
-    return ORB_EINVAL;
-  if (F->n < 0 || (F->n > 0 && (!F->keys || !F->descriptors)) || !F->scale_factors ||
-      F->n_levels <= 0 || F->n_levels > ORB_MAX_LEVELS || F->n >= (1 << 19))
-    return ORB_EINVAL;
-  *nmatches = 0;
-  if (F->n == 0) return ORB_OK;
-  std::lock_guard<std::mutex> g(m->mu);
+}  // extern "C"
+
+// orb_match_projection_local's inputs, one pinned block and one DMA in (six
+// pageable copies each staged by the runtime cost more than the kernels):
+// [nk, nm | keys | descriptors | uR | locked | tracks | map-point descriptors],
+// 16-B aligned
+struct LocalLayout {
+  size_t oKeys, oDesc, oUr, oLk, oMps, oMpd, inBytes;
+};
+static LocalLayout local_layout(int N, int M) {
+  auto al16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  LocalLayout L;
+  L.oKeys = 16;
+  L.oDesc = al16(L.oKeys + (size_t)N * sizeof(orb_keypoint_t));
+  L.oUr = al16(L.oDesc + (size_t)N * 32);
+  L.oLk = al16(L.oUr + (size_t)N * 4);
+  L.oMps = al16(L.oLk + (size_t)N);
+  L.oMpd = al16(L.oMps + (size_t)M * sizeof(orb_mp_track_t));
+  L.inBytes = al16(L.oMpd + (size_t)M * 32);
+  return L;
+}
+
+// The pinned input block for N keypoints and M map points (header written);
+// caller holds m->mu
+static orb_status_t local_stage(orb_matcher_t* m, int N, int M, LocalLayout* out) {
+  const LocalLayout L = local_layout(N, M);
+  orb_status_t st;
+  if ((st = m->hIn.ensure(L.inBytes))) return st;
+  const int32_t nk = N, nm = M;
+  memcpy(m->hIn.as<uint8_t>(), &nk, 4);
+  memcpy(m->hIn.as<uint8_t>() + 4, &nm, 4);
+  *out = L;
+  return ORB_OK;
+}
+
+// SearchByProjection(F, vpMapPoints) on the inputs staged in the pinned block:
+// one DMA in, grid + candidates + resolve, one DMA out; caller holds m->mu
+static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t* F, bool urOn,
+                              bool lkOn, float th, float nnratio, int32_t* kp_match,
+                              int32_t* nmatches) {
   hipSetDevice(m->device);
-  const int N = F->n, M = n_mp;
+  const LocalLayout L = local_layout(N, M);
   orb_status_t st;
   // (inputs live in dIn below; only the outputs and the matcher scratch here)
   if ((st = m->dKpMatch.ensure((size_t)N * 4 + 16))) return st;  // + the count (one D2H)
@@ -1784,67 +1812,39 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   if ((st = m->dCellIdx.ensure((size_t)N * 4))) return st;
   if ((st = m->dTopk.ensure((size_t)std::max(M, 1) * 16))) return st;
   if ((st = m->dNcand.ensure((size_t)std::max(M, 1) * 4))) return st;
-  hipStream_t s = m->stream;
-  CallOrder order(m->evLast, &m->lastStream, s);
-  if (order.status) return order.status;
-  // every input in one pinned block, one DMA in (six pageable copies each
-  // staged by the runtime cost more than the kernels): [nk, nm | keys |
-  // descriptors | uR | locked | tracks | map-point descriptors], 16-B aligned
-  auto al16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
-  const size_t oKeys = 16, oDesc = al16(oKeys + (size_t)N * sizeof(orb_keypoint_t));
-  const size_t oUr = al16(oDesc + (size_t)N * 32), oLk = al16(oUr + (size_t)N * 4);
-  const size_t oMps = al16(oLk + (size_t)N), oMpd = al16(oMps + (size_t)M * sizeof(orb_mp_track_t));
-  const size_t inBytes = al16(oMpd + (size_t)M * 32);
-  if ((st = m->hIn.ensure(inBytes))) return st;
-  if ((st = m->dIn.ensure(inBytes))) return st;
+  if ((st = m->dIn.ensure(L.inBytes))) return st;
   if ((st = m->hOutM.ensure((size_t)N * 4 + 16))) return st;
-  uint8_t* hin = m->hIn.as<uint8_t>();
-  const int32_t nk = N, nm = M;
-  memcpy(hin, &nk, 4);
-  memcpy(hin + 4, &nm, 4);
-  memcpy(hin + oKeys, F->keys, (size_t)N * sizeof(orb_keypoint_t));
-  memcpy(hin + oDesc, F->descriptors, (size_t)N * 32);
-  if (F->u_right) memcpy(hin + oUr, F->u_right, (size_t)N * 4);
-  if (kp_locked) memcpy(hin + oLk, kp_locked, (size_t)N);
-  if (M > 0) {
-    memcpy(hin + oMps, mps, (size_t)M * sizeof(orb_mp_track_t));
-    memcpy(hin + oMpd, mp_desc, (size_t)M * 32);
-  }
-  HIP_TRY(hipMemcpyAsync(m->dIn.p, hin, inBytes, hipMemcpyHostToDevice, s));
-  uint8_t* din = m->dIn.as<uint8_t>();
-  const orb_keypoint_t* dKeys = reinterpret_cast<const orb_keypoint_t*>(din + oKeys);
-  const uint8_t* dDesc = din + oDesc;
-  const int32_t* dNK = reinterpret_cast<const int32_t*>(din);
-  const int32_t* dNM = reinterpret_cast<const int32_t*>(din + 4);
-  const orb_mp_track_t* dMps = reinterpret_cast<const orb_mp_track_t*>(din + oMps);
-  const uint8_t* dMpd = din + oMpd;
-  const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
-                                       F->scale_factors, th, nnratio);
-  const float* ur = F->u_right ? reinterpret_cast<const float*>(din + oUr) : nullptr;
-  const uint8_t* lk = kp_locked ? din + oLk : nullptr;
   const bool stage = N <= orb_k_grid_stage_max();
   if (stage && (st = m->dProjStage.ensure((size_t)N * 16))) return st;
   const size_t jb = orb_k_proj_jacobi_bytes(N, std::max(M, 1), 1, m->resolveSchedule);
   if (jb && (st = m->dJac.ensure(jb))) return st;
+  hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
+  HIP_TRY(hipMemcpyAsync(m->dIn.p, m->hIn.p, L.inBytes, hipMemcpyHostToDevice, s));
+  uint8_t* din = m->dIn.as<uint8_t>();
+  const orb_keypoint_t* dKeys = reinterpret_cast<const orb_keypoint_t*>(din + L.oKeys);
+  const uint8_t* dDesc = din + L.oDesc;
+  const int32_t* dNK = reinterpret_cast<const int32_t*>(din);
+  const int32_t* dNM = reinterpret_cast<const int32_t*>(din + 4);
+  const orb_mp_track_t* dMps = reinterpret_cast<const orb_mp_track_t*>(din + L.oMps);
+  const uint8_t* dMpd = din + L.oMpd;
+  const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
+                                       F->scale_factors, th, nnratio);
+  const float* ur = urOn ? reinterpret_cast<const float*>(din + L.oUr) : nullptr;
+  const uint8_t* lk = lkOn ? din + L.oLk : nullptr;
   if (stage)
-    HIP_TRY(orb_k_grid_build_staged(dKeys, dNK, lk, ur,
-                                    N, P.minX, P.minY, P.invW, P.invH,
+    HIP_TRY(orb_k_grid_build_staged(dKeys, dNK, lk, ur, N, P.minX, P.minY, P.invW, P.invH,
                                     m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
                                     m->dProjStage.p, 1, s));
   else
-    HIP_TRY(orb_k_grid_build(dKeys, dNK, N, P.minX,
-                             P.minY, P.invW, P.invH, m->dCellStart.as<int32_t>(),
-                             m->dCellIdx.as<int32_t>(), 1, s));
-  HIP_TRY(orb_k_proj_candidates(dKeys, dDesc, ur, lk, N,
-                                dNK,
-                                dMps, dMpd,
-                                dNM, std::max(M, 1), M,
+    HIP_TRY(orb_k_grid_build(dKeys, dNK, N, P.minX, P.minY, P.invW, P.invH,
+                             m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), 1, s));
+  HIP_TRY(orb_k_proj_candidates(dKeys, dDesc, ur, lk, N, dNK, dMps, dMpd, dNM, std::max(M, 1), M,
                                 m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
-                                stage ? m->dProjStage.p : nullptr, &P,
-                                m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(), 1, s));
-  HIP_TRY(orb_k_proj_resolve(dKeys, dDesc, ur, lk,
-                             dNK, N, dMps,
-                             dMpd, dNM, std::max(M, 1),
+                                stage ? m->dProjStage.p : nullptr, &P, m->dTopk.as<uint32_t>(),
+                                m->dNcand.as<int32_t>(), 1, s));
+  HIP_TRY(orb_k_proj_resolve(dKeys, dDesc, ur, lk, dNK, N, dMps, dMpd, dNM, std::max(M, 1),
                              m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), &P,
                              m->dTopk.as<uint32_t>(), m->dNcand.as<int32_t>(),
                              m->dKpMatch.as<int32_t>(), m->dKpMatch.as<int32_t>() + N, 1,
@@ -1856,6 +1856,74 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
   memcpy(kp_match, m->hOutM.p, (size_t)N * 4);
   memcpy(nmatches, m->hOutM.as<uint8_t>() + (size_t)N * 4, 4);
   return ORB_OK;
+}
+
+static bool local_frame_ok(const orb_frame_t* F) {
+  return F && F->n >= 0 && F->scale_factors && F->n_levels > 0 && F->n_levels <= ORB_MAX_LEVELS &&
+         F->n < (1 << 19);
+}
+
+extern "C" {
+
+orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* F,
+                                        const uint8_t* kp_locked, int n_mp,
+                                        const orb_mp_track_t* mps, const uint8_t* mp_desc,
+                                        float th, float nnratio, int32_t* kp_match,
+                                        int32_t* nmatches) {
+  if (!m || !F || n_mp < 0 || (n_mp > 0 && (!mps || !mp_desc)) || !kp_match || !nmatches)
+    return ORB_EINVAL;
+  if (!local_frame_ok(F) || (F->n > 0 && (!F->keys || !F->descriptors))) return ORB_EINVAL;
+  *nmatches = 0;
+  if (F->n == 0) return ORB_OK;
+  std::lock_guard<std::mutex> g(m->mu);
+  const int N = F->n, M = n_mp;
+  LocalLayout L;
+  orb_status_t st = local_stage(m, N, M, &L);
+  if (st) return st;
+  uint8_t* hin = m->hIn.as<uint8_t>();
+  memcpy(hin + L.oKeys, F->keys, (size_t)N * sizeof(orb_keypoint_t));
+  memcpy(hin + L.oDesc, F->descriptors, (size_t)N * 32);
+  if (F->u_right) memcpy(hin + L.oUr, F->u_right, (size_t)N * 4);
+  if (kp_locked) memcpy(hin + L.oLk, kp_locked, (size_t)N);
+  if (M > 0) {
+    memcpy(hin + L.oMps, mps, (size_t)M * sizeof(orb_mp_track_t));
+    memcpy(hin + L.oMpd, mp_desc, (size_t)M * 32);
+  }
+  return local_run(m, N, M, F, F->u_right != nullptr, kp_locked != nullptr, th, nnratio, kp_match,
+                   nmatches);
+}
+
+orb_status_t orb_match_projection_local_stage(orb_matcher_t* m, int n_keys, int n_mp,
+                                              orb_local_stage_t* out) {
+  if (!m || !out || n_keys <= 0 || n_keys >= (1 << 19) || n_mp < 0) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  LocalLayout L;
+  orb_status_t st = local_stage(m, n_keys, n_mp, &L);
+  if (st) return st;
+  uint8_t* hin = m->hIn.as<uint8_t>();
+  out->keys = reinterpret_cast<orb_keypoint_t*>(hin + L.oKeys);
+  out->descriptors = hin + L.oDesc;
+  out->u_right = reinterpret_cast<float*>(hin + L.oUr);
+  out->kp_locked = hin + L.oLk;
+  out->mps = reinterpret_cast<orb_mp_track_t*>(hin + L.oMps);
+  out->mp_desc = hin + L.oMpd;
+  m->stagedN = n_keys;
+  m->stagedM = n_mp;
+  return ORB_OK;
+}
+
+orb_status_t orb_match_projection_local_staged(orb_matcher_t* m, const orb_frame_t* frame,
+                                               int n_mp, int stereo, int locked, float th,
+                                               float nnratio, int32_t* kp_match,
+                                               int32_t* nmatches) {
+  if (!m || !local_frame_ok(frame) || !kp_match || !nmatches) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  // the block must hold what _stage laid out for exactly these counts
+  if (frame->n <= 0 || frame->n != m->stagedN || n_mp != m->stagedM) return ORB_EINVAL;
+  m->stagedN = m->stagedM = -1;
+  *nmatches = 0;
+  return local_run(m, frame->n, n_mp, frame, stereo != 0, locked != 0, th, nnratio, kp_match,
+                   nmatches);
 }
 
 // ----------------------------------------------------------------- frustum

@@ -210,6 +210,42 @@ def test_search_by_projection_resolve_schedules(gpu, oracle, name, schedule, rou
             assert np.array_equal(km, km_ref), (w, i, np.nonzero(km != km_ref)[0][:10])
 
 
+@pytest.mark.parametrize("stereo,locked", [(False, True), (True, True), (False, False)])
+def test_search_by_projection_staged(gpu, oracle, stereo, locked):
+    """The zero-copy pair orb_match_projection_local_stage / _staged (inputs
+    written into the handle's pinned block, as integration/ORBmatcher.cc does)
+    gives the reference's assignments, mono and stereo, with and without
+    pre-locked keypoints; interleaved with the copying form on one handle."""
+    w, h = 1241, 376
+    k, d, scale = _frame(gpu, oracle, w, h, 1000, 3)
+    mps, mpd, lk = oracle.synth_local_map(3, k, d, 5000, w, h)
+    ur = None
+    if stereo:
+        rng = np.random.default_rng(4)
+        ur = np.where(rng.random(len(k)) < 0.6, k["x"] - rng.uniform(5, 60, len(k)), -1.0).astype(np.float32)
+        mps["proj_xr"] = np.where(rng.random(len(mps)) < 0.7, mps["proj_x"] - rng.uniform(4, 62, len(mps)),
+                                  -1.0).astype(np.float32)
+    lk = lk if locked else None
+    F = gpu.Frame(k, d, scale, w, h, u_right=ur)
+    m = gpu.ORBmatcher(0.8)
+    n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, mps, mpd, 1.0, 0.8, lk, u_right=ur)
+    for _ in range(2):
+        n1, km1 = m.SearchByProjectionStaged(F, mps, mpd, 1.0, lk)
+        n2, km2 = m.SearchByProjection(F, mps, mpd, 1.0, lk)
+        assert n1 == n_ref and np.array_equal(km1, km_ref)
+        assert n2 == n_ref and np.array_equal(km2, km_ref)
+    # _staged without a matching _stage (fresh handle, or a second call) is refused
+    import ctypes
+    nm = ctypes.c_int32(0)
+    out = np.zeros(F.N, np.int32)
+    f = F._c()
+    for h in (gpu.ORBmatcher(0.8).handle, m.handle):
+        with pytest.raises(gpu.OrbError):
+            gpu._check(gpu.lib().orb_match_projection_local_staged(
+                h, ctypes.byref(f), len(mps), 0, 0, 1.0, 0.8, out.ctypes.data, ctypes.byref(nm)),
+                "staged without stage")
+
+
 @pytest.mark.parametrize("schedule", [0, 1, 2, 3])
 def test_search_by_projection_batch_empty_map_stride(gpu, oracle, schedule):
     """mp_stride = 0 (no map point in any problem) under every schedule: no
