@@ -337,7 +337,12 @@ orb_status_t orb_match_projection_local(orb_matcher_t* m, const orb_frame_t* fra
  * n_keys), the bounds, levels and scale factors; its keys / descriptors /
  * u_right pointers are not read.  The pointers are valid until the next call
  * on this handle; the pair must not interleave with other calls on it (one
- * handle per thread, as the reference's per-call-site ORBmatcher objects). */
+ * handle per thread, as the reference's per-call-site ORBmatcher objects).
+ * Optional _begin, between _stage and _staged, once the frame's part (keys,
+ * descriptors, u_right, kp_locked) is written and before the map points are:
+ * it sends that part and builds the keypoint grid on the device while the
+ * caller flattens its map; stereo / locked must equal _staged's.  A _stage
+ * after a _begin without its _staged waits for the _begin's work first. */
 typedef struct orb_local_stage {
   orb_keypoint_t* keys;        /* n_keys */
   uint8_t* descriptors;        /* n_keys x 32 */
@@ -348,6 +353,8 @@ typedef struct orb_local_stage {
 } orb_local_stage_t;
 orb_status_t orb_match_projection_local_stage(orb_matcher_t* m, int n_keys, int n_mp,
                                               orb_local_stage_t* out);
+orb_status_t orb_match_projection_local_begin(orb_matcher_t* m, const orb_frame_t* frame,
+                                              int stereo, int locked);
 orb_status_t orb_match_projection_local_staged(orb_matcher_t* m, const orb_frame_t* frame,
                                                int n_mp, int stereo, int locked, float th,
                                                float nnratio, int32_t* kp_match,

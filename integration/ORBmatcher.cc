@@ -197,6 +197,10 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
   if (stereo) memcpy(S.u_right, F.mvuRight.data(), (size_t)N * 4);
   for (int i = 0; i < N; ++i)  // a claim by a point with observations locks the keypoint (:90-93)
     S.kp_locked[i] = F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0;
+  const orb_frame_t f = frame_view(F);
+  // the frame's part goes out and its keypoint grid is built while the map is flattened
+  check(orb_match_projection_local_begin(gpu(), &f, stereo ? 1 : 0, 1),
+        "SearchByProjection(F, vpMapPoints) begin");
   for (int i = 0; i < M; ++i) {
     MapPoint* p = vpMapPoints[i];
     orb_mp_track_t& t = S.mps[i];
@@ -212,7 +216,6 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
     // (a point skipped by :57-61 is never read: its descriptor is not copied)
     if (t.in_view && !t.bad) copy_descriptor(p, S.mp_desc + (size_t)i * 32);
   }
-  const orb_frame_t f = frame_view(F);
   thread_local vector<int32_t> kpMatch;
   kpMatch.resize(N);
   int32_t nmatches = 0;

@@ -111,6 +111,7 @@ def lib() -> ctypes.CDLL:
         "orb_extractor_extract_batch": (i32, [vp, vp, i32, i32, i32, sz, sz, vp, vp, i32, vp, vp]),
         "orb_extractor_batch_level": (i32, [vp, i32, i32, vp, vp, vp, vp]),
         "orb_match_projection_local_stage": (i32, [vp, i32, i32, vp]),
+        "orb_match_projection_local_begin": (i32, [vp, vp, i32, i32]),
         "orb_match_projection_local_staged": (i32, [vp, vp, i32, i32, i32, f32, f32, vp, vp]),
         "orb_extractor_stream": (vp, [vp]),
         "orb_extractor_profile": (i32, [vp, i32]),
@@ -541,10 +542,11 @@ class ORBmatcher:
         return nm.value, kp_match
 
     def SearchByProjectionStaged(self, F: Frame, mps: np.ndarray, mp_desc: np.ndarray, th: float,
-                                 kp_locked: np.ndarray | None = None):
+                                 kp_locked: np.ndarray | None = None, begin: bool = True):
         """SearchByProjection through the zero-copy pair
         orb_match_projection_local_stage / _staged: the inputs are written
-        straight into the handle's pinned block (as the C++ drop-in does)."""
+        straight into the handle's pinned block (as the C++ drop-in does);
+        with `begin`, _begin sends the frame's part before the map is written."""
         mps = np.ascontiguousarray(mps, MP_TRACK_DTYPE)
         mp_desc = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
         n, M = F.N, len(mps)
@@ -564,12 +566,15 @@ class ORBmatcher:
             view(st.u_right, np.float32, n)[:] = F.mvuRight
         if kp_locked is not None:
             view(st.kp_locked, np.uint8, n)[:] = kp_locked
+        f = F._c()
+        if begin:
+            _check(lib().orb_match_projection_local_begin(self._h, ctypes.byref(f), int(stereo),
+                                                          int(kp_locked is not None)), "begin")
         if M:
             view(st.mps, MP_TRACK_DTYPE, M)[:] = mps
             view(st.mp_desc, np.uint8, M * 32)[:] = mp_desc.reshape(-1)
         kp_match = np.full(n, -1, np.int32)
         nm = ctypes.c_int32(0)
-        f = F._c()
         _check(lib().orb_match_projection_local_staged(
             self._h, ctypes.byref(f), M, int(stereo), int(kp_locked is not None), th, self.mfNNratio,
             _ptr(kp_match), ctypes.byref(nm)), "SearchByProjectionStaged")

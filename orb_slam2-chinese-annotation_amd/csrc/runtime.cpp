@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <shared_mutex>
 #include <cmath>
@@ -236,6 +237,22 @@ struct CallOrder {
     if (!capture && hipEventRecord(ev, s) == hipSuccess) *last = s;
   }
 };
+
+// Wait for a stream whose results the caller reads next.  The synchronous
+// entry points (one frame, one SearchByProjection) sit on the tracking
+// thread's critical path, where hipStreamSynchronize returned 5-13 us after
+// the stream's last operation (profiles/r06_dropin_timeline.txt); polling the
+// stream returns within a query (~1 us) of it.  Bounded: past 2 ms of polling
+// the wait blocks as hipStreamSynchronize does.
+static hipError_t stream_wait(hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 1;; ++i) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e;
+    if ((i & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+      return hipStreamSynchronize(s);
+  }
+}
 
 // Growable device buffer.
 struct DevBuf {
@@ -751,7 +768,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (!rtab.empty())
     HIP_TRY(hipMemcpyAsync(h->dRtab.p, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice,
                            h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(stream_wait(h->stream));
   h->lastStream = nullptr;  // the previous call has finished (waited for above)
   h->plan = P;
   h->cells.swap(cells);
@@ -1287,7 +1304,7 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     h->lastImg0Pitch = pitch;
     h->lastImg0Stride = (int)dstride;
   }
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(stream_wait(h->stream));
   h->lastStream = nullptr;  // nothing of this handle is pending
   h->oneCap = cap;
   h->lastSingle = true;
@@ -1335,7 +1352,7 @@ static orb_status_t copy_level_to_host(orb_extractor_t* h, uint8_t* dst, size_t 
   uint8_t* ho = h->hLvl.as<uint8_t>();
   HIP_TRY(hipMemcpy2DAsync(ho, (size_t)w, src, src_stride, (size_t)w, hh, hipMemcpyDeviceToHost,
                            h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(stream_wait(h->stream));
   for (int y = 0; y < hh; ++y) memcpy(dst + (size_t)y * dst_stride, ho + (size_t)y * w, (size_t)w);
   return ORB_OK;
 }
@@ -1380,7 +1397,7 @@ orb_status_t orb_extractor_host_pyramid(orb_extractor_t* h, int level, const uin
     HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));
     HIP_TRY(hipMemcpyAsync(h->hPyr.p, h->dArena.p, (size_t)h->arenaBytes, hipMemcpyDeviceToHost,
                            h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(stream_wait(h->stream));
     h->pyrReadback = true;
     h->hPyrValid = true;
   }
@@ -1539,6 +1556,7 @@ struct orb_matcher {
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
   DevBuf dJac;  // Jacobi-resolve scratch (ORB_RESOLVE_JACOBI)
   int stagedN = -1, stagedM = -1;  // orb_match_projection_local_stage's layout
+  bool begun = false, begunStereo = false, begunLocked = false;  // _begin sent the frame's part
   int resolveSchedule = ORB_RESOLVE_AUTO;  // orb_matcher_set_resolve
   int jacobiRounds = 6;
   // stereo / frame / BoW scratch
@@ -1799,12 +1817,11 @@ static orb_status_t local_stage(orb_matcher_t* m, int N, int M, LocalLayout* out
 }
 
 // SearchByProjection(F, vpMapPoints) on the inputs staged in the pinned block:
-// one DMA in, grid + candidates + resolve, one DMA out; caller holds m->mu
-static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t* F, bool urOn,
-                              bool lkOn, float th, float nnratio, int32_t* kp_match,
-                              int32_t* nmatches) {
-  hipSetDevice(m->device);
-  const LocalLayout L = local_layout(N, M);
+// one DMA in, grid + candidates + resolve, one DMA out; caller holds m->mu.
+// In two parts when the frame's part of the block was sent ahead
+// (local_begin: its DMA and the keypoint grid run while the caller flattens
+// the map into the rest of the block).
+static orb_status_t local_ensure(orb_matcher_t* m, int N, int M, const LocalLayout& L) {
   orb_status_t st;
   // (inputs live in dIn below; only the outputs and the matcher scratch here)
   if ((st = m->dKpMatch.ensure((size_t)N * 4 + 16))) return st;  // + the count (one D2H)
@@ -1814,14 +1831,49 @@ static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t*
   if ((st = m->dNcand.ensure((size_t)std::max(M, 1) * 4))) return st;
   if ((st = m->dIn.ensure(L.inBytes))) return st;
   if ((st = m->hOutM.ensure((size_t)N * 4 + 16))) return st;
-  const bool stage = N <= orb_k_grid_stage_max();
-  if (stage && (st = m->dProjStage.ensure((size_t)N * 16))) return st;
+  if (N <= orb_k_grid_stage_max() && (st = m->dProjStage.ensure((size_t)N * 16))) return st;
   const size_t jb = orb_k_proj_jacobi_bytes(N, std::max(M, 1), 1, m->resolveSchedule);
   if (jb && (st = m->dJac.ensure(jb))) return st;
+  return ORB_OK;
+}
+
+// DMA of bytes [b0, b1) of the block, then (b0 == 0) the keypoint grid
+static orb_status_t local_front(orb_matcher_t* m, int N, const LocalLayout& L, const ProjParamsHost& P,
+                                bool urOn, bool lkOn, size_t b1, hipStream_t s) {
+  HIP_TRY(hipMemcpyAsync(m->dIn.p, m->hIn.p, b1, hipMemcpyHostToDevice, s));
+  uint8_t* din = m->dIn.as<uint8_t>();
+  const orb_keypoint_t* dKeys = reinterpret_cast<const orb_keypoint_t*>(din + L.oKeys);
+  const int32_t* dNK = reinterpret_cast<const int32_t*>(din);
+  const float* ur = urOn ? reinterpret_cast<const float*>(din + L.oUr) : nullptr;
+  const uint8_t* lk = lkOn ? din + L.oLk : nullptr;
+  if (N <= orb_k_grid_stage_max())
+    HIP_TRY(orb_k_grid_build_staged(dKeys, dNK, lk, ur, N, P.minX, P.minY, P.invW, P.invH,
+                                    m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
+                                    m->dProjStage.p, 1, s));
+  else
+    HIP_TRY(orb_k_grid_build(dKeys, dNK, N, P.minX, P.minY, P.invW, P.invH,
+                             m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), 1, s));
+  return ORB_OK;
+}
+
+static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t* F, bool urOn,
+                              bool lkOn, float th, float nnratio, int32_t* kp_match,
+                              int32_t* nmatches, bool begun = false) {
+  hipSetDevice(m->device);
+  const LocalLayout L = local_layout(N, M);
+  orb_status_t st;
+  if (!begun && (st = local_ensure(m, N, M, L))) return st;
   hipStream_t s = m->stream;
   CallOrder order(m->evLast, &m->lastStream, s);
   if (order.status) return order.status;
-  HIP_TRY(hipMemcpyAsync(m->dIn.p, m->hIn.p, L.inBytes, hipMemcpyHostToDevice, s));
+  const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
+                                       F->scale_factors, th, nnratio);
+  if (!begun) {
+    if ((st = local_front(m, N, L, P, urOn, lkOn, L.inBytes, s))) return st;
+  } else if (L.inBytes > L.oMps) {  // the map's part of the block
+    HIP_TRY(hipMemcpyAsync(m->dIn.as<uint8_t>() + L.oMps, m->hIn.as<uint8_t>() + L.oMps,
+                           L.inBytes - L.oMps, hipMemcpyHostToDevice, s));
+  }
   uint8_t* din = m->dIn.as<uint8_t>();
   const orb_keypoint_t* dKeys = reinterpret_cast<const orb_keypoint_t*>(din + L.oKeys);
   const uint8_t* dDesc = din + L.oDesc;
@@ -1829,17 +1881,9 @@ static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t*
   const int32_t* dNM = reinterpret_cast<const int32_t*>(din + 4);
   const orb_mp_track_t* dMps = reinterpret_cast<const orb_mp_track_t*>(din + L.oMps);
   const uint8_t* dMpd = din + L.oMpd;
-  const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
-                                       F->scale_factors, th, nnratio);
   const float* ur = urOn ? reinterpret_cast<const float*>(din + L.oUr) : nullptr;
   const uint8_t* lk = lkOn ? din + L.oLk : nullptr;
-  if (stage)
-    HIP_TRY(orb_k_grid_build_staged(dKeys, dNK, lk, ur, N, P.minX, P.minY, P.invW, P.invH,
-                                    m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
-                                    m->dProjStage.p, 1, s));
-  else
-    HIP_TRY(orb_k_grid_build(dKeys, dNK, N, P.minX, P.minY, P.invW, P.invH,
-                             m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(), 1, s));
+  const bool stage = N <= orb_k_grid_stage_max();
   HIP_TRY(orb_k_proj_candidates(dKeys, dDesc, ur, lk, N, dNK, dMps, dMpd, dNM, std::max(M, 1), M,
                                 m->dCellStart.as<int32_t>(), m->dCellIdx.as<int32_t>(),
                                 stage ? m->dProjStage.p : nullptr, &P, m->dTopk.as<uint32_t>(),
@@ -1851,7 +1895,7 @@ static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t*
                              m->resolveSchedule, m->jacobiRounds, m->dJac.as<int32_t>(), s));
   // one DMA out (count, then the matches) into pinned memory
   HIP_TRY(hipMemcpyAsync(m->hOutM.p, m->dKpMatch.p, (size_t)N * 4 + 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   order.settled();
   memcpy(kp_match, m->hOutM.p, (size_t)N * 4);
   memcpy(nmatches, m->hOutM.as<uint8_t>() + (size_t)N * 4, 4);
@@ -1897,6 +1941,11 @@ orb_status_t orb_match_projection_local_stage(orb_matcher_t* m, int n_keys, int 
                                               orb_local_stage_t* out) {
   if (!m || !out || n_keys <= 0 || n_keys >= (1 << 19) || n_mp < 0) return ORB_EINVAL;
   std::lock_guard<std::mutex> g(m->mu);
+  if (m->begun) {  // a _begin whose _staged never came: its DMA still reads the block
+    m->begun = false;
+    hipSetDevice(m->device);
+    HIP_TRY(stream_wait(m->stream));
+  }
   LocalLayout L;
   orb_status_t st = local_stage(m, n_keys, n_mp, &L);
   if (st) return st;
@@ -1912,6 +1961,29 @@ orb_status_t orb_match_projection_local_stage(orb_matcher_t* m, int n_keys, int 
   return ORB_OK;
 }
 
+orb_status_t orb_match_projection_local_begin(orb_matcher_t* m, const orb_frame_t* frame,
+                                              int stereo, int locked) {
+  if (!m || !local_frame_ok(frame)) return ORB_EINVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  if (frame->n <= 0 || frame->n != m->stagedN || m->begun) return ORB_EINVAL;
+  hipSetDevice(m->device);
+  const int N = frame->n, M = m->stagedM;
+  const LocalLayout L = local_layout(N, M);
+  orb_status_t st = local_ensure(m, N, M, L);
+  if (st) return st;
+  hipStream_t s = m->stream;
+  CallOrder order(m->evLast, &m->lastStream, s);
+  if (order.status) return order.status;
+  // (th and nnratio do not enter the grid)
+  const ProjParamsHost P = proj_params(frame->min_x, frame->max_x, frame->min_y, frame->max_y,
+                                       frame->n_levels, frame->scale_factors, 1.f, 0.f);
+  if ((st = local_front(m, N, L, P, stereo != 0, locked != 0, L.oMps, s))) return st;
+  m->begun = true;
+  m->begunStereo = stereo != 0;
+  m->begunLocked = locked != 0;
+  return ORB_OK;
+}
+
 orb_status_t orb_match_projection_local_staged(orb_matcher_t* m, const orb_frame_t* frame,
                                                int n_mp, int stereo, int locked, float th,
                                                float nnratio, int32_t* kp_match,
@@ -1919,11 +1991,15 @@ orb_status_t orb_match_projection_local_staged(orb_matcher_t* m, const orb_frame
   if (!m || !local_frame_ok(frame) || !kp_match || !nmatches) return ORB_EINVAL;
   std::lock_guard<std::mutex> g(m->mu);
   // the block must hold what _stage laid out for exactly these counts
-  if (frame->n <= 0 || frame->n != m->stagedN || n_mp != m->stagedM) return ORB_EINVAL;
+  const bool begun = m->begun;
+  m->begun = false;
+  const int sn = m->stagedN, sm = m->stagedM;
   m->stagedN = m->stagedM = -1;
+  if (frame->n <= 0 || frame->n != sn || n_mp != sm) return ORB_EINVAL;
+  if (begun && (m->begunStereo != (stereo != 0) || m->begunLocked != (locked != 0))) return ORB_EINVAL;
   *nmatches = 0;
   return local_run(m, frame->n, n_mp, frame, stereo != 0, locked != 0, th, nnratio, kp_match,
-                   nmatches);
+                   nmatches, begun);
 }
 
 // ----------------------------------------------------------------- frustum
@@ -1961,7 +2037,7 @@ orb_status_t orb_frustum(orb_matcher_t* m, int n_mp, const orb_map_point_t* mps,
   HIP_TRY(hipMemcpyAsync(tracks, m->dTracks.p, (size_t)n_mp * sizeof(orb_mp_track_t),
                          hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(n_in_view, m->dNInView.p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2084,7 +2160,7 @@ orb_status_t orb_stereo_match(orb_matcher_t* m, const orb_stereo_input_t* in, fl
                        m->dStRowStart.as<int32_t>(), m->dStRowIdx.as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(u_right, m->dUr.p, (size_t)NL * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(depth, m->dDepth.p, (size_t)NL * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2139,7 +2215,7 @@ orb_status_t orb_stereo_match_batch(orb_matcher_t* m, int n_pairs, orb_extractor
                        kp_stride, kp_stride, m->dPairLv.p, &P, d_u_right, d_depth, d_sad,
                        n_pairs, m->dStRowStart.as<int32_t>(), m->dStRowIdx.as<int32_t>(), s));
   // the pair-level pointer table must outlive the asynchronous launch
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2232,7 +2308,7 @@ orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_
   HIP_TRY(hipMemcpyAsync(m->hPyr.p, m->dUr.p, (size_t)nL * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(m->hPyr.as<uint8_t>() + (size_t)nL * 4, m->dDepth.p, (size_t)nL * 4,
                          hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   memcpy(u_right, m->hPyr.p, (size_t)nL * 4);
   memcpy(depth, m->hPyr.as<uint8_t>() + (size_t)nL * 4, (size_t)nL * 4);
   return ORB_OK;
@@ -2297,7 +2373,7 @@ orb_status_t orb_match_projection_frame(orb_matcher_t* m, const orb_frame_t* C,
                            m->dKpMatch.as<int32_t>(), m->dNMatch.as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(kp_match, m->dKpMatch.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2348,7 +2424,7 @@ orb_status_t orb_match_bow(orb_matcher_t* m, int n_kf, const uint8_t* kf_desc,
                     m->dTopk.as<int32_t>(), m->dNMatch.as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(f_match, m->dKpMatch.p, (size_t)n_f * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2436,7 +2512,7 @@ orb_status_t orb_search_for_initialization(orb_matcher_t* m, const orb_frame_t* 
   HIP_TRY(hipMemcpyAsync(matches12, m->dM12.p, (size_t)N1 * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(prev_matched, m->dPrev.p, (size_t)N1 * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, m->dNMatch.p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2490,7 +2566,7 @@ orb_status_t orb_distinctive_descriptors(orb_matcher_t* m, int n_mp, const int32
   if (descriptors)
     HIP_TRY(hipMemcpyAsync(descriptors, m->dBestDesc.p, (size_t)n_mp * 32, hipMemcpyDeviceToHost,
                            s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2620,10 +2696,10 @@ static orb_status_t pp_run(orb_matcher_t* m, int mode, const PPParamsHost& P, in
     HIP_TRY(hipMemcpyAsync(kp_match_host, m->sx[19].p, (size_t)K->n * 4, hipMemcpyDeviceToHost,
                            s));
     HIP_TRY(hipMemcpyAsync(count_host, m->sx[20].p, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(stream_wait(s));
   } else if (best_host) {
     HIP_TRY(hipMemcpyAsync(best_host, best, (size_t)n_mp * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(stream_wait(s));
     int c = 0;
     for (int i = 0; i < n_mp; ++i) c += best_host[i] >= 0;
     *count_host = c;
@@ -2779,7 +2855,7 @@ orb_status_t orb_search_by_sim3(orb_matcher_t* m, const orb_frame_t* kf1, const 
   if ((st = pp_run(m, 4, P1, 0, kf2, nullptr, kf1->n, mps1, valid1, already1, mp_desc1, nullptr,
                    nullptr, nullptr, nullptr, s, m->sx[21].as<int32_t>())))
     return st;
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   if ((st = pp_run(m, 4, P2, 4, kf1, nullptr, kf2->n, mps2, valid2, already2, mp_desc2, nullptr,
                    nullptr, nullptr, nullptr, s, m->sx[22].as<int32_t>())))
     return st;
@@ -2788,7 +2864,7 @@ orb_status_t orb_search_by_sim3(orb_matcher_t* m, const orb_frame_t* kf1, const 
                             out + kf1->n, s));
   HIP_TRY(hipMemcpyAsync(match12, out, (size_t)kf1->n * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nfound, out + kf1->n, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2844,7 +2920,7 @@ orb_status_t orb_match_bow_kf(orb_matcher_t* m, int n1, const uint8_t* desc1,
                     b[14].as<int32_t>(), b[15].as<int32_t>(), b[16].as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(match12, b[14].p, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, b[16].p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2915,7 +2991,7 @@ orb_status_t orb_search_for_triangulation(
       b[15].as<int32_t>(), b[16].as<int32_t>(), s));
   HIP_TRY(hipMemcpyAsync(match12, b[14].p, (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nmatches, b[16].p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -2981,7 +3057,7 @@ static orb_status_t vocab_build(orb_vocabulary* V, int n_nodes, const int32_t* p
   if ((st = upload(V->dWord, dword.data(), dword.size() * 4, s))) return st;
   if ((st = upload(V->dWeight, dweight.data(), dweight.size() * 8, s))) return st;
   if ((st = upload(V->dOrig, orig.data(), orig.size() * 4, s))) return st;
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -3169,7 +3245,7 @@ orb_status_t orb_vocabulary_transform(orb_vocabulary_t* V, int n, const uint8_t*
   int32_t counts[2];
   HIP_TRY(hipMemcpyAsync(&counts[0], V->dNW.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(&counts[1], V->dNFv.p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   *n_words = counts[0];
   *n_fv_nodes = counts[1];
   HIP_TRY(hipMemcpyAsync(bow_words, V->dBowW.p, (size_t)counts[0] * 4, hipMemcpyDeviceToHost, s));
@@ -3177,13 +3253,13 @@ orb_status_t orb_vocabulary_transform(orb_vocabulary_t* V, int n, const uint8_t*
   HIP_TRY(hipMemcpyAsync(fv_nodes, V->dFvN.p, (size_t)counts[1] * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(fv_offs, V->dFvO.p, (size_t)(counts[1] + 1) * 4, hipMemcpyDeviceToHost,
                          s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   const int nfeat = fv_offs[counts[1]];
   if (nfeat > 0)
     HIP_TRY(hipMemcpyAsync(fv_feats, V->dFvF.p, (size_t)nfeat * 4, hipMemcpyDeviceToHost, s));
   if (feat_word) HIP_TRY(hipMemcpyAsync(feat_word, V->dFWord.p, N * 4, hipMemcpyDeviceToHost, s));
   if (feat_node) HIP_TRY(hipMemcpyAsync(feat_node, V->dFNode.p, N * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -3248,7 +3324,7 @@ orb_status_t orb_undistort_points(orb_matcher_t* m, int n, const float* xy, cons
   if ((st = upload(m->dA, xy, (size_t)n * 8, s)) || (st = m->dB.ensure((size_t)n * 8))) return st;
   HIP_TRY(orb_k_undistort_points(&P, n, m->dA.as<float>(), m->dB.as<float>(), s));
   HIP_TRY(hipMemcpyAsync(out_xy, m->dB.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 
@@ -3273,7 +3349,7 @@ orb_status_t orb_undistort_keypoints(orb_matcher_t* m, int n, const orb_keypoint
   if ((st = upload(m->dA, keys, bytes, s)) || (st = m->dB.ensure(bytes))) return st;
   HIP_TRY(orb_k_undistort_keys(&P, 1, nullptr, n, n, m->dA.p, m->dB.p, 0, s));
   HIP_TRY(hipMemcpyAsync(keys_un, m->dB.p, bytes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(stream_wait(s));
   return ORB_OK;
 }
 

@@ -213,9 +213,12 @@ def test_search_by_projection_resolve_schedules(gpu, oracle, name, schedule, rou
 @pytest.mark.parametrize("stereo,locked", [(False, True), (True, True), (False, False)])
 def test_search_by_projection_staged(gpu, oracle, stereo, locked):
     """The zero-copy pair orb_match_projection_local_stage / _staged (inputs
-    written into the handle's pinned block, as integration/ORBmatcher.cc does)
-    gives the reference's assignments, mono and stereo, with and without
-    pre-locked keypoints; interleaved with the copying form on one handle."""
+    written into the handle's pinned block, as integration/ORBmatcher.cc does;
+    with and without _begin sending the frame's part and building the grid
+    before the map is written) gives the reference's assignments, mono and
+    stereo, with and without pre-locked keypoints; interleaved with the copying
+    form on one handle.  Misuse is refused: _staged without _stage, _begin
+    with other stereo / locked flags than _staged, a second _begin."""
     w, h = 1241, 376
     k, d, scale = _frame(gpu, oracle, w, h, 1000, 3)
     mps, mpd, lk = oracle.synth_local_map(3, k, d, 5000, w, h)
@@ -229,8 +232,8 @@ def test_search_by_projection_staged(gpu, oracle, stereo, locked):
     F = gpu.Frame(k, d, scale, w, h, u_right=ur)
     m = gpu.ORBmatcher(0.8)
     n_ref, km_ref = oracle.match_projection_local(k, d, scale, w, h, mps, mpd, 1.0, 0.8, lk, u_right=ur)
-    for _ in range(2):
-        n1, km1 = m.SearchByProjectionStaged(F, mps, mpd, 1.0, lk)
+    for begin in (True, False, True):  # with and without _begin, copying form between
+        n1, km1 = m.SearchByProjectionStaged(F, mps, mpd, 1.0, lk, begin=begin)
         n2, km2 = m.SearchByProjection(F, mps, mpd, 1.0, lk)
         assert n1 == n_ref and np.array_equal(km1, km_ref)
         assert n2 == n_ref and np.array_equal(km2, km_ref)
@@ -244,6 +247,19 @@ def test_search_by_projection_staged(gpu, oracle, stereo, locked):
             gpu._check(gpu.lib().orb_match_projection_local_staged(
                 h, ctypes.byref(f), len(mps), 0, 0, 1.0, 0.8, out.ctypes.data, ctypes.byref(nm)),
                 "staged without stage")
+    L = gpu.lib()
+    st = gpu._LocalStage()
+    gpu._check(L.orb_match_projection_local_stage(m.handle, F.N, len(mps), ctypes.byref(st)), "stage")
+    gpu._check(L.orb_match_projection_local_begin(m.handle, ctypes.byref(f), int(stereo), 1), "begin")
+    with pytest.raises(gpu.OrbError):  # second _begin
+        gpu._check(L.orb_match_projection_local_begin(m.handle, ctypes.byref(f), int(stereo), 1), "begin")
+    with pytest.raises(gpu.OrbError):  # flags differ from _begin's
+        gpu._check(L.orb_match_projection_local_staged(
+            m.handle, ctypes.byref(f), len(mps), int(not stereo), 1, 1.0, 0.8, out.ctypes.data,
+            ctypes.byref(nm)), "staged")
+    # a fresh stage after the abandoned _begin, then a normal call: exact again
+    n3, km3 = m.SearchByProjectionStaged(F, mps, mpd, 1.0, lk)
+    assert n3 == n_ref and np.array_equal(km3, km_ref)
 
 
 @pytest.mark.parametrize("schedule", [0, 1, 2, 3])

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Negative control of tests/test_gpu_stream_order.py: the library of commit
-# 2698f1c built with -DORB_CALL_ORDER=0 (no cross-stream waits; make
-# EXTRA_HIPFLAGS=-DORB_CALL_ORDER=0, copied to lib/variants/noorder.so) is
+# Negative control of tests/test_gpu_stream_order.py: the current library
+# built with -DORB_CALL_ORDER=0 (no cross-stream waits; tools/build_variant.sh noorder
+# "-DORB_CALL_ORDER=0" -> lib/variants/noorder.so) is
 # expected to FAIL the ordering tests (calls on two streams race on the
 # handle's scratch).  Prints the pytest summary and the rc.
 V=orb_slam2-chinese-annotation_amd/lib/variants/noorder.so
