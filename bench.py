@@ -1065,12 +1065,22 @@ def main():
         ext.profile(True)
     if args.timed_events in ("match", "both"):
         matcher.profile(True)
+    # diagnostic (ORB_BENCH_STEP_EVENTS=1, never in the driver's run): one
+    # timing event per step on the stream of its last match, and the host's
+    # clock when it has queued each step
+    step_diag = os.environ.get("ORB_BENCH_STEP_EVENTS") == "1"
+    step_ev, host_q = [], []
     t0 = time.perf_counter()
     g_first = g
     for k in range(args.steps):
         for _ in range(NB):
             launch(g)
             g += 1
+        if step_diag:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(ext_streams[(g - 1) % L] if inlane else match_streams[(g - 1) % MSN])
+            step_ev.append(e)
+            host_q.append(time.perf_counter())
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -1236,6 +1246,12 @@ def main():
         par = (f"frames sharded over {world} rank(s); one "
                f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-gather of the step's "
                f"per-frame keypoint counts per step")
+    if step_diag:
+        gpu_ms = [step_ev[i - 1].elapsed_time(step_ev[i]) for i in range(1, len(step_ev))]
+        host_ms = [(host_q[i] - t0) * 1e3 for i in range(len(host_q))]
+        print(json.dumps({"step_diag": {"gpu_step_ms": [round(v, 3) for v in gpu_ms],
+                                        "host_queued_ms": [round(v, 2) for v in host_ms]}}),
+              file=sys.stderr)
     result = {
         "metric": METRIC,
         "value": total_frames / elapsed,

@@ -2662,8 +2662,59 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
   }
 }
 
+// ============================================================ k_copy_pinned
+// Host -> device copy as a kernel on the caller's queue.  A copy-engine DMA's
+// completion reaches the next kernel on the compute queue ~7 us late
+// (profiles/r06_dropin_timeline.txt: the image's and the matcher inputs' DMAs
+// each followed by a 7 us idle gap); a kernel reading the pinned block over
+// PCIe hands over with no cross-engine wait.  The loads are system-coherent
+// (sc0 sc1: the host wrote the block just before the launch) and each thread
+// moves 16-byte words, grid-stride.  bytes and both addresses 16-byte aligned
+// (the launcher checks).
+__global__ __launch_bounds__(256) void k_copy_pinned(uint4* __restrict__ dst, const uint8_t* src,
+                                                     uint32_t n16) {
+  const __amdgpu_buffer_rsrc_t r = make_rsrc(src, n16 * 16u);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16u), 0, 17 /* sc0 sc1 */);
+    dst[i] = make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+  }
+}
+
+// Device -> host counterpart: dwords stored system-coherent (sc0 sc1: written
+// through to host memory, visible once the stream's completion is), as a
+// kernel on the caller's queue right behind the kernel that produced them (a
+// separate hipMemcpyAsync started 7 us after it, profiles/r06_dropin_timeline.txt).
+__global__ __launch_bounds__(256) void k_copy_to_pinned(uint8_t* dst, const uint32_t* __restrict__ src,
+                                                        uint32_t n4) {
+  const __amdgpu_buffer_rsrc_t r = make_rsrc(dst, n4 * 4u);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n4; i += gridDim.x * 256u)
+    __builtin_amdgcn_raw_buffer_store_b32(src[i], r, (int)(i * 4u), 0, 17 /* sc0 sc1 */);
+}
+
 // ------------------------------------------------------------ host launchers
 extern "C" {
+
+hipError_t orb_k_copy_pinned(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if ((bytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15) || bytes >= (1ull << 31))
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+  const uint32_t n16 = (uint32_t)(bytes >> 4);
+  const uint32_t grid = std::min<uint32_t>((n16 + 255) / 256, 512);
+  k_copy_pinned<<<grid, 256, 0, s>>>(reinterpret_cast<uint4*>(dst),
+                                     reinterpret_cast<const uint8_t*>(src), n16);
+  return hipGetLastError();
+}
+
+hipError_t orb_k_copy_to_pinned(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if ((bytes & 3) || ((uintptr_t)dst & 3) || ((uintptr_t)src & 3) || bytes >= (1ull << 31))
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+  const uint32_t n4 = (uint32_t)(bytes >> 2);
+  const uint32_t grid = std::min<uint32_t>((n4 + 255) / 256, 512);
+  k_copy_to_pinned<<<grid, 256, 0, s>>>(reinterpret_cast<uint8_t*>(dst),
+                                        reinterpret_cast<const uint32_t*>(src), n4);
+  return hipGetLastError();
+}
 
 hipError_t orb_k_upload_constants(hipStream_t s) {
   static int8_t pat[2 * ORB_PATTERN_POINTS];

@@ -31,6 +31,8 @@ hipError_t orb_k_pyr_resize(const uint8_t* src, long long srcImgPitch, int srcSt
                             int dh, const int* xofs, const void* alpha, const int* yofs,
                             const void* beta, int mode, int nimg, hipStream_t s);
 size_t orb_k_fast_band_lds(int bandElems);
+hipError_t orb_k_copy_pinned(void* dst, const void* src, size_t bytes, hipStream_t s);
+hipError_t orb_k_copy_to_pinned(void* dst, const void* src, size_t bytes, hipStream_t s);
 size_t orb_k_fast_cells_lds(int maxRows, int maxCols);
 bool orb_k_fast_cells_fits(const OrbPlanDesc* plan);
 
@@ -244,7 +246,11 @@ struct CallOrder {
 // the stream's last operation (profiles/r06_dropin_timeline.txt); polling the
 // stream returns within a query (~1 us) of it.  Bounded: past 2 ms of polling
 // the wait blocks as hipStreamSynchronize does.
+#ifndef ORB_POLL_WAIT
+#define ORB_POLL_WAIT 1  // A/B knob (0: hipStreamSynchronize)
+#endif
 static hipError_t stream_wait(hipStream_t s) {
+  if (!ORB_POLL_WAIT) return hipStreamSynchronize(s);
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned i = 1;; ++i) {
     const hipError_t e = hipStreamQuery(s);
@@ -1255,8 +1261,11 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
   uint8_t* d1 = h->dOne.as<uint8_t>();
   // one DMA in, the extraction, one DMA out of the count and every record slot
+  auto upload = [&]() -> orb_status_t {
+    HIP_TRY(orb_k_copy_pinned(h->dImg.p, h->hImg.p, pitch, h->stream));
+    return ORB_OK;
+  };
   auto enqueue = [&](bool capturing) -> orb_status_t {
-    HIP_TRY(hipMemcpyAsync(h->dImg.p, h->hImg.p, pitch, hipMemcpyHostToDevice, h->stream));
     orb_status_t r = run_batch(h, h->dImg.as<uint8_t>(), 1, dstride, pitch,
                                reinterpret_cast<orb_keypoint_t*>(d1 + kOff), d1 + dOff, cap,
                                reinterpret_cast<int32_t*>(d1), h->stream, capturing);
@@ -1268,8 +1277,13 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
     return ORB_OK;
   };
   if (h->prof.enabled) {  // (the stage events need the launches issued one by one)
-    if ((st = enqueue(false))) return st;
+    if ((st = upload()) || (st = enqueue(false))) return st;
   } else {
+    // the DMA in goes out before the graph, not as its first node: it runs
+    // while hipGraphLaunch is still being processed on the host (~20 us of
+    // host time before a graph's first node starts on the GPU,
+    // profiles/r06_dropin_timeline.txt)
+    if ((st = upload())) return st;
     const std::vector<const void*> key = {
         h->dImg.p, h->dOne.p, h->hImg.p, h->hOut.p, h->dArena.p, h->dCellKeys.p, h->dGKeys.p,
         h->dGNid.p, h->dCellCount.p, h->dOutKeys.p, h->dOutCount.p, h->dErr.p, h->dRtab.p,
@@ -1840,7 +1854,7 @@ static orb_status_t local_ensure(orb_matcher_t* m, int N, int M, const LocalLayo
 // DMA of bytes [b0, b1) of the block, then (b0 == 0) the keypoint grid
 static orb_status_t local_front(orb_matcher_t* m, int N, const LocalLayout& L, const ProjParamsHost& P,
                                 bool urOn, bool lkOn, size_t b1, hipStream_t s) {
-  HIP_TRY(hipMemcpyAsync(m->dIn.p, m->hIn.p, b1, hipMemcpyHostToDevice, s));
+  HIP_TRY(orb_k_copy_pinned(m->dIn.p, m->hIn.p, b1, s));
   uint8_t* din = m->dIn.as<uint8_t>();
   const orb_keypoint_t* dKeys = reinterpret_cast<const orb_keypoint_t*>(din + L.oKeys);
   const int32_t* dNK = reinterpret_cast<const int32_t*>(din);
@@ -1871,8 +1885,8 @@ static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t*
   if (!begun) {
     if ((st = local_front(m, N, L, P, urOn, lkOn, L.inBytes, s))) return st;
   } else if (L.inBytes > L.oMps) {  // the map's part of the block
-    HIP_TRY(hipMemcpyAsync(m->dIn.as<uint8_t>() + L.oMps, m->hIn.as<uint8_t>() + L.oMps,
-                           L.inBytes - L.oMps, hipMemcpyHostToDevice, s));
+    HIP_TRY(orb_k_copy_pinned(m->dIn.as<uint8_t>() + L.oMps, m->hIn.as<uint8_t>() + L.oMps,
+                              L.inBytes - L.oMps, s));
   }
   uint8_t* din = m->dIn.as<uint8_t>();
   const orb_keypoint_t* dKeys = reinterpret_cast<const orb_keypoint_t*>(din + L.oKeys);
@@ -1894,7 +1908,7 @@ static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t*
                              m->dKpMatch.as<int32_t>(), m->dKpMatch.as<int32_t>() + N, 1,
                              m->resolveSchedule, m->jacobiRounds, m->dJac.as<int32_t>(), s));
   // one DMA out (count, then the matches) into pinned memory
-  HIP_TRY(hipMemcpyAsync(m->hOutM.p, m->dKpMatch.p, (size_t)N * 4 + 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(orb_k_copy_to_pinned(m->hOutM.p, m->dKpMatch.p, (size_t)N * 4 + 4, s));
   HIP_TRY(stream_wait(s));
   order.settled();
   memcpy(kp_match, m->hOutM.p, (size_t)N * 4);

@@ -11,8 +11,8 @@ launch / wake-up latency).
                                           --memory-copy-trace [--hip-trace]
                                           --output-format csv
 
-The mono loop's calls are grouped by the image H2D (the largest copy) that
-opens each frame; the stereo loop after it is left out.
+A frame = the image's DMA in (the op before the first pyramid kernel of an
+extraction) up to the next frame's; the mono loop's frames only (--iters).
 """
 import argparse
 import csv
@@ -71,11 +71,12 @@ def analyze(a):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                    f"{'H2D' if 'HOST_TO_DEVICE' in kind.upper() or 'H2D' in kind.upper() else 'D2H' if 'DEVICE_TO_HOST' in kind.upper() or 'D2H' in kind.upper() else kind}:{size}"))
     ev.sort()
-    # a frame of the mono loop opens with the image H2D (W x H bytes)
-    starts = [i for i, e in enumerate(ev) if e[2].startswith("H2D") and e[2].endswith(":466616")]
-    if not starts:  # sizes absent: every group opens with an H2D after a >30 us idle gap
-        starts = [i for i, e in enumerate(ev)
-                  if e[2].startswith("H2D") and (i == 0 or e[0] - ev[i - 1][1] > 30_000)]
+    # a frame opens with the image's DMA in: the op just before the first
+    # pyramid kernel of each extraction
+    starts = []
+    for i, e in enumerate(ev):
+        if "k_pyr_resize" in e[2] and i > 0 and "k_pyr_resize" not in ev[i - 1][2]:
+            starts.append(i - 1)
     frames = []
     for j, i0 in enumerate(starts[:a.iters + 3]):  # the mono loop: warm-up + iters frames
         i1 = starts[j + 1] if j + 1 < len(starts) else len(ev)
