@@ -796,7 +796,34 @@ def kernel_table(iso, calls, pipelined_kern, n_prof, alg, batch):
 HARNESS_DIR = ROOT / "tests" / "integration_run"
 
 
-def dropin_leg(orb, imgs, maps, scale, args, threads, iters=500, nfr=16):
+def dropin_prepare(args, d, nfr=16, iters=500):
+    """The drop-in leg's inputs (child process `bench.py --dropin-prepare DIR`):
+    frames 0..nfr-1 of the bench stream (and their right views), each frame's
+    5,000-point local map built from its own keypoints exactly as the main
+    workload builds it (one-frame extraction, bit-identical to the batch's)."""
+    orb = load_package()
+    W, H, M = args.width, args.height, args.mappoints
+    d = Path(d)
+    ids = list(range(nfr))
+    imgs = synth_images(orb, args.seed, ids, W, H, 1)
+    right = synth_images(orb, args.seed, ids, W, H, 1, view=1)
+    ext = orb.ORBextractor(args.features, 1.2, 8, 20, 7)
+    tracks, descs = [], []
+    for f in ids:
+        k, dsc = ext(imgs[f])
+        mps, mpd, _ = orb.synth_local_map(args.seed + f, k, dsc, M, W, H)
+        tracks.append(np.ascontiguousarray(mps).view(np.uint8).reshape(-1))
+        descs.append(np.ascontiguousarray(mpd).reshape(-1))
+    imgs.tofile(d / "imgs.bin")
+    right.tofile(d / "imgsR.bin")
+    np.concatenate(tracks).tofile(d / "tracks.bin")
+    np.concatenate(descs).tofile(d / "mpdesc.bin")
+    np.asarray(ext.GetScaleFactors(), np.float32).tofile(d / "scale.bin")
+    (d / "meta.txt").write_text(f"{W} {H} {args.features} {M} {nfr} {iters} 386.1448 718.856")
+    ext.close()
+
+
+def dropin_leg(args, nfr=16, iters=500):
     """The reference-typed drop-ins (integration/*.cc, linked to the library by
     tests/integration_run) timed at ORB-SLAM2's own granularity, one frame per
     call: mono = ORBextractor::operator() + SearchByProjection(F, vpMapPoints)
@@ -804,42 +831,42 @@ def dropin_leg(orb, imgs, maps, scale, args, threads, iters=500, nfr=16):
     stereo = both extractions on two threads + Frame::ComputeStereoMatches.
     Both harness builds: ORB_AMD_GPU_STEREO (the recommended integration:
     nothing reads mvImagePyramid on the host) and the default (mvImagePyramid
-    mirrored to the host every call).  Median wall ms per frame / pair."""
+    mirrored to the host every call).  Median wall ms per frame / pair.
+    Run first, before this process touches the GPU: the inputs are made by a
+    child process, and the harness runs on an otherwise idle GPU, as
+    ORB-SLAM2's tracking thread would (after the batch workloads, the same
+    binary measured 0.30-0.33 ms per mono frame against 0.28-0.29 alone,
+    profiles/r06_dropin.txt)."""
     import subprocess
     import tempfile
 
-    W, H, M = args.width, args.height, args.mappoints
-    nfr = min(nfr, len(imgs), len(maps))
-    right = synth_images(orb, args.seed, list(range(nfr)), W, H, threads, view=1)
     out = {}
     with tempfile.TemporaryDirectory() as d:
-        d = Path(d)
-        np.ascontiguousarray(imgs[:nfr]).tofile(d / "imgs.bin")
-        np.ascontiguousarray(right).tofile(d / "imgsR.bin")
-        np.concatenate([np.ascontiguousarray(maps[i][0]).view(np.uint8).reshape(-1)
-                        for i in range(nfr)]).tofile(d / "tracks.bin")
-        np.concatenate([np.ascontiguousarray(maps[i][1]).reshape(-1)
-                        for i in range(nfr)]).tofile(d / "mpdesc.bin")
-        np.asarray(scale, np.float32).tofile(d / "scale.bin")
-        (d / "meta.txt").write_text(f"{W} {H} {args.features} {M} {nfr} {iters} 386.1448 718.856")
+        r = subprocess.run([sys.executable, str(Path(__file__).resolve()), "--dropin-prepare", d,
+                            "--seed", str(args.seed), "--width", str(args.width), "--height",
+                            str(args.height), "--features", str(args.features), "--mappoints",
+                            str(args.mappoints)], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            raise RuntimeError(f"dropin inputs: {r.stderr[-1000:]}")
         for key, exe in (("gpu_stereo_build", "dropin_harness_gpustereo"),
                          ("host_pyramid_build", "dropin_harness")):
             path = HARNESS_DIR / exe
             if not path.exists():
                 out[key] = f"{path.name} not built (make -C tests/integration_run)"
                 continue
-            r = subprocess.run([str(path), "time", str(d)], capture_output=True, text=True,
+            r = subprocess.run([str(path), "time", d], capture_output=True, text=True,
                                timeout=240)
             if r.returncode != 0:
                 raise RuntimeError(f"{exe} time: {r.stderr[-1000:]}")
-            out[key] = json.loads((d / "time.json").read_text())
+            out[key] = json.loads((Path(d) / "time.json").read_text())
     out["note"] = ("integration/ORBextractor.cc + ORBmatcher.cc (+ FrameStereo.cc) run by "
                    "tests/integration_run/harness.cc with stand-in cv::Mat / Frame / MapPoint, "
-                   f"1241x376 frames 0..{nfr - 1} of the bench stream (right views for stereo), "
-                   f"{args.features} feat mono / {2 * args.features} per image stereo, "
-                   f"SearchByProjection vs {M} MapPoint objects per frame, th 1, nnratio 0.8; "
-                   f"median of {iters} calls after 3 warm-up; PCIe-inclusive (host images in, "
-                   "host keypoints / descriptors / matches out)")
+                   f"{args.width}x{args.height} frames 0..{nfr - 1} of the bench stream (right "
+                   f"views for stereo), {args.features} feat mono / {2 * args.features} per image "
+                   f"stereo, SearchByProjection vs {args.mappoints} MapPoint objects per frame, "
+                   f"th 1, nnratio 0.8; median of {iters} calls after 3 warm-up; PCIe-inclusive "
+                   "(host images in, host keypoints / descriptors / matches out); run before the "
+                   "bench's workloads, on an idle GPU")
     return out
 
 
@@ -884,6 +911,7 @@ def main():
                     help="wall-clock sample of the all-cores oracle rate (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3 / C5 extra keys")
+    ap.add_argument("--dropin-prepare", metavar="DIR", help=argparse.SUPPRESS)
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the per-frame drop-in timing (tests/integration_run harness)")
     ap.add_argument("--threads", type=int, default=16, help="host threads for input synthesis")
@@ -909,11 +937,18 @@ def main():
                          "its extraction")
     args = ap.parse_args()
 
+    if args.dropin_prepare:  # child of dropin_leg
+        dropin_prepare(args, args.dropin_prepare)
+        return
     world, spawn = resolve_world(args.gpus, os.environ)
     if spawn:  # before any torch / HIP call in this process
         raise SystemExit(launch_ranks(world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dropin = None
+    if rank == 0 and world == 1 and not args.no_dropin and local == 0 \
+            and os.environ.get("ORB_BENCH_DEVICE") is None:
+        dropin = dropin_leg(args)  # first: before this process touches the GPU
     import torch
 
     if os.environ.get("ORB_BENCH_DEVICE") is not None:
@@ -1295,8 +1330,8 @@ def main():
         if args.host_frames <= 0:
             del d_img
         result.update(secondary_configs(orb, torch, args, dev, args.threads))
-    if rank == 0 and world == 1 and not args.no_dropin:
-        result["dropin"] = dropin_leg(orb, imgs, maps, scale, args, args.threads)
+    if dropin is not None:
+        result["dropin"] = dropin
     parity_ok = True
     if rank == 0:
         cpu_b, par = cpu_leg(imgs, maps, sample, args, scale, world == 1 and not args.no_cpu)

@@ -2388,11 +2388,19 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
       pitch = L.pitch;
     }
     const ImgRsrc im = img_rsrc(lvl, (uint32_t)((L.h - 1) * pitch + L.w));
+    // The realignment code: 0..3 = shift left by that many bytes (the row
+    // starts inside the first loaded dword); 4 + s = shift right by s bytes:
+    // the window of row 0 starts s bytes before the level's first byte
+    // (cx - 21 + sh < 0: a keypoint 19 or 20 px from the left edge), so the
+    // row is loaded from byte 0 and moved right (its first s bytes are
+    // columns < 0, which the column patch below fills from their reflections).
+    // Loading from the negative offset put the first 16 bytes out of the
+    // buffer's range (read as 0): wrong blurred samples near the top-left corner.
     auto load_row = [&](int r, uint32_t* d) {
       int y = P.cy - 21 + r;
       y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
-      const uint32_t o = (uint32_t)(y * pitch + P.cx - 21) + im.sh;
-      const uint32_t a0 = o & ~3u;
+      const int o = y * pitch + P.cx - 21 + (int)im.sh;
+      const uint32_t a0 = o < 0 ? 0u : ((uint32_t)o & ~3u);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(im.r, (int)(a0 + 16 * k), 0, 0);
@@ -2401,7 +2409,7 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
         d[4 * k + 2] = (uint32_t)v[2];
         d[4 * k + 3] = (uint32_t)v[3];
       }
-      return o & 3u;
+      return o < 0 ? 4u + (uint32_t)(-o) : ((uint32_t)o & 3u);
     };
     if (second) {
       sha = load_row(2 * hl, ra);
@@ -2409,9 +2417,16 @@ __global__ DESC_LAUNCH_BOUNDS void k_orient_desc(
     }
   };
   auto realign = [&](uint32_t* d, uint32_t sh) {
+    if (sh < 4) {
 #pragma unroll
-    for (int k = 0; k < 11; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-    d[11] = __builtin_amdgcn_alignbyte(0u, d[11], sh);
+      for (int k = 0; k < 11; ++k) d[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      d[11] = __builtin_amdgcn_alignbyte(0u, d[11], sh);
+    } else {  // right by sh - 4 bytes (row 0 of a window over the left edge)
+      const uint32_t rs = 8u - sh;
+#pragma unroll
+      for (int k = 11; k > 0; --k) d[k] = __builtin_amdgcn_alignbyte(d[k], d[k - 1], rs);
+      d[0] = __builtin_amdgcn_alignbyte(d[0], 0u, rs);
+    }
   };
   auto store_row = [&](uint32_t* rowp, const uint32_t* d) {
     uint4* dst = reinterpret_cast<uint4*>(rowp);

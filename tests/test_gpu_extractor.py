@@ -318,6 +318,57 @@ def _batch_vs_oracle(gpu, oracle, imgs, nf=1000, sf=1.2, nl=8):
         assert desc[f, : cnt[f]].tobytes() == dr.tobytes(), f
 
 
+BENCH_SEED = 0x4B495454  # bench.py's default --seed
+# frames of the bench stream with a keypoint 19-20 px from the top-left corner
+# whose rotated pattern samples reach rows 0-3 (tools/probe/stream_parity.py:
+# 43 of the stream's 8,192 frames, all on level 0)
+CORNER_FRAMES = [577, 587, 597, 628, 2829, 3299, 3304, 3306]
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_orient_window_over_top_left_corner(gpu, oracle, shift):
+    """k_orient_desc stages each keypoint's 43-row window from the 4-aligned
+    byte at or below column cx - 21.  For a keypoint at x = 19 or 20 that byte
+    lies before the level's first byte in row 0 (a negative offset: the first
+    16-byte load fell out of the buffer's range and read as zeros, so a
+    descriptor bit or two of such keypoints differed from the reference's on
+    43 of the bench's 8,192 frames).  Row 0 is now loaded from byte 0 and
+    shifted right.  The bench frames that showed it, through the batch entry
+    point with the images `shift` bytes past a 4-byte boundary (the offset's
+    sign depends on it) and through the one-frame path."""
+    torch = pytest.importorskip("torch")
+    w, h, B = 1241, 376, len(CORNER_FRAMES)
+    imgs = [gpu.synth_image(BENCH_SEED, f, w, h) for f in CORNER_FRAMES]
+    pitch = w * h + 4
+    buf = np.zeros(pitch * B + 16, np.uint8)
+    for f, im in enumerate(imgs):
+        buf[shift + f * pitch: shift + f * pitch + w * h] = im.reshape(-1)
+    ext = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    cap = ext.capacity(w, h)
+    d_buf = torch.from_numpy(buf).cuda()
+    d_kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ext.extract_batch(d_buf.data_ptr() + shift, B, w, h, w, pitch, d_kps.data_ptr(),
+                      d_desc.data_ptr(), cap, d_cnt.data_ptr())
+    torch.cuda.synchronize()
+    kps = d_kps.cpu().numpy().view(gpu.KEYPOINT_DTYPE).reshape(B, cap)
+    desc = d_desc.cpu().numpy()
+    cnt = d_cnt.cpu().numpy()
+    for f in range(B):
+        kr, dr, _ = oracle.extract(imgs[f], 1000, 1.2, 8, 20, 7)
+        corner = (kr["x"] <= 20.5) & (kr["y"] <= 21.5) & (kr["octave"] == 0)
+        assert corner.any(), CORNER_FRAMES[f]  # the case is really exercised
+        assert cnt[f] == len(kr)
+        assert kps[f, : cnt[f]].tobytes() == kr.tobytes(), CORNER_FRAMES[f]
+        bad = np.nonzero((desc[f, : cnt[f]] != dr).any(1))[0]
+        assert len(bad) == 0, (CORNER_FRAMES[f], kr[bad][:4])
+        if shift == 0:
+            k1, d1 = ext(imgs[f])
+            assert k1.tobytes() == kr.tobytes() and np.array_equal(d1, dr), CORNER_FRAMES[f]
+
+
 def test_batch_hard_cases_vs_oracle(gpu, oracle):
     """Batches of >= 4 frames take the one-wave-per-cell FAST kernel (level 0 on
     the side stream); single frames take the band kernel.  The hard single-frame
