@@ -4,6 +4,11 @@ of any mismatch: which keypoints, their level / position / angle, how many
 descriptor bits differ, and what the one-frame path gives for that frame.
 
   stream_parity.py [--frames 8192] [--start 0] [--batch 1024] [--threads 16]
+                   [--width W --height H --features N] [--match M]
+
+--match M: also SearchByProjection(F, localMap) of every frame against its own
+M-point synthetic local map (bench.py's maps), device-batched, against the
+oracle's assignments.
 """
 import argparse
 import json
@@ -28,6 +33,7 @@ def main():
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--features", type=int, default=1000)
+    ap.add_argument("--match", type=int, default=0)
     a = ap.parse_args()
     import torch
     from conftest import load_pkg
@@ -84,6 +90,57 @@ def main():
         res = list(ex.map(check, range(len(ids))))
     bad = [(i, r) for i, r in res if r is not None]
     print(f"{len(bad)} of {len(ids)} frames differ from the oracle", flush=True)
+    if a.match:
+        M = a.match
+        scale = np.float32(ext.GetScaleFactors())
+        maps = [None] * len(ids)
+
+        def mk(i):
+            n = int(n_all[i])
+            maps[i] = orb.synth_local_map(a.seed + ids[i], k_all[i, :n], d_all[i, :n], M, W, H)
+        with ThreadPoolExecutor(a.threads) as ex:
+            list(ex.map(mk, range(len(ids))))
+        mt = orb.ORBmatcher(0.8)
+        km_all = np.zeros((len(ids), cap), np.int32)
+        nm_all = np.zeros(len(ids), np.int32)
+        for b0 in range(0, len(ids), B):
+            nb = min(B, len(ids) - b0)
+            mps = np.stack([maps[i][0] for i in range(b0, b0 + nb)])
+            mpd = np.stack([maps[i][1] for i in range(b0, b0 + nb)])
+            lk = np.zeros((nb, cap), np.uint8)
+            for j in range(nb):
+                lk[j, :n_all[b0 + j]] = maps[b0 + j][2]
+            t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)
+            dk, dd, dl = t(k_all[b0:b0 + nb]), t(d_all[b0:b0 + nb]), t(lk)
+            dm, dmd = t(mps), t(mpd)
+            dn = torch.from_numpy(n_all[b0:b0 + nb].copy()).to(dev)
+            dnm = torch.full((nb,), M, dtype=torch.int32, device=dev)
+            dkm = torch.zeros((nb, cap), dtype=torch.int32, device=dev)
+            dnmt = torch.zeros(nb, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            mt.search_by_projection_batch(nb, dk.data_ptr(), dd.data_ptr(), dn.data_ptr(),
+                                          dl.data_ptr(), cap, dm.data_ptr(), dmd.data_ptr(),
+                                          dnm.data_ptr(), M, W, H, scale, 1.0, dkm.data_ptr(),
+                                          dnmt.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            km_all[b0:b0 + nb] = dkm.cpu().numpy()
+            nm_all[b0:b0 + nb] = dnmt.cpu().numpy()
+
+        def mcheck(i):
+            n = int(n_all[i])
+            mps, mpd, lk = maps[i]
+            n_ref, km_ref = oracle.match_projection_local(k_all[i, :n], d_all[i, :n], scale, W, H,
+                                                          mps, mpd, 1.0, 0.8, lk)
+            ok = n_ref == nm_all[i] and np.array_equal(km_all[i, :n], km_ref)
+            return i, None if ok else {"nmatch": [int(nm_all[i]), int(n_ref)],
+                                       "kp_diff": int((km_all[i, :n] != km_ref).sum())}
+        with ThreadPoolExecutor(a.threads) as ex:
+            mres = list(ex.map(mcheck, range(len(ids))))
+        mbad = [(i, r) for i, r in mres if r is not None]
+        print(f"SearchByProjection vs {M} map points: {len(mbad)} of {len(ids)} frames differ "
+              f"(mean matches {nm_all.mean():.1f})", flush=True)
+        for i, r in mbad[:10]:
+            print(json.dumps({"frame": ids[i], **r}), flush=True)
     for i, r in bad[:12]:
         single = None
         k1, d1 = ext(imgs[i])
