@@ -16,12 +16,39 @@ __device__ __forceinline__ int grid_cell(const orb_keypoint_t& k, float minX, fl
   return px * ORB_GRID_ROWS + py;
 }
 
+// Candidate lists of the map points with more than TOPK candidates: the
+// resolves' exact re-scan of such a point (its top-K ran dry: too many of its
+// candidates taken) reads the list instead of walking the grid -- one thread's
+// chain of dependent grid, keypoint and descriptor loads (15-30 us per point,
+// the whole workgroup waiting on it: one-frame SearchByProjection 40-150 us
+// instead of 21 us on the frames that had one, profiles/r06_dropin.txt).
+// k_proj_candidates writes the list of a point with TOPK < count <= OVF_CAP
+// (its window candidates that pass the level, lock and stereo tests, in scan
+// order, packed as the top-K entries) into one of OVF_SLOTS lists per problem;
+// a point past OVF_CAP or beyond the slots keeps the grid re-scan.
+#define OVF_CAP 16
+#define OVF_SLOTS 512
 struct ProjParams {
   float minX, minY, invW, invH;
   float th, nnratio;
   int nLevels;
   float scale[ORB_MAX_LEVELS];
+  uint32_t* ovf;     // OVF_SLOTS x OVF_CAP entries per problem, or null (no lists)
+  uint32_t* ovfCtr;  // per problem: the call's gen << 20 | slots taken
+  uint32_t gen;      // 1..4095, a new value per call (no reset of ovfCtr needed)
 };
+
+// A list slot of problem counter `ctr` for the call `gen`: the first
+// allocation of a call finds another call's tag and restarts the count.
+__device__ __forceinline__ int ovf_alloc(uint32_t* ctr, uint32_t gen) {
+  uint32_t v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (true) {
+    const uint32_t n = (v >> 20) == gen ? v + 1u : ((gen << 20) | 1u);
+    const uint32_t old = atomicCAS(ctr, v, n);
+    if (old == v) return (int)(n & 0xFFFFFu) - 1;
+    v = old;
+  }
+}
 
 // Top-K entry: keypoint index (19b) | distance (9b) << 19 | octave (4b) << 28.
 __device__ __forceinline__ uint32_t pack_cand(int idx, int dist, int oct) {

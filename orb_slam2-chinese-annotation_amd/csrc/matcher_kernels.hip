@@ -320,9 +320,16 @@ __global__ __launch_bounds__(256) void k_grid_build4(const orb_keypoint_t* __res
 // ncand of the projection matcher: the candidate count, with the point's
 // has_obs (a claim by it locks the keypoint) in bit 30, so the resolve reads one
 // word per point for both; -1 = not in view / bad
+// and (bits 19-29) 1 + the slot of its candidate list (0: none, ProjParams.ovf)
 #define NC_OBS 0x40000000
-__device__ __forceinline__ int nc_count(int v) { return v < 0 ? v : (v & (NC_OBS - 1)); }
+#define NC_SLOT_SHIFT 19
+__device__ __forceinline__ int nc_count(int v) { return v < 0 ? v : (v & ((1 << NC_SLOT_SHIFT) - 1)); }
 __device__ __forceinline__ bool nc_obs(int v) { return v >= 0 && (v & NC_OBS) != 0; }
+__device__ __forceinline__ int nc_slot(int v) { return v < 0 ? -1 : ((v >> NC_SLOT_SHIFT) & 0x7FF) - 1; }
+// problem p's list `slot` (nc_slot >= 0 only when ProjParams.ovf is set)
+__device__ __forceinline__ const uint32_t* ovf_list(const ProjParams& P, int p, int slot) {
+  return P.ovf + ((size_t)p * OVF_SLOTS + slot) * OVF_CAP;
+}
 
 // PPT: map points per thread (a workgroup covers WG * PPT points, the grid
 // staged once for all of them)
@@ -429,9 +436,37 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
     ++count;
     top.insert(pack_cand(idx, dist, oct), dist);
   };
+  // GetFeaturesInArea (src/Frame.cc:368-424) over the staged grid: fn(idx |
+  // octave << 24) for every window keypoint passing the level, lock and stereo
+  // tests, in scan order
+  auto walk = [&](auto&& fn) {
+    const float x = mp.proj_x, y = mp.proj_y;
+    const int nMinCellX = max(0, (int)floorf((x - P.minX - rs) * P.invW));
+    const int nMaxCellX = min(ORB_GRID_COLS - 1, (int)ceilf((x - P.minX + rs) * P.invW));
+    const int nMinCellY = max(0, (int)floorf((y - P.minY - rs) * P.invH));
+    const int nMaxCellY = min(ORB_GRID_ROWS - 1, (int)ceilf((y - P.minY + rs) * P.invH));
+    if (nMinCellX >= ORB_GRID_COLS || nMaxCellX < 0 || nMinCellY >= ORB_GRID_ROWS || nMaxCellY < 0)
+      return;
+    const int minL = lvl - 1, maxL = lvl;
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+      for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
+        const int c = ix * ORB_GRID_ROWS + iy;
+        const int e = gCS[c + 1];
+        for (int j = gCS[c]; j < e; ++j) {
+          const uint4 E = gKp[j];
+          const int oct = (int)((E.z >> 24) & 0x7Fu);
+          if (oct < minL || oct > maxL) continue;
+          const float dx = __uint_as_float(E.x) - x, dy = __uint_as_float(E.y) - y;
+          if (!(fabsf(dx) < rs && fabsf(dy) < rs) || (E.z >> 31) != 0) continue;
+          const float ur = __uint_as_float(E.w);
+          if (ur > 0 && fabsf(mp.proj_xr - ur) > rs) continue;
+          fn((E.z & 0xFFFFFFu) | ((uint32_t)oct << 24));
+        }
+      }
+    }
+  };
   if (staged) {
-    // GetFeaturesInArea (src/Frame.cc:368-424) over the staged grid.  Window
-    // candidates that pass the lock and stereo tests queue up (scan order) and
+    // Window candidates that pass the lock and stereo tests queue up (scan order) and
     // are scored PROJ_QB at a time, so their descriptor loads overlap.
     // the queue lives in registers (qe[k] written through selects, no LDS:
     // C5's staged frame already takes 76 KB of LDS per workgroup)
@@ -453,37 +488,14 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
         top.insert(pack_cand((int)(qe[k] & 0xFFFFFFu), dist, (int)(qe[k] >> 24)), dist);
       }
     };
-    const float x = mp.proj_x, y = mp.proj_y;
-    const int nMinCellX = max(0, (int)floorf((x - P.minX - rs) * P.invW));
-    const int nMaxCellX = min(ORB_GRID_COLS - 1, (int)ceilf((x - P.minX + rs) * P.invW));
-    const int nMinCellY = max(0, (int)floorf((y - P.minY - rs) * P.invH));
-    const int nMaxCellY = min(ORB_GRID_ROWS - 1, (int)ceilf((y - P.minY + rs) * P.invH));
-    if (nMinCellX < ORB_GRID_COLS && nMaxCellX >= 0 && nMinCellY < ORB_GRID_ROWS &&
-        nMaxCellY >= 0) {
-      const int minL = lvl - 1, maxL = lvl;
-      for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
-        for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
-          const int c = ix * ORB_GRID_ROWS + iy;
-          const int e = gCS[c + 1];
-          for (int j = gCS[c]; j < e; ++j) {
-            const uint4 E = gKp[j];
-            const int oct = (int)((E.z >> 24) & 0x7Fu);
-            if (oct < minL || oct > maxL) continue;
-            const float dx = __uint_as_float(E.x) - x, dy = __uint_as_float(E.y) - y;
-            if (!(fabsf(dx) < rs && fabsf(dy) < rs) || (E.z >> 31) != 0) continue;
-            const float ur = __uint_as_float(E.w);
-            if (ur > 0 && fabsf(mp.proj_xr - ur) > rs) continue;
-            const uint32_t qv = (E.z & 0xFFFFFFu) | ((uint32_t)oct << 24);
+    walk([&](uint32_t qv) {
 #pragma unroll
-            for (int k = 0; k < PROJ_QB; ++k) qe[k] = nq == k ? qv : qe[k];
-            if (++nq == PROJ_QB) {
-              flush(PROJ_QB);
-              nq = 0;
-            }
-          }
-        }
+      for (int k = 0; k < PROJ_QB; ++k) qe[k] = nq == k ? qv : qe[k];
+      if (++nq == PROJ_QB) {
+        flush(PROJ_QB);
+        nq = 0;
       }
-    }
+    });
     if (nq) flush(nq);
   } else {
     for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
@@ -492,7 +504,32 @@ __global__ __launch_bounds__(WG) void k_proj_candidates(
                          });
   }
   top.store(topk + mg * TOPK);
-  ncand[mg] = count | (mp.has_obs ? NC_OBS : 0);
+  // more candidates than the top-K holds: the whole list, in scan order, for
+  // the resolves' re-scan (a second walk of the window; rare: C4's maps have
+  // at most 4-6 candidates per point)
+  int slot = -1;
+  if (count > TOPK && count <= OVF_CAP && P.ovf) {
+    slot = ovf_alloc(P.ovfCtr + p, P.gen);
+    if (slot >= OVF_SLOTS) slot = -1;
+  }
+  if (slot >= 0) {
+    uint32_t* lst = P.ovf + ((size_t)p * OVF_SLOTS + slot) * OVF_CAP;
+    int n = 0;
+    auto put = [&](int idx, int oct) {
+      const int dist = hamming256(q, load_desc(D + (size_t)idx * 32));
+      if (dist < 256 && n < OVF_CAP) lst[n++] = pack_cand(idx, dist, oct);
+    };
+    if (staged)
+      walk([&](uint32_t qv) { put((int)(qv & 0xFFFFFFu), (int)(qv >> 24)); });
+    else
+      for_features_in_area(K, cs, ci, P, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl,
+                           [&](int idx, const orb_keypoint_t& kp) {
+                             if ((LK && LK[idx]) || (UR && UR[idx] > 0 && fabsf(mp.proj_xr - UR[idx]) > rs))
+                               return;
+                             put(idx, kp.octave);
+                           });
+  }
+  ncand[mg] = count | (mp.has_obs ? NC_OBS : 0) | ((slot + 1) << NC_SLOT_SHIFT);
   }
 }
 
@@ -555,7 +592,7 @@ __global__ __launch_bounds__(64 * NW) void k_proj_resolve(
         if (m < M) {
           cTop[j] = *reinterpret_cast<const uint4*>(topk + (pbase + m) * TOPK);
           const int v = ncand[pbase + m];
-          cN[j] = nc_count(v);
+          cN[j] = v;  // raw: count, obs, list slot
           cObs[j] = nc_obs(v);
         }
       }
@@ -563,12 +600,13 @@ __global__ __launch_bounds__(64 * NW) void k_proj_resolve(
     }
     const int m = start + t;
     const bool active = m < M;
-    int nc = -1;
+    int nc = -1, ncRaw = -1;
     uint32_t e[TOPK];
     bool hasObs = false;
     if (active) {
       const int j = m - cb;
-      nc = cN[j];
+      ncRaw = cN[j];
+      nc = nc_count(ncRaw);
       const uint4 t4 = cTop[j];
       e[0] = t4.x; e[1] = t4.y; e[2] = t4.z; e[3] = t4.w;
       hasObs = cObs[j] != 0;
@@ -594,6 +632,7 @@ __global__ __launch_bounds__(64 * NW) void k_proj_resolve(
       }
     }
     const bool slow = nc > TOPK && found < 2;
+    const int slowSlot = nc_slot(ncRaw);
     bool accept = false;
     if (nc > 0 && !slow && bestDist <= 100)
       accept = !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2);
@@ -613,7 +652,26 @@ __global__ __launch_bounds__(64 * NW) void k_proj_resolve(
     for (int i = 0; i < NW; ++i) commit = min(commit, sFirst[i]);
     if (sSlow) {
       // exact re-scan of the first point of the window, thread 0, current locks
-      if (t == 0) {
+      if (t == 0 && slowSlot >= 0) {  // the point's candidate list (scan order)
+        const uint32_t* lst = ovf_list(P, p, slowSlot);
+        int bd = 256, bl = -1, bd2 = 256, bl2 = -1, bi = -1;
+        for (int j = 0; j < nc; ++j) {
+          const uint32_t ce = lst[j];
+          const int idx = cand_idx(ce);
+          if (lock_test(bm, idx)) continue;
+          const int dist = cand_dist(ce);
+          if (dist < bd) {
+            bd2 = bd; bd = dist; bl2 = bl; bl = cand_oct(ce); bi = idx;
+          } else if (dist < bd2) {
+            bl2 = cand_oct(ce); bd2 = dist;
+          }
+        }
+        if (bd <= 100 && !(bl == bl2 && (float)bd > nnratio * (float)bd2)) {
+          atomicMax(&km[bi], m);
+          if (cObs[m - cb]) bm[bi >> 5] |= 1u << (bi & 31);
+          ++matches;
+        }
+      } else if (t == 0) {
         const size_t mg = pbase + m;
         const orb_mp_track_t mp = mps[mg];
         const int lvl = mp.level;
@@ -687,9 +745,38 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __noinline__ int fp_slow(int m, const int* cur, const orb_mp_track_t* mpp,
                                     const uint8_t* mpd, const orb_keypoint_t* K, const uint8_t* D,
                                     const uint8_t* LK, const float* UR, const int32_t* cs,
-                                    const int32_t* ci, const ProjParams P) {
+                                    const int32_t* ci, const ProjParams P, const uint32_t* lst,
+                                    int nl) {
   // (P by value: a reference would put the caller's copy in scratch memory
   // and every fp_choose would read nnratio from there)
+  if (lst) {  // the point's candidate list (scan order; static tests applied)
+    uint32_t e[OVF_CAP];
+#pragma unroll
+    for (int j = 0; j < OVF_CAP; j += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(lst + j);
+      e[j] = v.x; e[j + 1] = v.y; e[j + 2] = v.z; e[j + 3] = v.w;
+    }
+    // every claim read issued before any is used (entries past nl read entry
+    // 0's keypoint and are ignored): one memory round trip
+    int cv[OVF_CAP];
+#pragma unroll
+    for (int j = 0; j < OVF_CAP; ++j) cv[j] = cur[cand_idx(j < nl ? e[j] : e[0])];
+    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+#pragma unroll
+    for (int j = 0; j < OVF_CAP; ++j) {
+      if (j >= nl || cv[j] < m) continue;
+      const int dist = cand_dist(e[j]);
+      if (dist < bestDist) {
+        bestDist2 = bestDist; bestDist = dist;
+        bestLevel2 = bestLevel; bestLevel = cand_oct(e[j]); bestIdx = cand_idx(e[j]);
+      } else if (dist < bestDist2) {
+        bestLevel2 = cand_oct(e[j]); bestDist2 = dist;
+      }
+    }
+    const bool accept = bestIdx >= 0 && bestDist <= 100 &&
+                        !(bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2);
+    return accept ? bestIdx : -1;
+  }
   const orb_mp_track_t mp = *mpp;
   const int lvl = mp.level;
   float r = (double)mp.view_cos > 0.998 ? 2.5f : 4.0f;
@@ -725,7 +812,8 @@ __device__ __forceinline__ int fp_choose(const uint32_t (&e)[TOPK], int nc, int 
                                          const orb_mp_track_t* mpp, const uint8_t* mpd,
                                          const orb_keypoint_t* K, const uint8_t* D,
                                          const uint8_t* LK, const float* UR, const int32_t* cs,
-                                         const int32_t* ci, const ProjParams& P) {
+                                         const int32_t* ci, const ProjParams& P,
+                                         const uint32_t* lst) {
   int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
   int found = 0;
   const int avail = nc < TOPK ? nc : TOPK;
@@ -749,7 +837,7 @@ __device__ __forceinline__ int fp_choose(const uint32_t (&e)[TOPK], int nc, int 
     found += use ? 1 : 0;
   }
   // top-K ran dry: exact scan of the point's area under the same locks
-  if (nc > TOPK && found < 2) return fp_slow(m, cur, mpp, mpd, K, D, LK, UR, cs, ci, P);
+  if (nc > TOPK && found < 2) return fp_slow(m, cur, mpp, mpd, K, D, LK, UR, cs, ci, P, lst, nc);
   const bool accept = bestIdx >= 0 && bestDist <= 100 &&
                       !(bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2);
   return accept ? bestIdx : -1;
@@ -852,12 +940,15 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
   auto window = [&](int start, In (&in)[PPT]) {
     uint32_t e[PPT][TOPK];
     int nc[PPT], prev[PPT], acc[PPT];
+    const uint32_t* lst[PPT];
     bool obs[PPT];
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
       const int m = start + k * T + t;
       e[k][0] = in[k].e.x; e[k][1] = in[k].e.y; e[k][2] = in[k].e.z; e[k][3] = in[k].e.w;
       nc[k] = m < M ? nc_count(in[k].nc) : -1;
+      const int sl = m < M ? nc_slot(in[k].nc) : -1;
+      lst[k] = sl >= 0 ? ovf_list(P, p, sl) : nullptr;
       obs[k] = m < M && nc_obs(in[k].nc);
       prev[k] = -1;  // this point's claim in the previous round
       acc[k] = -1;
@@ -870,7 +961,7 @@ __global__ __launch_bounds__(T) void k_proj_resolve_fp(
       for (int k = 0; k < PPT; ++k) {
         const int m = start + k * T + t;
         acc[k] = nc[k] > 0 ? fp_choose(e[k], nc[k], m, cur, mps + pbase + m, mpDesc + (pbase + m) * 32,
-                                       K, D, LK, UR, cs, ci, P)
+                                       K, D, LK, UR, cs, ci, P, lst[k])
                            : -1;
         const int claim = obs[k] ? acc[k] : -1;
         if (claim >= 0) atomicMin(&nxt[claim], m);
@@ -1052,11 +1143,13 @@ __global__ __launch_bounds__(JAC_T) void k_proj_jacobi(
     int acc = -1;
     if (nc > 0) {
       const uint32_t e[TOPK] = {q[k].x, q[k].y, q[k].z, q[k].w};
+      const int sl = nc_slot(ncv[k]);
       acc = fp_choose(e, nc, m, cur, mps + pbase + m, mpDesc + (pbase + m) * 32,
                       keys + (size_t)p * kpStride, desc + (size_t)p * kpStride * 32,
                       locked ? locked + (size_t)p * kpStride : nullptr,
                       uright ? uright + (size_t)p * kpStride : nullptr,
-                      cellStart + (size_t)p * (GRID_CELLS + 1), cellIdx + (size_t)p * kpStride, P);
+                      cellStart + (size_t)p * (GRID_CELLS + 1), cellIdx + (size_t)p * kpStride, P,
+                      sl >= 0 ? ovf_list(P, p, sl) : nullptr);
     }
     dec[m] = acc;
     const bool obs = acc >= 0 && hasObs;
@@ -1294,6 +1387,11 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
 }
 
 size_t orb_k_proj_params_size(void) { return sizeof(ProjParams); }
+
+// bytes of the candidate-list pool (ProjParams.ovf) of n problems
+size_t orb_k_proj_ovf_bytes(int nproblems) {
+  return (size_t)std::max(nproblems, 1) * OVF_SLOTS * OVF_CAP * 4;
+}
 
 
 }  // extern "C"

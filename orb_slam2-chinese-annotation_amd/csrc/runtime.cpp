@@ -98,6 +98,7 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
 int orb_k_proj_resolve_kernel(int nproblems, int kpStride, int mpStride, int schedule);
 size_t orb_k_proj_jacobi_bytes(int kpStride, int mpStride, int nproblems, int schedule);
 size_t orb_k_proj_params_size(void);
+size_t orb_k_proj_ovf_bytes(int nproblems);
 size_t orb_k_stereo_params_size(void);
 hipError_t orb_k_stereo(const orb_keypoint_t* lkeys, const uint8_t* ldesc, const int32_t* nleft,
                         const orb_keypoint_t* rkeys, const uint8_t* rdesc, const int32_t* nright,
@@ -1509,11 +1510,14 @@ static FrustumParamsHost frustum_params(const orb_camera_t* cam, float min_x, fl
   return f;
 }
 
-struct ProjParamsHost {  // mirrors ProjParams in matcher_kernels.hip
+struct ProjParamsHost {  // mirrors ProjParams in matcher_common.h
   float minX, minY, invW, invH;
   float th, nnratio;
   int nLevels;
   float scale[ORB_MAX_LEVELS];
+  uint32_t* ovf;
+  uint32_t* ovfCtr;
+  uint32_t gen;
 };
 
 struct StereoParamsHost {  // mirrors StereoParams in matcher_kernels.hip
@@ -1569,6 +1573,8 @@ struct orb_matcher {
   DevBuf dKeys, dDesc, dUr, dLocked, dNKeys, dMps, dMpDesc, dNMps, dCellStart, dCellIdx, dTopk,
       dNcand, dKpMatch, dNMatch, dA, dB, dOut;
   DevBuf dJac;  // Jacobi-resolve scratch (ORB_RESOLVE_JACOBI)
+  DevBuf dOvf, dOvfCtr;  // candidate lists of SearchByProjection(F, localMap) (ProjParams.ovf)
+  uint32_t ovfGen = 0;
   int stagedN = -1, stagedM = -1;  // orb_match_projection_local_stage's layout
   bool begun = false, begunStereo = false, begunLocked = false;  // _begin sent the frame's part
   int resolveSchedule = ORB_RESOLVE_AUTO;  // orb_matcher_set_resolve
@@ -1655,7 +1661,7 @@ void orb_matcher_destroy(orb_matcher_t* m) {
                     &m->dMapPts, &m->dPose, &m->dTracks, &m->dNInView, &m->dK1, &m->dD1,
                     &m->dK2, &m->dD2, &m->dN1, &m->dN2, &m->dPrev, &m->dList, &m->dM12,
                     &m->dOffs, &m->dObsDesc, &m->dBest, &m->dBestDesc, &m->dInitQ,
-                    &m->dInitStage, &m->dInitCounts};
+                    &m->dInitStage, &m->dInitCounts, &m->dOvf, &m->dOvfCtr};
   for (DevBuf* b : bufs) b->release();
   m->hPyr.release();
   m->hIn.release();
@@ -1694,6 +1700,22 @@ static ProjParamsHost proj_params(float min_x, float max_x, float min_y, float m
   return P;
 }
 
+// The candidate-list pool of n problems for this call (ProjParams.ovf): the
+// per-problem slot counters are tagged with the call's gen, so they need no
+// reset between calls -- only a zero fill when (re)allocated.
+static orb_status_t ovf_pool(orb_matcher_t* m, int nproblems, ProjParamsHost& P, hipStream_t s) {
+  orb_status_t st;
+  if ((st = m->dOvf.ensure(orb_k_proj_ovf_bytes(nproblems)))) return st;
+  const void* old = m->dOvfCtr.p;
+  if ((st = m->dOvfCtr.ensure((size_t)std::max(nproblems, 1) * 4))) return st;
+  if (m->dOvfCtr.p != old) HIP_TRY(hipMemsetAsync(m->dOvfCtr.p, 0, m->dOvfCtr.bytes, s));
+  m->ovfGen = m->ovfGen % 4095u + 1u;
+  P.ovf = m->dOvf.as<uint32_t>();
+  P.ovfCtr = m->dOvfCtr.as<uint32_t>();
+  P.gen = m->ovfGen;
+  return ORB_OK;
+}
+
 orb_status_t orb_match_projection_local_batch(
     orb_matcher_t* m, int n_problems, const orb_keypoint_t* d_keys, const uint8_t* d_desc,
     const int32_t* d_nkeys, const uint8_t* d_locked, int kp_stride,
@@ -1711,9 +1733,10 @@ orb_status_t orb_match_projection_local_batch(
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
   CallOrder order(m->evLast, &m->lastStream, s);
   if (order.status) return order.status;
-  const ProjParamsHost P =
+  ProjParamsHost P =
       proj_params(min_x, max_x, min_y, max_y, n_levels, scale_factors, th, nnratio);
   orb_status_t st;
+  if ((st = ovf_pool(m, n_problems, P, s))) return st;
   if ((st = m->dCellStart.ensure((size_t)n_problems * (ORB_GRID_COLS * ORB_GRID_ROWS + 1) * 4)))
     return st;
   if ((st = m->dCellIdx.ensure((size_t)n_problems * kp_stride * 4))) return st;
@@ -1880,8 +1903,9 @@ static orb_status_t local_run(orb_matcher_t* m, int N, int M, const orb_frame_t*
   hipStream_t s = m->stream;
   CallOrder order(m->evLast, &m->lastStream, s);
   if (order.status) return order.status;
-  const ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
-                                       F->scale_factors, th, nnratio);
+  ProjParamsHost P = proj_params(F->min_x, F->max_x, F->min_y, F->max_y, F->n_levels,
+                                 F->scale_factors, th, nnratio);
+  if ((st = ovf_pool(m, 1, P, s))) return st;
   if (!begun) {
     if ((st = local_front(m, N, L, P, urOn, lkOn, L.inBytes, s))) return st;
   } else if (L.inBytes > L.oMps) {  // the map's part of the block
