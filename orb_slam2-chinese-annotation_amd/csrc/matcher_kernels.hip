@@ -1306,6 +1306,12 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
 #endif
 #define RESOLVE_FP_MIN_MAP 20000
 #define RESOLVE_FP_FEW 8
+#ifndef RESOLVE_AUTO_FP
+#define RESOLVE_AUTO_FP 0  // 1: every call takes the fixed-point kernel (A/B knob)
+#endif
+#ifndef RESOLVE_W1_MIN
+#define RESOLVE_W1_MIN 128  // calls of at least this many problems take k_proj_resolve<1> (A/B knob)
+#endif
 #define RESOLVE_FP_LDS_MAX (160 * 1024 - 1024)
 
 int orb_k_proj_resolve_kernel(int nproblems, int kpStride, int mpStride, int schedule) {
@@ -1313,11 +1319,12 @@ int orb_k_proj_resolve_kernel(int nproblems, int kpStride, int mpStride, int sch
   if (fpFits) {
     if (schedule == ORB_RESOLVE_JACOBI) return ORB_RESOLVE_KERNEL_JACOBI;
     if (schedule == ORB_RESOLVE_FIXED_POINT) return ORB_RESOLVE_KERNEL_FIXED_POINT;
-    if (schedule == ORB_RESOLVE_AUTO && (mpStride >= RESOLVE_FP_MIN_MAP || nproblems <= RESOLVE_FP_FEW))
+    if (schedule == ORB_RESOLVE_AUTO && (mpStride >= RESOLVE_FP_MIN_MAP || nproblems <= RESOLVE_FP_FEW ||
+                                         RESOLVE_AUTO_FP))
       return ORB_RESOLVE_KERNEL_FIXED_POINT;
   }
   if (mpStride >= RESOLVE_FP_MIN_MAP) return ORB_RESOLVE_KERNEL_PREFIX_W8;
-  return nproblems >= 128 ? ORB_RESOLVE_KERNEL_PREFIX_W1 : ORB_RESOLVE_KERNEL_PREFIX_W4;
+  return nproblems >= RESOLVE_W1_MIN ? ORB_RESOLVE_KERNEL_PREFIX_W1 : ORB_RESOLVE_KERNEL_PREFIX_W4;
 }
 
 // bytes of Jacobi-resolve scratch for n problems (0 unless that schedule runs)
