@@ -210,6 +210,82 @@ def test_search_by_projection_resolve_schedules(gpu, oracle, name, schedule, rou
             assert np.array_equal(km, km_ref), (w, i, np.nonzero(km != km_ref)[0][:10])
 
 
+def _cluster_problem(oracle, seed, n_keys=900, M=6000):
+    """Keypoints on a 3-px lattice in a few clusters (windows of 5-16 keypoints at
+    level 0-1, dozens at level 5-7) and map points over them whose descriptors are
+    near-copies: claims with observations lock keypoints fast, so many points run
+    out of their top-4 and need the exact re-scan -- from their candidate list
+    (<= 16 candidates) or from the grid (more)."""
+    rng = np.random.default_rng(seed)
+    w, h = 640, 480
+    scale = oracle.params(1000)["scale"]
+    k = np.zeros(n_keys, oracle.KEYPOINT_DTYPE)
+    cx = rng.uniform(60, w - 60, 6)
+    cy = rng.uniform(60, h - 60, 6)
+    c = rng.integers(0, 6, n_keys)
+    k["x"] = (cx[c] + 3.0 * rng.integers(-7, 8, n_keys)).astype(np.float32)
+    k["y"] = (cy[c] + 3.0 * rng.integers(-7, 8, n_keys)).astype(np.float32)
+    k["octave"] = rng.choice([0, 0, 0, 1, 1, 5, 6, 7], n_keys)
+    k["size"] = 31.0
+    k["class_id"] = -1
+    d = rng.integers(0, 256, (n_keys, 32), dtype=np.uint8)
+    mps = np.zeros(M, oracle.MP_TRACK_DTYPE)
+    src = rng.integers(0, n_keys, M)
+    mps["proj_x"] = k["x"][src] + rng.uniform(-1.5, 1.5, M).astype(np.float32)
+    mps["proj_y"] = k["y"][src] + rng.uniform(-1.5, 1.5, M).astype(np.float32)
+    mps["proj_xr"] = -1.0
+    mps["level"] = np.minimum(k["octave"][src] + rng.integers(0, 2, M), 7)
+    mps["view_cos"] = np.where(rng.random(M) < 0.5, 0.999, 0.9).astype(np.float32)
+    mps["in_view"] = 1
+    mps["has_obs"] = rng.random(M) < 0.9
+    mpd = d[src].copy()
+    mpd ^= np.packbits(rng.random((M, 256)) < 0.06, axis=1, bitorder="little")
+    locked = (rng.random(n_keys) < 0.05).astype(np.uint8)
+    return k, d, scale, w, h, mps, mpd, locked
+
+
+@pytest.mark.parametrize("schedule", [0, 1, 2, 3])
+def test_search_by_projection_rescan_lists(gpu, oracle, schedule):
+    """The resolves' exact re-scan (a point's top-4 ran dry) through the candidate
+    lists k_proj_candidates writes for points with 5-16 candidates, and through the
+    grid walk for points with more, under every schedule, as one problem and as a
+    device batch of 8 problems; index-exact against the oracle.  The clusters make
+    both kinds of point common (checked on the oracle's side)."""
+    torch = pytest.importorskip("torch")
+    probs = [_cluster_problem(oracle, 40 + i) for i in range(8)]
+    m = gpu.ORBmatcher(0.8)
+    m.set_resolve(schedule, 6)
+    refs = []
+    for (k, d, scale, w, h, mps, mpd, lk) in probs:
+        refs.append(oracle.match_projection_local(k, d, scale, w, h, mps, mpd, 1.0, 0.8, lk))
+        n, km = m.SearchByProjection(gpu.Frame(k, d, scale, w, h), mps, mpd, 1.0, lk)
+        assert n == refs[-1][0] and np.array_equal(km, refs[-1][1])
+    # the same problems as one device batch
+    k0 = probs[0][0]
+    P, cap, M = len(probs), len(k0), len(probs[0][5])
+    kk = np.stack([p[0] for p in probs])
+    dd = np.stack([p[1] for p in probs])
+    lk = np.stack([p[7] for p in probs])
+    mp = np.stack([p[5] for p in probs])
+    md = np.stack([p[6] for p in probs])
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).cuda()
+    dk, dde, dl, dm, dmd = t(kk), t(dd), t(lk), t(mp), t(md)
+    dn = torch.full((P,), cap, dtype=torch.int32, device="cuda")
+    dnm = torch.full((P,), M, dtype=torch.int32, device="cuda")
+    dkm = torch.zeros((P, cap), dtype=torch.int32, device="cuda")
+    dnmt = torch.zeros(P, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    w, h, scale = probs[0][3], probs[0][4], probs[0][2]
+    m.search_by_projection_batch(P, dk.data_ptr(), dde.data_ptr(), dn.data_ptr(), dl.data_ptr(), cap,
+                                 dm.data_ptr(), dmd.data_ptr(), dnm.data_ptr(), M, w, h, scale, 1.0,
+                                 dkm.data_ptr(), dnmt.data_ptr())
+    torch.cuda.synchronize()
+    km = dkm.cpu().numpy()
+    nm = dnmt.cpu().numpy()
+    for i, (n_ref, km_ref) in enumerate(refs):
+        assert nm[i] == n_ref and np.array_equal(km[i], km_ref), i
+
+
 @pytest.mark.parametrize("stereo,locked", [(False, True), (True, True), (False, False)])
 def test_search_by_projection_staged(gpu, oracle, stereo, locked):
     """The zero-copy pair orb_match_projection_local_stage / _staged (inputs
