@@ -21,7 +21,7 @@ profiled pass of the same launches after it -- no event sits inside the timed
 region; HBM bytes per SURVEY §8(d) as
 the primary fraction, VALU issue beside it), `host_input` (the same pipeline
 fed from pinned host memory: H2D of every frame and D2H of every result, the
-drop-in's PCIe-inclusive rate, never `value`), `parity_sample` (8 frames of
+drop-in's PCIe-inclusive rate, never `value`), `parity_sample` (64 frames of
 the timed pipeline's own output buffers re-computed by the CPU oracle, bit for
 bit; a mismatch exits non-zero) and `cpu_baseline` (the C++ CPU oracle, single
 thread, on a bounded sample of the same workload).
@@ -192,7 +192,7 @@ def host_cpu():
     return model, os.cpu_count()
 
 
-def snapshot_sample(sets, g_end, n_sets, n_batches, B, orb, per_set=2):
+def snapshot_sample(sets, g_end, n_sets, n_batches, B, orb, per_set=16):
     """Host copies of `per_set` frames of each buffer set as the timed region
     left it: set j holds launch gg's outputs for the last n_sets launches gg
     (batch gg % n_batches).  Returns [(frame index, keypoints, descriptors,
@@ -216,19 +216,22 @@ def cpu_leg(imgs, maps, sample, args, scale, timed):
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # CPU oracle: checker / baseline only
 
-    bad = []
-    for f, k, d, km, nm in sample:
+    def check(smp):
+        f, k, d, km, nm = smp
         kr, dr, _ = oracle.extract(imgs[f], args.features, 1.2, 8, 20, 7)
         mps, mpd, locked = maps[f]
         n_ref, km_ref = oracle.match_projection_local(kr, dr, scale, args.width, args.height, mps,
                                                       mpd, 1.0, 0.8, locked[: len(kr)])
         ok = (k.tobytes() == kr.tobytes() and d.tobytes() == dr.tobytes() and nm == n_ref
               and np.array_equal(km, km_ref))
-        if not ok:
-            bad.append({"frame": int(f), "n": int(len(k)), "n_ref": int(len(kr)),
-                        "keys": k.tobytes() == kr.tobytes(), "desc": d.tobytes() == dr.tobytes(),
-                        "nmatch": int(nm), "nmatch_ref": int(n_ref),
-                        "kp_match_diff": int(np.sum(km != km_ref)) if len(km) == len(km_ref) else -1})
+        if ok:
+            return None
+        return {"frame": int(f), "n": int(len(k)), "n_ref": int(len(kr)),
+                "keys": k.tobytes() == kr.tobytes(), "desc": d.tobytes() == dr.tobytes(),
+                "nmatch": int(nm), "nmatch_ref": int(n_ref),
+                "kp_match_diff": int(np.sum(km != km_ref)) if len(km) == len(km_ref) else -1}
+
+    bad = [r for r in parallel_map(check, sample, args.threads) if r is not None]
     if bad:
         print("bench.py parity_sample mismatch:", json.dumps(bad), file=sys.stderr, flush=True)
     par = {"frames": [int(s[0]) for s in sample], "bit_exact": not bad, "mismatched": bad,
@@ -1130,7 +1133,7 @@ def main():
     counts_ok = bool(torch.equal(step_counts[last_k].cpu(), torch.from_numpy(cnt_h)))
     if not counts_ok:
         raise RuntimeError("timed-step keypoint counts differ from the untimed pass")
-    # the timed pipeline's own outputs for 8 sampled frames of its last launches
+    # the timed pipeline's own outputs for 64 sampled frames of its last launches
     # (keypoints, descriptors, matches), checked against the oracle in the CPU leg
     sample = snapshot_sample(sets, g, NS, NB, B, orb)
     gather_ok = None
