@@ -9,6 +9,9 @@ descriptor bits differ, and what the one-frame path gives for that frame.
 --match M: also SearchByProjection(F, localMap) of every frame against its own
 M-point synthetic local map (bench.py's maps), device-batched, against the
 oracle's assignments.
+--stereo: every frame is a stereo pair (view 0 left, view 1 right): both
+extractions and ComputeStereoMatches (device-batched, orb_stereo_match_batch)
+against the oracle's mvuRight / mvDepth, bit for bit.
 """
 import argparse
 import json
@@ -34,7 +37,10 @@ def main():
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--features", type=int, default=1000)
     ap.add_argument("--match", type=int, default=0)
+    ap.add_argument("--stereo", action="store_true")
     a = ap.parse_args()
+    if a.stereo:
+        return stereo(a)
     import torch
     from conftest import load_pkg
     import oracle
@@ -148,6 +154,82 @@ def main():
         single = bool(len(k1) == len(kr) and np.array_equal(d1, dr) and
                       k1.tobytes() == kr.tobytes())
         print(json.dumps({"frame": ids[i], **r, "one_frame_path_exact": single}), flush=True)
+
+
+def stereo(a):
+    import torch
+    from conftest import load_pkg
+    import oracle
+    orb = load_pkg()
+    W, H, B, NF = a.width, a.height, a.batch, a.features
+    bf, fx = 386.1448, 718.856
+    ids = list(range(a.start, a.start + a.frames))
+    lib = orb.lib()
+    views = []
+    for v in (0, 1):
+        im = np.empty((len(ids), H, W), np.uint8)
+        with ThreadPoolExecutor(a.threads) as ex:
+            list(ex.map(lambda i: lib.orb_synth_image(a.seed, ids[i], v, W, H, im[i].ctypes.data, W),
+                        range(len(ids))))
+        views.append(im)
+    L = orb.ORBextractor(NF, 1.2, 8, 20, 7)
+    R = orb.ORBextractor(NF, 1.2, 8, 20, 7)
+    mt = orb.ORBmatcher()
+    cap = L.capacity(W, H)
+    dev = torch.device("cuda", 0)
+    ur_all = np.zeros((len(ids), cap), np.float32)
+    dp_all = np.zeros((len(ids), cap), np.float32)
+    n_all = np.zeros(len(ids), np.int32)
+    for b0 in range(0, len(ids), B):
+        nb = min(B, len(ids) - b0)
+        outs = []
+        for ext, im in ((L, views[0]), (R, views[1])):
+            d_img = torch.from_numpy(im[b0:b0 + nb]).to(dev)
+            k = torch.zeros((nb, cap, 7), dtype=torch.int32, device=dev)
+            de = torch.zeros((nb, cap, 32), dtype=torch.uint8, device=dev)
+            n = torch.zeros(nb, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            ext.extract_batch(d_img.data_ptr(), nb, W, H, W, W * H, k.data_ptr(), de.data_ptr(), cap,
+                              n.data_ptr())
+            torch.cuda.synchronize()
+            outs.append((d_img, k, de, n))
+        ur = torch.zeros((nb, cap), dtype=torch.float32, device=dev)
+        dp = torch.zeros((nb, cap), dtype=torch.float32, device=dev)
+        sad = torch.zeros((nb, cap), dtype=torch.int32, device=dev)
+        (_, kl, dl, nl), (_, kr, dr, nr) = outs
+        mt.stereo_match_batch(nb, L, R, kl.data_ptr(), dl.data_ptr(), nl.data_ptr(), kr.data_ptr(),
+                              dr.data_ptr(), nr.data_ptr(), cap, bf, fx, ur.data_ptr(), dp.data_ptr(),
+                              sad.data_ptr())
+        torch.cuda.synchronize()
+        ur_all[b0:b0 + nb] = ur.cpu().numpy()
+        dp_all[b0:b0 + nb] = dp.cpu().numpy()
+        n_all[b0:b0 + nb] = nl.cpu().numpy()
+    print(f"extracted and stereo-matched {len(ids)} pairs on the GPU", flush=True)
+    p = oracle.params(NF)
+
+    def check(i):
+        kl, dl, _ = oracle.extract(views[0][i], NF, 1.2, 8, 20, 7)
+        kr, dr, _ = oracle.extract(views[1][i], NF, 1.2, 8, 20, 7)
+        ur_ref, dp_ref = oracle.stereo_match(kl, dl, p["scale"], kr, dr, oracle.pyramid(views[0][i]),
+                                             oracle.pyramid(views[1][i]), p["inv_scale"], bf, fx, W, H)
+        n = int(n_all[i])
+        if n != len(kl):
+            return i, {"count": [n, len(kl)]}
+        bad = np.nonzero((ur_all[i, :n].view(np.uint32) != ur_ref.view(np.uint32)) |
+                         (dp_all[i, :n].view(np.uint32) != dp_ref.view(np.uint32)))[0]
+        if len(bad) == 0:
+            return i, None
+        return i, {"differ": int(len(bad)), "first": [int(j) for j in bad[:4]],
+                   "gpu": [float(ur_all[i, j]) for j in bad[:4]], "ref": [float(ur_ref[j]) for j in bad[:4]]}
+
+    with ThreadPoolExecutor(a.threads) as ex:
+        res = list(ex.map(check, range(len(ids))))
+    bad = [(i, r) for i, r in res if r is not None]
+    matched = float((ur_all > 0).sum()) / len(ids)
+    print(f"ComputeStereoMatches: {len(bad)} of {len(ids)} pairs differ from the oracle "
+          f"(mean {matched:.1f} left keypoints with a match)", flush=True)
+    for i, r in bad[:10]:
+        print(json.dumps({"pair": ids[i], **r}), flush=True)
 
 
 if __name__ == "__main__":
