@@ -9,6 +9,8 @@ descriptor bits differ, and what the one-frame path gives for that frame.
 --match M: also SearchByProjection(F, localMap) of every frame against its own
 M-point synthetic local map (bench.py's maps), device-batched, against the
 oracle's assignments.
+--one-frame: every frame through the one-frame entry point (ORBextractor
+operator(): k_fast_band, the register octree, k_orient_desc<1>) instead.
 --stereo: every frame is a stereo pair (view 0 left, view 1 right): both
 extractions and ComputeStereoMatches (device-batched, orb_stereo_match_batch)
 against the oracle's mvuRight / mvDepth, bit for bit.
@@ -38,6 +40,7 @@ def main():
     ap.add_argument("--features", type=int, default=1000)
     ap.add_argument("--match", type=int, default=0)
     ap.add_argument("--stereo", action="store_true")
+    ap.add_argument("--one-frame", action="store_true")
     a = ap.parse_args()
     if a.stereo:
         return stereo(a)
@@ -61,6 +64,13 @@ def main():
     n_all = np.zeros(len(ids), np.int32)
     for b0 in range(0, len(ids), B):
         nb = min(B, len(ids) - b0)
+        if a.one_frame:
+            for i in range(b0, b0 + nb):
+                k1, d1 = ext(imgs[i])
+                n_all[i] = len(k1)
+                k_all[i, :len(k1)] = k1
+                d_all[i, :len(k1)] = d1
+            continue
         d_img = torch.from_numpy(imgs[b0:b0 + nb]).to(dev)
         dk = torch.zeros((nb, cap, 7), dtype=torch.int32, device=dev)
         dd = torch.zeros((nb, cap, 32), dtype=torch.uint8, device=dev)
@@ -72,7 +82,8 @@ def main():
         k_all[b0:b0 + nb] = dk.cpu().numpy().view(orb.KEYPOINT_DTYPE).reshape(nb, cap)
         d_all[b0:b0 + nb] = dd.cpu().numpy()
         n_all[b0:b0 + nb] = dn.cpu().numpy()
-    print(f"extracted {len(ids)} frames on the GPU", flush=True)
+    print(f"extracted {len(ids)} frames on the GPU ({'one-frame calls' if a.one_frame else 'batches'})",
+          flush=True)
 
     def check(i):
         kr, dr, _ = oracle.extract(imgs[i], NF, 1.2, 8, 20, 7)
