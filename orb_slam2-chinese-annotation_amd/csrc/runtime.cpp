@@ -1842,9 +1842,20 @@ static LocalLayout local_layout(int N, int M) {
 
 // The pinned input block for N keypoints and M map points (header written);
 // caller holds m->mu
+// A _begin whose _staged never came (or failed): its DMA may still read the
+// pinned block, so wait for it before the block is rewritten; caller holds m->mu
+static orb_status_t local_abandon(orb_matcher_t* m) {
+  if (!m->begun) return ORB_OK;
+  m->begun = false;
+  hipSetDevice(m->device);
+  HIP_TRY(stream_wait(m->stream));
+  return ORB_OK;
+}
+
 static orb_status_t local_stage(orb_matcher_t* m, int N, int M, LocalLayout* out) {
   const LocalLayout L = local_layout(N, M);
   orb_status_t st;
+  if ((st = local_abandon(m))) return st;
   if ((st = m->hIn.ensure(L.inBytes))) return st;
   const int32_t nk = N, nm = M;
   memcpy(m->hIn.as<uint8_t>(), &nk, 4);
@@ -1979,11 +1990,6 @@ orb_status_t orb_match_projection_local_stage(orb_matcher_t* m, int n_keys, int 
                                               orb_local_stage_t* out) {
   if (!m || !out || n_keys <= 0 || n_keys >= (1 << 19) || n_mp < 0) return ORB_EINVAL;
   std::lock_guard<std::mutex> g(m->mu);
-  if (m->begun) {  // a _begin whose _staged never came: its DMA still reads the block
-    m->begun = false;
-    hipSetDevice(m->device);
-    HIP_TRY(stream_wait(m->stream));
-  }
   LocalLayout L;
   orb_status_t st = local_stage(m, n_keys, n_mp, &L);
   if (st) return st;
@@ -2030,11 +2036,14 @@ orb_status_t orb_match_projection_local_staged(orb_matcher_t* m, const orb_frame
   std::lock_guard<std::mutex> g(m->mu);
   // the block must hold what _stage laid out for exactly these counts
   const bool begun = m->begun;
-  m->begun = false;
   const int sn = m->stagedN, sm = m->stagedM;
   m->stagedN = m->stagedM = -1;
-  if (frame->n <= 0 || frame->n != sn || n_mp != sm) return ORB_EINVAL;
-  if (begun && (m->begunStereo != (stereo != 0) || m->begunLocked != (locked != 0))) return ORB_EINVAL;
+  if (frame->n <= 0 || frame->n != sn || n_mp != sm ||
+      (begun && (m->begunStereo != (stereo != 0) || m->begunLocked != (locked != 0)))) {
+    const orb_status_t st = local_abandon(m);  // (the block must be staged again)
+    return st ? st : ORB_EINVAL;
+  }
+  m->begun = false;
   *nmatches = 0;
   return local_run(m, frame->n, n_mp, frame, stereo != 0, locked != 0, th, nnratio, kp_match,
                    nmatches, begun);
