@@ -1706,9 +1706,9 @@ static ProjParamsHost proj_params(float min_x, float max_x, float min_y, float m
 static orb_status_t ovf_pool(orb_matcher_t* m, int nproblems, ProjParamsHost& P, hipStream_t s) {
   orb_status_t st;
   if ((st = m->dOvf.ensure(orb_k_proj_ovf_bytes(nproblems)))) return st;
-  const void* old = m->dOvfCtr.p;
+  const size_t oldBytes = m->dOvfCtr.bytes;  // (a reallocation may return the old address)
   if ((st = m->dOvfCtr.ensure((size_t)std::max(nproblems, 1) * 4))) return st;
-  if (m->dOvfCtr.p != old) HIP_TRY(hipMemsetAsync(m->dOvfCtr.p, 0, m->dOvfCtr.bytes, s));
+  if (m->dOvfCtr.bytes != oldBytes) HIP_TRY(hipMemsetAsync(m->dOvfCtr.p, 0, m->dOvfCtr.bytes, s));
   m->ovfGen = m->ovfGen % 4095u + 1u;
   P.ovf = m->dOvf.as<uint32_t>();
   P.ovfCtr = m->dOvfCtr.as<uint32_t>();
