@@ -1233,6 +1233,16 @@ orb_status_t orb_extractor_extract_batch(orb_extractor_t* h, const uint8_t* d_im
   return ORB_OK;
 }
 
+// Row pitch of the one-frame path's staged image (pinned and device): the
+// width itself (the kernels take any stride), so a contiguous caller image is
+// staged with one memcpy instead of one per row
+#ifndef ONE_PITCH_ALIGN
+#define ONE_PITCH_ALIGN 1  // (A/B knob: 64 = rows padded to 64 bytes)
+#endif
+static size_t one_stride(int width) {
+  return ((size_t)width + ONE_PITCH_ALIGN - 1) / ONE_PITCH_ALIGN * ONE_PITCH_ALIGN;
+}
+
 orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int width,
                                    int height, size_t stride, orb_keypoint_t* keypoints,
                                    uint8_t* descriptors, int capacity, int* n_keypoints) {
@@ -1244,26 +1254,30 @@ orb_status_t orb_extractor_extract(orb_extractor_t* h, const uint8_t* image, int
   orb_status_t st = build_plan(h, width, height);
   if (st) return st;
   const int cap = h->plan.slotsPerImage;
-  const size_t dstride = ((size_t)width + 63) & ~(size_t)63;
+  const size_t dstride = one_stride(width);
   const size_t pitch = dstride * height;
+  const size_t pitch16 = (pitch + 15) & ~(size_t)15;  // k_copy_pinned moves 16-byte words
   const size_t kOff = 16, dOff = kOff + (size_t)cap * sizeof(orb_keypoint_t);
   const size_t outBytes = dOff + (size_t)cap * 32;
   if ((st = ensure_batch(h, 1))) return st;
-  if ((st = h->dImg.ensure(pitch))) return st;
+  if ((st = h->dImg.ensure(pitch16))) return st;
   if ((st = h->dOne.ensure(outBytes))) return st;
-  if ((st = h->hImg.ensure(pitch))) return st;
+  if ((st = h->hImg.ensure(pitch16))) return st;
   if ((st = h->hOut.ensure(outBytes))) return st;
   if (h->pyrReadback && (st = h->hPyr.ensure((size_t)std::max<long long>(h->arenaBytes, 1)))) return st;
   h->hPyrValid = false;
   // a batch call may still run on a caller's stream (CallOrder)
   if (must_wait(h->lastStream, h->stream)) HIP_TRY(hipStreamWaitEvent(h->stream, h->evBatch, 0));
   // image -> pinned staging at the device row pitch
-  for (int y = 0; y < height; ++y)
-    memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
+  if (stride == dstride)
+    memcpy(h->hImg.p, image, pitch);
+  else
+    for (int y = 0; y < height; ++y)
+      memcpy(h->hImg.as<uint8_t>() + (size_t)y * dstride, image + (size_t)y * stride, (size_t)width);
   uint8_t* d1 = h->dOne.as<uint8_t>();
   // one DMA in, the extraction, one DMA out of the count and every record slot
   auto upload = [&]() -> orb_status_t {
-    HIP_TRY(orb_k_copy_pinned(h->dImg.p, h->hImg.p, pitch, h->stream));
+    HIP_TRY(orb_k_copy_pinned(h->dImg.p, h->hImg.p, pitch16, h->stream));
     return ORB_OK;
   };
   auto enqueue = [&](bool capturing) -> orb_status_t {
@@ -1400,7 +1414,7 @@ orb_status_t orb_extractor_host_pyramid(orb_extractor_t* h, int level, const uin
   if (height) *height = d.h;
   if (level == 0) {  // the call's own pinned staging of the image
     *data = h->hImg.as<uint8_t>();
-    if (stride) *stride = ((size_t)d.w + 63) & ~(size_t)63;
+    if (stride) *stride = one_stride(d.w);
     return ORB_OK;
   }
   if (!h->hPyrValid) {
@@ -2320,8 +2334,8 @@ orb_status_t orb_stereo_match_extracted(orb_matcher_t* m, orb_extractor_t* left_
     if (l == 0) {  // level 0 = the image staged by orb_extractor_extract
       lv.L[0] = left_ext->dImg.as<uint8_t>();
       lv.R[0] = right_ext->dImg.as<uint8_t>();
-      P.strideL[0] = (int)(((size_t)dl.w + 63) & ~(size_t)63);
-      P.strideR[0] = (int)(((size_t)dr.w + 63) & ~(size_t)63);
+      P.strideL[0] = (int)one_stride(dl.w);
+      P.strideR[0] = (int)one_stride(dr.w);
     } else {
       lv.L[l] = left_ext->dArena.as<uint8_t>() + dl.arenaOff;
       lv.R[l] = right_ext->dArena.as<uint8_t>() + dr.arenaOff;
