@@ -75,18 +75,23 @@ void ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoi
   assert(image.type() == CV_8UC1);  // :1100
   const int cap = orb_extractor_capacity(mpGpu, image.cols, image.rows);
   if (cap < 0) throw std::runtime_error("ORBextractor::operator(): unsupported image size");
-  _keypoints.resize(cap);
-  Mat desc(cap, 32, CV_8U);
+  // the library writes up to `cap` records; they land in per-thread scratch kept
+  // across calls (sizing the caller's vector to `cap` first value-initialised
+  // thousands of KeyPoints per frame, and a fresh descriptor Mat each call)
+  thread_local std::vector<KeyPoint> kpScratch;
+  thread_local std::vector<uint8_t> descScratch;
+  if ((int)kpScratch.size() < cap) kpScratch.resize(cap);
+  if (descScratch.size() < (size_t)cap * 32) descScratch.resize((size_t)cap * 32);
   int n = 0;
   check(orb_extractor_extract(mpGpu, image.ptr<uint8_t>(), image.cols, image.rows, image.step,
-                              reinterpret_cast<orb_keypoint_t*>(_keypoints.data()),
-                              desc.ptr<uint8_t>(), cap, &n),
+                              reinterpret_cast<orb_keypoint_t*>(kpScratch.data()),
+                              descScratch.data(), cap, &n),
         "operator()");
-  _keypoints.resize(n);  // :1127-1128 clears and refills
+  _keypoints.assign(kpScratch.begin(), kpScratch.begin() + n);  // :1127-1128 clears and refills
   if (n == 0)
     _descriptors.release();  // :1118-1121
   else
-    desc.rowRange(0, n).copyTo(_descriptors);
+    Mat(n, 32, CV_8U, descScratch.data(), 32).copyTo(_descriptors);
 #ifndef ORB_AMD_GPU_STEREO
   // mvImagePyramid aliases the library's pinned host mirror of this call's
   // levels (one DMA in the call's graph, no copy here), valid until the next
