@@ -1302,7 +1302,10 @@ hipError_t orb_k_proj_candidates(const orb_keypoint_t* keys, const uint8_t* desc
 //    problem not settled (only on request: the rounds compete with a
 //    concurrent extraction for every CU, profiles/r04_c5_stages.txt).
 #ifndef RESOLVE_FP_T
-#define RESOLVE_FP_T 1024  // threads of k_proj_resolve_fp (1024-point windows: 1024 / T points per thread)
+#define RESOLVE_FP_T 1024  // threads of k_proj_resolve_fp (RESOLVE_FP_W / T points per thread)
+#endif
+#ifndef RESOLVE_FP_W
+#define RESOLVE_FP_W 1024  // points per window of k_proj_resolve_fp (A/B knob)
 #endif
 #define RESOLVE_FP_MIN_MAP 20000
 #define RESOLVE_FP_FEW 8
@@ -1348,7 +1351,7 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
   if (kern == ORB_RESOLVE_KERNEL_FIXED_POINT || kern == ORB_RESOLVE_KERNEL_JACOBI) {
     const size_t ldsFp = (size_t)kpStride * 12;
     if (ldsFp > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)k_proj_resolve_fp<RESOLVE_FP_T, 1024 / RESOLVE_FP_T>,
+      hipError_t e = hipFuncSetAttribute((const void*)k_proj_resolve_fp<RESOLVE_FP_T, RESOLVE_FP_W / RESOLVE_FP_T>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsFp);
       if (e != hipSuccess) return e;
     }
@@ -1370,7 +1373,7 @@ hipError_t orb_k_proj_resolve(const orb_keypoint_t* keys, const uint8_t* desc,
       done = jacScratch + R;
       doneStride = js;
     }
-    hipLaunchKernelGGL((k_proj_resolve_fp<RESOLVE_FP_T, 1024 / RESOLVE_FP_T>), dim3(nproblems), dim3(RESOLVE_FP_T),
+    hipLaunchKernelGGL((k_proj_resolve_fp<RESOLVE_FP_T, RESOLVE_FP_W / RESOLVE_FP_T>), dim3(nproblems), dim3(RESOLVE_FP_T),
                        ldsFp, s, keys, desc,
                        uright, locked, nkeys, kpStride, mps, mpDesc, nmps, mpStride, cellStart,
                        cellIdx, P, topk, ncand, kpMatch, nmatches, done, doneStride);
