@@ -442,6 +442,7 @@ struct orb_extractor {
   std::vector<OrbCellDesc> cells;
   long long arenaBytes = 0, blurBytes = 0;
   int maxCellsPerLevel = 0, nodeCapMax = 0, ldsKeyCap = 0;
+  int nResizePairs = 0;  // resize launches per call with the level pairs (PYR_PAIR_MAX_IMAGES)
   DevBuf dCells, dRtab, dTiles, dBands;
 
   // batch scratch
@@ -520,6 +521,12 @@ static void compute_tables(orb_extractor* h) {
 // octree roots, output slots) and upload its tables.
 #ifndef PYR_FUSE2
 #define PYR_FUSE2 1  // level pairs in one k_pyr_resize2 launch where they fit (0: one launch per level)
+#endif
+#ifndef PYR_PAIR_MAX_IMAGES
+// calls of at most this many images take the level pairs; larger batches one
+// launch per level: the pairs save a frame 4 us of latency but cost batches
+// 0.3-1 % (C4), 1.5 % (C3) and 2 % (C5) (profiles/r06_resize2_fast_runs.txt)
+#define PYR_PAIR_MAX_IMAGES 8
 #endif
 static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   if (h->planW == W && h->planH == H) return ORB_OK;
@@ -787,6 +794,7 @@ static orb_status_t build_plan(orb_extractor* h, int W, int H) {
   h->octNodeBytes = octGlobal ? (long long)((nodeBytes + 255) & ~(size_t)255) : 0;
   h->planW = W;
   h->planH = H;
+  h->nResizePairs = nResize;
   h->prof.launchesPerCall[0] = nResize;
   h->batchCap = 0;  // scratch layout depends on the plan
   return ORB_OK;
@@ -906,14 +914,17 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
   // one-launch chain k_pyr_chain measured slower, 0.0386 vs 0.0269 ms per
   // frame, profiles/r04_step11.txt)
   PROF_REC(ev, pf.b(ev, 0), s);
+  const bool pairs = B <= PYR_PAIR_MAX_IMAGES;
+  h->prof.launchesPerCall[0] = pairs ? h->nResizePairs : P.nlevels - 1;
   for (int l = 1; l < P.nlevels; ++l) {
     const OrbLevelDesc& d = P.lv[l];
     const OrbLevelDesc& sd = P.lv[l - 1];
     const uint8_t* src = l == 1 ? d_images : arena + sd.arenaOff;
     const long long srcPitch = l == 1 ? (long long)imgPitch : ap;
     const int srcStride = l == 1 ? (int)stride : sd.pitch;
-    const int top = d.resize2 ? l + 1 : l;  // last level this launch writes
-    if (d.resize2) {
+    const bool pair = pairs && d.resize2;
+    const int top = pair ? l + 1 : l;  // last level this launch writes
+    if (pair) {
       const OrbLevelDesc& e = P.lv[l + 1];
       HIP_TRY(orb_k_pyr_resize2(src, srcPitch, srcStride, sd.w, sd.h, arena + d.arenaOff, ap, d.pitch,
                                 d.w, d.h, rt + d.rtabX, rt + d.rtabX + d.w, rt + d.rtabY,
@@ -926,7 +937,7 @@ static orb_status_t run_batch(orb_extractor* h, const uint8_t* d_images, int B, 
                                rt + d.rtabY + d.h, d.resizeMode, B, s));
     }
     l = top;
-    if (l >= sideLevels && l - (d.resize2 ? 1 : 0) <= sideLevels) {  // this launch wrote level sideLevels
+    if (l >= sideLevels && l - (pair ? 1 : 0) <= sideLevels) {  // this launch wrote level sideLevels
       if (sideEnd > l0End) {
         HIP_TRY(hipEventRecord(h->evLvl, s));
         HIP_TRY(hipStreamWaitEvent(side, h->evLvl, 0));

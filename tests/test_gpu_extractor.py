@@ -101,6 +101,35 @@ def test_pyramid_level_pairs_batch(gpu, oracle, w, h, sf, nl, launches):
             assert np.array_equal(got, ref[l]), f"image {i} level {l}: {(got != ref[l]).sum()} px differ"
 
 
+@pytest.mark.parametrize("w,h,sf,nl", [(1241, 376, 1.2, 8), (1920, 1080, 1.2, 8), (997, 613, 1.2, 7)])
+def test_pyramid_unpaired_batch(gpu, oracle, w, h, sf, nl):
+    """Batches of more than PYR_PAIR_MAX_IMAGES (8) images build the pyramid one
+    launch per level (k_pyr_resize; the level pairs cost batches throughput,
+    runtime.cpp): nl - 1 launches, every level bit-identical to the oracle."""
+    torch = pytest.importorskip("torch")
+    B = 9
+    imgs = np.stack([gpu.synth_image(23, f, w, h) for f in range(B)])
+    ext = gpu.ORBextractor(1000, sf, nl, 20, 7)
+    cap = ext.capacity(w, h)
+    d_img = torch.from_numpy(imgs).cuda()
+    d_k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    d_d = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ext.profile(True)
+    ext.extract_batch(d_img.data_ptr(), B, w, h, w, w * h, d_k.data_ptr(), d_d.data_ptr(), cap,
+                      d_n.data_ptr())
+    torch.cuda.synchronize()
+    name, _, n = ext.profile_read(0)
+    ext.profile(False)
+    assert name == "k_pyr_resize" and n == nl - 1, (name, n)
+    for i in (0, B - 1):
+        ref = oracle.pyramid(imgs[i], sf, nl)
+        for l in range(1, nl):
+            got = ext.batch_level(i, l)
+            assert np.array_equal(got, ref[l]), f"image {i} level {l}: {(got != ref[l]).sum()} px differ"
+
+
 @pytest.mark.parametrize("w,h", [(640, 480), (1241, 376), (1920, 1080), (403, 301)])
 def test_blurred_levels_bit_exact(gpu, oracle, w, h):
     """GaussianBlur(7x7, sigma 2, REFLECT_101) of every level (src/ORBextractor.cc:1143-1145)."""
